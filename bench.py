@@ -1,0 +1,187 @@
+#!/usr/bin/env python
+"""Flagship benchmark: GPT-2 1.3B, FSDP full-shard, bf16, fused AdamW + global grad-norm clipping,
+synthetic tokens (random-init weights), seq 1024, 8 sequences per GPU (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gpt2-fsdp|gpt2-ddp|resnet50-ddp]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Times exactly K optimizer steps bracketed by barrier + device synchronize, takes the MAX over ranks,
+and prints ONE JSON line on rank 0 whose ``value`` is the whole-job throughput.
+Metric/config follow BASELINE.json ("tokens/sec GPT-2-1.3B FSDP ... at 1/2/4/8 MI355X"; ResNet-50 DDP
+samples/sec via --workload resnet50-ddp).  BASELINE.md publishes no reference number -> vs_baseline null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp"])
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--micro-batch", type=int, default=None)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--grad-clip", type=float, default=1.0)
+    ap.add_argument("--reshard", type=int, default=1, help="FSDP reshard after forward (FULL_SHARD)")
+    ap.add_argument("--act-ckpt", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pytorch_distributedtraining_amd.ops import _lib
+    _lib.require()  # fail loudly if the HIP kernels are missing
+    from pytorch_distributedtraining_amd.parallel import Comm
+    comm = Comm()
+
+    torch.manual_seed(1234)
+    if args.workload.startswith("gpt2"):
+        result = bench_gpt2(args, comm, dev, world, rank)
+    else:
+        result = bench_resnet(args, comm, dev, world, rank)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def timed_loop(step_fn, args, comm, dev):
+    import torch
+    for i in range(args.warmup):
+        step_fn()
+        if i == 0:
+            torch.cuda.synchronize(dev)
+            log(f"[bench] warmup step 0 done")
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step_fn()
+        if (i + 1) % 10 == 0:
+            log(f"[bench] step {i + 1}/{args.steps}")
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    comm.all_reduce(t, "max")
+    return float(t.item())
+
+
+def bench_gpt2(args, comm, dev, world, rank):
+    import torch
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel import FullyShardedDataParallel, MixedPrecision, ShardingStrategy
+
+    fsdp = args.workload == "gpt2-fsdp"
+    name = args.model or ("gpt2-1.3b" if fsdp else "gpt2-124m")
+    mb = args.micro_batch or 8
+    S = args.seq
+    with torch.device(dev):
+        model = build_gpt2(name, n_positions=max(1024, S), activation_checkpointing=bool(args.act_ckpt))
+    nparams = model.num_params()
+    flops_tok = model.flops_per_token(S)
+    if fsdp:
+        strat = ShardingStrategy.FULL_SHARD if args.reshard else ShardingStrategy.SHARD_GRAD_OP
+        model = FullyShardedDataParallel(model, sharding_strategy=strat, mixed_precision=MixedPrecision(),
+                                         comm=comm, device=dev)
+        params = model.flat_parameters()
+        sharded = True
+        par = f"fsdp{world}"
+    else:
+        from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+        model = DistributedDataParallel(model, comm=comm, compute_dtype=torch.bfloat16)
+        params = [p for p in model.parameters()]
+        sharded = False
+        par = f"dp{world}"
+    opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    V = model.module.config.vocab_size if hasattr(model, "module") else model.config.vocab_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    batches = [torch.randint(0, 50257, (mb, S + 1), device=dev, generator=g) for _ in range(4)]
+    state = {"i": 0, "loss": None}
+
+    def step():
+        b = batches[state["i"] % len(batches)]
+        state["i"] += 1
+        loss = model(b[:, :-1], labels=b[:, 1:])
+        loss.backward()
+        _, coef, found = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=sharded, apply=False)
+        opt.step(grad_scale=coef)
+        opt.zero_grad(set_to_none=True)
+        state["loss"] = loss
+
+    dt = timed_loop(step, args, comm, dev)
+    tokens = world * mb * S * args.steps
+    tps = tokens / dt
+    log(f"[bench] {name} params={nparams/1e9:.3f}B loss={float(state['loss'].item()):.4f} "
+        f"step={1000*dt/args.steps:.1f}ms MFU(bf16 2.5PF/GPU)={tps*flops_tok/world/2.5e15*100:.1f}%")
+    metric = "tokens/sec GPT-2-1.3B FSDP (whole node)" if fsdp and name == "gpt2-1.3b" else \
+        f"tokens/sec {name} {'FSDP' if fsdp else 'DDP'} (whole node)"
+    return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
+                       "micro_batch_per_gpu": mb, "params": nparams, "sharding": "full_shard" if args.reshard else
+                       "shard_grad_op", "optimizer": "fused AdamW + global-norm clip"}}
+
+
+def bench_resnet(args, comm, dev, world, rank):
+    import torch
+    from pytorch_distributedtraining_amd.models.resnet import resnet50
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+
+    mb = args.micro_batch or 256
+    model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    model = DistributedDataParallel(model, comm=comm, compute_dtype=torch.bfloat16)
+    params = list(model.parameters())
+    opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (mb,), device=dev)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = crit(model(x), y)
+        loss.backward()
+        _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
+        opt.step(grad_scale=coef)
+        opt.zero_grad(set_to_none=True)
+
+    dt = timed_loop(step, args, comm, dev)
+    sps = world * mb * args.steps / dt
+    return {"metric": "samples/sec ResNet-50 DDP (whole node)", "value": round(sps, 2), "unit": "samples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "resnet50", "global_batch": world * mb, "seq_len": None, "parallelism": f"dp{world}",
+                       "image": "3x224x224"}}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,290 @@
+// Memory-bound elementwise kernels for gfx950: bias+GELU (tanh / erf) fwd+bwd, SwiGLU fwd+bwd,
+// rotary embedding (RoPE) fwd/bwd, fp8 (OCP e4m3fn) quantise/dequantise with per-tensor amax,
+// and an fp32->bf16 cast.  All use 16-byte vector accesses (8 x bf16 per lane).
+//
+// Parity targets: GPT-2 MLP (bias + gelu_new), SwinIR MLP (nn.GELU = erf form),
+// Llama-3 MLP (SwiGLU) and attention (RoPE, rotate-half convention), BASELINE.json north star
+// "bf16/fp8 loss-scaled cast".
+#include "common.h"
+#include <hip/hip_fp8.h>
+
+using namespace pdt;
+
+namespace {
+
+constexpr int NT = 256;
+constexpr float kSqrt2OverPi = 0.7978845608028654f;
+constexpr float kGeluC = 0.044715f;
+constexpr float kInvSqrt2 = 0.7071067811865476f;
+
+template <bool TANH>
+__device__ __forceinline__ float gelu_f(float u) {
+  if (TANH) {
+    const float t = tanhf(kSqrt2OverPi * (u + kGeluC * u * u * u));
+    return 0.5f * u * (1.f + t);
+  } else {
+    return 0.5f * u * (1.f + erff(u * kInvSqrt2));
+  }
+}
+template <bool TANH>
+__device__ __forceinline__ float gelu_grad(float u) {
+  if (TANH) {
+    const float inner = kSqrt2OverPi * (u + kGeluC * u * u * u);
+    const float t = tanhf(inner);
+    return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kGeluC * u * u);
+  } else {
+    const float cdf = 0.5f * (1.f + erff(u * kInvSqrt2));
+    const float pdf = 0.3989422804014327f * __expf(-0.5f * u * u);
+    return cdf + u * pdf;
+  }
+}
+
+// y = gelu(h + bias); N % 8 == 0 (vector path).  bias may be null.
+template <typename T, typename B, bool TANH>
+__global__ __launch_bounds__(NT) void bias_gelu_fwd_kernel(const T* __restrict__ h, const B* __restrict__ bias,
+                                                           T* __restrict__ y, int64_t n8, int N) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    const int64_t e = i * 8;
+    float v[8], b[8];
+    Vec8<T>::load(h + e, v);
+    if (bias) Vec8<B>::load(bias + (int)(e % N), b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gelu_f<TANH>(bias ? v[k] + b[k] : v[k]);
+    Vec8<T>::store(y + e, v);
+  }
+}
+
+template <typename T, typename B, bool TANH>
+__global__ __launch_bounds__(NT) void bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ h,
+                                                           const B* __restrict__ bias, T* __restrict__ dh,
+                                                           int64_t n8, int N) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    const int64_t e = i * 8;
+    float v[8], g[8], b[8];
+    Vec8<T>::load(h + e, v);
+    Vec8<T>::load(dy + e, g);
+    if (bias) Vec8<B>::load(bias + (int)(e % N), b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] *= gelu_grad<TANH>(bias ? v[k] + b[k] : v[k]);
+    Vec8<T>::store(dh + e, g);
+  }
+}
+
+// SwiGLU on a fused [rows, 2F] projection: y[r, j] = silu(x[r, j]) * x[r, F + j]
+template <typename T>
+__global__ __launch_bounds__(NT) void swiglu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
+                                                        int F) {
+  const int64_t n8 = rows * (F / 8);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / (F / 8);
+    const int j = (int)(i % (F / 8)) * 8;
+    float a[8], b[8], o[8];
+    Vec8<T>::load(x + r * 2 * F + j, a);
+    Vec8<T>::load(x + r * 2 * F + F + j, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = a[k] / (1.f + __expf(-a[k])) * b[k];
+    Vec8<T>::store(y + r * F + j, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                        T* __restrict__ dx, int64_t rows, int F) {
+  const int64_t n8 = rows * (F / 8);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / (F / 8);
+    const int j = (int)(i % (F / 8)) * 8;
+    float a[8], b[8], g[8], da[8], db[8];
+    Vec8<T>::load(x + r * 2 * F + j, a);
+    Vec8<T>::load(x + r * 2 * F + F + j, b);
+    Vec8<T>::load(dy + r * F + j, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float s = 1.f / (1.f + __expf(-a[k]));
+      const float silu = a[k] * s;
+      db[k] = g[k] * silu;
+      da[k] = g[k] * b[k] * (s * (1.f + a[k] * (1.f - s)));
+    }
+    Vec8<T>::store(dx + r * 2 * F + j, da);
+    Vec8<T>::store(dx + r * 2 * F + F + j, db);
+  }
+}
+
+// RoPE (rotate-half): x viewed as [rows = B*S*H, D] with row r at position s = (r / H) % S + pos0.
+// out[i] = x[i] c - x[i+D/2] s_ ; out[i+D/2] = x[i+D/2] c + x[i] s_   (sign = -1 for backward).
+// cos/sin tables: [S_max, D/2] fp32.  Handles a row stride so q and k can be rotated in place
+// inside a fused qkv buffer.
+template <typename T>
+__global__ __launch_bounds__(NT) void rope_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
+                                                  int64_t row_stride_in, int64_t row_stride_out, int H, int S,
+                                                  int D, int pos0, const float* __restrict__ cosb,
+                                                  const float* __restrict__ sinb, float sign) {
+  const int half = D / 2, h8 = half / 8;
+  const int64_t n = rows * h8;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / h8;
+    const int j = (int)(i % h8) * 8;
+    const int s = (int)((r / H) % S) + pos0;
+    float a[8], b[8], c[8], sn[8], o1[8], o2[8];
+    Vec8<T>::load(x + r * row_stride_in + j, a);
+    Vec8<T>::load(x + r * row_stride_in + half + j, b);
+    Vec8<float>::load(cosb + (int64_t)s * half + j, c);
+    Vec8<float>::load(sinb + (int64_t)s * half + j, sn);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float ss = sign * sn[k];
+      o1[k] = a[k] * c[k] - b[k] * ss;
+      o2[k] = b[k] * c[k] + a[k] * ss;
+    }
+    Vec8<T>::store(y + r * row_stride_out + j, o1);
+    Vec8<T>::store(y + r * row_stride_out + half + j, o2);
+  }
+}
+
+// fp8 e4m3fn (OCP, gfx950) quantisation with a per-tensor scale read from device memory;
+// the same pass records amax(|x|) (for delayed scaling) with an integer atomicMax on the float bits.
+template <typename T>
+__global__ __launch_bounds__(NT) void fp8_quant_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
+                                                       int64_t n, const float* __restrict__ scale,
+                                                       unsigned int* __restrict__ amax_bits) {
+  const float sc = scale ? *scale : 1.f;
+  float amax = 0.f;
+  for (int64_t i = (blockIdx.x * (int64_t)NT + threadIdx.x) * 8; i < n; i += (int64_t)gridDim.x * NT * 8) {
+    if (i + 8 <= n) {
+      float v[8];
+      Vec8<T>::load(x + i, v);
+      uint64_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        amax = fmaxf(amax, fabsf(v[k]));
+        const __hip_fp8_storage_t b = __hip_cvt_float_to_fp8(v[k] * sc, __HIP_SATFINITE, __HIP_E4M3);
+        packed |= (uint64_t)b << (8 * k);
+      }
+      *reinterpret_cast<uint64_t*>(q + i) = packed;
+    } else {
+      for (int64_t j = i; j < n; ++j) {
+        const float v = to_f<T>(x[j]);
+        amax = fmaxf(amax, fabsf(v));
+        q[j] = __hip_cvt_float_to_fp8(v * sc, __HIP_SATFINITE, __HIP_E4M3);
+      }
+    }
+  }
+  if (amax_bits) {
+    amax = wave_max(amax);
+    if ((threadIdx.x & 63) == 0) atomicMax(amax_bits, __float_as_uint(amax));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void fp8_dequant_kernel(const uint8_t* __restrict__ q, T* __restrict__ y, int64_t n,
+                                                         const float* __restrict__ scale_inv) {
+  const float si = scale_inv ? *scale_inv : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    __hip_fp8_e4m3 v;
+    v.__x = q[i];
+    y[i] = from_f<T>((float)v * si);
+  }
+}
+
+__global__ __launch_bounds__(NT) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                           int64_t n) {
+  for (int64_t i = (blockIdx.x * (int64_t)NT + threadIdx.x) * 8; i < n; i += (int64_t)gridDim.x * NT * 8) {
+    if (i + 8 <= n) {
+      float v[8];
+      Vec8<float>::load(x + i, v);
+      Vec8<bf16_t>::store(y + i, v);
+    } else {
+      for (int64_t j = i; j < n; ++j) y[j] = f2bf(x[j]);
+    }
+  }
+}
+
+}  // namespace
+
+PDT_API int pdt_bias_gelu_fwd(const void* h, const void* bias, void* y, int64_t rows, int N, int dt, int bdt,
+                              int tanh_approx, hipStream_t st) {
+  if (N % 8) return (int)hipErrorInvalidValue;
+  const int64_t n8 = rows * N / 8;
+  const int grid = grid_for(n8, NT, 256 * 16);
+#define PDT_L(T, B, TH) bias_gelu_fwd_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)h, (const B*)bias, (T*)y, n8, N)
+  if (dt == kBF16) {
+    if (bdt == kF32) { if (tanh_approx) PDT_L(bf16_t, float, true); else PDT_L(bf16_t, float, false); }
+    else { if (tanh_approx) PDT_L(bf16_t, bf16_t, true); else PDT_L(bf16_t, bf16_t, false); }
+  } else {
+    if (bdt == kF32) { if (tanh_approx) PDT_L(float, float, true); else PDT_L(float, float, false); }
+    else { if (tanh_approx) PDT_L(float, bf16_t, true); else PDT_L(float, bf16_t, false); }
+  }
+#undef PDT_L
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_bias_gelu_bwd(const void* dy, const void* h, const void* bias, void* dh, int64_t rows, int N, int dt,
+                              int bdt, int tanh_approx, hipStream_t st) {
+  if (N % 8) return (int)hipErrorInvalidValue;
+  const int64_t n8 = rows * N / 8;
+  const int grid = grid_for(n8, NT, 256 * 16);
+#define PDT_L(T, B, TH) \
+  bias_gelu_bwd_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh, n8, N)
+  if (dt == kBF16) {
+    if (bdt == kF32) { if (tanh_approx) PDT_L(bf16_t, float, true); else PDT_L(bf16_t, float, false); }
+    else { if (tanh_approx) PDT_L(bf16_t, bf16_t, true); else PDT_L(bf16_t, bf16_t, false); }
+  } else {
+    if (bdt == kF32) { if (tanh_approx) PDT_L(float, float, true); else PDT_L(float, float, false); }
+    else { if (tanh_approx) PDT_L(float, bf16_t, true); else PDT_L(float, bf16_t, false); }
+  }
+#undef PDT_L
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_swiglu_fwd(const void* x, void* y, int64_t rows, int F, int dt, hipStream_t st) {
+  if (F % 8) return (int)hipErrorInvalidValue;
+  const int grid = grid_for(rows * F / 8, NT, 256 * 16);
+  if (dt == kBF16) swiglu_fwd_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, (bf16_t*)y, rows, F);
+  else swiglu_fwd_kernel<float><<<grid, NT, 0, st>>>((const float*)x, (float*)y, rows, F);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_swiglu_bwd(const void* dy, const void* x, void* dx, int64_t rows, int F, int dt, hipStream_t st) {
+  if (F % 8) return (int)hipErrorInvalidValue;
+  const int grid = grid_for(rows * F / 8, NT, 256 * 16);
+  if (dt == kBF16)
+    swiglu_bwd_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, rows, F);
+  else
+    swiglu_bwd_kernel<float><<<grid, NT, 0, st>>>((const float*)dy, (const float*)x, (float*)dx, rows, F);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_rope(const void* x, void* y, int64_t rows, int64_t stride_in, int64_t stride_out, int H, int S, int D,
+                     int pos0, const float* cosb, const float* sinb, int backward, int dt, hipStream_t st) {
+  if ((D / 2) % 8) return (int)hipErrorInvalidValue;
+  const int grid = grid_for(rows * (D / 16), NT, 256 * 16);
+  const float sign = backward ? -1.f : 1.f;
+  if (dt == kBF16)
+    rope_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, (bf16_t*)y, rows, stride_in, stride_out, H, S, D, pos0,
+                                             cosb, sinb, sign);
+  else
+    rope_kernel<float><<<grid, NT, 0, st>>>((const float*)x, (float*)y, rows, stride_in, stride_out, H, S, D, pos0,
+                                            cosb, sinb, sign);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_fp8_quant(const void* x, void* q, int64_t n, int dt, const float* scale, unsigned int* amax_bits,
+                          hipStream_t st) {
+  const int grid = grid_for(n / 8 + 1, NT, 256 * 8);
+  if (dt == kBF16) fp8_quant_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, (uint8_t*)q, n, scale, amax_bits);
+  else fp8_quant_kernel<float><<<grid, NT, 0, st>>>((const float*)x, (uint8_t*)q, n, scale, amax_bits);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_fp8_dequant(const void* q, void* y, int64_t n, int dt, const float* scale_inv, hipStream_t st) {
+  const int grid = grid_for(n, NT, 256 * 8);
+  if (dt == kBF16) fp8_dequant_kernel<bf16_t><<<grid, NT, 0, st>>>((const uint8_t*)q, (bf16_t*)y, n, scale_inv);
+  else fp8_dequant_kernel<float><<<grid, NT, 0, st>>>((const uint8_t*)q, (float*)y, n, scale_inv);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_cast_f32_bf16(const float* x, void* y, int64_t n, hipStream_t st) {
+  const int grid = grid_for(n / 8 + 1, NT, 256 * 8);
+  cast_f32_bf16_kernel<<<grid, NT, 0, st>>>(x, (bf16_t*)y, n);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,558 @@
+// Causal / full flash attention (forward + backward) for gfx950, bf16 in/out, fp32 softmax state.
+// Head dims 64 and 128, GQA (H % Hkv == 0), strided q/k/v so a fused [B, S, 3, H, D] projection
+// is consumed in place.
+//
+// Built on v_mfma_f32_32x32x16_bf16 with the "accumulator as the next MFMA's operand" idiom
+// (cdna_hip_programming.md §3): scores are computed transposed (S^T = K Q^T) so that each lane owns
+// one query row -- the softmax max/sum are lane-local (+ one xor-32 exchange), and the probability
+// registers are reused directly as the B operand of O^T += V^T P^T with no LDS round trip.  The
+// key order inside each 16-key MFMA step is the permutation that idiom implies
+// (key = 16s + 8(j>>2) + 4h + (j&3)); the A operands that pair with it (V^T, dO^T, Q^T, K^T) are
+// staged TRANSPOSED in LDS with a +4-element row pad (136-B stride: conflict-free 8-B reads), and the
+// row-major operands (K, V, Q, dO) are staged with a 16-B-chunk XOR swizzle (conflict-free b128 reads).
+//
+// Forward: workgroup = 4 waves x 32 query rows (BM = 128), 64-key tiles, register-staged prefetch
+// of the next K/V tile overlapping the current tile's MFMAs (T14), heavy (diagonal-rich) blocks
+// launched first under the causal mask.
+// Backward: FA2-style split into (a) delta = rowsum(dO*O), (b) dK/dV kernel (workgroup owns 128
+// keys of one kv head and sweeps every query head of its GQA group, so dK/dV need no cross-workgroup
+// sum), (c) dQ kernel (workgroup owns 128 query rows).  No atomics: bitwise deterministic.
+//
+// Used by the GPT-2 / Llama models (BASELINE.json configs 3-5; SURVEY.md K16 "flash attention
+// (causal, head_dim 64/128)").
+#include "common.h"
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+constexpr int NT = 256;
+constexpr int TILE = 64;          // rows per staged LDS tile
+constexpr int TLD = TILE + 4;     // transposed-image row stride (elements)
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// accumulator register r of a 32x32 tile, lane half h -> row index inside the tile
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <int D>
+struct TileIO {
+  static constexpr int CH = D / 8;                // 16-B chunks per row
+  static constexpr int NCH = TILE * CH / NT;      // chunks per thread per tile
+  // global -> registers (zero rows >= nrows)
+  __device__ __forceinline__ static void load(const bf16_t* base, int64_t row_stride, int row0, int nrows,
+                                              u16x8 (&r)[NCH]) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int row = c / CH, ch = c % CH;
+      if (row0 + row < nrows) {
+        r[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + row) * row_stride + ch * 8);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[i][k] = 0;
+      }
+    }
+  }
+  // registers -> row-major swizzled LDS image [TILE][D]
+  __device__ __forceinline__ static void store_rows(bf16_t* lds, const u16x8 (&r)[NCH]) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int row = c / CH, ch = c % CH;
+      *reinterpret_cast<u16x8*>(lds + row * D + ((ch ^ (row & (CH - 1))) * 8)) = r[i];
+    }
+  }
+  // registers -> transposed LDS image [D][TLD]
+  __device__ __forceinline__ static void store_trans(bf16_t* lds, const u16x8 (&r)[NCH]) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int row = c / CH, ch = c % CH;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lds[(ch * 8 + k) * TLD + row] = r[i][k];
+    }
+  }
+  // A/B fragment from the row-major image: row `row`, k-step ks, lane half h -> d = 16ks + 8h .. +7
+  __device__ __forceinline__ static u16x8 row_frag(const bf16_t* lds, int row, int ks, int h) {
+    const int ch = 2 * ks + h;
+    return *reinterpret_cast<const u16x8*>(lds + row * D + ((ch ^ (row & (CH - 1))) * 8));
+  }
+};
+
+// fragment from a transposed image: row d, permuted 16-key step starting at kb:
+// elements j=0..3 -> keys kb + 4h + j, j=4..7 -> keys kb + 8 + 4h + (j-4)
+__device__ __forceinline__ u16x8 trans_frag(const bf16_t* lds, int d, int kb, int h) {
+  const bf16_t* p = lds + d * TLD + kb + 4 * h;
+  const u16x4 a = *reinterpret_cast<const u16x4*>(p);
+  const u16x4 b = *reinterpret_cast<const u16x4*>(p + 8);
+  u16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// pack registers 8s..8s+7 of an fp32 accumulator into a bf16 fragment
+__device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
+  return r;
+}
+
+struct AttnParams {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v;
+  bf16_t* o; float* lse;
+  const bf16_t* dout; bf16_t* dq; bf16_t* dk; bf16_t* dv; float* delta;
+  int64_t q_sb, q_ss, q_sh;   // element strides: batch, seq, head
+  int64_t k_sb, k_ss, k_sh;
+  int64_t v_sb, v_ss, v_sh;
+  int64_t o_sb, o_ss, o_sh;   // also used for dout / dq (same layout as o / q)
+  int64_t do_sb, do_ss, do_sh;
+  int64_t dq_sb, dq_ss, dq_sh;
+  int64_t dk_sb, dk_ss, dk_sh;
+  int64_t dv_sb, dv_ss, dv_sh;
+  int B, H, Hkv, Sq, Sk;
+  float scale;   // softmax scale (natural domain)
+};
+
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
+  using IO = TileIO<D>;
+  constexpr int KS = D / 16, DT = D / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[TILE * D + D * TLD];
+  bf16_t* Ks = smem;
+  bf16_t* Vt = smem + TILE * D;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;  // bottom-right aligned causal mask
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+    }
+  }
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m = -INFINITY, l = 0.f;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+
+  u16x8 kr[IO::NCH], vr[IO::NCH];
+  if (ntiles > 0) {
+    IO::load(Kp, p.k_ss, 0, p.Sk, kr);
+    IO::load(Vp, p.v_ss, 0, p.Sk, vr);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    IO::store_rows(Ks, kr);
+    IO::store_trans(Vt, vr);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
+      IO::load(Vp, p.v_ss, (t + 1) * TILE, p.Sk, vr);
+    }
+    const int k0 = t * TILE;
+    if (CAUSAL && k0 > qw + 31 + off) continue;  // every key of the tile is in this wave's future
+
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[kt] = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s[kt]);
+    }
+    const bool need_mask = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = s[kt][r] * sl2;
+        if (need_mask) {
+          const int key = k0 + kt * 32 + acc_row(r, h);
+          if (key >= p.Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
+        }
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float msub = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = exp2f(m - msub);
+    float ls = 0.f;
+    u16x8 pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = exp2f(s[kt][r] - msub);
+        s[kt][r] = pv;
+        ls += pv;
+      }
+      pf[kt][0] = pack8(s[kt], 0);
+      pf[kt][1] = pack8(s[kt], 1);
+    }
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+          o[dt] = mfma32(trans_frag(Vt, dt * 32 + c32, kt * 32 + 16 * ss, h), pf[kt][ss], o[dt]);
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < p.Sq) {
+    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
+        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
+      }
+    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward (a): delta[b, h, q] = sum_d dO * O
+// ------------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(NT) void fa_bwd_delta_kernel(AttnParams p) {
+  const int64_t idx = blockIdx.x * (int64_t)NT + threadIdx.x;  // over B*H*Sq
+  const int64_t total = (int64_t)p.B * p.H * p.Sq;
+  if (idx >= total) return;
+  const int q = (int)(idx % p.Sq);
+  const int hq = (int)((idx / p.Sq) % p.H);
+  const int b = (int)(idx / ((int64_t)p.Sq * p.H));
+  const bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)q * p.o_ss;
+  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh + (int64_t)q * p.do_ss;
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < D; c += 8) {
+    float a[8], g[8];
+    Vec8<bf16_t>::load(Op + c, a);
+    Vec8<bf16_t>::load(Gp + c, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
+  }
+  p.delta[idx] = acc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward (b): dK, dV.  Workgroup = 128 keys (4 waves x 32) of kv head hk; sweeps the q heads of
+// the group and the query tiles (64 rows) that can see those keys.
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
+  using IO = TileIO<D>;
+  constexpr int KS = D / 16, DT = D / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D + 2 * D * TLD];
+  __shared__ float lse_s[TILE], dl_s[TILE];
+  bf16_t* Qs = smem;
+  bf16_t* Gs = smem + TILE * D;        // dO row-major
+  bf16_t* Qt = smem + 2 * TILE * D;    // Q^T
+  bf16_t* Gt = Qt + D * TLD;           // dO^T
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hk = blockIdx.y;
+  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;
+  const int group = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int kw = kb * 128 + w * 32, key = kw + c32;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  u16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (key < p.Sk) {
+      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
+      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
+    }
+  }
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, kb * 128 - off) / TILE * TILE;
+  for (int hi = 0; hi < group; ++hi) {
+    const int hq = hk * group + hi;
+    const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+    const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+    const float* Lp = p.lse + ((int64_t)b * p.H + hq) * p.Sq;
+    const float* Dp = p.delta + ((int64_t)b * p.H + hq) * p.Sq;
+    for (int q0 = qstart; q0 < p.Sq; q0 += TILE) {
+      {
+        u16x8 r[IO::NCH];
+        __syncthreads();
+        IO::load(Qp, p.q_ss, q0, p.Sq, r);
+        IO::store_rows(Qs, r);
+        IO::store_trans(Qt, r);
+        IO::load(Gp, p.do_ss, q0, p.Sq, r);
+        IO::store_rows(Gs, r);
+        IO::store_trans(Gt, r);
+        if (threadIdx.x < TILE) {
+          const int q = q0 + threadIdx.x;
+          lse_s[threadIdx.x] = q < p.Sq ? Lp[q] * LOG2E : INFINITY;
+          dl_s[threadIdx.x] = q < p.Sq ? Dp[q] : 0.f;
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qb0 = q0 + qs * 32;
+        if (CAUSAL && qb0 + 31 + off < kw) continue;  // all queries of the subtile precede these keys
+        f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = mfma32(IO::row_frag(Qs, qs * 32 + c32, ks, h), kf[ks], s);
+          dp = mfma32(IO::row_frag(Gs, qs * 32 + c32, ks, h), vf[ks], dp);
+        }
+        // S rows = queries (registers), columns = keys (lanes)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = qs * 32 + acc_row(r, h);
+          const int q = q0 + qi;
+          float pv = exp2f(s[r] * sl2 - lse_s[qi]);
+          if (key >= p.Sk || (CAUSAL && key > q + off)) pv = 0.f;
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - dl_s[qi]);
+        }
+        const u16x8 pf0 = pack8(s, 0), pf1 = pack8(s, 1);
+        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma32(trans_frag(Gt, dt * 32 + c32, qs * 32, h), pf0, dv[dt]);
+          dv[dt] = mfma32(trans_frag(Gt, dt * 32 + c32, qs * 32 + 16, h), pf1, dv[dt]);
+          dk[dt] = mfma32(trans_frag(Qt, dt * 32 + c32, qs * 32, h), df0, dk[dt]);
+          dk[dt] = mfma32(trans_frag(Qt, dt * 32 + c32, qs * 32 + 16, h), df1, dk[dt]);
+        }
+      }
+    }
+  }
+  if (key < p.Sk) {
+    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
+    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 a, c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
+        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
+        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward (c): dQ.  Workgroup = 128 query rows (4 waves x 32) of head hq; sweeps key tiles.
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
+  using IO = TileIO<D>;
+  constexpr int KS = D / 16, DT = D / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D + D * TLD];
+  bf16_t* Ks = smem;
+  bf16_t* Vs = smem + TILE * D;
+  bf16_t* Kt = smem + 2 * TILE * D;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  u16x8 qf[KS], gf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) {
+      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
+    }
+  }
+  const float lse2 = qrow < p.Sq ? p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : INFINITY;
+  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  u16x8 kr[IO::NCH], vr[IO::NCH];
+  if (ntiles > 0) {
+    IO::load(Kp, p.k_ss, 0, p.Sk, kr);
+    IO::load(Vp, p.v_ss, 0, p.Sk, vr);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    IO::store_rows(Ks, kr);
+    IO::store_trans(Kt, kr);
+    IO::store_rows(Vs, vr);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
+      IO::load(Vp, p.v_ss, (t + 1) * TILE, p.Sk, vr);
+    }
+    const int k0 = t * TILE;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int kb0 = k0 + kt * 32;
+      if (CAUSAL && kb0 > qw + 31 + off) continue;
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s);
+        dp = mfma32(IO::row_frag(Vs, kt * 32 + c32, ks, h), gf[ks], dp);
+      }
+      // S^T: rows = keys (registers), columns = queries (lanes)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb0 + acc_row(r, h);
+        float pv = exp2f(s[r] * sl2 - lse2);
+        if (key >= p.Sk || (CAUSAL && key > qrow + off)) pv = 0.f;
+        dp[r] = pv * (dp[r] - dl);
+      }
+      const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dq[dt] = mfma32(trans_frag(Kt, dt * 32 + c32, kt * 32, h), df0, dq[dt]);
+        dq[dt] = mfma32(trans_frag(Kt, dt * 32 + c32, kt * 32 + 16, h), df1, dq[dt]);
+      }
+    }
+  }
+  if (qrow < p.Sq) {
+    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
+        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
+      }
+  }
+}
+
+template <int D>
+int launch_fwd(const AttnParams& p, int causal, hipStream_t st) {
+  dim3 grid((p.Sq + 127) / 128, p.H, p.B);
+  if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
+  else fa_fwd_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  return (int)hipGetLastError();
+}
+
+template <int D>
+int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
+  const int64_t rows = (int64_t)p.B * p.H * p.Sq;
+  fa_bwd_delta_kernel<D><<<(rows + NT - 1) / NT, NT, 0, st>>>(p);
+  dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
+  dim3 gq((p.Sq + 127) / 128, p.H, p.B);
+  if (causal) {
+    fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(p);
+    fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(p);
+  } else {
+    fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(p);
+    fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(p);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// strides[0..11]: q(b,s,h) k(b,s,h) v(b,s,h) o(b,s,h), in elements; D contiguous everywhere.
+PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                               const int64_t* strides, int B, int H, int Hkv, int Sq, int Sk, int D, float scale,
+                               int causal, hipStream_t st) {
+  if (H % Hkv != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  AttnParams p{};
+  p.q = (const bf16_t*)q; p.k = (const bf16_t*)k; p.v = (const bf16_t*)v; p.o = (bf16_t*)o; p.lse = lse;
+  p.q_sb = strides[0]; p.q_ss = strides[1]; p.q_sh = strides[2];
+  p.k_sb = strides[3]; p.k_ss = strides[4]; p.k_sh = strides[5];
+  p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
+  p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
+  p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
+  return D == 64 ? launch_fwd<64>(p, causal, st) : launch_fwd<128>(p, causal, st);
+}
+
+// strides[0..23]: q k v o dout dq dk dv, each (b, s, h).  delta: fp32 workspace of B*H*Sq.
+PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
+                               const void* dout, void* dq, void* dk, void* dv, float* delta, const int64_t* strides,
+                               int B, int H, int Hkv, int Sq, int Sk, int D, float scale, int causal, hipStream_t st) {
+  if (H % Hkv != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  AttnParams p{};
+  p.q = (const bf16_t*)q; p.k = (const bf16_t*)k; p.v = (const bf16_t*)v; p.o = (bf16_t*)o;
+  p.lse = const_cast<float*>(lse); p.dout = (const bf16_t*)dout;
+  p.dq = (bf16_t*)dq; p.dk = (bf16_t*)dk; p.dv = (bf16_t*)dv; p.delta = delta;
+  p.q_sb = strides[0]; p.q_ss = strides[1]; p.q_sh = strides[2];
+  p.k_sb = strides[3]; p.k_ss = strides[4]; p.k_sh = strides[5];
+  p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
+  p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
+  p.do_sb = strides[12]; p.do_ss = strides[13]; p.do_sh = strides[14];
+  p.dq_sb = strides[15]; p.dq_ss = strides[16]; p.dq_sh = strides[17];
+  p.dk_sb = strides[18]; p.dk_ss = strides[19]; p.dk_sh = strides[20];
+  p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
+  p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
+  return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
+}

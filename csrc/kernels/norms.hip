@@ -1,0 +1,363 @@
+// LayerNorm and RMSNorm forward/backward for gfx950.
+//
+// Fast path: one wave64 per row, the row held in registers (8 elements per lane per 512-column
+// slab, ITERS slabs), 16-byte loads/stores, fp32 statistics.  Exact two-pass variance from the
+// register copy (no Welford needed because the row never leaves the VGPRs).  Backward keeps
+// per-lane dgamma/dbeta partial sums in registers across the rows a wave visits and writes one
+// partial row per wave; a deterministic column-reduce kernel folds them.
+// Fallback (N % 8 != 0 or N > 8192): one workgroup per row streaming from global memory.
+//
+// Reference parity: SwinIR LayerNorm sites (Stoke-DDP.py:206-208), GPT-2/Llama norms
+// (BASELINE.json configs 3-5); semantics of torch.nn.functional.layer_norm / rms_norm.
+#include "common.h"
+
+using namespace pdt;
+
+namespace {
+
+constexpr int NT = 256;      // threads per block
+constexpr int RPB = NT / 64; // rows per block (one per wave)
+
+template <typename T, typename W, int ITERS, bool RMS>
+__global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                      const W* __restrict__ b, T* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int rows, int N, float eps) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float invN = 1.f / (float)N;
+  for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
+    const T* xr = x + (int64_t)row * N;
+    float v[ITERS][8];
+    float s = 0.f;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int col = it * 512 + lane * 8;
+      if (col < N) {
+        Vec8<T>::load(xr + col, v[it]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[it][k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += RMS ? v[it][k] * v[it][k] : v[it][k];
+    }
+    s = wave_sum(s);
+    float mean = 0.f, rstd;
+    if (RMS) {
+      rstd = rsqrtf(s * invN + eps);
+    } else {
+      mean = s * invN;
+      float q = 0.f;
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int col = it * 512 + lane * 8;
+        if (col < N) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { float d = v[it][k] - mean; q += d * d; }
+        }
+      }
+      q = wave_sum(q);
+      rstd = rsqrtf(q * invN + eps);
+    }
+    T* yr = y + (int64_t)row * N;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int col = it * 512 + lane * 8;
+      if (col < N) {
+        float wv[8], bv[8], o[8];
+        Vec8<W>::load(w + col, wv);
+        if (!RMS && b != nullptr) Vec8<W>::load(b + col, bv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float t = (v[it][k] - mean) * rstd * wv[k];
+          o[k] = (!RMS && b != nullptr) ? t + bv[k] : t;
+        }
+        Vec8<T>::store(yr + col, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename T, typename W, int ITERS, bool RMS>
+__global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                      const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                      float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                      int rows, int N) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float invN = 1.f / (float)N;
+  float dwa[ITERS][8], dba[ITERS][8];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; }
+
+  for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
+    const T* xr = x + (int64_t)row * N;
+    const T* gr = dy + (int64_t)row * N;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[ITERS][8], g[ITERS][8];
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int col = it * 512 + lane * 8;
+      if (col < N) {
+        float xv[8], dv[8], wv[8];
+        Vec8<T>::load(xr + col, xv);
+        Vec8<T>::load(gr + col, dv);
+        Vec8<W>::load(w + col, wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[it][k] = (xv[k] - mean) * rstd;
+          g[it][k] = dv[k] * wv[k];
+          a += g[it][k] * xh[it][k];
+          bsum += g[it][k];
+          dwa[it][k] += dv[k] * xh[it][k];
+          dba[it][k] += dv[k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { xh[it][k] = 0.f; g[it][k] = 0.f; }
+      }
+    }
+    a = wave_sum(a) * invN;
+    bsum = RMS ? 0.f : wave_sum(bsum) * invN;
+    T* dxr = dx + (int64_t)row * N;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int col = it * 512 + lane * 8;
+      if (col < N) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[it][k] - bsum - xh[it][k] * a);
+        Vec8<T>::store(dxr + col, o);
+      }
+    }
+  }
+  // one partial row per wave
+  const int prow = blockIdx.x * RPB + wid;
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int col = it * 512 + lane * 8;
+    if (col < N) {
+      Vec8<float>::store(dw_part + (int64_t)prow * N + col, dwa[it]);
+      if (db_part) Vec8<float>::store(db_part + (int64_t)prow * N + col, dba[it]);
+    }
+  }
+}
+
+// ---- fallback: one block per row, streamed from global memory ----
+template <typename T, typename W, bool RMS>
+__global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, const W* __restrict__ w,
+                                                       const W* __restrict__ b, T* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int rows, int N, float eps) {
+  __shared__ float red[RPB];
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const T* xr = x + (int64_t)row * N;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < N; c += NT) { float v = to_f<T>(xr[c]); s += RMS ? v * v : v; }
+    s = block_sum<RPB>(s, red);
+    float mean = 0.f, rstd;
+    if (RMS) {
+      rstd = rsqrtf(s / N + eps);
+    } else {
+      mean = s / N;
+      float q = 0.f;
+      for (int c = threadIdx.x; c < N; c += NT) { float d = to_f<T>(xr[c]) - mean; q += d * d; }
+      q = block_sum<RPB>(q, red);
+      rstd = rsqrtf(q / N + eps);
+    }
+    T* yr = y + (int64_t)row * N;
+    for (int c = threadIdx.x; c < N; c += NT) {
+      float t = (to_f<T>(xr[c]) - mean) * rstd * to_f<W>(w[c]);
+      if (!RMS && b != nullptr) t += to_f<W>(b[c]);
+      yr[c] = from_f<T>(t);
+    }
+    if (threadIdx.x == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename T, typename W, bool RMS>
+__global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                       float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                       int rows, int N) {
+  // partial row per block: rows handled by this block are accumulated straight into it
+  __shared__ float red[RPB];
+  float* dwp = dw_part + (int64_t)blockIdx.x * N;
+  float* dbp = db_part ? db_part + (int64_t)blockIdx.x * N : nullptr;
+  for (int c = threadIdx.x; c < N; c += NT) { dwp[c] = 0.f; if (dbp) dbp[c] = 0.f; }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const T* xr = x + (int64_t)row * N;
+    const T* gr = dy + (int64_t)row * N;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float a = 0.f, bs = 0.f;
+    for (int c = threadIdx.x; c < N; c += NT) {
+      float xh = (to_f<T>(xr[c]) - mean) * rstd, d = to_f<T>(gr[c]);
+      float g = d * to_f<W>(w[c]);
+      a += g * xh; bs += g;
+      dwp[c] += d * xh;
+      if (dbp) dbp[c] += d;
+    }
+    a = block_sum<RPB>(a, red) / N;
+    bs = RMS ? 0.f : block_sum<RPB>(bs, red) / N;
+    T* dxr = dx + (int64_t)row * N;
+    for (int c = threadIdx.x; c < N; c += NT) {
+      float xh = (to_f<T>(xr[c]) - mean) * rstd;
+      float g = to_f<T>(gr[c]) * to_f<W>(w[c]);
+      dxr[c] = from_f<T>(rstd * (g - bs - xh * a));
+    }
+  }
+}
+
+// Column reduction of a [R, N] fp32 partial matrix into out[N] (type W).  Block = 64 columns x 4
+// row-slices; deterministic order.
+template <typename W>
+__global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int R, int N,
+                                                        W* __restrict__ out, int accumulate) {
+  __shared__ float red[RPB][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < N)
+    for (int r = wid; r < R; r += RPB) s += part[(int64_t)r * N + col];
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && col < N) {
+    float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (accumulate) t += to_f<W>(out[col]);
+    out[col] = from_f<W>(t);
+  }
+}
+
+template <typename T, typename W, bool RMS>
+int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows, int N,
+               float eps, hipStream_t st) {
+  const T* X = (const T*)x; const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
+  if (N % 8 == 0 && N <= 8192) {
+    const int grid = grid_for(rows, RPB, 256 * 16);
+    const int iters = (N + 511) / 512;
+#define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, Wt, B, Y, mean, rstd, rows, N, eps)
+    if (iters <= 1) PDT_NF(1);
+    else if (iters <= 2) PDT_NF(2);
+    else if (iters <= 4) PDT_NF(4);
+    else if (iters <= 8) PDT_NF(8);
+    else PDT_NF(16);
+#undef PDT_NF
+  } else {
+    norm_fwd_generic<T, W, RMS><<<grid_for(rows, 1, 256 * 8), NT, 0, st>>>(X, Wt, B, Y, mean, rstd, rows, N, eps);
+  }
+  return (int)hipGetLastError();
+}
+
+// workspace: fp32, >= 2 * pdt_norm_bwd_partial_rows(rows, N) * N floats
+int bwd_partial_rows(int rows, int N) {
+  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, 256) * RPB;
+  return grid_for(rows, 1, 512);
+}
+
+template <typename T, typename W, bool RMS>
+int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
+               void* dw, void* db, float* ws, int rows, int N, int accumulate, hipStream_t st) {
+  const T* DY = (const T*)dy; const T* X = (const T*)x; const W* Wt = (const W*)w; T* DX = (T*)dx;
+  const int R = bwd_partial_rows(rows, N);
+  float* dwp = ws;
+  float* dbp = (db != nullptr) ? ws + (int64_t)R * N : nullptr;
+  if (N % 8 == 0 && N <= 8192) {
+    const int grid = R / RPB;
+    const int iters = (N + 511) / 512;
+#define PDT_NB(I) norm_bwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(DY, X, Wt, mean, rstd, DX, dwp, dbp, rows, N)
+    if (iters <= 1) PDT_NB(1);
+    else if (iters <= 2) PDT_NB(2);
+    else if (iters <= 4) PDT_NB(4);
+    else if (iters <= 8) PDT_NB(8);
+    else PDT_NB(16);
+#undef PDT_NB
+  } else {
+    norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DX, dwp, dbp, rows, N);
+  }
+  const int cg = (N + 63) / 64;
+  if (dw) col_reduce_kernel<W><<<cg, NT, 0, st>>>(dwp, R, N, (W*)dw, accumulate);
+  if (db) col_reduce_kernel<W><<<cg, NT, 0, st>>>(dbp, R, N, (W*)db, accumulate);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// dtype codes: x/y in {kF32, kBF16}; w/b in {kF32, kBF16}.  rms=1 selects RMSNorm (b ignored, mean unused).
+PDT_API int pdt_norm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
+                         int N, float eps, int xdt, int wdt, int rms, hipStream_t st) {
+#define PDT_DISPATCH(R)                                                                             \
+  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, w, b, y, mean, rstd, rows, N, eps, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, w, b, y, mean, rstd, rows, N, eps, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, w, b, y, mean, rstd, rows, N, eps, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, w, b, y, mean, rstd, rows, N, eps, st);
+  if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
+#undef PDT_DISPATCH
+  return (int)hipErrorInvalidValue;
+}
+
+PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return 2 * bwd_partial_rows(rows, N) * N; }
+
+PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
+                         void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt, int rms, int accumulate,
+                         hipStream_t st) {
+#define PDT_DISPATCH(R)                                                                                         \
+  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_bwd<float, bf16_t, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);
+  if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
+#undef PDT_DISPATCH
+  return (int)hipErrorInvalidValue;
+}
+
+// Column sums of a [rows, N] matrix (T) into out[N] (W) -- bias gradients.  ws >= R*N floats where
+// R = pdt_colsum_partial_rows(rows).
+namespace {
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* __restrict__ x, int rows, int N, int rows_per,
+                                                            float* __restrict__ part) {
+  // block: 256 threads x 8 columns = 2048 columns per block in x; blockIdx.y = row slab
+  const int col = (blockIdx.x * NT + threadIdx.x) * 8;
+  if (col >= N) return;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(rows, r0 + rows_per);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    float v[8];
+    Vec8<T>::load(x + (int64_t)r * N + col, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += v[k];
+  }
+  Vec8<float>::store(part + (int64_t)blockIdx.y * N + col, acc);
+}
+}  // namespace
+
+PDT_API int pdt_colsum_partial_rows(int rows) { return rows < 256 ? rows : 256; }
+
+PDT_API int pdt_colsum(const void* x, int rows, int N, int xdt, void* out, int odt, float* ws, int accumulate,
+                       hipStream_t st) {
+  if (N % 8 != 0) return (int)hipErrorInvalidValue;
+  const int R = pdt_colsum_partial_rows(rows);
+  const int rows_per = (rows + R - 1) / R;
+  const int Ruse = (rows + rows_per - 1) / rows_per;
+  dim3 grid((N / 8 + NT - 1) / NT, Ruse);
+  if (xdt == kBF16) colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, rows_per, ws);
+  else colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, rows_per, ws);
+  const int cg = (N + 63) / 64;
+  if (odt == kBF16) col_reduce_kernel<bf16_t><<<cg, NT, 0, st>>>(ws, Ruse, N, (bf16_t*)out, accumulate);
+  else col_reduce_kernel<float><<<cg, NT, 0, st>>>(ws, Ruse, N, (float*)out, accumulate);
+  return (int)hipGetLastError();
+}

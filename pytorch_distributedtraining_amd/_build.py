@@ -1,0 +1,122 @@
+"""Ahead-of-time build of the native parts of pytorch_distributedtraining_amd.
+
+Two artefacts, both built IN-TREE so they travel with the repository snapshot to the GPU box:
+
+* ``lib/libpdt_kernels.so`` -- every HIP kernel under ``csrc/kernels/*.hip``, compiled by ``hipcc``
+  for gfx950 (MI355X / CDNA4) only.  Plain C ABI (``pdt_*``), loaded with ctypes after ``import torch``
+  so it binds to the same HIP runtime (soname ``libamdhip64.so.7``) torch already mapped.
+* ``_pdt_runtime*.so`` -- the host-side C++ runtime (bucket planner, ZeRO/FSDP shard planners,
+  collective sequence tracer, pinned prefetch ring), a pybind11 module compiled by g++.
+
+No hipify, no torch cpp_extension, no CUDA: the sources are written for CDNA4 directly.
+Incremental: an artefact is rebuilt only when a source or header is newer than it.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "pytorch_distributedtraining_amd")
+KERNEL_DIR = os.path.join(ROOT, "csrc", "kernels")
+RUNTIME_DIR = os.path.join(ROOT, "csrc", "runtime")
+BUILD_DIR = os.path.join(ROOT, "build", "native")
+KERNEL_LIB = os.path.join(PKG, "lib", "libpdt_kernels.so")
+ARCH = os.environ.get("PDT_OFFLOAD_ARCH", "gfx950")
+
+HIPCC_FLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    "-munsafe-fp-atomics", "-ffp-contract=fast", "-Wno-unused-result",
+]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the gfx950 kernels)")
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed:\n{' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
+    srcs = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.h")))
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(KERNEL_LIB), exist_ok=True)
+    hipcc = _hipcc()
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(BUILD_DIR, os.path.basename(s)[:-4] + f".{ARCH}.o")
+        objs.append(o)
+        if _newer(o, [s] + headers + [__file__]):
+            todo.append((s, o))
+    jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_run, [hipcc, *HIPCC_FLAGS, "-I", KERNEL_DIR, "-c", s, "-o", o], verbose)
+                    for s, o in todo]
+            for f in futs:
+                f.result()
+    if _newer(KERNEL_LIB, objs):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", KERNEL_LIB], verbose)
+    return KERNEL_LIB
+
+
+def runtime_ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG, "_pdt_runtime" + suffix)
+
+
+def build_runtime(verbose: bool = False) -> str:
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(RUNTIME_DIR, "*.cpp")))
+    headers = sorted(glob.glob(os.path.join(RUNTIME_DIR, "*.h")))
+    out = runtime_ext_path()
+    if not srcs:
+        return out
+    if _newer(out, srcs + headers + [__file__]):
+        cxx = os.environ.get("CXX", "g++")
+        inc = [pybind11.get_include(), sysconfig.get_paths()["include"]]
+        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
+               "-Wno-unused-function", "-pthread"]
+        for i in inc:
+            cmd += ["-I", i]
+        cmd += ["-I", RUNTIME_DIR, *srcs, "-o", out]
+        if os.environ.get("PDT_SANITIZE"):
+            cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        _run(cmd, verbose)
+    return out
+
+
+def build_all(verbose: bool = False) -> None:
+    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+        a = ex.submit(build_runtime, verbose)
+        b = ex.submit(build_kernels, verbose)
+        a.result()
+        b.result()
+
+
+if __name__ == "__main__":
+    build_all(verbose="-v" in sys.argv)
+    print("built:", KERNEL_LIB, runtime_ext_path())

@@ -1,0 +1,156 @@
+"""GPT-2 family (124M / 350M / 774M / 1.3B) built on the gfx950 kernels.
+
+BASELINE.json configs 3 (GPT-2 124M DDP) and 4 (GPT-2 1.3B FSDP, the flagship bench).
+MI355X-first choices:
+  * attention = one fused qkv GEMM (hipBLASLt) -> ``flash_attn_qkvpacked`` (hand MFMA kernel) reading
+    the [B, S, 3, H, D] projection in place and writing dq/dk/dv into one packed gradient;
+  * MLP = GEMM without bias -> fused bias+GELU(tanh) kernel (saves the pre-activation once);
+  * LayerNorm = wave-per-row HIP kernel (bf16 activations, fp32 statistics);
+  * LM head tied to the token embedding, loss = fused softmax-CE with in-place backward;
+  * vocab padded to a multiple of 128 (50257 -> 50304) so the head GEMM tiles cleanly;
+  * dropout omitted (0.0), as in throughput benchmarks of this class.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
+from ..ops.norms import LayerNorm
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50304
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    layer_norm_epsilon: float = 1e-5
+    activation_checkpointing: bool = False
+
+    @property
+    def head_dim(self):
+        return self.n_embd // self.n_head
+
+
+GPT2_CONFIGS = {
+    "gpt2-124m": dict(n_embd=768, n_layer=12, n_head=12),
+    "gpt2-350m": dict(n_embd=1024, n_layer=24, n_head=16),
+    "gpt2-774m": dict(n_embd=1280, n_layer=36, n_head=20),
+    # GPT-2 "1.3B" (GPT-3 XL shape): L24, d2048; 16 heads x 128 keeps head_dim MFMA-friendly
+    "gpt2-1.3b": dict(n_embd=2048, n_layer=24, n_head=16),
+    "gpt2-tiny": dict(n_embd=128, n_layer=2, n_head=2, vocab_size=512, n_positions=256),
+}
+
+
+def gpt2_config(name: str, **overrides) -> GPT2Config:
+    kw = dict(GPT2_CONFIGS[name])
+    kw.update(overrides)
+    return GPT2Config(**kw)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.n_head = cfg.n_head
+        self.head_dim = cfg.head_dim
+        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+
+    def forward(self, x):
+        B, S, C = x.shape
+        qkv = self.c_attn(x).view(B, S, 3, self.n_head, self.head_dim)
+        y = flash_attn_qkvpacked(qkv, causal=True)
+        return self.c_proj(y.reshape(B, S, C))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+
+    def forward(self, x):
+        h = F.linear(x, self.c_fc.weight)            # hipBLASLt GEMM, bias folded into the GELU kernel
+        h = bias_gelu(h, self.c_fc.bias, approximate="tanh")
+        return self.c_proj(h)
+
+
+class GPT2Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.ln_1 = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
+        self.attn = CausalSelfAttention(cfg)
+        self.ln_2 = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        x = x + self.mlp(self.ln_2(x))
+        return x
+
+
+class GPT2LMHeadModel(nn.Module):
+    """forward(input_ids, labels=None) -> loss (if labels) else logits."""
+
+    block_class = GPT2Block
+
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.config = cfg
+        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        std = 0.02
+        proj_std = 0.02 / math.sqrt(2 * self.config.n_layer)
+        for name, p in self.named_parameters():
+            if name.endswith("c_proj.weight"):
+                nn.init.normal_(p, 0.0, proj_std)
+            elif name.endswith(".weight") and p.dim() == 2:
+                nn.init.normal_(p, 0.0, std)
+            elif name.endswith(".bias"):
+                nn.init.zeros_(p)
+        for m in self.modules():
+            if isinstance(m, LayerNorm):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def num_params(self, non_embedding=False):
+        n = sum(p.numel() for p in self.parameters())
+        if non_embedding:
+            n -= self.wpe.weight.numel()
+        return n
+
+    def flops_per_token(self, seq_len: int) -> float:
+        """6N + attention (12 L S d) training FLOPs per token (causal halving not applied)."""
+        c = self.config
+        n = self.num_params(non_embedding=True)
+        return 6 * n + 12 * c.n_layer * seq_len * c.n_embd
+
+    def forward(self, input_ids, labels=None):
+        B, S = input_ids.shape
+        pos = torch.arange(S, device=input_ids.device)
+        x = self.wte(input_ids) + self.wpe(pos)
+        for blk in self.h:
+            if self.config.activation_checkpointing and self.training:
+                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+            else:
+                x = blk(x)
+        x = self.ln_f(x)
+        logits = F.linear(x, self.wte.weight)   # tied head
+        if labels is None:
+            return logits
+        return cross_entropy(logits, labels, inplace_backward=True)
+
+
+def build_gpt2(name: str = "gpt2-124m", **overrides) -> GPT2LMHeadModel:
+    return GPT2LMHeadModel(gpt2_config(name, **overrides))

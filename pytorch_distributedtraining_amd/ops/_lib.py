@@ -1,0 +1,146 @@
+"""ctypes binding of ``lib/libpdt_kernels.so`` (the gfx950 HIP kernels).
+
+The library is loaded lazily, after ``import torch``, so its ``libamdhip64.so.7`` dependency resolves
+to the HIP runtime torch already mapped (one runtime, one set of streams).  Every entry point takes
+raw device pointers plus the current HIP stream handle and returns a ``hipError_t``.
+
+Policy: a GPU tensor ALWAYS goes through the HIP kernels -- if the library is missing on a GPU box
+the op raises (no silent eager fallback).  CPU tensors use the PyTorch reference math; that path
+exists for the CPU unit tests and the gloo multi-process tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                         "libpdt_kernels.so")
+_lock = threading.Lock()
+_lib = None
+_load_error: Exception | None = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+
+# name -> argtypes (restype is always c_int)
+_SIGS = {
+    "pdt_adamw_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float,
+                     c_float, c_float, c_int, c_void_p, c_void_p, c_void_p],
+    "pdt_l2norm_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
+    "pdt_cast_f32_bf16_mt": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
+                     c_int, c_int, c_void_p],
+    "pdt_norm_bwd_workspace_floats": [c_int, c_int],
+    "pdt_norm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_colsum_partial_rows": [c_int],
+    "pdt_colsum": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p],
+    "pdt_bias_gelu_fwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_bias_gelu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_swiglu_fwd": [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_rope": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                 c_int, c_int, c_void_p],
+    "pdt_fp8_quant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "pdt_fp8_dequant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p],
+    "pdt_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
+    "pdt_ce_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_int, c_void_p],
+    "pdt_ce_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int64,
+                   c_int, c_int, c_void_p],
+    "pdt_flash_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                           c_int, c_int, c_float, c_int, c_void_p],
+    "pdt_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
+                           c_void_p],
+    "pdt_syncbn_stats": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                         c_void_p],
+    "pdt_syncbn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p],
+    "pdt_syncbn_bwd_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                             c_int, c_int, c_int, c_int, c_void_p],
+}
+
+F32, BF16, F16 = 0, 1, 2
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    if dt == torch.float16:
+        return F16
+    raise TypeError(f"unsupported dtype for HIP kernel: {dt}")
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load():
+    """Return the loaded kernel library (raises if it cannot be loaded)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            _load_error = FileNotFoundError(
+                f"{_LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or python -m pytorch_distributedtraining_amd._build)")
+            raise _load_error
+        lib = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = args
+            fn.restype = c_int
+        _lib = lib
+        return _lib
+
+
+def available() -> bool:
+    """True when a GPU is present and the HIP kernel library loads."""
+    if not torch.cuda.is_available():
+        return False
+    try:
+        load()
+        return True
+    except Exception:  # pragma: no cover - reported by require()
+        return False
+
+
+def require():
+    """The kernel library, or a loud error (used by every GPU code path)."""
+    try:
+        return load()
+    except Exception as e:  # pragma: no cover
+        raise RuntimeError(f"pytorch_distributedtraining_amd HIP kernels unavailable: {e}") from e
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def check(err: int, name: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"HIP kernel {name} failed with hipError_t={err}")
+
+
+def call(name: str, *args) -> None:
+    lib = require()
+    check(getattr(lib, name)(*args), name)

@@ -1,0 +1,127 @@
+"""Flash attention (causal / full, GQA) backed by the gfx950 MFMA kernels in csrc/kernels/flash_attn.hip.
+
+Layout: q [B, Sq, H, D], k/v [B, Sk, Hkv, D] -- any strides with a contiguous head dim, so the
+views of a fused qkv projection are consumed in place.  ``flash_attn_qkvpacked`` additionally writes
+dq/dk/dv straight into one packed gradient buffer (no scatter/cat in backward).
+
+CPU tensors use the exact-math reference (torch SDPA) -- used by the CPU tests only.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _strides(t):
+    return [t.stride(0), t.stride(1), t.stride(2)]
+
+
+def _check(t, name):
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"flash_attn: {name} must be bf16 (got {t.dtype})")
+    if t.stride(-1) != 1:
+        raise ValueError(f"flash_attn: {name} head dim must be contiguous")
+    if t.data_ptr() % 16 or any(s % 8 for s in t.stride()[:-1]):
+        raise ValueError(f"flash_attn: {name} must be 16-byte aligned with strides multiple of 8")
+
+
+def _fwd(q, k, v, causal, scale):
+    B, Sq, H, D = q.shape
+    Sk, Hkv = k.shape[1], k.shape[2]
+    o = torch.empty((B, Sq, H, D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+    strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o), dtype=torch.int64)
+    _lib.call("pdt_flash_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+              strides.data_ptr(), B, H, Hkv, Sq, Sk, D, float(scale), 1 if causal else 0,
+              _lib.stream_handle(q.device))
+    return o, lse
+
+
+def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale):
+    B, Sq, H, D = q.shape
+    Sk, Hkv = k.shape[1], k.shape[2]
+    delta = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+    do = do if (do.stride(-1) == 1 and all(s % 8 == 0 for s in do.stride()[:-1])) else do.contiguous()
+    strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
+                           + _strides(dk) + _strides(dv), dtype=torch.int64)
+    _lib.call("pdt_flash_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+              do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), delta.data_ptr(), strides.data_ptr(),
+              B, H, Hkv, Sq, Sk, D, float(scale), 1 if causal else 0, _lib.stream_handle(q.device))
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        for t, n in ((q, "q"), (k, "k"), (v, "v")):
+            _check(t, n)
+        o, lse = _fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        _bwd(q, k, v, o, lse, do, dq, dk, dv, ctx.causal, ctx.scale)
+        return dq, dk, dv, None, None
+
+
+class _FlashAttnPackedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, causal, scale):
+        _check(qkv, "qkv")
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o, lse = _fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        _bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
+             ctx.causal, ctx.scale)
+        return dqkv, None, None
+
+
+def _reference(q, k, v, causal, scale):
+    # [B, S, H, D] -> [B, H, S, D]; GQA by repeating kv heads
+    H, Hkv = q.shape[2], k.shape[2]
+    qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    if Hkv != H:
+        kt = kt.repeat_interleave(H // Hkv, dim=1)
+        vt = vt.repeat_interleave(H // Hkv, dim=1)
+    Sq, Sk = q.shape[1], k.shape[1]
+    mask = None
+    if causal:
+        mask = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(diagonal=Sk - Sq)
+    o = F.scaled_dot_product_attention(qt.float(), kt.float(), vt.float(), attn_mask=mask, scale=scale)
+    return o.transpose(1, 2).to(q.dtype)
+
+
+def flash_attn(q, k, v, causal: bool = True, scale: float | None = None):
+    """softmax(q k^T * scale [+ causal mask]) v with q [B,Sq,H,D], k/v [B,Sk,Hkv,D]; returns [B,Sq,H,D]."""
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
+    if not q.is_cuda:
+        return _reference(q, k, v, causal, scale)
+    return _FlashAttnFn.apply(q, k, v, causal, scale)
+
+
+def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None):
+    """qkv [B, S, 3, H, D] -> o [B, S, H, D]."""
+    scale = 1.0 / math.sqrt(qkv.shape[-1]) if scale is None else scale
+    if not qkv.is_cuda:
+        return _reference(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal, scale)
+    return _FlashAttnPackedFn.apply(qkv, causal, scale)
+
+
+def supported(head_dim: int) -> bool:
+    return head_dim in (64, 128)

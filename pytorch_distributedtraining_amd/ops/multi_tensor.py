@@ -1,0 +1,222 @@
+"""Multi-tensor launches: fused AdamW, fused L2 norm (+ non-finite check), clip coefficient, scale.
+
+One HIP launch covers an arbitrary list of tensors through a device-resident table
+(``csrc/kernels/multi_tensor.hip``).  The engines keep parameters/gradients in flat buffers so their
+tables have a single entry; user parameter lists get one table per (dtype, group).
+
+Reference parity: AdamW as configured in Stoke-DDP.py:226-235 / Fairscale-DDP.py:78-86 (math order
+of torch/optim/adam.py:419-547), clip_grad_norm_ as configured by Stoke-DDP.py:253
+(torch/nn/utils/clip_grad.py:50-186).
+"""
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import torch
+
+from . import _lib
+
+META = 6
+DEFAULT_CHUNK = 32768
+
+
+class TensorTable:
+    """Device table describing up to 5 aligned tensor lists (+ numel) for a multi-tensor kernel.
+
+    ``cols`` is a list of columns, each a list of tensors (or None) of equal length; column 0 defines
+    the numel.  The table holds raw pointers, so the caller must keep the tensors alive and must
+    rebuild the table if any storage is reallocated (``key()`` changes).
+    """
+
+    def __init__(self, cols: Sequence[Sequence[torch.Tensor | None]], chunk: int = DEFAULT_CHUNK):
+        assert 1 <= len(cols) <= 5
+        n = len(cols[0])
+        for c in cols:
+            assert len(c) == n
+        self.chunk = int(chunk)
+        self.cols = [list(c) for c in cols]
+        self.numels = [t.numel() for t in cols[0]]
+        dev = cols[0][0].device if n else torch.device("cpu")
+        meta = torch.zeros((max(n, 1), META), dtype=torch.int64)
+        blk = []
+        for i in range(n):
+            for j, col in enumerate(cols):
+                t = col[i]
+                if t is not None:
+                    assert t.is_contiguous(), "multi-tensor kernels need contiguous tensors"
+                    assert t.numel() == self.numels[i]
+                    meta[i, j] = t.data_ptr()
+            meta[i, 5] = self.numels[i]
+            for c in range((self.numels[i] + self.chunk - 1) // self.chunk):
+                blk.append((i, c))
+        self.nblocks = len(blk)
+        blk_t = torch.tensor(blk if blk else [(0, 0)], dtype=torch.int32)
+        if dev.type == "cuda":
+            self.meta = meta.to(dev, non_blocking=False)
+            self.blk = blk_t.to(dev, non_blocking=False)
+        else:
+            self.meta, self.blk = meta, blk_t
+        self._key = self.make_key(cols)
+        self.device = dev
+
+    @staticmethod
+    def make_key(cols) -> tuple:
+        return tuple((t.data_ptr(), t.numel()) if t is not None else None for c in cols for t in c)
+
+    def key(self) -> tuple:
+        return self._key
+
+
+class TableCache:
+    """Rebuilds a TensorTable only when the pointer set changes."""
+
+    def __init__(self):
+        self._tables = {}
+
+    def get(self, name, cols, chunk=DEFAULT_CHUNK) -> TensorTable:
+        key = TensorTable.make_key(cols)
+        t = self._tables.get(name)
+        if t is None or t.key() != key:
+            t = TensorTable(cols, chunk)
+            self._tables[name] = t
+        return t
+
+
+_cache = TableCache()
+
+
+def l2norm_sq(tensors: Sequence[torch.Tensor], out: torch.Tensor | None = None, accumulate=False,
+              table: TensorTable | None = None) -> torch.Tensor:
+    """Sum of squares over all tensors as a 1-element fp32 device tensor (no host sync)."""
+    tensors = [t for t in tensors if t is not None and t.numel() > 0]
+    if not tensors:
+        o = out if out is not None else torch.zeros(1, dtype=torch.float32)
+        if not accumulate:
+            o.zero_()
+        return o
+    dev = tensors[0].device
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=dev)
+    if dev.type != "cuda":
+        s = torch.zeros((), dtype=torch.float32)
+        for t in tensors:
+            s = s + t.detach().float().pow(2).sum()
+        if accumulate:
+            out.add_(s)
+        else:
+            out.copy_(s.reshape(1))
+        return out
+    by_dt = {}
+    for t in tensors:
+        by_dt.setdefault(t.dtype, []).append(t)
+    first = True
+    for dt, ts in by_dt.items():
+        tab = table if (table is not None and len(by_dt) == 1) else _cache.get(("l2", dt, len(ts)), [ts])
+        partial = torch.empty(max(tab.nblocks, 1), dtype=torch.float32, device=dev)
+        _lib.call("pdt_l2norm_mt", tab.meta.data_ptr(), tab.blk.data_ptr(), tab.nblocks, tab.chunk,
+                  _lib.dtype_code(dt), partial.data_ptr(), out.data_ptr(), 1 if (accumulate or not first) else 0,
+                  _lib.stream_handle(dev))
+        first = False
+    return out
+
+
+def clip_coef(total_sq: torch.Tensor, max_norm: float, inv_scale: torch.Tensor | float = 1.0):
+    """From an (all-reduced) sum of squares: (norm, grad_multiplier, found_inf) device tensors.
+
+    grad_multiplier = min(1, max_norm/(norm+1e-6)) * inv_scale; max_norm<=0 disables clipping."""
+    dev = total_sq.device
+    norm = torch.empty(1, dtype=torch.float32, device=dev)
+    coef = torch.empty(1, dtype=torch.float32, device=dev)
+    found = torch.empty(1, dtype=torch.int32, device=dev)
+    if dev.type != "cuda":
+        inv = float(inv_scale) if not torch.is_tensor(inv_scale) else float(inv_scale.reshape(-1)[0])
+        sq = float(total_sq.reshape(-1)[0])
+        fin = math.isfinite(sq)
+        nrm = math.sqrt(sq) * inv if fin else float("nan") if sq != sq else float("inf")
+        c = min(max_norm / (nrm + 1e-6), 1.0) if (max_norm > 0 and fin) else 1.0
+        norm.fill_(nrm)
+        coef.fill_(c * inv)
+        found.fill_(0 if fin else 1)
+        return norm, coef, found
+    if torch.is_tensor(inv_scale):
+        inv_ptr, inv_val = inv_scale.data_ptr(), 1.0
+    else:
+        inv_ptr, inv_val = 0, float(inv_scale)
+    _lib.call("pdt_clip_coef", total_sq.data_ptr(), float(max_norm), inv_ptr, inv_val, norm.data_ptr(),
+              coef.data_ptr(), found.data_ptr(), _lib.stream_handle(dev))
+    return norm, coef, found
+
+
+def scale_(tensors: Sequence[torch.Tensor], s: torch.Tensor) -> None:
+    """In-place multiply every tensor by the device scalar ``s``."""
+    tensors = [t for t in tensors if t is not None and t.numel() > 0]
+    if not tensors:
+        return
+    dev = tensors[0].device
+    if dev.type != "cuda":
+        for t in tensors:
+            t.mul_(s.to(t.dtype))
+        return
+    by_dt = {}
+    for t in tensors:
+        by_dt.setdefault(t.dtype, []).append(t)
+    for dt, ts in by_dt.items():
+        tab = _cache.get(("scale", dt, len(ts)), [ts])
+        _lib.call("pdt_scale_mt", tab.meta.data_ptr(), tab.blk.data_ptr(), tab.nblocks, tab.chunk,
+                  _lib.dtype_code(dt), s.data_ptr(), _lib.stream_handle(dev))
+
+
+def adamw_step(params, grads, exp_avgs, exp_avg_sqs, *, lr: float, beta1: float, beta2: float, eps: float,
+               weight_decay: float, step: int, decoupled: bool = True, grad_scale: torch.Tensor | None = None,
+               found_inf: torch.Tensor | None = None, out_bf16=None, table: TensorTable | None = None) -> None:
+    """One fused (multi-tensor) AdamW update.  fp32 params/state; grads fp32 or bf16.
+
+    grad_scale: optional device scalar multiplied into every gradient (unscale x clip coefficient).
+    found_inf: optional device int32 flag; non-zero skips the update (GradScaler semantics).
+    out_bf16: optional list of bf16 tensors receiving the updated params (low-precision compute copy /
+    all-gather input for the sharded engines)."""
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    step_size = lr / bc1
+    bc2_sqrt = math.sqrt(bc2)
+    if len(params) == 0:
+        return
+    dev = params[0].device
+    if dev.type != "cuda":
+        if found_inf is not None and int(found_inf.reshape(-1)[0]) != 0:
+            return
+        gs = None if grad_scale is None else grad_scale.reshape(())
+        for i, p in enumerate(params):
+            g = grads[i].float()
+            if gs is not None:
+                g = g * gs
+            m, v = exp_avgs[i], exp_avg_sqs[i]
+            if decoupled:
+                p.mul_(1 - lr * weight_decay)
+            elif weight_decay != 0:
+                g = g + weight_decay * p
+            m.mul_(beta1).add_(g, alpha=1 - beta1)
+            v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+            denom = v.sqrt() / bc2_sqrt + eps
+            p.addcdiv_(m, denom, value=-step_size)
+            if out_bf16 is not None and out_bf16[i] is not None:
+                out_bf16[i].copy_(p)
+        return
+    gdt = grads[0].dtype
+    if table is None:
+        cols = [list(params), list(grads), list(exp_avgs), list(exp_avg_sqs)]
+        cols.append(list(out_bf16) if out_bf16 is not None else [None] * len(params))
+        table = _cache.get(("adamw", gdt, len(params), id(params[0])), cols)
+    _lib.call("pdt_adamw_mt", table.meta.data_ptr(), table.blk.data_ptr(), table.nblocks, table.chunk,
+              _lib.dtype_code(gdt), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+              float(step_size), float(bc2_sqrt), 1 if decoupled else 0, _lib.ptr(grad_scale), _lib.ptr(found_inf),
+              _lib.stream_handle(dev))
+
+
+def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
+    assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() == dst.numel()
+    if src.device.type != "cuda":
+        dst.copy_(src)
+        return
+    _lib.call("pdt_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), _lib.stream_handle(src.device))

@@ -1,0 +1,138 @@
+"""LayerNorm / RMSNorm with hand-written gfx950 forward and backward kernels.
+
+Drop-in modules (`LayerNorm`, `RMSNorm`) keep torch's parameter names (``weight``, ``bias``) so
+state_dicts stay interchangeable with ``torch.nn.LayerNorm`` checkpoints (north star: same
+state_dict / checkpoint layout).  SURVEY.md K3 (LayerNorm sites in SwinIR / GPT-2) and K16
+(RMSNorm for Llama-3).
+"""
+from __future__ import annotations
+
+import numbers
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _norm_fwd(x2, w, b, eps, rms):
+    rows, n = x2.shape
+    y = torch.empty_like(x2)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
+    mean = None if rms else torch.empty(rows, dtype=torch.float32, device=x2.device)
+    _lib.call("pdt_norm_fwd", x2.data_ptr(), w.data_ptr(), _lib.ptr(b), y.data_ptr(), _lib.ptr(mean),
+              rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype),
+              1 if rms else 0, _lib.stream_handle(x2.device))
+    return y, mean, rstd
+
+
+def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms):
+    rows, n = x2.shape
+    lib = _lib.require()
+    dx = torch.empty_like(x2)
+    dw = torch.empty_like(w)
+    db = torch.empty_like(w) if need_b else None
+    ws = torch.empty(lib.pdt_norm_bwd_workspace_floats(rows, n), dtype=torch.float32, device=x2.device)
+    _lib.call("pdt_norm_bwd", dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), _lib.ptr(mean), rstd.data_ptr(),
+              dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), rows, n, _lib.dtype_code(x2.dtype),
+              _lib.dtype_code(w.dtype), 1 if rms else 0, 0, _lib.stream_handle(x2.device))
+    return dx, dw, db
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, mean, rstd = _norm_fwd(x2, weight, bias, eps, rms=False)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.has_bias = bias is not None
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
+        dx, dw, db = _norm_bwd(dy2, x2, w, mean, rstd, ctx.has_bias, rms=False)
+        return dx.view(dy.shape), dw, db, None
+
+
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, _, rstd = _norm_fwd(x2, weight, None, eps, rms=True)
+        ctx.save_for_backward(x2, weight, rstd)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
+        dx, dw, _ = _norm_bwd(dy2, x2, w, None, rstd, False, rms=True)
+        return dx.view(dy.shape), dw, None
+
+
+def _use_native(x):
+    return x.is_cuda
+
+
+def layer_norm(x, weight, bias=None, eps=1e-5):
+    """LayerNorm over the last dim.  bf16/fp32 activations, bf16/fp32 affine params."""
+    if not _use_native(x):
+        y = F.layer_norm(x.float(), (x.shape[-1],), weight.float(), None if bias is None else bias.float(), eps)
+        return y.to(x.dtype)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return _LayerNormFn.apply(x, weight, bias, eps)
+
+
+def rms_norm(x, weight, eps=1e-6):
+    if not _use_native(x):
+        xf = x.float()
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
+        return y.to(x.dtype)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return _RMSNormFn.apply(x, weight, eps)
+
+
+class LayerNorm(nn.Module):
+    """Same parameters/state_dict as torch.nn.LayerNorm (last-dim only)."""
+
+    def __init__(self, normalized_shape, eps=1e-5, elementwise_affine=True, bias=True, device=None, dtype=None):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (int(normalized_shape),)
+        assert len(normalized_shape) == 1, "only last-dim LayerNorm is supported"
+        self.normalized_shape = tuple(normalized_shape)
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(normalized_shape, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.zeros(normalized_shape, device=device, dtype=dtype)) if bias else None
+
+    def forward(self, x):
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            # autocast would run layer_norm in fp32; we keep bf16 activations and fp32 statistics
+            x = x.to(torch.get_autocast_dtype("cuda"))
+            with torch.autocast("cuda", enabled=False):
+                return layer_norm(x, self.weight, self.bias, self.eps)
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+    def extra_repr(self):
+        return f"{self.normalized_shape}, eps={self.eps}"
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim, eps=1e-6, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim, device=device, dtype=dtype))
+
+    def forward(self, x):
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            x = x.to(torch.get_autocast_dtype("cuda"))
+            with torch.autocast("cuda", enabled=False):
+                return rms_norm(x, self.weight, self.eps)
+        return rms_norm(x, self.weight, self.eps)

@@ -1,0 +1,69 @@
+"""Rotary position embedding (rotate-half convention, Llama-3) with a gfx950 kernel.
+
+cos/sin tables are precomputed once on the host side of the model (fp32 [S_max, D/2]) -- on-device
+trig per element would turn this memory-bound op VALU-bound (cdna_hip_programming.md App. B).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def rope_tables(head_dim: int, max_seq: int, theta: float = 500000.0, device=None, scaling=None):
+    """cos, sin fp32 tables of shape [max_seq, head_dim // 2]."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling is not None:
+        inv = scaling(inv)
+    pos = torch.arange(max_seq, dtype=torch.float64)
+    f = torch.outer(pos, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def _rope_ref(x, cos, sin, pos0, sign):
+    S, D = x.shape[1], x.shape[-1]
+    c = cos[pos0:pos0 + S].view(1, S, 1, D // 2).to(torch.float32)
+    s = sin[pos0:pos0 + S].view(1, S, 1, D // 2).to(torch.float32) * sign
+    xf = x.float()
+    a, b = xf[..., : D // 2], xf[..., D // 2:]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1).to(x.dtype)
+
+
+def _launch(x, y, cos, sin, pos0, backward):
+    B, S, H, D = x.shape
+    _lib.call("pdt_rope", x.data_ptr(), y.data_ptr(), B * S * H, x.stride(2), y.stride(2), H, S, D, int(pos0),
+              cos.data_ptr(), sin.data_ptr(), 1 if backward else 0, _lib.dtype_code(x.dtype),
+              _lib.stream_handle(x.device))
+
+
+def _rows_ok(t):
+    B, S, H, D = t.shape
+    return t.stride(3) == 1 and t.stride(1) == H * t.stride(2) and t.stride(0) == S * t.stride(1)
+
+
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, pos0):
+        if not _rows_ok(x):
+            x = x.contiguous()
+        y = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        _launch(x, y, cos, sin, pos0, backward=False)
+        ctx.save_for_backward(cos, sin)
+        ctx.pos0 = pos0
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        dy = dy if _rows_ok(dy) else dy.contiguous()
+        dx = torch.empty(dy.shape, dtype=dy.dtype, device=dy.device)
+        _launch(dy, dx, cos, sin, ctx.pos0, backward=True)
+        return dx, None, None, None
+
+
+def apply_rope(x, cos, sin, pos0: int = 0):
+    """x: [B, S, H, D] (rows of H*D contiguous); returns the rotated tensor (new storage)."""
+    D = x.shape[-1]
+    if not x.is_cuda or (D // 2) % 8 != 0 or x.dtype not in (torch.float32, torch.bfloat16):
+        return _rope_ref(x, cos, sin, pos0, 1.0)
+    return _RopeFn.apply(x, cos, sin, pos0)

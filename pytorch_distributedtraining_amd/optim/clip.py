@@ -1,0 +1,58 @@
+"""Gradient clipping by global L2 norm with one fused norm launch and (for sharded engines) ONE
+1-float all-reduce.  Semantics of torch.nn.utils.clip_grad_norm_ (clip_grad.py:50-186:
+coef = max_norm / (total_norm + 1e-6), clamped to 1); reference config ClipGradNormConfig(max_norm=0.1,
+norm_type=2.0) in Stoke-DDP.py:253.  With ``apply=False`` the coefficient is returned as a device
+scalar so the caller can fold it into the fused AdamW step (no extra pass over the gradients).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import multi_tensor as mt
+
+
+def grad_norm_sq(parameters, comm=None, sharded=False) -> torch.Tensor:
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if not grads:
+        dev = next(iter(parameters)).device if parameters else torch.device("cpu")
+        return torch.zeros(1, dtype=torch.float32, device=dev)
+    total = mt.l2norm_sq(grads)
+    if sharded and comm is not None and comm.world_size > 1:
+        comm.all_reduce(total, "sum")
+    return total
+
+
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, comm=None, sharded: bool = False,
+                    inv_scale=1.0, apply: bool = True):
+    """Returns (total_norm, grad_multiplier, found_inf) device tensors.
+
+    sharded=True: each rank holds a disjoint shard of the gradients (ZeRO/FSDP) -> the squared norms
+    are summed across ranks.  inv_scale: 1/loss_scale for fp16 (the norm is of the unscaled grads).
+    apply=True multiplies the grads in place (torch semantics); False leaves that to the optimizer."""
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    parameters = list(parameters)
+    if norm_type != 2.0:
+        grads = [p.grad for p in parameters if p.grad is not None]
+        if norm_type == float("inf"):
+            local = torch.stack([g.detach().abs().max().float() for g in grads]).max().reshape(1)
+            if sharded and comm is not None:
+                comm.all_reduce(local, "max")
+            total = local
+        else:
+            local = sum(g.detach().float().abs().pow(norm_type).sum() for g in grads).reshape(1)
+            if sharded and comm is not None:
+                comm.all_reduce(local, "sum")
+            total = local.pow(1.0 / norm_type)
+        inv = inv_scale if not torch.is_tensor(inv_scale) else inv_scale.float()
+        total = total * inv
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) * inv
+        found = (~torch.isfinite(total)).to(torch.int32)
+        if apply:
+            mt.scale_(grads, coef)
+        return total, coef, found
+    sq = grad_norm_sq(parameters, comm, sharded)
+    norm, coef, found = mt.clip_coef(sq, max_norm, inv_scale)
+    if apply:
+        mt.scale_([p.grad for p in parameters if p.grad is not None], coef)
+    return norm, coef, found

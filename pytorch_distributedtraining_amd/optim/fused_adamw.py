@@ -1,0 +1,81 @@
+"""FusedAdamW: torch.optim-compatible AdamW whose step is ONE gfx950 multi-tensor launch per
+(param group, grad dtype).
+
+* ``param_groups`` / ``state_dict`` layout identical to torch.optim.AdamW
+  ({state: {idx: {step, exp_avg, exp_avg_sq}}, param_groups: [...]}, torch/optim/optimizer.py:677-760),
+  so LR schedulers (OneCycleLR cycling betas, Stoke-DDP.py:300) and checkpoints interoperate.
+* Sync-free mixed precision: ``step(grad_scale=t, found_inf=f)`` takes device scalars produced by the
+  fused clip / unscale kernels; no host round trip between backward and the update.
+* Sharded engines: a parameter carrying ``_pdt_lp_shard`` (FSDP / ZeRO flat shards) gets its bf16
+  compute copy written by the same kernel (fused cast epilogue = the all-gather input).
+
+Reference: AdamW(lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4) in Stoke-DDP.py:226-235
+and Fairscale-DDP.py:78-86; math order torch/optim/adam.py:419-547.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from ..ops import multi_tensor as mt
+
+
+class FusedAdamW(Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
+                 decoupled=True, **_ignored):
+        if amsgrad:
+            raise ValueError("FusedAdamW: amsgrad is not supported")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled=decoupled)
+        super().__init__(params, defaults)
+        self._tables = mt.TableCache()
+
+    def _init_state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format, dtype=torch.float32)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format, dtype=torch.float32)
+        return st
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: torch.Tensor | None = None, found_inf: torch.Tensor | None = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            beta1, beta2 = group["betas"]
+            lr = float(group["lr"]) if not torch.is_tensor(group["lr"]) else float(group["lr"].item())
+            buckets = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdamW does not support sparse gradients")
+                if p.dtype != torch.float32:
+                    raise TypeError("FusedAdamW keeps fp32 master params; wrap low-precision models with an "
+                                    "engine (FSDP/ZeRO) or keep params fp32 and use autocast")
+                st = self._init_state(p)
+                st["step"] += 1
+                key = (p.grad.dtype, int(st["step"].item()), p.device)
+                buckets.setdefault(key, []).append(p)
+            for (gdt, step, dev), ps in buckets.items():
+                grads = [p.grad.contiguous() if not p.grad.is_contiguous() else p.grad for p in ps]
+                ms = [self.state[p]["exp_avg"] for p in ps]
+                vs = [self.state[p]["exp_avg_sq"] for p in ps]
+                lps = [getattr(p, "_pdt_lp_shard", None) for p in ps]
+                has_lp = any(x is not None for x in lps)
+                table = None
+                if dev.type == "cuda":
+                    cols = [ps, grads, ms, vs, lps if has_lp else [None] * len(ps)]
+                    table = self._tables.get((gi, gdt, step > 0), cols)
+                mt.adamw_step(ps, grads, ms, vs, lr=lr, beta1=beta1, beta2=beta2, eps=group["eps"],
+                              weight_decay=group["weight_decay"], step=step, decoupled=group.get("decoupled", True),
+                              grad_scale=grad_scale, found_inf=found_inf, out_bf16=lps if has_lp else None,
+                              table=table)
+                for p in ps:
+                    if getattr(p, "_pdt_lp_shard", None) is not None:
+                        p._pdt_lp_version = p._version   # compute copy already refreshed by the kernel
+        return loss

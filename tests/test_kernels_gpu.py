@@ -1,0 +1,286 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (MI355X)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def test_native_library_is_loaded():
+    from pytorch_distributedtraining_amd.ops import _lib
+    lib = _lib.require()
+    assert lib is not None and _lib.available()
+
+
+@pytest.mark.parametrize("N", [768, 2048, 4096, 100, 10000])
+@pytest.mark.parametrize("xdt,wdt", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
+                                     (torch.bfloat16, torch.float32)])
+def test_layer_norm(N, xdt, wdt):
+    from pytorch_distributedtraining_amd.ops import layer_norm
+    rows = 333
+    x = torch.randn(rows, N, device=DEV).to(xdt).requires_grad_()
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(wdt).requires_grad_()
+    b = (0.1 * torch.randn(N, device=DEV)).to(wdt).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.layer_norm(xr, (N,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    tol = 1e-2 if xdt == torch.bfloat16 else 1e-5
+    assert rel_err(y, yr) < tol
+    assert rel_err(x.grad, xr.grad) < tol * 2
+    assert rel_err(w.grad, wr.grad) < tol * 2
+    assert rel_err(b.grad, br.grad) < tol * 2
+
+
+@pytest.mark.parametrize("N", [4096, 2048, 96])
+def test_rms_norm(N):
+    from pytorch_distributedtraining_amd.ops import rms_norm
+    x = torch.randn(257, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_()
+    y = rms_norm(x, w, 1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("approx", ["tanh", "none"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_bias_gelu(approx, dt):
+    from pytorch_distributedtraining_amd.ops import bias_gelu
+    h = torch.randn(300, 1024, device=DEV).to(dt).requires_grad_()
+    b = (0.5 * torch.randn(1024, device=DEV)).to(dt).requires_grad_()
+    y = bias_gelu(h, b, approximate=approx)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    hr, br = h.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = F.gelu(hr + br, approximate=approx)
+    yr.backward(dy.float())
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-5
+    assert rel_err(y, yr) < tol
+    assert rel_err(h.grad, hr.grad) < tol
+    assert rel_err(b.grad, br.grad) < tol
+
+
+def test_swiglu():
+    from pytorch_distributedtraining_amd.ops import swiglu
+    x = torch.randn(129, 2 * 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = swiglu(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    yr = F.silu(xr[:, :512]) * xr[:, 512:]
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2 and rel_err(x.grad, xr.grad) < 1e-2
+
+
+def test_rope():
+    from pytorch_distributedtraining_amd.ops import apply_rope, rope_tables
+    from pytorch_distributedtraining_amd.ops.rope import _rope_ref
+    B, S, H, D = 2, 100, 4, 128
+    cos, sin = rope_tables(D, 256, device=DEV)
+    x = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = apply_rope(x, cos, sin, pos0=3)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    yr = _rope_ref(xr, cos, sin, 3, 1.0)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2 and rel_err(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [50304, 1000, 50257])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_cross_entropy(V, dt):
+    from pytorch_distributedtraining_amd.ops import cross_entropy
+    x = (3 * torch.randn(257, V, device=DEV)).to(dt).requires_grad_()
+    t = torch.randint(0, V, (257,), device=DEV)
+    t[5] = -100
+    loss = cross_entropy(x, t)
+    loss.backward()
+    xr = x.detach().float().requires_grad_()
+    lr = F.cross_entropy(xr, t, ignore_index=-100)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 2e-3 * max(1, abs(lr.item()))
+    assert rel_err(x.grad, xr.grad) < (2e-2 if dt == torch.bfloat16 else 1e-4)
+
+
+def _attn_ref(q, k, v, causal, scale):
+    H, Hkv = q.shape[2], k.shape[2]
+    qt, kt, vt = (t.float().transpose(1, 2) for t in (q, k, v))
+    kt = kt.repeat_interleave(H // Hkv, 1)
+    vt = vt.repeat_interleave(H // Hkv, 1)
+    s = qt @ kt.transpose(-1, -2) * scale
+    if causal:
+        Sq, Sk = q.shape[1], k.shape[1]
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(Sk - Sq)
+        s = s.masked_fill(~m, float("-inf"))
+    return (s.softmax(-1) @ vt).transpose(1, 2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,H,Hkv", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 1024, 2, 1), (1, 77, 2, 2)])
+def test_flash_attn(D, causal, B, S, H, Hkv):
+    from pytorch_distributedtraining_amd.ops import flash_attn
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D))
+    orf.backward(do.float())
+    assert rel_err(o, orf) < 1e-2
+    assert rel_err(q.grad, qr.grad) < 2e-2
+    assert rel_err(k.grad, kr.grad) < 2e-2
+    assert rel_err(v.grad, vr.grad) < 2e-2
+
+
+def test_flash_attn_qkvpacked_matches_unpacked():
+    from pytorch_distributedtraining_amd.ops import flash_attn, flash_attn_qkvpacked
+    qkv = torch.randn(2, 300, 3, 4, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_qkvpacked(qkv, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    x = qkv.detach().clone().requires_grad_()
+    o2 = flash_attn(x[:, :, 0], x[:, :, 1], x[:, :, 2], causal=True)
+    o2.backward(do)
+    assert torch.equal(o, o2)
+    assert torch.equal(qkv.grad, x.grad)
+
+
+def test_flash_attn_cross_length():
+    from pytorch_distributedtraining_amd.ops import flash_attn
+    q = torch.randn(1, 64, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(1, 192, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(1, 192, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=True)
+    o.sum().backward()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, True, 1 / math.sqrt(128))
+    orf.sum().backward()
+    assert rel_err(o, orf) < 1e-2 and rel_err(k.grad, kr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_fused_adamw_matches_torch(gdt):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    shapes = [(1000,), (33, 17), (4096, 3), (5,)]
+    ps = [torch.randn(s, device=DEV) for s in shapes]
+    p1 = [torch.nn.Parameter(p.clone()) for p in ps]
+    p2 = [torch.nn.Parameter(p.clone()) for p in ps]
+    o1 = FusedAdamW(p1, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    o2 = torch.optim.AdamW(p2, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    for _ in range(5):
+        gs = [torch.randn(s, device=DEV) for s in shapes]
+        for a, b, g in zip(p1, p2, gs):
+            a.grad = g.to(gdt)
+            b.grad = g.to(gdt).float()
+        o1.step()
+        o2.step()
+    for a, b in zip(p1, p2):
+        assert (a - b).abs().max().item() < 1e-5
+    sd1, sd2 = o1.state_dict(), o2.state_dict()
+    assert sd1["state"].keys() == sd2["state"].keys()
+    for k in sd1["state"]:
+        assert float(sd1["state"][k]["step"]) == float(sd2["state"][k]["step"])
+        assert torch.allclose(sd1["state"][k]["exp_avg"], sd2["state"][k]["exp_avg"], atol=1e-6)
+
+
+def test_clip_grad_norm_matches_torch():
+    from pytorch_distributedtraining_amd.optim import clip_grad_norm_
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in [(1000,), (77, 3), (65536,)]]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    for p, q in zip(ps, qs):
+        g = torch.randn_like(p)
+        p.grad, q.grad = g.clone(), g.clone()
+    n1, _, found = clip_grad_norm_(ps, 0.1)
+    n2 = torch.nn.utils.clip_grad_norm_(qs, 0.1)
+    assert abs(n1.item() - n2.item()) < 1e-3 * n2.item()
+    assert int(found.item()) == 0
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p.grad, q.grad, rtol=1e-5, atol=1e-7)
+    ps[0].grad[3] = float("inf")
+    _, _, found = clip_grad_norm_(ps, 0.1)
+    assert int(found.item()) == 1
+
+
+def test_adamw_skips_on_found_inf_and_uses_grad_scale():
+    from pytorch_distributedtraining_amd.ops import adamw_step
+    p = torch.randn(1000, device=DEV)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    g = torch.randn_like(p)
+    p0 = p.clone()
+    adamw_step([p], [g], [m], [v], lr=1e-2, beta1=0.9, beta2=0.99, eps=1e-8, weight_decay=0.0, step=1,
+               found_inf=torch.ones(1, dtype=torch.int32, device=DEV))
+    assert torch.equal(p, p0)
+    pa, ma, va = p.clone(), m.clone(), v.clone()
+    adamw_step([p], [g * 4], [m], [v], lr=1e-2, beta1=0.9, beta2=0.99, eps=1e-8, weight_decay=0.0, step=1,
+               grad_scale=torch.full((1,), 0.25, device=DEV))
+    adamw_step([pa], [g], [ma], [va], lr=1e-2, beta1=0.9, beta2=0.99, eps=1e-8, weight_decay=0.0, step=1)
+    assert torch.allclose(p, pa, atol=1e-6)
+
+
+def test_fp8_roundtrip():
+    from pytorch_distributedtraining_amd.ops import dequantize_fp8, quantize_fp8
+    x = torch.randn(10001, device=DEV, dtype=torch.bfloat16) * 3
+    scale = torch.full((1,), 2.0, device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    q = quantize_fp8(x, scale, amax)
+    ref = (x.float() * 2.0).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q, ref.view(torch.uint8))
+    assert abs(amax.item() - x.float().abs().max().item()) < 1e-6
+    y = dequantize_fp8(q, torch.full((1,), 0.5, device=DEV), torch.float32)
+    assert torch.allclose(y, ref.float() * 0.5)
+
+
+def test_gpt2_fsdp_step_matches_fp32_reference():
+    """Whole-model check: FSDP(bf16 HIP kernels) loss/grad-norm vs the same model in fp32 torch math."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel import FullyShardedDataParallel
+    torch.manual_seed(0)
+    ref = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2)
+    sd = {k: v.clone() for k, v in ref.state_dict().items()}
+    x = torch.randint(0, 512, (2, 129))
+    loss_ref = ref(x[:, :-1], labels=x[:, 1:])
+    loss_ref.backward()
+    gn_ref = torch.sqrt(sum(p.grad.float().pow(2).sum() for p in ref.parameters())).item()
+    model = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2)
+    model.load_state_dict(sd)
+    model = FullyShardedDataParallel(model, device=DEV)
+    xd = x.to(DEV)
+    loss = model(xd[:, :-1], labels=xd[:, 1:])
+    loss.backward()
+    norm, coef, _ = clip_grad_norm_(model.flat_parameters(), 1e9, apply=False)
+    assert abs(loss.item() - loss_ref.item()) < 2e-2 * loss_ref.item()
+    assert abs(norm.item() - gn_ref) < 5e-2 * gn_ref
+    opt = FusedAdamW(model.flat_parameters(), lr=1e-3)
+    opt.step(grad_scale=coef)
+    opt.zero_grad()
+    l2 = model(xd[:, :-1], labels=xd[:, 1:])
+    assert l2.item() < loss.item()
+    sd2 = model.state_dict()
+    assert set(sd2) == set(sd)
