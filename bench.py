@@ -109,14 +109,14 @@ def bench_gpt2(args, comm, dev, world, rank):
     if fsdp:
         strat = ShardingStrategy.FULL_SHARD if args.reshard else ShardingStrategy.SHARD_GRAD_OP
         model = FullyShardedDataParallel(model, sharding_strategy=strat, mixed_precision=MixedPrecision(),
-                                         comm=comm, device=dev)
+                                         comm=comm, device=dev, keep_low_precision_grads=True)
         params = model.flat_parameters()
         sharded = True
         par = f"fsdp{world}"
     else:
         from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
         model = DistributedDataParallel(model, comm=comm, compute_dtype=torch.bfloat16)
-        params = [p for p in model.parameters()]
+        params = model.optimizer_parameters()
         sharded = False
         par = f"dp{world}"
     opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)

@@ -32,7 +32,6 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 constexpr int NT = 256;
 constexpr int TILE = 64;          // rows per staged LDS tile
-constexpr int TLD = TILE + 4;     // transposed-image row stride (elements)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -50,6 +49,22 @@ __device__ __forceinline__ f32x16 zero16() {
 
 // accumulator register r of a 32x32 tile, lane half h -> row index inside the tile
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Row-major bf16 tile image [TILE][D] with a 16-byte-chunk XOR swizzle that is conflict-free for BOTH
+// access kinds the kernels issue (cdna_hip_programming.md §5.5 T2/T10, layout (b) "one image for row
+// reads AND transposed reads"):
+//   * ds_read_b128 row reads: 16 consecutive rows, same logical chunk -> 16 distinct slots;
+//   * ds_read_b64_tr_b16 transposed reads: 4 aligned rows x 4 chunks per 32-lane half -> distinct slots.
+// D=128 (256-B rows): phys = c ^ ((r&3)<<2 | (r>>2)&3).  D=64 (128-B rows, two rows per 256-B bank
+// row): phys = c ^ (((r>>1)&1)<<2 | (r>>2)&3).
+template <int D>
+__device__ __forceinline__ int swz(int r, int c) {
+  if constexpr (D == 128) return r * 128 + ((c ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 3);
+  else return r * 64 + ((c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) << 3);
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 template <int D>
 struct TileIO {
@@ -70,43 +85,35 @@ struct TileIO {
       }
     }
   }
-  // registers -> row-major swizzled LDS image [TILE][D]
-  __device__ __forceinline__ static void store_rows(bf16_t* lds, const u16x8 (&r)[NCH]) {
+  // registers -> swizzled LDS image (16-B writes)
+  __device__ __forceinline__ static void store(bf16_t* lds, const u16x8 (&r)[NCH]) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = threadIdx.x + i * NT;
       const int row = c / CH, ch = c % CH;
-      *reinterpret_cast<u16x8*>(lds + row * D + ((ch ^ (row & (CH - 1))) * 8)) = r[i];
+      *reinterpret_cast<u16x8*>(lds + swz<D>(row, ch)) = r[i];
     }
   }
-  // registers -> transposed LDS image [D][TLD]
-  __device__ __forceinline__ static void store_trans(bf16_t* lds, const u16x8 (&r)[NCH]) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = threadIdx.x + i * NT;
-      const int row = c / CH, ch = c % CH;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) lds[(ch * 8 + k) * TLD + row] = r[i][k];
-    }
-  }
-  // A/B fragment from the row-major image: row `row`, k-step ks, lane half h -> d = 16ks + 8h .. +7
+  // row fragment: row `row`, k-step ks, lane half h -> elements d = 16ks + 8h .. +7
   __device__ __forceinline__ static u16x8 row_frag(const bf16_t* lds, int row, int ks, int h) {
-    const int ch = 2 * ks + h;
-    return *reinterpret_cast<const u16x8*>(lds + row * D + ((ch ^ (row & (CH - 1))) * 8));
+    return *reinterpret_cast<const u16x8*>(lds + swz<D>(row, 2 * ks + h));
+  }
+  // transposed fragment (A operand for the permuted-k MFMA): lane l gets column d = 32dt + (l&31) of
+  // rows {kb + 4h + j} (j<4) and {kb + 8 + 4h + j-4} (j>=4), via two ds_read_b64_tr_b16.
+  __device__ __forceinline__ static u16x8 tr_frag(const bf16_t* lds, int dt, int kb, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+    const int r1 = kb + 4 * (g >> 1) + q;
+    const int o1 = swz<D>(r1, col >> 3) + (col & 7);
+    const int o2 = swz<D>(r1 + 8, col >> 3) + (col & 7);
+    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + o1));
+    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + o2));
+    u16x8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
   }
 };
-
-// fragment from a transposed image: row d, permuted 16-key step starting at kb:
-// elements j=0..3 -> keys kb + 4h + j, j=4..7 -> keys kb + 8 + 4h + (j-4)
-__device__ __forceinline__ u16x8 trans_frag(const bf16_t* lds, int d, int kb, int h) {
-  const bf16_t* p = lds + d * TLD + kb + 4 * h;
-  const u16x4 a = *reinterpret_cast<const u16x4*>(p);
-  const u16x4 b = *reinterpret_cast<const u16x4*>(p + 8);
-  u16x8 r;
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-  return r;
-}
 
 // pack registers 8s..8s+7 of an fp32 accumulator into a bf16 fragment
 __device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
@@ -115,6 +122,8 @@ __device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
   for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
   return r;
 }
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 struct AttnParams {
   const bf16_t* q; const bf16_t* k; const bf16_t* v;
@@ -139,9 +148,9 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
   using IO = TileIO<D>;
   constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[TILE * D + D * TLD];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
   bf16_t* Ks = smem;
-  bf16_t* Vt = smem + TILE * D;
+  bf16_t* Vs = smem + TILE * D;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int b = blockIdx.z, hq = blockIdx.y;
@@ -179,8 +188,8 @@ __global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
-    IO::store_rows(Ks, kr);
-    IO::store_trans(Vt, vr);
+    IO::store(Ks, kr);
+    IO::store(Vs, vr);
     __syncthreads();
     if (t + 1 < ntiles) {
       IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
@@ -213,14 +222,14 @@ __global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
     const float msub = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = exp2f(m - msub);
+    const float alpha = fast_exp2(m - msub);
     float ls = 0.f;
     u16x8 pf[2][2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(s[kt][r] - msub);
+        const float pv = fast_exp2(s[kt][r] - msub);
         s[kt][r] = pv;
         ls += pv;
       }
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
-          o[dt] = mfma32(trans_frag(Vt, dt * 32 + c32, kt * 32 + 16 * ss, h), pf[kt][ss], o[dt]);
+          o[dt] = mfma32(IO::tr_frag(Vs, dt, kt * 32 + 16 * ss, lane), pf[kt][ss], o[dt]);
     }
   }
   const float lt = l + __shfl_xor(l, 32, 64);
@@ -290,12 +299,10 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
   using IO = TileIO<D>;
   constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D + 2 * D * TLD];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
   __shared__ float lse_s[TILE], dl_s[TILE];
   bf16_t* Qs = smem;
-  bf16_t* Gs = smem + TILE * D;        // dO row-major
-  bf16_t* Qt = smem + 2 * TILE * D;    // Q^T
-  bf16_t* Gt = Qt + D * TLD;           // dO^T
+  bf16_t* Gs = smem + TILE * D;        // dO
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int b = blockIdx.z, hk = blockIdx.y;
@@ -330,22 +337,26 @@ __global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
     const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
     const float* Lp = p.lse + ((int64_t)b * p.H + hq) * p.Sq;
     const float* Dp = p.delta + ((int64_t)b * p.H + hq) * p.Sq;
+    u16x8 qr[IO::NCH], gr[IO::NCH];
+    if (qstart < p.Sq) {
+      IO::load(Qp, p.q_ss, qstart, p.Sq, qr);
+      IO::load(Gp, p.do_ss, qstart, p.Sq, gr);
+    }
     for (int q0 = qstart; q0 < p.Sq; q0 += TILE) {
       {
-        u16x8 r[IO::NCH];
         __syncthreads();
-        IO::load(Qp, p.q_ss, q0, p.Sq, r);
-        IO::store_rows(Qs, r);
-        IO::store_trans(Qt, r);
-        IO::load(Gp, p.do_ss, q0, p.Sq, r);
-        IO::store_rows(Gs, r);
-        IO::store_trans(Gt, r);
+        IO::store(Qs, qr);
+        IO::store(Gs, gr);
         if (threadIdx.x < TILE) {
           const int q = q0 + threadIdx.x;
           lse_s[threadIdx.x] = q < p.Sq ? Lp[q] * LOG2E : INFINITY;
           dl_s[threadIdx.x] = q < p.Sq ? Dp[q] : 0.f;
         }
         __syncthreads();
+        if (q0 + TILE < p.Sq) {
+          IO::load(Qp, p.q_ss, q0 + TILE, p.Sq, qr);
+          IO::load(Gp, p.do_ss, q0 + TILE, p.Sq, gr);
+        }
       }
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
         for (int r = 0; r < 16; ++r) {
           const int qi = qs * 32 + acc_row(r, h);
           const int q = q0 + qi;
-          float pv = exp2f(s[r] * sl2 - lse_s[qi]);
+          float pv = fast_exp2(s[r] * sl2 - lse_s[qi]);
           if (key >= p.Sk || (CAUSAL && key > q + off)) pv = 0.f;
           s[r] = pv;
           dp[r] = pv * (dp[r] - dl_s[qi]);
@@ -371,10 +382,10 @@ __global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
         const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          dv[dt] = mfma32(trans_frag(Gt, dt * 32 + c32, qs * 32, h), pf0, dv[dt]);
-          dv[dt] = mfma32(trans_frag(Gt, dt * 32 + c32, qs * 32 + 16, h), pf1, dv[dt]);
-          dk[dt] = mfma32(trans_frag(Qt, dt * 32 + c32, qs * 32, h), df0, dk[dt]);
-          dk[dt] = mfma32(trans_frag(Qt, dt * 32 + c32, qs * 32 + 16, h), df1, dk[dt]);
+          dv[dt] = mfma32(IO::tr_frag(Gs, dt, qs * 32, lane), pf0, dv[dt]);
+          dv[dt] = mfma32(IO::tr_frag(Gs, dt, qs * 32 + 16, lane), pf1, dv[dt]);
+          dk[dt] = mfma32(IO::tr_frag(Qs, dt, qs * 32, lane), df0, dk[dt]);
+          dk[dt] = mfma32(IO::tr_frag(Qs, dt, qs * 32 + 16, lane), df1, dk[dt]);
         }
       }
     }
@@ -402,10 +413,9 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
   using IO = TileIO<D>;
   constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D + D * TLD];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
   bf16_t* Ks = smem;
   bf16_t* Vs = smem + TILE * D;
-  bf16_t* Kt = smem + 2 * TILE * D;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const int b = blockIdx.z, hq = blockIdx.y;
@@ -446,9 +456,8 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
-    IO::store_rows(Ks, kr);
-    IO::store_trans(Kt, kr);
-    IO::store_rows(Vs, vr);
+    IO::store(Ks, kr);
+    IO::store(Vs, vr);
     __syncthreads();
     if (t + 1 < ntiles) {
       IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
@@ -469,15 +478,15 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb0 + acc_row(r, h);
-        float pv = exp2f(s[r] * sl2 - lse2);
+        float pv = fast_exp2(s[r] * sl2 - lse2);
         if (key >= p.Sk || (CAUSAL && key > qrow + off)) pv = 0.f;
         dp[r] = pv * (dp[r] - dl);
       }
       const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        dq[dt] = mfma32(trans_frag(Kt, dt * 32 + c32, kt * 32, h), df0, dq[dt]);
-        dq[dt] = mfma32(trans_frag(Kt, dt * 32 + c32, kt * 32 + 16, h), df1, dq[dt]);
+        dq[dt] = mfma32(IO::tr_frag(Ks, dt, kt * 32, lane), df0, dq[dt]);
+        dq[dt] = mfma32(IO::tr_frag(Ks, dt, kt * 32 + 16, lane), df1, dq[dt]);
       }
     }
   }

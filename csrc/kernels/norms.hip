@@ -221,23 +221,47 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
   }
 }
 
-// Column reduction of a [R, N] fp32 partial matrix into out[N] (type W).  Block = 64 columns x 4
-// row-slices; deterministic order.
-template <typename W>
+// Column reduction of a [R, N] fp32 partial matrix into out[N] (type W), two levels so the
+// read of the partials is spread over many CUs (one level with N/64 blocks left most of the chip idle:
+// 7.8 ms/step at GPT-2 1.3B).  Level 1: grid (N/64, RS) blocks of 64 columns x 4 row-lanes, each
+// folding R/RS rows into part2[RS, N].  Level 2: the same kernel with RS = 1 writing out.
+// Deterministic order throughout.
+template <typename W, bool FINAL>
 __global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int R, int N,
-                                                        W* __restrict__ out, int accumulate) {
+                                                        W* __restrict__ out, float* __restrict__ part2,
+                                                        int accumulate) {
   __shared__ float red[RPB][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
+  const int per = (R + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
   float s = 0.f;
   if (col < N)
-    for (int r = wid; r < R; r += RPB) s += part[(int64_t)r * N + col];
+    for (int r = r0 + wid; r < r1; r += RPB) s += part[(int64_t)r * N + col];
   red[wid][lane] = s;
   __syncthreads();
   if (wid == 0 && col < N) {
     float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    if (accumulate) t += to_f<W>(out[col]);
-    out[col] = from_f<W>(t);
+    if (FINAL) {
+      if (accumulate) t += to_f<W>(out[col]);
+      out[col] = from_f<W>(t);
+    } else {
+      part2[(int64_t)blockIdx.y * N + col] = t;
+    }
+  }
+}
+
+// ws2 must hold >= 64 * N floats
+template <typename W>
+void col_reduce(const float* part, int R, int N, W* out, float* ws2, int accumulate, hipStream_t st) {
+  const int cg = (N + 63) / 64;
+  int rs = 1;
+  while (rs < 64 && cg * rs < 512 && R / (rs * 2) >= 8) rs *= 2;
+  if (rs == 1) {
+    col_reduce_kernel<W, true><<<dim3(cg, 1), NT, 0, st>>>(part, R, N, out, nullptr, accumulate);
+  } else {
+    col_reduce_kernel<W, false><<<dim3(cg, rs), NT, 0, st>>>(part, R, N, out, ws2, accumulate);
+    col_reduce_kernel<W, true><<<dim3(cg, 1), NT, 0, st>>>(ws2, rs, N, out, nullptr, accumulate);
   }
 }
 
@@ -261,7 +285,7 @@ int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean
   return (int)hipGetLastError();
 }
 
-// workspace: fp32, >= 2 * pdt_norm_bwd_partial_rows(rows, N) * N floats
+// workspace: fp32, >= (2 * pdt_norm_bwd_partial_rows(rows, N) + 128) * N floats
 int bwd_partial_rows(int rows, int N) {
   if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, 256) * RPB;
   return grid_for(rows, 1, 512);
@@ -287,9 +311,9 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   } else {
     norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DX, dwp, dbp, rows, N);
   }
-  const int cg = (N + 63) / 64;
-  if (dw) col_reduce_kernel<W><<<cg, NT, 0, st>>>(dwp, R, N, (W*)dw, accumulate);
-  if (db) col_reduce_kernel<W><<<cg, NT, 0, st>>>(dbp, R, N, (W*)db, accumulate);
+  float* ws2 = ws + (int64_t)2 * R * N;
+  if (dw) col_reduce<W>(dwp, R, N, (W*)dw, ws2, accumulate, st);
+  if (db) col_reduce<W>(dbp, R, N, (W*)db, ws2 + (int64_t)64 * N, accumulate, st);
   return (int)hipGetLastError();
 }
 
@@ -308,7 +332,7 @@ PDT_API int pdt_norm_fwd(const void* x, const void* w, const void* b, void* y, f
   return (int)hipErrorInvalidValue;
 }
 
-PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return 2 * bwd_partial_rows(rows, N) * N; }
+PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return (2 * bwd_partial_rows(rows, N) + 128) * N; }
 
 PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
                          void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt, int rms, int accumulate,
@@ -345,19 +369,20 @@ __global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* __restrict_
 }
 }  // namespace
 
-PDT_API int pdt_colsum_partial_rows(int rows) { return rows < 256 ? rows : 256; }
+// workspace for pdt_colsum: pdt_colsum_partial_rows(rows) * N + 64 * N floats
+PDT_API int pdt_colsum_partial_rows(int rows) { return (rows < 256 ? rows : 256) + 64; }
 
 PDT_API int pdt_colsum(const void* x, int rows, int N, int xdt, void* out, int odt, float* ws, int accumulate,
                        hipStream_t st) {
   if (N % 8 != 0) return (int)hipErrorInvalidValue;
-  const int R = pdt_colsum_partial_rows(rows);
+  const int R = pdt_colsum_partial_rows(rows) - 64;
   const int rows_per = (rows + R - 1) / R;
   const int Ruse = (rows + rows_per - 1) / rows_per;
   dim3 grid((N / 8 + NT - 1) / NT, Ruse);
   if (xdt == kBF16) colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, rows_per, ws);
   else colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, rows_per, ws);
-  const int cg = (N + 63) / 64;
-  if (odt == kBF16) col_reduce_kernel<bf16_t><<<cg, NT, 0, st>>>(ws, Ruse, N, (bf16_t*)out, accumulate);
-  else col_reduce_kernel<float><<<cg, NT, 0, st>>>(ws, Ruse, N, (float*)out, accumulate);
+  float* ws2 = ws + (int64_t)R * N;
+  if (odt == kBF16) col_reduce<bf16_t>(ws, Ruse, N, (bf16_t*)out, ws2, accumulate, st);
+  else col_reduce<float>(ws, Ruse, N, (float*)out, ws2, accumulate, st);
   return (int)hipGetLastError();
 }

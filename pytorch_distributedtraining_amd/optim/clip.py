@@ -9,10 +9,11 @@ from __future__ import annotations
 import torch
 
 from ..ops import multi_tensor as mt
+from ._grads import grad_of
 
 
 def grad_norm_sq(parameters, comm=None, sharded=False) -> torch.Tensor:
-    grads = [p.grad for p in parameters if p.grad is not None]
+    grads = [grad_of(p) for p in parameters if grad_of(p) is not None]
     if not grads:
         dev = next(iter(parameters)).device if parameters else torch.device("cpu")
         return torch.zeros(1, dtype=torch.float32, device=dev)
@@ -33,7 +34,7 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, comm=No
         parameters = [parameters]
     parameters = list(parameters)
     if norm_type != 2.0:
-        grads = [p.grad for p in parameters if p.grad is not None]
+        grads = [grad_of(p) for p in parameters if grad_of(p) is not None]
         if norm_type == float("inf"):
             local = torch.stack([g.detach().abs().max().float() for g in grads]).max().reshape(1)
             if sharded and comm is not None:
@@ -54,5 +55,5 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, comm=No
     sq = grad_norm_sq(parameters, comm, sharded)
     norm, coef, found = mt.clip_coef(sq, max_norm, inv_scale)
     if apply:
-        mt.scale_([p.grad for p in parameters if p.grad is not None], coef)
+        mt.scale_([grad_of(p) for p in parameters if grad_of(p) is not None], coef)
     return norm, coef, found

@@ -18,6 +18,7 @@ import torch
 from torch.optim import Optimizer
 
 from ..ops import multi_tensor as mt
+from ._grads import grad_of
 
 
 class FusedAdamW(Optimizer):
@@ -50,19 +51,20 @@ class FusedAdamW(Optimizer):
             lr = float(group["lr"]) if not torch.is_tensor(group["lr"]) else float(group["lr"].item())
             buckets = {}
             for p in group["params"]:
-                if p.grad is None:
+                g = grad_of(p)
+                if g is None:
                     continue
-                if p.grad.is_sparse:
+                if g.is_sparse:
                     raise RuntimeError("FusedAdamW does not support sparse gradients")
                 if p.dtype != torch.float32:
                     raise TypeError("FusedAdamW keeps fp32 master params; wrap low-precision models with an "
                                     "engine (FSDP/ZeRO) or keep params fp32 and use autocast")
                 st = self._init_state(p)
                 st["step"] += 1
-                key = (p.grad.dtype, int(st["step"].item()), p.device)
+                key = (g.dtype, int(st["step"].item()), p.device)
                 buckets.setdefault(key, []).append(p)
             for (gdt, step, dev), ps in buckets.items():
-                grads = [p.grad.contiguous() if not p.grad.is_contiguous() else p.grad for p in ps]
+                grads = [grad_of(p) if grad_of(p).is_contiguous() else grad_of(p).contiguous() for p in ps]
                 ms = [self.state[p]["exp_avg"] for p in ps]
                 vs = [self.state[p]["exp_avg_sq"] for p in ps]
                 lps = [getattr(p, "_pdt_lp_shard", None) for p in ps]

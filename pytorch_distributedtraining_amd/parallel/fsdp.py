@@ -184,10 +184,14 @@ class _Unit:
             if h is not None:
                 h.wait()
             fp = self.flat_param
-            if fp.grad is None:
-                fp.grad = out.to(torch.float32) if out.dtype != torch.float32 else out.clone()
-            else:
+            if fp.grad is not None:
                 fp.grad.add_(out)
+            elif self.owner.keep_low_precision_grads and out.dtype != torch.float32:
+                # the reduced bf16 shard gradient is handed to the fused optimizer as is (no fp32 cast
+                # pass, half the optimizer's gradient read); overwritten every synced backward
+                fp._pdt_grad = out
+            else:
+                fp.grad = out.to(torch.float32) if out.dtype != torch.float32 else out.clone()
         self.pending.clear()
 
 
@@ -216,12 +220,17 @@ class FullyShardedDataParallel(nn.Module):
         mixed_precision: compute/all-gather dtype and gradient reduce dtype (bf16 / bf16 default).
         comm: collective layer (default: the initialised default process group).
         forward_prefetch / backward_prefetch: overlap the next unit's all-gather with compute.
+        keep_low_precision_grads: leave the reduced shard gradient in ``reduce_dtype`` as
+            ``flat_param._pdt_grad`` (read by FusedAdamW / clip_grad_norm_) instead of materialising an
+            fp32 ``.grad`` -- use with the framework's fused optimizer.
     """
 
     def __init__(self, module: nn.Module, wrap_classes=None, sharding_strategy=ShardingStrategy.FULL_SHARD,
                  mixed_precision: MixedPrecision | None = None, comm: Comm | None = None, device=None,
-                 forward_prefetch: bool = True, backward_prefetch: bool = True, sync_module_states: bool = True):
+                 forward_prefetch: bool = True, backward_prefetch: bool = True, sync_module_states: bool = True,
+                 keep_low_precision_grads: bool = False):
         super().__init__()
+        self.keep_low_precision_grads = keep_low_precision_grads
         self.module = module
         self.comm = comm or default_comm()
         self.mp = mixed_precision or MixedPrecision()

@@ -196,7 +196,10 @@ def test_fused_adamw_matches_torch(gdt):
     for _ in range(5):
         gs = [torch.randn(s, device=DEV) for s in shapes]
         for a, b, g in zip(p1, p2, gs):
-            a.grad = g.to(gdt)
+            if gdt == torch.float32:
+                a.grad = g
+            else:
+                a._pdt_grad = g.to(gdt)      # low-precision grad next to an fp32 master (engine path)
             b.grad = g.to(gdt).float()
         o1.step()
         o2.step()
