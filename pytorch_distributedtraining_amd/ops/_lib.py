@@ -59,13 +59,14 @@ _SIGS = {
     "pdt_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                            c_void_p],
-    "pdt_syncbn_stats": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                         c_void_p],
-    "pdt_syncbn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+    "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int,
+                         c_int, c_void_p],
+    "pdt_syncbn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p,
                               c_void_p],
-    "pdt_syncbn_bwd_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
-                             c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_syncbn_bwd_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_int64, c_int, c_int64, c_int, c_int, c_void_p],
 }
 
 F32, BF16, F16 = 0, 1, 2

@@ -45,22 +45,25 @@ class _FlatGroup:
             for li, o in zip(pl, offs):
                 self.offset_of[li] = base + o
             base += n
-        self.flat_param = torch.zeros(total, dtype=dtype, device=device)
         self.flat_grad = torch.zeros(total, dtype=dtype, device=device)
         self.bucket_views = []
         base = 0
         for (_bid, _pl, _offs, n) in buckets:
             self.bucket_views.append(self.flat_grad[base:base + n])
             base += n
-        with torch.no_grad():
+        self.master = None
+        self.flat_param = None
+        if master:
+            # compute-dtype mode: params become views of one flat low-precision buffer that the fused
+            # optimizer rewrites from the fp32 master in its epilogue
+            self.flat_param = torch.zeros(total, dtype=dtype, device=device)
+            with torch.no_grad():
+                for li, p in enumerate(params):
+                    o = self.offset_of[li]
+                    self.flat_param[o:o + p.numel()].copy_(p.detach().reshape(-1))
             for li, p in enumerate(params):
                 o = self.offset_of[li]
-                self.flat_param[o:o + p.numel()].copy_(p.detach().reshape(-1))
-        for li, p in enumerate(params):
-            o = self.offset_of[li]
-            p.data = self.flat_param[o:o + p.numel()].view(p.shape)
-        self.master = None
-        if master:
+                p.data = self.flat_param[o:o + p.numel()].view(p.shape)
             m = nn.Parameter(self.flat_param.detach().to(torch.float32))
             m._pdt_lp_shard = self.flat_param
             m._pdt_lp_version = m._version

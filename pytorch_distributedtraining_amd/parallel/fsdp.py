@@ -103,6 +103,11 @@ class _Unit:
             self.state = self.GATHERED
         else:
             self.full = torch.empty(self.total, dtype=self.mp.param_dtype, device=self.device)
+            # The collective writes through a second tensor object that aliases the same storage but
+            # has its OWN version counter: re-gathering in backward must not look like an in-place
+            # modification of the views autograd saved in forward.
+            self._comm_buf = torch.empty(0, dtype=self.mp.param_dtype, device=self.device)
+            self._comm_buf.set_(self.full.untyped_storage(), 0, (self.total,))
             self._free_full()
 
     def refresh_lp(self, force=False):
@@ -133,7 +138,7 @@ class _Unit:
         if self.state != self.SHARDED:
             return
         self._alloc_full()
-        self.handle = self.comm.all_gather(self.full, self.lp_shard, async_op=True)
+        self.handle = self.comm.all_gather(self._comm_buf, self.lp_shard, async_op=True)
         self.state = self.GATHERING
 
     def wait(self):
@@ -249,6 +254,7 @@ class FullyShardedDataParallel(nn.Module):
         self._order_frozen = False
         self._callback_queued = False
         self._orig_keys = list(module.state_dict().keys())
+        self._param_fqns = [n for n, _ in module.named_parameters()]
 
         if sync_module_states and self.comm.world_size > 1:
             # identical init on all ranks (rank 0 wins), like sync_module_states=True
@@ -468,6 +474,13 @@ class FullyShardedDataParallel(nn.Module):
             return destination
         return ordered
 
+    def full_optim_state_dict(self, optimizer):
+        """Optimizer state in torch layout keyed by ORIGINAL parameter index (unflattened, fp32)."""
+        return _full_optim_state(self, optimizer)
+
+    def load_full_optim_state_dict(self, optimizer, sd):
+        _load_full_optim_state(self, optimizer, sd)
+
     def load_state_dict(self, state_dict, strict: bool = True):
         missing = []
         rank = self.comm.rank
@@ -497,6 +510,70 @@ class FullyShardedDataParallel(nn.Module):
         if strict and (missing or unexpected):
             raise RuntimeError(f"FSDP load_state_dict: missing={missing} unexpected={unexpected}")
         return res
+
+
+def _full_optim_state(fsdp, optimizer):
+    idx_of = {f: i for i, f in enumerate(fsdp._param_fqns)}
+    state = {}
+    flat_to_idx = {}
+    for u in fsdp.all_units():
+        idxs = [idx_of[fqn] for (_m, _pn, fqn, _s) in u.params if fqn in idx_of]
+        flat_to_idx[id(u.flat_param)] = idxs
+        st = optimizer.state.get(u.flat_param)
+        if not st:
+            continue
+        full = {k: fsdp._gather_full_fp32(u, v.detach()) for k, v in st.items()
+                if torch.is_tensor(v) and v.dim() == 1 and v.numel() == u.shard_numel}
+        for (m, pn, fqn, shape), off, n in zip(u.params, u.offsets, u.numels):
+            if fqn not in idx_of:
+                continue
+            ent = {k: v[off:off + n].view(shape).clone() for k, v in full.items()}
+            for k, v in st.items():
+                if k not in ent:
+                    ent[k] = v.clone() if torch.is_tensor(v) else v
+            state[idx_of[fqn]] = ent
+    groups = []
+    for g in optimizer.param_groups:
+        d = {k: v for k, v in g.items() if k != "params"}
+        d["params"] = sorted(i for p in g["params"] for i in flat_to_idx.get(id(p), []))
+        groups.append(d)
+    return {"state": state, "param_groups": groups}
+
+
+def _load_full_optim_state(fsdp, optimizer, sd):
+    idx_of = {f: i for i, f in enumerate(fsdp._param_fqns)}
+    st_all = sd["state"]
+    rank = fsdp.comm.rank
+    if sd.get("param_groups"):
+        hp = {k: v for k, v in sd["param_groups"][0].items() if k != "params"}
+        for g in optimizer.param_groups:
+            g.update(hp)
+    for u in fsdp.all_units():
+        s0 = rank * u.shard_numel
+        keys, step = None, None
+        for (_m, _pn, fqn, _s) in u.params:
+            e = st_all.get(idx_of.get(fqn, -1), st_all.get(str(idx_of.get(fqn, -1))))
+            if e is not None:
+                keys = [k for k, v in e.items() if torch.is_tensor(v) and v.dim() > 0]
+                step = e.get("step")
+                break
+        if keys is None:
+            continue
+        new = {}
+        for k in keys:
+            shard = torch.zeros(u.shard_numel, dtype=torch.float32, device=u.flat_param.device)
+            for (_m, _pn, fqn, _shape), off, n in zip(u.params, u.offsets, u.numels):
+                e = st_all.get(idx_of.get(fqn, -1), st_all.get(str(idx_of.get(fqn, -1))))
+                if e is None:
+                    continue
+                t = e[k].reshape(-1)
+                a, b = max(off, s0), min(off + n, s0 + u.shard_numel)
+                if a < b:
+                    shard[a - s0:b - s0].copy_(t[a - off:b - off].to(shard.device, torch.float32))
+            new[k] = shard
+        if step is not None:
+            new["step"] = step.clone() if torch.is_tensor(step) else torch.tensor(float(step))
+        optimizer.state[u.flat_param] = new
 
 
 def _flatten(x):

@@ -1,0 +1,390 @@
+"""The training facade: wrap an nn.Module, get a distributed training loop with mixed precision,
+gradient accumulation / clipping, sharded optimizers and checkpointing -- the capability the reference
+obtains from Stoke (Stoke-DDP.py:240-254 construction; :73-86,116-118,142-145,274-301 use).
+
+Same method names and semantics as the reference exercises them:
+    model(x) / loss(out, tgt) / backward(loss) / step() / detach_and_sync_loss(loss) /
+    print_ema_loss(prepend_msg) / print_on_devices(msg) / model_access / optimizer / world_size / rank /
+    DataLoader(dataset, sampler, ...) / save(path, name) -> (path, tag) / load(path, tag)
+* ``loss()`` divides by grad_accum_steps in training mode; ``backward()`` runs under the engine's
+  ``no_sync()`` on non-boundary micro-steps; ``step()`` acts only on accumulation boundaries:
+  (unscale ->) clip -> optimizer step -> zero grads.  effective batch = per-device x accum x world.
+* MI355X-first execution underneath: RCCL engines from ``parallel`` (bucketed DDP, ZeRO-1 OSS,
+  ZeRO-2 ShardedDDP, FSDP), the fused AdamW and fused clip/unscale kernels (gradient multiplier and
+  found_inf stay on device -- no host sync between backward and update), bf16 autocast by default,
+  loss/EMA synchronisation only when printed.
+"""
+from __future__ import annotations
+
+import contextlib
+import uuid
+
+import torch
+import torch.nn as nn
+
+from ..data.loader import DeviceDataLoader
+from ..optim import FusedAdamW, GradScaler, clip_grad_norm_
+from ..parallel.comm import Comm
+from ..utils import checkpoint as ckpt
+from ..utils.dist import init_distributed
+from ..utils.logging import RankLogger
+from .configs import (AMPConfig, ClipGradConfig, ClipGradNormConfig, DDPConfig, DeepspeedConfig, DistributedOptions,
+                      FairscaleFSDPConfig, FairscaleOSSConfig, FairscaleSDDPConfig, FP16Options, StokeOptimizer,
+                      find_config)
+from .status import TrainerStatus
+
+
+def _val(x):
+    return x.value if hasattr(x, "value") else x
+
+
+class Trainer:
+    def __init__(self, model: nn.Module, optimizer, loss, batch_size_per_device: int, grad_accum_steps: int = 1,
+                 grad_clip=None, gpu: bool = False, fp16=None, distributed=None, fairscale_oss: bool = False,
+                 fairscale_sddp: bool = False, fairscale_fsdp: bool = False, configs=None, info_rank=0,
+                 verbose: bool = True, ema_weight: float = 0.1, comm: Comm | None = None):
+        self.verbose = verbose
+        self.logger = RankLogger(info_rank, verbose)
+        self._loss_fn = loss
+        self.batch_size = int(batch_size_per_device)
+        self.grad_accum = int(grad_accum_steps)
+        self.grad_clip = grad_clip
+        self.gpu = bool(gpu) and torch.cuda.is_available()
+        fp16 = _val(fp16)
+        distributed = _val(distributed)
+        ds_cfg = find_config(configs, DeepspeedConfig)
+        if distributed == "deepspeed" and ds_cfg is not None:
+            stage = ds_cfg.zero_optimization.stage
+            fairscale_oss = stage >= 1 or fairscale_oss
+            fairscale_sddp = stage >= 2 or fairscale_sddp
+            if stage >= 3:
+                fairscale_fsdp, fairscale_oss, fairscale_sddp = True, False, False
+            distributed = "ddp"
+        if distributed == "fsdp":
+            fairscale_fsdp = True
+        self.fp16 = {"apex_O1": "amp", "apex_O2": "bf16", "deepspeed": "bf16"}.get(fp16, fp16)
+        self.ddp_config = find_config(configs, DDPConfig) or DDPConfig()
+        self.amp_config = find_config(configs, AMPConfig) or AMPConfig()
+        self.oss_config = find_config(configs, FairscaleOSSConfig) or FairscaleOSSConfig()
+        self.sddp_config = find_config(configs, FairscaleSDDPConfig) or FairscaleSDDPConfig()
+        self.fsdp_config = find_config(configs, FairscaleFSDPConfig) or FairscaleFSDPConfig()
+
+        # ---- process group / device
+        self.distributed = distributed if distributed is not None or fairscale_fsdp else None
+        if fairscale_fsdp and self.distributed is None:
+            self.distributed = "fsdp"
+        if self.distributed is not None:
+            backend = self.ddp_config.backend if self.gpu else "gloo"
+            if self.ddp_config.local_rank is not None and self.gpu:
+                torch.cuda.set_device(int(self.ddp_config.local_rank))
+            self.rank_, self.world_size_, self.device = init_distributed(backend, self.ddp_config.timeout_s)
+            if not self.gpu:
+                self.device = torch.device("cpu")
+        else:
+            self.rank_, self.world_size_ = 0, 1
+            self.device = torch.device("cuda", torch.cuda.current_device()) if self.gpu else torch.device("cpu")
+        self.comm = comm or Comm()
+        self.status = TrainerStatus(self.gpu, self.distributed, self.fp16, fairscale_oss, fairscale_sddp,
+                                    fairscale_fsdp, self.grad_accum, self.batch_size, self.world_size_).validate()
+
+        # ---- precision
+        self.scaler = None
+        self.autocast_dtype = None
+        if self.fp16 == "amp":
+            self.autocast_dtype = torch.float16
+            a = self.amp_config
+            self.scaler = GradScaler(a.init_scale, a.growth_factor, a.backoff_factor, a.growth_interval,
+                                     comm=self.comm, sharded=fairscale_sddp or fairscale_fsdp)
+        elif self.fp16 == "bf16" and not fairscale_fsdp:
+            self.autocast_dtype = torch.bfloat16
+
+        # ---- model / engines
+        if self.distributed is not None and self.ddp_config.convert_to_sync_batch_norm and not fairscale_fsdp:
+            from ..parallel.syncbn import convert_sync_batchnorm
+            model = convert_sync_batchnorm(model, self.comm)
+        self._module = model
+        opt_spec = optimizer if isinstance(optimizer, StokeOptimizer) else StokeOptimizer(**optimizer) \
+            if isinstance(optimizer, dict) else StokeOptimizer(optimizer)
+        opt_cls = self._fused_equivalent(opt_spec.optimizer)
+        kw = dict(opt_spec.optimizer_kwargs)
+        self._sharded_grads = False
+        if fairscale_fsdp:
+            from ..parallel.fsdp import FullyShardedDataParallel, MixedPrecision, ShardingStrategy
+            c = self.fsdp_config
+            mp = MixedPrecision(c.param_dtype if self.fp16 in ("bf16", None) and self.gpu else torch.float32,
+                                c.reduce_dtype if self.gpu else torch.float32)
+            if c.activation_checkpointing and hasattr(model, "config"):
+                model.config.activation_checkpointing = True
+            self._engine = FullyShardedDataParallel(
+                model.to(self.device), wrap_classes=c.wrap_classes or None,
+                sharding_strategy=ShardingStrategy(c.sharding_strategy), mixed_precision=mp, comm=self.comm,
+                device=self.device, forward_prefetch=c.forward_prefetch, backward_prefetch=c.backward_prefetch,
+                keep_low_precision_grads=opt_cls is FusedAdamW)
+            self._optimizer = opt_cls(self._engine.flat_parameters(), **kw)
+            self._clip_params = self._engine.flat_parameters
+            self._sharded_grads = True
+        else:
+            model.to(self.device)
+            if fairscale_oss:
+                from ..parallel.zero import OSS
+                if fairscale_sddp:
+                    self._optimizer = OSS(model.parameters(), optim=opt_cls, comm=self.comm,
+                                          broadcast_fp16=self.oss_config.broadcast_fp16, **kw)
+                    from ..parallel.zero import ShardedDataParallel
+                    s = self.sddp_config
+                    self._engine = ShardedDataParallel(model, self._optimizer, comm=self.comm,
+                                                       broadcast_buffers=s.broadcast_buffers,
+                                                       sync_models_at_startup=s.sync_models_at_startup,
+                                                       reduce_buffer_size=s.reduce_buffer_size,
+                                                       reduce_fp16=s.reduce_fp16)
+                    self._clip_params = self._optimizer.owned_params
+                    self._sharded_grads = True
+                else:
+                    self._engine = self._make_ddp(model, rebuild=False)
+                    self._optimizer = OSS(model.parameters(), optim=opt_cls, comm=self.comm,
+                                          broadcast_fp16=self.oss_config.broadcast_fp16, **kw)
+                    self._clip_params = lambda: list(self._module.parameters())
+            elif self.distributed is not None:
+                self._engine = self._make_ddp(model, rebuild=True)
+                self._optimizer = opt_cls(model.parameters(), **kw)
+                self._clip_params = lambda: list(self._module.parameters())
+            else:
+                self._engine = model
+                self._optimizer = opt_cls(model.parameters(), **kw)
+                self._clip_params = lambda: list(self._module.parameters())
+
+        # ---- counters / meters
+        self._backward_steps = 0
+        self._grad_accum_counter = 0
+        self._optimizer_steps = 0
+        self._ema_weight = ema_weight
+        self._ema = None           # device tensor
+        self._last_loss = None
+        self._training = True
+        if verbose:
+            self.logger.print(f"[Trainer] {self.status.as_dict()} device={self.device}")
+
+    # ------------------------------------------------------------------ construction helpers
+    def _fused_equivalent(self, cls):
+        """torch AdamW/Adam -> the framework's fused AdamW on GPU (identical math and state layout)."""
+        if self.gpu and cls in (torch.optim.AdamW, FusedAdamW):
+            return FusedAdamW
+        if self.gpu and cls is torch.optim.Adam:
+            return lambda params, **kw: FusedAdamW(params, decoupled=False, **kw)
+        return cls
+
+    def _make_ddp(self, model, rebuild):
+        from ..parallel.ddp import DistributedDataParallel
+        c = self.ddp_config
+        return DistributedDataParallel(model, comm=self.comm, device=self.device, bucket_cap_mb=c.bucket_cap_mb,
+                                       first_bucket_mb=c.first_bucket_mb, broadcast_buffers=c.broadcast_buffers,
+                                       find_unused_parameters=c.find_unused_parameters, reduce_dtype=c.reduce_dtype,
+                                       rebuild_buckets=rebuild)
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def model_access(self) -> nn.Module:
+        return self._module
+
+    @property
+    def optimizer(self):
+        return self._optimizer
+
+    @property
+    def world_size(self) -> int:
+        return self.world_size_
+
+    @property
+    def rank(self) -> int:
+        return self.rank_
+
+    @property
+    def effective_batch_size(self) -> int:
+        return self.status.effective_batch_size
+
+    @property
+    def backward_steps(self) -> int:
+        return self._backward_steps
+
+    @property
+    def optimizer_steps(self) -> int:
+        return self._optimizer_steps
+
+    @property
+    def grad_accum_step(self) -> int:
+        return self._grad_accum_counter
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size_ > 1
+
+    @property
+    def ema_loss(self):
+        return None if self._ema is None else float(self._ema)
+
+    # ------------------------------------------------------------------ forward / loss / backward / step
+    def _autocast(self):
+        if self.autocast_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(self.device.type, dtype=self.autocast_dtype)
+
+    def model(self, *args, **kwargs):
+        with self._autocast():
+            return self._engine(*args, **kwargs)
+
+    __call__ = model
+
+    def loss(self, *args, **kwargs):
+        with self._autocast():
+            out = self._loss_fn(*args, **kwargs)
+        if isinstance(out, (list, tuple)):
+            out = sum(out)
+        d = out.detach().float()
+        self._ema = d.clone() if self._ema is None else self._ema * (1 - self._ema_weight) + d * self._ema_weight
+        self._last_loss = d
+        if self._module.training and self.grad_accum > 1:
+            out = out / self.grad_accum
+        return out
+
+    def _is_boundary(self) -> bool:
+        return (self._grad_accum_counter + 1) % self.grad_accum == 0
+
+    def backward(self, loss):
+        boundary = self._is_boundary()
+        scaled = self.scaler.scale(loss) if self.scaler is not None else loss
+        use_no_sync = (not boundary) and self.ddp_config.no_sync and hasattr(self._engine, "no_sync")
+        with (self._engine.no_sync() if use_no_sync else contextlib.nullcontext()):
+            scaled.backward()
+        self._backward_steps += 1
+        self._grad_accum_counter = (self._grad_accum_counter + 1) % self.grad_accum
+
+    def step(self):
+        if self._grad_accum_counter != 0:
+            return False   # not an accumulation boundary
+        params = self._clip_params() if callable(self._clip_params) else self._clip_params
+        opt = self._optimizer
+        fused = isinstance(opt, FusedAdamW) or (hasattr(opt, "optim") and isinstance(getattr(opt, "optim", None),
+                                                                                    FusedAdamW))
+        inv_scale = 1.0 / self.scaler.get_scale() if self.scaler is not None else 1.0
+        max_norm = self.grad_clip.max_norm if isinstance(self.grad_clip, ClipGradNormConfig) else 0.0
+        norm_type = self.grad_clip.norm_type if isinstance(self.grad_clip, ClipGradNormConfig) else 2.0
+        if isinstance(self.grad_clip, ClipGradConfig):
+            for p in params:
+                if p.grad is not None:
+                    if self.scaler is not None:
+                        p.grad.mul_(inv_scale)
+                    p.grad.clamp_(-self.grad_clip.clip_value, self.grad_clip.clip_value)
+            inv_scale = 1.0
+        need_stats = self.scaler is not None or max_norm > 0
+        coef = found = None
+        if need_stats:
+            _, coef, found = clip_grad_norm_(params, max_norm, norm_type=norm_type, comm=self.comm,
+                                             sharded=self._sharded_grads, inv_scale=inv_scale, apply=not fused)
+            if self.scaler is not None:
+                self.scaler._pending = (coef, found)
+        if fused:
+            opt.step(grad_scale=coef, found_inf=found)
+        else:
+            if found is None or int(found.item()) == 0:
+                opt.step()
+        if self.scaler is not None:
+            self.scaler.update()
+        self.zero_grads()
+        self._optimizer_steps += 1
+        return True
+
+    def zero_grads(self):
+        if hasattr(self._engine, "zero_grad") and self._engine is not self._module:
+            self._engine.zero_grad()
+        self._optimizer.zero_grad(set_to_none=True)
+
+    # ------------------------------------------------------------------ loss sync / printing
+    def detach_and_sync_loss(self, loss, device=None):
+        t = loss.detach().float().reshape(1).clone()
+        self.comm.all_reduce(t, "avg")
+        return float(t.item())
+
+    def print_ema_loss(self, prepend_msg: str = "Current EMA Loss", postpend_msg: str = ""):
+        if self._ema is None:
+            return
+        t = self._ema.reshape(1).clone()
+        self.comm.all_reduce(t, "avg")
+        self.logger.print(f"{prepend_msg}: {float(t.item()):.5f} {postpend_msg}".rstrip())
+
+    def print_on_devices(self, msg, rank=None):
+        self.logger.print(msg, ranks=None if rank is None else (rank if isinstance(rank, (list, tuple)) else [rank]))
+
+    def print(self, msg):
+        self.logger.print(msg)
+
+    def barrier(self):
+        self.comm.barrier()
+
+    def reset_ema(self):
+        self._ema = None
+
+    def train(self):
+        self._module.train()
+
+    def eval(self):
+        self._module.eval()
+
+    # ------------------------------------------------------------------ data
+    def DataLoader(self, dataset, **kwargs):
+        kwargs.setdefault("batch_size", self.batch_size)
+        return DeviceDataLoader(dataset, device=self.device, **kwargs)
+
+    # ------------------------------------------------------------------ checkpointing
+    def _model_state(self):
+        eng = self._engine
+        if hasattr(eng, "sharding_strategy"):           # FSDP: full unflattened fp32 state dict
+            return eng.state_dict()
+        if hasattr(eng, "full_state_dict"):
+            return eng.full_state_dict()
+        return self._module.state_dict()
+
+    def _optimizer_state(self):
+        opt = self._optimizer
+        if hasattr(opt, "consolidate_state_dict"):
+            opt.consolidate_state_dict(recipient_rank=0)
+            return opt.state_dict() if self.rank_ == 0 else None
+        if hasattr(self._engine, "full_optim_state_dict"):
+            return self._engine.full_optim_state_dict(opt)
+        return opt.state_dict()
+
+    def save(self, path: str, name: str | None = None, extension: str = "pt", create_directory: bool = True,
+             extras: dict | None = None):
+        name = name or uuid.uuid4().hex[:8]
+        model_state = self._model_state()
+        opt_state = self._optimizer_state()
+        return ckpt.save_checkpoint(
+            path, name, model_state=model_state, optimizer_state=opt_state,
+            scaler_state=self.scaler.state_dict() if self.scaler is not None else None,
+            backward_step=self._backward_steps, grad_accum_step=self._grad_accum_counter,
+            optimizer_step=self._optimizer_steps, status=self.status.as_dict(), extras=extras, extension=extension,
+            rank=self.rank_, barrier=self.barrier if self.is_distributed else None, create_directory=create_directory)
+
+    def load(self, path: str, tag: str, strict: bool = True, extension: str = "pt"):
+        payload = ckpt.load_checkpoint(path, tag, extension=extension,
+                                       map_location=self.device if self.device.type == "cpu" else "cpu")
+        eng = self._engine
+        if hasattr(eng, "sharding_strategy"):
+            eng.load_state_dict(payload["model_state_dict"], strict=strict)
+        elif hasattr(eng, "load_full_state_dict"):
+            eng.load_full_state_dict(payload["model_state_dict"], strict=strict)
+        else:
+            self._module.load_state_dict(payload["model_state_dict"], strict=strict)
+        if payload.get("optimizer_state_dict") is not None:
+            if hasattr(eng, "load_full_optim_state_dict"):
+                eng.load_full_optim_state_dict(self._optimizer, payload["optimizer_state_dict"])
+            else:
+                self._optimizer.load_state_dict(payload["optimizer_state_dict"])
+        if self.scaler is not None and payload.get("scaler_state_dict"):
+            self.scaler.load_state_dict(payload["scaler_state_dict"])
+        self._backward_steps = payload["backward_step"]
+        self._grad_accum_counter = payload["grad_accum_step"]
+        self._optimizer_steps = payload["optimizer_step"]
+        return payload.get("extras")
+
+
+Stoke = Trainer

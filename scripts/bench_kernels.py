@@ -7,8 +7,12 @@ import json
 import math
 import sys
 
-import torch
-import torch.nn.functional as F
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 
 
 def timeit(fn, iters=20, warmup=3):

@@ -1,0 +1,59 @@
+"""Multi-process test harness: N local processes on 127.0.0.1 over gloo (the reference's own
+'cluster without a cluster' pattern, Fairscale-DDP.py:27,122-132), results returned via files."""
+import os
+import pickle
+import socket
+import tempfile
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(rank, world, port, fn, args, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = fn(rank, world, *args)
+        err = None
+    except Exception:
+        res, err = None, traceback.format_exc()
+    finally:
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump((res, err), f)
+
+
+def run_workers(fn, world=2, *args, timeout=240):
+    """Run fn(rank, world, *args) in `world` spawned processes; return the list of results."""
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_entry, args=(world, _free_port(), fn, args, d), nprocs=world, join=False,
+                                 start_method="spawn")
+        ctx.join(timeout)
+        for p in ctx.processes:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            if not os.path.exists(path):
+                raise RuntimeError(f"rank {r} produced no result (crashed or timed out)")
+            with open(path, "rb") as f:
+                res, err = pickle.load(f)
+            if err:
+                raise RuntimeError(f"rank {r} failed:\n{err}")
+            out.append(res)
+        return out
