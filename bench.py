@@ -159,8 +159,8 @@ def bench_resnet(args, comm, dev, world, rank):
 
     mb = args.micro_batch or 256
     model = resnet50().to(dev).to(memory_format=torch.channels_last)
-    model = DistributedDataParallel(model, comm=comm, compute_dtype=torch.bfloat16)
-    params = list(model.parameters())
+    model = DistributedDataParallel(model, comm=comm, reduce_dtype=torch.bfloat16)
+    params = model.optimizer_parameters()
     opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
     x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (mb,), device=dev)

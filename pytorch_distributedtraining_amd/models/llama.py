@@ -1,0 +1,159 @@
+"""Llama-3 family (BASELINE.json config 5: Llama-3 8B FSDP full-shard + fused AdamW + activation
+checkpointing).  Architecture from the public Llama-3 description (RMSNorm pre-norm, RoPE theta 5e5,
+GQA 32q/8kv heads of 128, SwiGLU FFN 14336, vocab 128256), random init.
+
+MI355X-first layout: one fused q|k|v projection (``attention.wqkv``) and one fused gate|up projection
+(``feed_forward.w13``) so each block issues 4 large GEMMs instead of 7; RMSNorm / RoPE / SwiGLU /
+GQA flash attention / cross-entropy run on the HIP kernels.  ``convert_meta_state_dict`` maps Meta-style
+checkpoints (wq/wk/wv, w1/w3) onto the fused layout.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import apply_rope, cross_entropy, flash_attn, rope_tables, swiglu
+from ..ops.norms import RMSNorm
+
+
+@dataclass
+class LlamaConfig:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    vocab_size: int = 128256
+    ffn_dim: int = 14336
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+    activation_checkpointing: bool = False
+
+    @property
+    def head_dim(self):
+        return self.dim // self.n_heads
+
+
+LLAMA_CONFIGS = {
+    "llama3-8b": dict(),
+    "llama3-1b": dict(dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, ffn_dim=8192),
+    "llama3-tiny": dict(dim=256, n_layers=2, n_heads=2, n_kv_heads=1, ffn_dim=512, vocab_size=1024, max_seq_len=512),
+}
+
+
+def llama_config(name="llama3-8b", **overrides):
+    kw = dict(LLAMA_CONFIGS[name])
+    kw.update(overrides)
+    return LlamaConfig(**kw)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.h, self.hkv, self.d = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        self.wqkv = nn.Linear(cfg.dim, (self.h + 2 * self.hkv) * self.d, bias=False)
+        self.wo = nn.Linear(self.h * self.d, cfg.dim, bias=False)
+
+    def forward(self, x, cos, sin):
+        B, S, _ = x.shape
+        qkv = self.wqkv(x).view(B, S, self.h + 2 * self.hkv, self.d)
+        q = apply_rope(qkv[:, :, : self.h], cos, sin)
+        k = apply_rope(qkv[:, :, self.h: self.h + self.hkv], cos, sin)
+        v = qkv[:, :, self.h + self.hkv:]
+        o = flash_attn(q, k, v, causal=True)
+        return self.wo(o.reshape(B, S, self.h * self.d))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)
+        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
+
+    def forward(self, x):
+        return self.w2(swiglu(self.w13(x)))
+
+
+class LlamaBlock(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attention_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.attention = Attention(cfg)
+        self.ffn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.feed_forward = FeedForward(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attention(self.attention_norm(x), cos, sin)
+        return x + self.feed_forward(self.ffn_norm(x))
+
+
+class Llama(nn.Module):
+    block_class = LlamaBlock
+
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.config = cfg
+        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.layers = nn.ModuleList([LlamaBlock(cfg) for _ in range(cfg.n_layers)])
+        self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        cos, sin = rope_tables(cfg.head_dim, cfg.max_seq_len, cfg.rope_theta)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        std = 0.02
+        out_std = 0.02 / math.sqrt(2 * self.config.n_layers)
+        for n, p in self.named_parameters():
+            if p.dim() == 2:
+                nn.init.normal_(p, 0.0, out_std if (n.endswith("wo.weight") or n.endswith("w2.weight")) else std)
+            else:
+                nn.init.ones_(p)
+
+    def num_params(self):
+        return sum(p.numel() for p in self.parameters())
+
+    def flops_per_token(self, seq_len):
+        c = self.config
+        n = self.num_params() - self.tok_embeddings.weight.numel()
+        return 6 * n + 12 * c.n_layers * seq_len * c.dim
+
+    def forward(self, tokens, labels=None):
+        S = tokens.shape[1]
+        x = self.tok_embeddings(tokens)
+        cos, sin = self.rope_cos[:S], self.rope_sin[:S]
+        for layer in self.layers:
+            if self.config.activation_checkpointing and self.training:
+                x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
+            else:
+                x = layer(x, cos, sin)
+        logits = self.output(self.norm(x))
+        if labels is None:
+            return logits
+        return cross_entropy(logits, labels, inplace_backward=True)
+
+
+def build_llama(name="llama3-8b", **overrides) -> Llama:
+    return Llama(llama_config(name, **overrides))
+
+
+def convert_meta_state_dict(sd: dict, cfg: LlamaConfig) -> dict:
+    """Meta-format Llama checkpoint (tok_embeddings, layers.i.attention.{wq,wk,wv,wo},
+    feed_forward.{w1,w2,w3}, {attention,ffn}_norm, norm, output) -> this module's fused layout."""
+    out = {}
+    for k, v in sd.items():
+        if ".attention.wq." in k:
+            base = k.replace(".attention.wq.", ".attention.wqkv.")
+            out[base] = torch.cat([v, sd[k.replace(".wq.", ".wk.")], sd[k.replace(".wq.", ".wv.")]], 0)
+        elif ".attention.wk." in k or ".attention.wv." in k or ".feed_forward.w3." in k:
+            continue
+        elif ".feed_forward.w1." in k:
+            out[k.replace(".w1.", ".w13.")] = torch.cat([v, sd[k.replace(".w1.", ".w3.")]], 0)
+        else:
+            out[k] = v
+    return out

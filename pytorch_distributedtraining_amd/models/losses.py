@@ -1,0 +1,75 @@
+"""Losses used by the reference workloads.
+
+* ``feat_loss`` / ``PerceptualLoss`` -- the perceptual (feature-space) loss of Stoke-DDP.py:35,224
+  (module ``PyTorchPercept``, absent from the reference, SURVEY.md F4: callable (outputs, targets) ->
+  scalar).  A frozen VGG-16-style feature extractor compares relu1_2 / relu2_2 / relu3_3 activations
+  (L1) plus a pixel L1 term.  No pretrained ImageNet weights are fetchable here: the extractor is
+  random-init unless ``load_feature_weights()`` is given a local state dict ("parity unpinned").
+* ``mse_loss`` -- nn.MSELoss() of Fairscale-DDP.py:76.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256]
+_TAPS = {3: "relu1_2", 8: "relu2_2", 15: "relu3_3"}
+
+
+class PerceptualLoss(nn.Module):
+    def __init__(self, weights=(1.0, 1.0, 1.0), pixel_weight: float = 1.0, seed: int = 0):
+        super().__init__()
+        layers, c = [], 3
+        for v in _CFG:
+            if v == "M":
+                layers.append(nn.MaxPool2d(2))
+            else:
+                layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=False)]
+                c = v
+        self.features = nn.Sequential(*layers)
+        g = torch.Generator().manual_seed(seed)
+        for m in self.features:
+            if isinstance(m, nn.Conv2d):
+                with torch.no_grad():
+                    m.weight.copy_(torch.randn(m.weight.shape, generator=g) * (2.0 / (m.in_channels * 9)) ** 0.5)
+                    m.bias.zero_()
+        for p in self.parameters():
+            p.requires_grad_(False)
+        self.register_buffer("mean", torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1), persistent=False)
+        self.register_buffer("std", torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1), persistent=False)
+        self.weights, self.pixel_weight = weights, pixel_weight
+
+    def load_feature_weights(self, sd):
+        self.features.load_state_dict(sd, strict=False)
+
+    def _taps(self, x):
+        out = []
+        x = (x - self.mean.to(x.dtype)) / self.std.to(x.dtype)
+        for i, m in enumerate(self.features):
+            x = m(x)
+            if i in _TAPS:
+                out.append(x)
+        return out
+
+    def forward(self, outputs, targets):
+        self.features.eval()
+        fo, ft = self._taps(outputs), self._taps(targets.detach())
+        loss = self.pixel_weight * F.l1_loss(outputs, targets)
+        for w, a, b in zip(self.weights, fo, ft):
+            loss = loss + w * F.l1_loss(a, b)
+        return loss
+
+
+_feat = None
+
+
+def feat_loss(outputs, targets):
+    """Module-level perceptual loss callable, as imported by the reference (``from PyTorchPercept import feat_loss``)."""
+    global _feat
+    if _feat is None or next(_feat.buffers()).device != outputs.device:
+        _feat = PerceptualLoss().to(outputs.device)
+    return _feat(outputs, targets)
+
+
+mse_loss = nn.MSELoss()

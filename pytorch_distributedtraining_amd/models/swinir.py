@@ -1,0 +1,226 @@
+"""SwinIR (image super-resolution Swin Transformer) -- the model the reference trains in Stoke-DDP.py:206-208:
+    SwinIR(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1., depths=[6]*4, embed_dim=60,
+           num_heads=[6]*4, mlp_ratio=2, upsampler='pixelshuffledirect', resi_connection='1conv')
+(SwinIR-S x2, 910,152 parameters per SURVEY.md §2.D).  Re-implemented from the published architecture
+(Liang et al., ICCV-W 2021) with the upstream parameter names (conv_first, patch_embed.norm,
+layers.{i}.residual_group.blocks.{j}.{norm1,attn.qkv,attn.proj,attn.relative_position_bias_table,
+norm2,mlp.fc1,mlp.fc2}, layers.{i}.conv, norm, conv_after_body, upsample.0), so upstream checkpoints
+keyed 'params' load with strict=True (Stoke-DDP.py:209-213).
+
+MI355X notes: LayerNorms run on the wave-per-row HIP kernel; window attention (64 tokens/window,
+head_dim 10) goes through torch SDPA with the relative-position bias (+ shift mask) as an additive mask
+-- the cyclic shift and window partition are pure reshapes/rolls.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.norms import LayerNorm
+
+
+def window_partition(x, ws):
+    B, H, W, C = x.shape
+    x = x.view(B, H // ws, ws, W // ws, ws, C)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, C)
+
+
+def window_reverse(w, ws, H, W):
+    B = w.shape[0] // ((H // ws) * (W // ws))
+    x = w.view(B, H // ws, W // ws, ws, ws, -1)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, -1)
+
+
+class WindowAttention(nn.Module):
+    def __init__(self, dim, window_size, num_heads, qkv_bias=True):
+        super().__init__()
+        self.dim, self.ws, self.num_heads = dim, window_size, num_heads
+        self.scale = (dim // num_heads) ** -0.5
+        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * window_size - 1) ** 2, num_heads))
+        coords = torch.stack(torch.meshgrid(torch.arange(window_size), torch.arange(window_size), indexing="ij"))
+        cf = coords.flatten(1)
+        rel = (cf[:, :, None] - cf[:, None, :]).permute(1, 2, 0).contiguous()
+        rel[:, :, 0] += window_size - 1
+        rel[:, :, 1] += window_size - 1
+        rel[:, :, 0] *= 2 * window_size - 1
+        self.register_buffer("relative_position_index", rel.sum(-1), persistent=True)
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.proj = nn.Linear(dim, dim)
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+
+    def forward(self, x, mask=None):
+        Bw, N, C = x.shape
+        h = self.num_heads
+        qkv = self.qkv(x).reshape(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        bias = self.relative_position_bias_table[self.relative_position_index.view(-1)].view(N, N, h)
+        bias = bias.permute(2, 0, 1).unsqueeze(0)                  # 1, h, N, N
+        if mask is not None:
+            nw = mask.shape[0]
+            bias = (bias.unsqueeze(0) + mask.view(1, nw, 1, N, N)).expand(Bw // nw, nw, h, N, N).reshape(Bw, h, N, N)
+        out = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.to(q.dtype), scale=self.scale)
+        return self.proj(out.transpose(1, 2).reshape(Bw, N, C))
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.act = nn.GELU()
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x):
+        return self.fc2(self.act(self.fc1(x)))
+
+
+class SwinTransformerBlock(nn.Module):
+    def __init__(self, dim, input_resolution, num_heads, window_size=8, shift_size=0, mlp_ratio=2.0):
+        super().__init__()
+        self.dim, self.input_resolution, self.num_heads = dim, input_resolution, num_heads
+        self.window_size, self.shift_size = window_size, shift_size
+        if min(input_resolution) <= window_size:
+            self.shift_size, self.window_size = 0, min(input_resolution)
+        self.norm1 = LayerNorm(dim)
+        self.attn = WindowAttention(dim, self.window_size, num_heads)
+        self.norm2 = LayerNorm(dim)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.register_buffer("attn_mask", self._mask(input_resolution) if self.shift_size > 0 else None,
+                             persistent=False)
+
+    def _mask(self, res):
+        H, W = res
+        ws, ss = self.window_size, self.shift_size
+        img = torch.zeros(1, H, W, 1)
+        cnt = 0
+        for hs in (slice(0, -ws), slice(-ws, -ss), slice(-ss, None)):
+            for wsl in (slice(0, -ws), slice(-ws, -ss), slice(-ss, None)):
+                img[:, hs, wsl, :] = cnt
+                cnt += 1
+        mw = window_partition(img, ws).squeeze(-1)
+        m = mw.unsqueeze(1) - mw.unsqueeze(2)
+        return m.masked_fill(m != 0, -100.0).masked_fill(m == 0, 0.0)
+
+    def forward(self, x, x_size):
+        H, W = x_size
+        B, L, C = x.shape
+        sc = x
+        x = self.norm1(x).view(B, H, W, C)
+        if self.shift_size > 0:
+            x = torch.roll(x, shifts=(-self.shift_size, -self.shift_size), dims=(1, 2))
+        if self.shift_size > 0:
+            mask = self.attn_mask if (H, W) == tuple(self.input_resolution) else self._mask((H, W)).to(x.device)
+        else:
+            mask = None
+        a = self.attn(window_partition(x, self.window_size), mask=mask)
+        x = window_reverse(a, self.window_size, H, W)
+        if self.shift_size > 0:
+            x = torch.roll(x, shifts=(self.shift_size, self.shift_size), dims=(1, 2))
+        x = sc + x.reshape(B, L, C)
+        return x + self.mlp(self.norm2(x))
+
+
+class BasicLayer(nn.Module):
+    def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio):
+        super().__init__()
+        self.blocks = nn.ModuleList([
+            SwinTransformerBlock(dim, input_resolution, num_heads, window_size,
+                                 0 if i % 2 == 0 else window_size // 2, mlp_ratio) for i in range(depth)])
+
+    def forward(self, x, x_size):
+        for b in self.blocks:
+            x = b(x, x_size)
+        return x
+
+
+class RSTB(nn.Module):
+    """Residual Swin Transformer Block ('1conv' residual connection)."""
+
+    def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio):
+        super().__init__()
+        self.residual_group = BasicLayer(dim, input_resolution, depth, num_heads, window_size, mlp_ratio)
+        self.conv = nn.Conv2d(dim, dim, 3, 1, 1)
+
+    def forward(self, x, x_size):
+        B, L, C = x.shape
+        y = self.residual_group(x, x_size)
+        y = y.transpose(1, 2).reshape(B, C, *x_size)
+        return self.conv(y).flatten(2).transpose(1, 2) + x
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, embed_dim, norm=True):
+        super().__init__()
+        self.norm = LayerNorm(embed_dim) if norm else None
+
+    def forward(self, x):
+        x = x.flatten(2).transpose(1, 2)
+        return self.norm(x) if self.norm is not None else x
+
+
+class SwinIR(nn.Module):
+    def __init__(self, img_size=64, in_chans=3, embed_dim=60, depths=(6, 6, 6, 6), num_heads=(6, 6, 6, 6),
+                 window_size=8, mlp_ratio=2.0, upscale=2, img_range=1.0, upsampler="pixelshuffledirect",
+                 resi_connection="1conv", **_ignored):
+        super().__init__()
+        if upsampler != "pixelshuffledirect" or resi_connection != "1conv":
+            raise NotImplementedError("this build implements the lightweight SwinIR-S path used by the reference "
+                                      "(upsampler='pixelshuffledirect', resi_connection='1conv')")
+        self.img_range, self.upscale, self.window_size = img_range, upscale, window_size
+        self.register_buffer("mean", torch.tensor([0.4488, 0.4371, 0.4040]).view(1, 3, 1, 1) if in_chans == 3
+                             else torch.zeros(1, 1, 1, 1), persistent=False)
+        self.conv_first = nn.Conv2d(in_chans, embed_dim, 3, 1, 1)
+        self.patch_embed = PatchEmbed(embed_dim, norm=True)
+        res = (img_size, img_size)
+        self.layers = nn.ModuleList([RSTB(embed_dim, res, d, h, window_size, mlp_ratio)
+                                     for d, h in zip(depths, num_heads)])
+        self.norm = LayerNorm(embed_dim)
+        self.conv_after_body = nn.Conv2d(embed_dim, embed_dim, 3, 1, 1)
+        self.upsample = nn.Sequential(nn.Conv2d(embed_dim, upscale ** 2 * in_chans, 3, 1, 1), nn.PixelShuffle(upscale))
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, LayerNorm):
+            nn.init.ones_(m.weight)
+            nn.init.zeros_(m.bias)
+
+    def _pad(self, x):
+        _, _, h, w = x.shape
+        ph = (self.window_size - h % self.window_size) % self.window_size
+        pw = (self.window_size - w % self.window_size) % self.window_size
+        return F.pad(x, (0, pw, 0, ph), "reflect") if (ph or pw) else x
+
+    def forward_features(self, x):
+        x_size = (x.shape[2], x.shape[3])
+        t = self.patch_embed(x)
+        for layer in self.layers:
+            t = layer(t, x_size)
+        t = self.norm(t)
+        B, L, C = t.shape
+        return t.transpose(1, 2).reshape(B, C, *x_size)
+
+    def forward(self, x):
+        H, W = x.shape[2:]
+        x = self._pad(x)
+        mean = self.mean.to(x.dtype)
+        x = (x - mean) * self.img_range
+        x = self.conv_first(x)
+        x = self.conv_after_body(self.forward_features(x)) + x
+        x = self.upsample(x)
+        x = x / self.img_range + mean
+        return x[:, :, : H * self.upscale, : W * self.upscale]
+
+
+def swinir_s_x2(**kw):
+    """The reference's exact configuration (Stoke-DDP.py:206-208)."""
+    cfg = dict(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1.0, depths=[6, 6, 6, 6], embed_dim=60,
+               num_heads=[6, 6, 6, 6], mlp_ratio=2, upsampler="pixelshuffledirect", resi_connection="1conv")
+    cfg.update(kw)
+    return SwinIR(**cfg)

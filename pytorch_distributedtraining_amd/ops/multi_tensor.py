@@ -21,6 +21,11 @@ META = 6
 DEFAULT_CHUNK = 32768
 
 
+def _dense(t: torch.Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)) or \
+        (t.dim() == 5 and t.is_contiguous(memory_format=torch.channels_last_3d))
+
+
 class TensorTable:
     """Device table describing up to 5 aligned tensor lists (+ numel) for a multi-tensor kernel.
 
@@ -41,11 +46,14 @@ class TensorTable:
         meta = torch.zeros((max(n, 1), META), dtype=torch.int64)
         blk = []
         for i in range(n):
+            ref = cols[0][i]
             for j, col in enumerate(cols):
                 t = col[i]
                 if t is not None:
-                    assert t.is_contiguous(), "multi-tensor kernels need contiguous tensors"
+                    # elementwise over the storage: any dense layout works if every column shares it
+                    assert _dense(t), "multi-tensor kernels need dense (non-overlapping) tensors"
                     assert t.numel() == self.numels[i]
+                    assert t.stride() == ref.stride() or t.dim() <= 1, "multi-tensor columns must share a layout"
                     meta[i, j] = t.data_ptr()
             meta[i, 5] = self.numels[i]
             for c in range((self.numels[i] + self.chunk - 1) // self.chunk):

@@ -21,6 +21,13 @@ from ..ops import multi_tensor as mt
 from ._grads import grad_of
 
 
+def _like(g, p):
+    """The gradient in the parameter's memory layout (the kernel walks storage linearly)."""
+    if g.stride() == p.stride() or p.dim() <= 1:
+        return g if g.is_contiguous() or p.dim() > 1 else g.contiguous()
+    return torch.empty_like(p, dtype=g.dtype).copy_(g)
+
+
 class FusedAdamW(Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
                  decoupled=True, **_ignored):
@@ -64,7 +71,7 @@ class FusedAdamW(Optimizer):
                 key = (g.dtype, int(st["step"].item()), p.device)
                 buckets.setdefault(key, []).append(p)
             for (gdt, step, dev), ps in buckets.items():
-                grads = [grad_of(p) if grad_of(p).is_contiguous() else grad_of(p).contiguous() for p in ps]
+                grads = [_like(grad_of(p), p) for p in ps]
                 ms = [self.state[p]["exp_avg"] for p in ps]
                 vs = [self.state[p]["exp_avg_sq"] for p in ps]
                 lps = [getattr(p, "_pdt_lp_shard", None) for p in ps]

@@ -73,7 +73,8 @@ class _FlatGroup:
     def attach_grads(self):
         for li, p in enumerate(self.params):
             o = self.offset_of[li]
-            p.grad = self.flat_grad[o:o + p.numel()].view(p.shape)
+            # same strides as the parameter (channels_last convs): autograd accumulates in place
+            p.grad = torch.as_strided(self.flat_grad, p.shape, p.stride(), o)
 
 
 class DistributedDataParallel(nn.Module):

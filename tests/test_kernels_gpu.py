@@ -343,4 +343,5 @@ def test_ddp_bf16_engine_single_gpu_step():
     assert losses[-1] < losses[0]
     w = m.h[0].attn.c_attn.weight
     assert w.dtype == torch.bfloat16
-    assert torch.allclose(w.float().reshape(-1)[:8], params[0].detach()[:8].bfloat16().float()) or True
+    g = ddp.groups[0]
+    assert torch.equal(g.flat_param, params[0].detach().bfloat16())   # compute copy refreshed by the kernel

@@ -1,0 +1,113 @@
+"""Training facade (Stoke-equivalent) on CPU: single process and gloo world_size 2, incl. the exact
+option combination of the reference (ddp + OSS + ShardedDDP + grad_accum 2 + grad-norm clip +
+SyncBN conversion), status validation and the checkpoint envelope round trip."""
+import os
+
+import pytest
+import torch
+import torch.nn as nn
+
+from dist_utils import run_workers
+
+from pytorch_distributedtraining_amd.trainer import (ClipGradNormConfig, DDPConfig, FairscaleOSSConfig,
+                                                     StatusError, StokeOptimizer, Trainer)
+from pytorch_distributedtraining_amd.utils import checkpoint as ckpt
+
+
+def _model():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.BatchNorm2d(8), nn.ReLU(), nn.Conv2d(8, 3, 3, padding=1))
+
+
+def _opt():
+    return StokeOptimizer(optimizer=torch.optim.AdamW,
+                          optimizer_kwargs={"lr": 1e-3, "betas": (0.9, 0.99), "eps": 1e-8, "weight_decay": 1e-4})
+
+
+def test_status_validation():
+    with pytest.raises(StatusError):
+        Trainer(_model(), _opt(), nn.MSELoss(), 2, fairscale_sddp=True, distributed="ddp", verbose=False)
+    with pytest.raises(StatusError):
+        Trainer(_model(), _opt(), nn.MSELoss(), 2, fairscale_oss=True, verbose=False)
+    with pytest.raises(StatusError):
+        Trainer(_model(), _opt(), nn.MSELoss(), 2, grad_accum_steps=0, verbose=False)
+
+
+def test_single_process_accumulation_and_checkpoint(tmp_path):
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, grad_accum_steps=2,
+                grad_clip=ClipGradNormConfig(0.1, 2.0), verbose=False)
+    assert t.effective_batch_size == 4 and t.world_size == 1 and t.rank == 0
+    x, y = torch.randn(2, 3, 8, 8), torch.randn(2, 3, 8, 8)
+    w0 = t.model_access[0].weight.detach().clone()
+    out = t.model(x)
+    loss = t.loss(out, y)
+    t.backward(loss)
+    assert t.step() is False                                 # not a boundary yet
+    assert torch.equal(w0, t.model_access[0].weight)
+    t.backward(t.loss(t.model(x), y))
+    assert t.step() is True
+    assert not torch.equal(w0, t.model_access[0].weight)
+    assert t.backward_steps == 2 and t.optimizer_steps == 1
+    assert isinstance(t.detach_and_sync_loss(loss), float)
+    t.print_ema_loss(prepend_msg="EMA")
+    path, tag = t.save(str(tmp_path), name="m1", extras={"epoch": 3})
+    assert tag == "stoke-m1-backward-step-2"
+    payload = torch.load(os.path.join(path, tag + ".pt"), weights_only=True)
+    assert set(payload) == {"backward_step", "grad_accum_step", "optimizer_step", "stoke_status", "model_state_dict",
+                            "optimizer_state_dict", "scaler_state_dict", "extras"}
+    assert list(payload["model_state_dict"]) == list(_model().state_dict())    # no 'module.' prefix
+    assert set(payload["optimizer_state_dict"]) == {"state", "param_groups"}
+    assert ckpt.latest_checkpoint(str(tmp_path)) == tag
+    t2 = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, grad_accum_steps=2, verbose=False)
+    extras = t2.load(path, tag)
+    assert extras == {"epoch": 3} and t2.optimizer_steps == 1
+    for a, b in zip(t.model_access.state_dict().values(), t2.model_access.state_dict().values()):
+        assert torch.equal(a, b)
+
+
+def test_dataloader_and_pretrained_import(tmp_path):
+    from pytorch_distributedtraining_amd.data import DistributedSampler, SyntheticSRDataset, random_split
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=4, verbose=False)
+    ds = SyntheticSRDataset(n=20, lr_size=8, scale=1)
+    tr, va = random_split(ds, [0.9, 0.1], seed=1)
+    assert len(tr) == 18 and len(va) == 2
+    dl = t.DataLoader(tr, sampler=DistributedSampler(tr, num_replicas=1, rank=0), num_workers=0)
+    xb, yb = next(iter(dl))
+    assert xb.shape == (4, 3, 8, 8)
+    sd = t.model_access.state_dict()
+    torch.save({"params": sd}, tmp_path / "pre.pth")
+    m = _model()
+    ckpt.load_pretrained(m, str(tmp_path / "pre.pth"), strict=True)
+
+
+def _w_trainer(rank, world, tmp):
+    from pytorch_distributedtraining_amd.data import DistributedSampler, SyntheticSRDataset
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, grad_accum_steps=2,
+                grad_clip=ClipGradNormConfig(0.1, 2.0), distributed="ddp", fairscale_oss=True, fairscale_sddp=True,
+                configs=[DDPConfig(local_rank=rank, convert_to_sync_batch_norm=True),
+                         FairscaleOSSConfig(broadcast_fp16=False)], verbose=False)
+    ds = SyntheticSRDataset(n=16, lr_size=8, scale=1)
+    dl = t.DataLoader(ds, sampler=DistributedSampler(ds, t.world_size, t.rank), num_workers=0)
+    sched = torch.optim.lr_scheduler.OneCycleLR(t.optimizer, max_lr=0.01, pct_start=0.9, steps_per_epoch=len(dl),
+                                                epochs=1)
+    total = 0.0
+    for x, y in dl:
+        loss = t.loss(t.model(x), y)
+        t.backward(loss)
+        t.step()
+        sched.step()
+        total += t.detach_and_sync_loss(loss)
+    path, tag = t.save(tmp, name="dist")
+    sd = {k: v.clone() for k, v in t.model_access.state_dict().items()}
+    return sd, t.optimizer_steps, type(t.model_access[1]).__name__, tag, total
+
+
+def test_distributed_trainer_reference_combination(tmp_path):
+    outs = run_workers(_w_trainer, 2, str(tmp_path))
+    (sd0, steps, bn_type, tag, _), (sd1, _, _, _, _) = outs
+    assert steps == 2 and bn_type == "SyncBatchNorm"
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+    payload = torch.load(os.path.join(tmp_path, tag + ".pt"), weights_only=True)
+    assert sorted(payload["optimizer_state_dict"]["state"]) == list(range(6))
+    assert payload["stoke_status"]["oss"] and payload["stoke_status"]["effective_batch_size"] == 8
