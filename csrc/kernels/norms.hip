@@ -19,10 +19,13 @@ constexpr int NT = 256;      // threads per block
 constexpr int RPB = NT / 64; // rows per block (one per wave)
 
 template <typename T, typename W, int ITERS, bool RMS>
-__global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+__global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                      T* __restrict__ sum_out, const W* __restrict__ w,
                                                       const W* __restrict__ b, T* __restrict__ y,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                       int rows, int N, float eps) {
+  // optional fused residual: s = x + res is written to sum_out and normalised (saves one full pass of
+  // the residual stream per norm site)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float invN = 1.f / (float)N;
   for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
@@ -34,6 +37,15 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
       const int col = it * 512 + lane * 8;
       if (col < N) {
         Vec8<T>::load(xr + col, v[it]);
+        if (res != nullptr) {
+          float r8[8];
+          Vec8<T>::load(res + (int64_t)row * N + col, r8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[it][k] += r8[k];
+          Vec8<T>::store(sum_out + (int64_t)row * N + col, v[it]);
+          // normalise exactly what was stored (bf16-rounded sum)
+          Vec8<T>::load(sum_out + (int64_t)row * N + col, v[it]);
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[it][k] = 0.f;
@@ -82,26 +94,29 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
   }
 }
 
+// Backward: one wave per row, the row's x/dy held in registers as raw 16-byte vectors; dgamma/dbeta
+// are accumulated for the whole workgroup in LDS (ds_add_f32, distinct columns per lane) and written
+// as ONE partial row per workgroup (4x fewer partials than per-wave rows, and no per-lane accumulator
+// arrays: 8 waves/CU fit at N=2048 and N=8192 no longer spills).  Optional ``dres``: the gradient of
+// the fused residual sum, added into dx in the same pass.
 template <typename T, typename W, int ITERS, bool RMS>
 __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const W* __restrict__ w, const float* __restrict__ mean_in,
-                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                      float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                      int rows, int N) {
+                                                      const float* __restrict__ rstd_in, const T* __restrict__ dres,
+                                                      T* __restrict__ dx, float* __restrict__ dw_part,
+                                                      float* __restrict__ db_part, int rows, int N) {
+  extern __shared__ __attribute__((aligned(16))) float sacc[];   // [2][N]
+  float* sdw = sacc;
+  float* sdb = sacc + N;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float invN = 1.f / (float)N;
-  float dwa[ITERS][8], dba[ITERS][8];
-#pragma unroll
-  for (int it = 0; it < ITERS; ++it)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; }
-
+  for (int i = threadIdx.x; i < 2 * N; i += NT) sacc[i] = 0.f;
+  __syncthreads();
   for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
     const T* xr = x + (int64_t)row * N;
     const T* gr = dy + (int64_t)row * N;
     const float mean = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
-    float xh[ITERS][8], g[ITERS][8];
     float a = 0.f, bsum = 0.f;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -113,16 +128,13 @@ __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, 
         Vec8<W>::load(w + col, wv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xh[it][k] = (xv[k] - mean) * rstd;
-          g[it][k] = dv[k] * wv[k];
-          a += g[it][k] * xh[it][k];
-          bsum += g[it][k];
-          dwa[it][k] += dv[k] * xh[it][k];
-          dba[it][k] += dv[k];
+          const float xh = (xv[k] - mean) * rstd;
+          const float g = dv[k] * wv[k];
+          a += g * xh;
+          bsum += g;
+          atomicAdd(&sdw[col + k], dv[k] * xh);
+          if (!RMS) atomicAdd(&sdb[col + k], dv[k]);
         }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { xh[it][k] = 0.f; g[it][k] = 0.f; }
       }
     }
     a = wave_sum(a) * invN;
@@ -132,34 +144,44 @@ __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, 
     for (int it = 0; it < ITERS; ++it) {
       const int col = it * 512 + lane * 8;
       if (col < N) {
-        float o[8];
+        float xv[8], dv[8], wv[8], o[8];
+        Vec8<T>::load(xr + col, xv);   // L1/L2-resident re-read (keeps VGPRs low)
+        Vec8<T>::load(gr + col, dv);
+        Vec8<W>::load(w + col, wv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[it][k] - bsum - xh[it][k] * a);
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[k] * wv[k] - bsum - (xv[k] - mean) * rstd * a);
+        if (dres != nullptr) {
+          float r8[8];
+          Vec8<T>::load(dres + (int64_t)row * N + col, r8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r8[k];
+        }
         Vec8<T>::store(dxr + col, o);
       }
     }
   }
-  // one partial row per wave
-  const int prow = blockIdx.x * RPB + wid;
-#pragma unroll
-  for (int it = 0; it < ITERS; ++it) {
-    const int col = it * 512 + lane * 8;
-    if (col < N) {
-      Vec8<float>::store(dw_part + (int64_t)prow * N + col, dwa[it]);
-      if (db_part) Vec8<float>::store(db_part + (int64_t)prow * N + col, dba[it]);
-    }
+  __syncthreads();
+  for (int c = threadIdx.x * 4; c < N; c += NT * 4) {
+    *reinterpret_cast<f32x4*>(dw_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdw + c);
+    if (db_part) *reinterpret_cast<f32x4*>(db_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdb + c);
   }
 }
 
 // ---- fallback: one block per row, streamed from global memory ----
 template <typename T, typename W, bool RMS>
-__global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, const W* __restrict__ w,
+__global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, const T* __restrict__ res,
+                                                       T* __restrict__ sum_out, const W* __restrict__ w,
                                                        const W* __restrict__ b, T* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                        int rows, int N, float eps) {
   __shared__ float red[RPB];
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    const T* xr = x + (int64_t)row * N;
+    if (res != nullptr) {
+      for (int c = threadIdx.x; c < N; c += NT)
+        sum_out[(int64_t)row * N + c] = from_f<T>(to_f<T>(x[(int64_t)row * N + c]) + to_f<T>(res[(int64_t)row * N + c]));
+      __syncthreads();
+    }
+    const T* xr = (res != nullptr ? sum_out : x) + (int64_t)row * N;
     float s = 0.f;
     for (int c = threadIdx.x; c < N; c += NT) { float v = to_f<T>(xr[c]); s += RMS ? v * v : v; }
     s = block_sum<RPB>(s, red);
@@ -189,7 +211,8 @@ __global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, 
 template <typename T, typename W, bool RMS>
 __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x,
                                                        const W* __restrict__ w, const float* __restrict__ mean_in,
-                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                       const float* __restrict__ rstd_in, const T* __restrict__ dres,
+                                                       T* __restrict__ dx,
                                                        float* __restrict__ dw_part, float* __restrict__ db_part,
                                                        int rows, int N) {
   // partial row per block: rows handled by this block are accumulated straight into it
@@ -216,7 +239,9 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
     for (int c = threadIdx.x; c < N; c += NT) {
       float xh = (to_f<T>(xr[c]) - mean) * rstd;
       float g = to_f<T>(gr[c]) * to_f<W>(w[c]);
-      dxr[c] = from_f<T>(rstd * (g - bs - xh * a));
+      float o = rstd * (g - bs - xh * a);
+      if (dres != nullptr) o += to_f<T>(dres[(int64_t)row * N + c]);
+      dxr[c] = from_f<T>(o);
     }
   }
 }
@@ -266,13 +291,14 @@ void col_reduce(const float* part, int R, int N, W* out, float* ws2, int accumul
 }
 
 template <typename T, typename W, bool RMS>
-int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows, int N,
-               float eps, hipStream_t st) {
-  const T* X = (const T*)x; const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
+int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y, float* mean,
+               float* rstd, int rows, int N, float eps, hipStream_t st) {
+  const T* X = (const T*)x; const T* R = (const T*)res; T* S = (T*)sum_out;
+  const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
   if (N % 8 == 0 && N <= 8192) {
     const int grid = grid_for(rows, RPB, 256 * 16);
     const int iters = (N + 511) / 512;
-#define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, Wt, B, Y, mean, rstd, rows, N, eps)
+#define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N, eps)
     if (iters <= 1) PDT_NF(1);
     else if (iters <= 2) PDT_NF(2);
     else if (iters <= 4) PDT_NF(4);
@@ -280,28 +306,30 @@ int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean
     else PDT_NF(16);
 #undef PDT_NF
   } else {
-    norm_fwd_generic<T, W, RMS><<<grid_for(rows, 1, 256 * 8), NT, 0, st>>>(X, Wt, B, Y, mean, rstd, rows, N, eps);
+    norm_fwd_generic<T, W, RMS><<<grid_for(rows, 1, 256 * 8), NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N, eps);
   }
   return (int)hipGetLastError();
 }
 
-// workspace: fp32, >= (2 * pdt_norm_bwd_partial_rows(rows, N) + 128) * N floats
+// fast path: one partial row per workgroup (LDS-accumulated); fallback: one per block
 int bwd_partial_rows(int rows, int N) {
-  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, 256) * RPB;
+  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, 512);
   return grid_for(rows, 1, 512);
 }
 
+// workspace: fp32, >= (2 * bwd_partial_rows(rows, N) + 128) * N floats
 template <typename T, typename W, bool RMS>
-int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-               void* dw, void* db, float* ws, int rows, int N, int accumulate, hipStream_t st) {
+int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
+               void* dx, void* dw, void* db, float* ws, int rows, int N, int accumulate, hipStream_t st) {
   const T* DY = (const T*)dy; const T* X = (const T*)x; const W* Wt = (const W*)w; T* DX = (T*)dx;
+  const T* DR = (const T*)dres;
   const int R = bwd_partial_rows(rows, N);
   float* dwp = ws;
   float* dbp = (db != nullptr) ? ws + (int64_t)R * N : nullptr;
   if (N % 8 == 0 && N <= 8192) {
-    const int grid = R / RPB;
     const int iters = (N + 511) / 512;
-#define PDT_NB(I) norm_bwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(DY, X, Wt, mean, rstd, DX, dwp, dbp, rows, N)
+    const size_t lds = 2 * (size_t)N * sizeof(float);
+#define PDT_NB(I) norm_bwd_kernel<T, W, I, RMS><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N)
     if (iters <= 1) PDT_NB(1);
     else if (iters <= 2) PDT_NB(2);
     else if (iters <= 4) PDT_NB(4);
@@ -309,7 +337,7 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
     else PDT_NB(16);
 #undef PDT_NB
   } else {
-    norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DX, dwp, dbp, rows, N);
+    norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N);
   }
   float* ws2 = ws + (int64_t)2 * R * N;
   if (dw) col_reduce<W>(dwp, R, N, (W*)dw, ws2, accumulate, st);
@@ -320,13 +348,15 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
 }  // namespace
 
 // dtype codes: x/y in {kF32, kBF16}; w/b in {kF32, kBF16}.  rms=1 selects RMSNorm (b ignored, mean unused).
-PDT_API int pdt_norm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
-                         int N, float eps, int xdt, int wdt, int rms, hipStream_t st) {
-#define PDT_DISPATCH(R)                                                                             \
-  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, w, b, y, mean, rstd, rows, N, eps, st); \
-  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, w, b, y, mean, rstd, rows, N, eps, st);   \
-  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, w, b, y, mean, rstd, rows, N, eps, st);     \
-  if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, w, b, y, mean, rstd, rows, N, eps, st);
+// res/sum_out (nullable): fused residual -- sum_out = x + res is written and normalised.
+PDT_API int pdt_norm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
+                         float* mean, float* rstd, int rows, int N, float eps, int xdt, int wdt, int rms,
+                         hipStream_t st) {
+#define PDT_DISPATCH(R)                                                                                      \
+  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);
   if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
 #undef PDT_DISPATCH
   return (int)hipErrorInvalidValue;
@@ -334,14 +364,15 @@ PDT_API int pdt_norm_fwd(const void* x, const void* w, const void* b, void* y, f
 
 PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return (2 * bwd_partial_rows(rows, N) + 128) * N; }
 
-PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-                         void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt, int rms, int accumulate,
-                         hipStream_t st) {
+// dres (nullable): gradient arriving at the fused residual sum, added into dx.
+PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                         const void* dres, void* dx, void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt,
+                         int rms, int accumulate, hipStream_t st) {
 #define PDT_DISPATCH(R)                                                                                         \
-  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st); \
-  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);   \
-  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);     \
-  if (xdt == kF32 && wdt == kBF16) return launch_bwd<float, bf16_t, R>(dy, x, w, mean, rstd, dx, dw, db, ws, rows, N, accumulate, st);
+  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_bwd<float, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);
   if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
 #undef PDT_DISPATCH
   return (int)hipErrorInvalidValue;

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
+from ..ops.linear import Linear
 from ..ops.norms import LayerNorm
 
 
@@ -59,8 +60,8 @@ class CausalSelfAttention(nn.Module):
         super().__init__()
         self.n_head = cfg.n_head
         self.head_dim = cfg.head_dim
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = Linear(cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         B, S, C = x.shape
@@ -72,8 +73,8 @@ class CausalSelfAttention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.c_fc = Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         h = F.linear(x, self.c_fc.weight)            # hipBLASLt GEMM, bias folded into the GELU kernel
@@ -89,10 +90,15 @@ class GPT2Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
         self.mlp = MLP(cfg)
 
-    def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        x = x + self.mlp(self.ln_2(x))
-        return x
+    def forward(self, x, pending=None):
+        """(x, pending) -> (x', mlp_out): the residual adds are fused into the following LayerNorm
+        kernels (``pending`` is the previous block's branch output not yet added to the stream)."""
+        if pending is None:
+            h = self.ln_1(x)
+        else:
+            h, x = self.ln_1.forward_add(x, pending)
+        y, x = self.ln_2.forward_add(x, self.attn(h))
+        return x, self.mlp(y)
 
 
 class GPT2LMHeadModel(nn.Module):
@@ -139,13 +145,14 @@ class GPT2LMHeadModel(nn.Module):
     def forward(self, input_ids, labels=None):
         B, S = input_ids.shape
         pos = torch.arange(S, device=input_ids.device)
-        x = self.wte(input_ids) + self.wpe(pos)
+        x = self.wte(input_ids)
+        pending = self.wpe(pos).unsqueeze(0).expand(B, S, -1)
         for blk in self.h:
             if self.config.activation_checkpointing and self.training:
-                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+                x, pending = torch.utils.checkpoint.checkpoint(blk, x, pending, use_reentrant=False)
             else:
-                x = blk(x)
-        x = self.ln_f(x)
+                x, pending = blk(x, pending)
+        x, _ = self.ln_f.forward_add(x, pending)
         logits = F.linear(x, self.wte.weight)   # tied head
         if labels is None:
             return logits

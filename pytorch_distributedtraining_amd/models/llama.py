@@ -86,9 +86,14 @@ class LlamaBlock(nn.Module):
         self.ffn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.feed_forward = FeedForward(cfg)
 
-    def forward(self, x, cos, sin):
-        x = x + self.attention(self.attention_norm(x), cos, sin)
-        return x + self.feed_forward(self.ffn_norm(x))
+    def forward(self, x, cos, sin, pending=None):
+        """(x, pending) -> (x', ffn_out); residual adds fused into the next RMSNorm kernel."""
+        if pending is None:
+            h = self.attention_norm(x)
+        else:
+            h, x = self.attention_norm.forward_add(x, pending)
+        y, x = self.ffn_norm.forward_add(x, self.attention(h, cos, sin))
+        return x, self.feed_forward(y)
 
 
 class Llama(nn.Module):
@@ -127,12 +132,14 @@ class Llama(nn.Module):
         S = tokens.shape[1]
         x = self.tok_embeddings(tokens)
         cos, sin = self.rope_cos[:S], self.rope_sin[:S]
+        pending = None
         for layer in self.layers:
             if self.config.activation_checkpointing and self.training:
-                x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
+                x, pending = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, pending, use_reentrant=False)
             else:
-                x = layer(x, cos, sin)
-        logits = self.output(self.norm(x))
+                x, pending = layer(x, cos, sin, pending)
+        h = self.norm(x) if pending is None else self.norm.forward_add(x, pending)[0]
+        logits = self.output(h)
         if labels is None:
             return logits
         return cross_entropy(logits, labels, inplace_backward=True)

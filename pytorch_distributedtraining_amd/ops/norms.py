@@ -16,18 +16,19 @@ import torch.nn.functional as F
 from . import _lib
 
 
-def _norm_fwd(x2, w, b, eps, rms):
+def _norm_fwd(x2, w, b, eps, rms, res2=None):
     rows, n = x2.shape
     y = torch.empty_like(x2)
+    s = torch.empty_like(x2) if res2 is not None else None
     rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
     mean = None if rms else torch.empty(rows, dtype=torch.float32, device=x2.device)
-    _lib.call("pdt_norm_fwd", x2.data_ptr(), w.data_ptr(), _lib.ptr(b), y.data_ptr(), _lib.ptr(mean),
-              rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype),
-              1 if rms else 0, _lib.stream_handle(x2.device))
-    return y, mean, rstd
+    _lib.call("pdt_norm_fwd", x2.data_ptr(), _lib.ptr(res2), _lib.ptr(s), w.data_ptr(), _lib.ptr(b), y.data_ptr(),
+              _lib.ptr(mean), rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype),
+              _lib.dtype_code(w.dtype), 1 if rms else 0, _lib.stream_handle(x2.device))
+    return y, mean, rstd, s
 
 
-def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms):
+def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms, dres2=None):
     rows, n = x2.shape
     lib = _lib.require()
     dx = torch.empty_like(x2)
@@ -35,8 +36,8 @@ def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms):
     db = torch.empty_like(w) if need_b else None
     ws = torch.empty(lib.pdt_norm_bwd_workspace_floats(rows, n), dtype=torch.float32, device=x2.device)
     _lib.call("pdt_norm_bwd", dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), _lib.ptr(mean), rstd.data_ptr(),
-              dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), rows, n, _lib.dtype_code(x2.dtype),
-              _lib.dtype_code(w.dtype), 1 if rms else 0, 0, _lib.stream_handle(x2.device))
+              _lib.ptr(dres2), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), rows, n,
+              _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype), 1 if rms else 0, 0, _lib.stream_handle(x2.device))
     return dx, dw, db
 
 
@@ -45,7 +46,7 @@ class _LayerNormFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, eps):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
-        y, mean, rstd = _norm_fwd(x2, weight, bias, eps, rms=False)
+        y, mean, rstd, _ = _norm_fwd(x2, weight, bias, eps, rms=False)
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.has_bias = bias is not None
         return y.view(shape)
@@ -63,7 +64,7 @@ class _RMSNormFn(torch.autograd.Function):
     def forward(ctx, x, weight, eps):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
-        y, _, rstd = _norm_fwd(x2, weight, None, eps, rms=True)
+        y, _, rstd, _ = _norm_fwd(x2, weight, None, eps, rms=True)
         ctx.save_for_backward(x2, weight, rstd)
         return y.view(shape)
 
@@ -73,6 +74,40 @@ class _RMSNormFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
         dx, dw, _ = _norm_bwd(dy2, x2, w, None, rstd, False, rms=True)
         return dx.view(dy.shape), dw, None
+
+
+class _AddNormFn(torch.autograd.Function):
+    """(y, s) = (norm(x + r), x + r) in one pass; backward folds the residual gradient ds into dx."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps, rms):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        r2 = r.reshape(-1, shape[-1]).contiguous()
+        y, mean, rstd, s = _norm_fwd(x2, weight, bias, eps, rms, res2=r2)
+        ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.has_bias, ctx.rms = bias is not None, rms
+        return y.view(shape), s.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, w, mean, rstd = ctx.saved_tensors
+        n = s.shape[-1]
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dy2 = dy.reshape(-1, n).contiguous()
+        ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
+        dx, dw, db = _norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2)
+        dx = dx.view(dy.shape)
+        return dx, dx, dw, db, None, None
+
+
+def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False):
+    """Fused residual add + LayerNorm/RMSNorm: returns (norm(x + r), x + r)."""
+    if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16) or r.dtype != x.dtype:
+        s = x + r
+        return (rms_norm(s, weight, eps) if rms else layer_norm(s, weight, bias, eps)), s
+    return _AddNormFn.apply(x, r, weight, bias, eps, rms)
 
 
 def _use_native(x):
@@ -120,8 +155,20 @@ class LayerNorm(nn.Module):
                 return layer_norm(x, self.weight, self.bias, self.eps)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
+    def forward_add(self, x, r):
+        """(LN(x + r), x + r) with one kernel pass."""
+        return _ln_forward_add(self, x, r, rms=False)
+
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"
+
+
+def _ln_forward_add(mod, x, r, rms):
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return add_norm(x.to(dt), r.to(dt), mod.weight, getattr(mod, "bias", None), mod.eps, rms)
+    return add_norm(x, r, mod.weight, getattr(mod, "bias", None), mod.eps, rms)
 
 
 class RMSNorm(nn.Module):
@@ -136,3 +183,6 @@ class RMSNorm(nn.Module):
             with torch.autocast("cuda", enabled=False):
                 return rms_norm(x, self.weight, self.eps)
         return rms_norm(x, self.weight, self.eps)
+
+    def forward_add(self, x, r):
+        return _ln_forward_add(self, x, r, rms=True)

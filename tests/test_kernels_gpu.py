@@ -345,3 +345,66 @@ def test_ddp_bf16_engine_single_gpu_step():
     assert w.dtype == torch.bfloat16
     g = ddp.groups[0]
     assert torch.equal(g.flat_param, params[0].detach().bfloat16())   # compute copy refreshed by the kernel
+
+
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("N", [2048, 96, 4096])
+def test_fused_add_norm(rms, N):
+    from pytorch_distributedtraining_amd.ops.norms import add_norm
+    x = torch.randn(300, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(300, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_()
+    b = None if rms else (0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_()
+    y, s = add_norm(x, r, w, b, 1e-5, rms=rms)
+    dy, ds = torch.randn_like(y), torch.randn_like(s)
+    torch.autograd.backward([y, s], [dy, ds])
+    xr, rr, wr = (t.detach().float().requires_grad_() for t in (x, r, w))
+    br = None if rms else b.detach().float().requires_grad_()
+    sr = xr + rr
+    if rms:
+        yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = F.layer_norm(sr, (N,), wr, br, 1e-5)
+    torch.autograd.backward([yr, sr], [dy.float(), ds.float()])
+    assert rel_err(s, sr) < 1e-2 and rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(r.grad, rr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    if not rms:
+        assert rel_err(b.grad, br.grad) < 2e-2
+
+
+def test_llama_tiny_fsdp_step():
+    from pytorch_distributedtraining_amd.models.llama import build_llama
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel import FullyShardedDataParallel
+    torch.manual_seed(0)
+    ref = build_llama("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1)      # head_dim 128, GQA 2:1
+    sd = {k: v.clone() for k, v in ref.state_dict().items()}
+    x = torch.randint(0, 1024, (2, 129))
+    lref = ref(x[:, :-1], labels=x[:, 1:])
+    m = build_llama("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1)
+    m.load_state_dict(sd)
+    m = FullyShardedDataParallel(m, device=DEV, keep_low_precision_grads=True)
+    opt = FusedAdamW(m.flat_parameters(), lr=1e-3)
+    xd = x.to(DEV)
+    l0 = m(xd[:, :-1], labels=xd[:, 1:])
+    assert abs(l0.item() - lref.item()) < 3e-2 * lref.item()
+    for _ in range(3):
+        loss = m(xd[:, :-1], labels=xd[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    assert loss.item() < l0.item()
+
+
+def test_linear_colsum_bias_grad():
+    from pytorch_distributedtraining_amd.ops.linear import linear
+    x = torch.randn(4, 100, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (0.05 * torch.randn(512, 256, device=DEV)).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = linear(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    F.linear(xr, wr, br).backward(dy.float())
+    assert rel_err(x.grad, xr.grad) < 1e-2 and rel_err(w.grad, wr.grad) < 1e-2 and rel_err(b.grad, br.grad) < 1e-2
