@@ -21,6 +21,7 @@
 // Used by the GPT-2 / Llama models (BASELINE.json configs 3-5; SURVEY.md K16 "flash attention
 // (causal, head_dim 64/128)").
 #include "common.h"
+#include <stdlib.h>
 
 using namespace pdt;
 
@@ -197,6 +198,159 @@ __global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
     }
     const int k0 = t * TILE;
     if (CAUSAL && k0 > qw + 31 + off) continue;  // every key of the tile is in this wave's future
+
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[kt] = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s[kt]);
+    }
+    const bool need_mask = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = s[kt][r] * sl2;
+        if (need_mask) {
+          const int key = k0 + kt * 32 + acc_row(r, h);
+          if (key >= p.Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
+        }
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float msub = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = fast_exp2(m - msub);
+    float ls = 0.f;
+    u16x8 pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = fast_exp2(s[kt][r] - msub);
+        s[kt][r] = pv;
+        ls += pv;
+      }
+      pf[kt][0] = pack8(s[kt], 0);
+      pf[kt][1] = pack8(s[kt], 1);
+    }
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+          o[dt] = mfma32(IO::tr_frag(Vs, dt, kt * 32 + 16 * ss, lane), pf[kt][ss], o[dt]);
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < p.Sq) {
+    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
+        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
+      }
+    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward v3: K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into a 2-deep LDS ring -- no
+// staging registers, ONE barrier per 64-key tile (the barrier's vmcnt(0) retires the tile this
+// iteration reads; the DMA for tile t+1 is issued right after it and overlaps tile t's MFMAs).
+// The XOR swizzle is applied on the per-lane SOURCE address (the DMA destination is lane-linear,
+// cdna_hip_programming.md §5.4 rule 21); rows past Sk are clamped to a real row and masked.
+// ------------------------------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ int swz_f(int r) {
+  if constexpr (D == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int D>
+__device__ __forceinline__ void dma_tile(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
+                                         int w, int lane) {
+  constexpr int RPI = 1024 / (D * 2);   // rows per wave-instruction (1 KiB per instruction)
+  constexpr int NI = 16 / RPI;          // instructions per wave (each wave fills 16 rows)
+  constexpr int LPR = 64 / RPI;         // lanes per row
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int row = 16 * w + RPI * i + lane / LPR;
+    const int pc = lane % LPR;
+    const int c = pc ^ swz_f<D>(row);
+    int g = row0 + row;
+    g = g < nrows ? g : nrows - 1;
+    const bf16_t* src = base + (int64_t)g * row_stride + c * 8;
+    bf16_t* dst = lds + (16 * w + RPI * i) * D;   // wave-uniform base; lane l lands at +16 B * l
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
+  using IO = TileIO<D>;
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
+    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+  }
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+    }
+  }
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m = -INFINITY, l = 0.f;
+
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();   // vmcnt(0): tile t resident; every wave is done with the buffer refilled below
+    if (t + 1 < ntiles) {
+      bf16_t* nb = smem + ((t + 1) & 1) * 2 * TE;
+      dma_tile<D>(Kp, p.k_ss, (t + 1) * TILE, p.Sk, nb, w, lane);
+      dma_tile<D>(Vp, p.v_ss, (t + 1) * TILE, p.Sk, nb + TE, w, lane);
+    }
+    const bf16_t* Ks = smem + (t & 1) * 2 * TE;
+    const bf16_t* Vs = Ks + TE;
+    const int k0 = t * TILE;
+    if (CAUSAL && k0 > qw + 31 + off) continue;
 
     f32x16 s[2];
 #pragma unroll
@@ -505,10 +659,15 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
 }
 
 template <int D>
-int launch_fwd(const AttnParams& p, int causal, hipStream_t st) {
+int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   dim3 grid((p.Sq + 127) / 128, p.H, p.B);
-  if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
-  else fa_fwd_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  if (variant == 2) {
+    if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
+    else fa_fwd_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else {
+    if (causal) fa_fwd_v3_kernel<D, true><<<grid, NT, 0, st>>>(p);
+    else fa_fwd_v3_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  }
   return (int)hipGetLastError();
 }
 
@@ -542,7 +701,11 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
   p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  return D == 64 ? launch_fwd<64>(p, causal, st) : launch_fwd<128>(p, causal, st);
+  static const int variant = [] {
+    const char* e = getenv("PDT_FA_FWD");
+    return e ? atoi(e) : 3;
+  }();
+  return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
 
 // strides[0..23]: q k v o dout dq dk dv, each (b, s, h).  delta: fp32 workspace of B*H*Sq.
