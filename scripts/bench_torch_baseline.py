@@ -1,0 +1,123 @@
+#!/usr/bin/env python
+"""Stock PyTorch-ROCm baseline for the flagship benchmark ("the comparison baseline is
+stock PyTorch-ROCm DDP / FSDP over RCCL on the same MI355X node").
+
+Same model shape (GPT-2 1.3B: L24, d2048, 16x128 heads, vocab 50304, seq 1024), same per-GPU batch,
+same synthetic data and optimizer settings as ``bench.py``, but built only from stock components:
+nn.Linear / nn.LayerNorm / F.scaled_dot_product_attention / F.gelu / F.cross_entropy,
+torch.distributed.fsdp.FullyShardedDataParallel (FULL_SHARD, bf16 MixedPrecision) and
+torch.optim.AdamW(fused=True) + torch.nn.utils.clip_grad_norm_.  Prints one JSON line like bench.py.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Block(nn.Module):
+    def __init__(self, d, h):
+        super().__init__()
+        self.h = h
+        self.ln_1 = nn.LayerNorm(d)
+        self.c_attn = nn.Linear(d, 3 * d)
+        self.c_proj = nn.Linear(d, d)
+        self.ln_2 = nn.LayerNorm(d)
+        self.c_fc = nn.Linear(d, 4 * d)
+        self.c_proj2 = nn.Linear(4 * d, d)
+
+    def forward(self, x):
+        B, S, C = x.shape
+        q, k, v = self.c_attn(self.ln_1(x)).view(B, S, 3, self.h, C // self.h).permute(2, 0, 3, 1, 4)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, S, C)
+        x = x + self.c_proj(y)
+        return x + self.c_proj2(F.gelu(self.c_fc(self.ln_2(x)), approximate="tanh"))
+
+
+class GPT(nn.Module):
+    def __init__(self, V=50304, S=1024, d=2048, L=24, h=16):
+        super().__init__()
+        self.wte = nn.Embedding(V, d)
+        self.wpe = nn.Embedding(S, d)
+        self.h = nn.ModuleList([Block(d, h) for _ in range(L)])
+        self.ln_f = nn.LayerNorm(d)
+        for p in self.parameters():
+            if p.dim() == 2:
+                nn.init.normal_(p, 0, 0.02)
+
+    def forward(self, idx, labels):
+        x = self.wte(idx) + self.wpe(torch.arange(idx.shape[1], device=idx.device))
+        for b in self.h:
+            x = b(x)
+        logits = F.linear(self.ln_f(x), self.wte.weight)
+        return F.cross_entropy(logits.view(-1, logits.shape[-1]).float(), labels.reshape(-1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--seq", type=int, default=1024)
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(lr)
+    dev = torch.device("cuda", lr)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
+    from torch.distributed.fsdp.wrap import ModuleWrapPolicy
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = GPT(S=a.seq)
+    n = sum(p.numel() for p in model.parameters())
+    model = FSDP(model, sharding_strategy=ShardingStrategy.FULL_SHARD, auto_wrap_policy=ModuleWrapPolicy({Block}),
+                 mixed_precision=MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16), device_id=dev,
+                 use_orig_params=False, limit_all_gathers=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, fused=True)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    batches = [torch.randint(0, 50257, (a.micro_batch, a.seq + 1), device=dev, generator=g) for _ in range(4)]
+
+    def step(i):
+        b = batches[i % 4]
+        loss = model(b[:, :-1], b[:, 1:])
+        loss.backward()
+        model.clip_grad_norm_(1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    tps = world * a.micro_batch * a.seq * a.steps / dt
+    if rank == 0:
+        print(f"[torch-baseline] params={n/1e9:.3f}B loss={loss.item():.4f} step={1000*dt/a.steps:.1f}ms",
+              file=sys.stderr)
+        print(json.dumps({"metric": "tokens/sec GPT-2-1.3B FSDP (whole node) -- stock PyTorch-ROCm baseline",
+                          "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
+                          "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_gpu": a.micro_batch,
+                          "seq_len": a.seq, "stack": "torch FSDP + SDPA + nn.LayerNorm + fused torch AdamW"}))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+"""Infrastructure on CPU: models (param counts / state_dict names), checkpoint envelope helpers,
+launcher failure detection + restarts, fault injection, collective consistency tracer, loaders."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+from dist_utils import run_workers
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_model_parameter_counts():
+    from pytorch_distributedtraining_amd.models.gpt2 import build_gpt2
+    from pytorch_distributedtraining_amd.models.llama import build_llama
+    from pytorch_distributedtraining_amd.models.resnet import resnet18, resnet50
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
+    m = swinir_s_x2()
+    assert sum(p.numel() for p in m.parameters()) == 910_152           # SURVEY.md §2.D (SwinIR-S x2)
+    assert len(list(m.parameters())) == 330
+    assert "layers.0.residual_group.blocks.0.attn.relative_position_bias_table" in m.state_dict()
+    assert abs(sum(p.numel() for p in resnet50().parameters()) - 25.557e6) < 1e4
+    assert abs(sum(p.numel() for p in resnet18().parameters()) - 11.69e6) < 1e4
+    with torch.device("meta"):
+        assert abs(build_gpt2("gpt2-1.3b").num_params() - 1.3137e9) < 1e6
+        assert abs(build_gpt2("gpt2-124m").num_params() - 124.4e6) < 1e6
+        assert abs(build_llama("llama3-8b").num_params() - 8.03e9) < 1e7
+
+
+def test_swinir_and_srnet_shapes():
+    from pytorch_distributedtraining_amd.models.srnet import Net
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
+    x = torch.rand(2, 3, 24, 20)
+    assert swinir_s_x2()(x).shape == (2, 3, 48, 40)          # non-multiple-of-window input is padded
+    assert Net(upscale_factor=2)(x).shape == (2, 3, 48, 40)
+
+
+def test_llama_meta_checkpoint_conversion():
+    from pytorch_distributedtraining_amd.models.llama import build_llama, convert_meta_state_dict
+    m = build_llama("llama3-tiny")
+    sd = m.state_dict()
+    meta = {}
+    h, hkv, d = 2, 1, 128
+    for k, v in sd.items():
+        if k.endswith("attention.wqkv.weight"):
+            meta[k.replace("wqkv", "wq")] = v[: h * d]
+            meta[k.replace("wqkv", "wk")] = v[h * d: (h + hkv) * d]
+            meta[k.replace("wqkv", "wv")] = v[(h + hkv) * d:]
+        elif k.endswith("feed_forward.w13.weight"):
+            f = v.shape[0] // 2
+            meta[k.replace("w13", "w1")] = v[:f]
+            meta[k.replace("w13", "w3")] = v[f:]
+        else:
+            meta[k] = v
+    back = convert_meta_state_dict(meta, m.config)
+    assert set(back) == set(sd)
+    for k in sd:
+        assert torch.equal(back[k], sd[k])
+
+
+def test_metrics_and_perceptual_loss():
+    from pytorch_distributedtraining_amd.models import metrics
+    from pytorch_distributedtraining_amd.models.losses import feat_loss
+    a = torch.rand(2, 3, 16, 16)
+    assert metrics.mae(a, a) == 0.0 and metrics.psnr(a, a) == float("inf")
+    b = (a + 0.1).clamp(0, 1)
+    assert 15 < metrics.psnr(a, b) < 30
+    l0 = feat_loss(a, a)
+    l1 = feat_loss(b, a)
+    assert float(l0) == 0.0 and float(l1) > 0
+
+
+def test_launcher_success_and_failure_detection(tmp_path):
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os, sys\nsys.exit(0 if os.environ['WORLD_SIZE']=='2' else 3)\n")
+    r = subprocess.run([sys.executable, "-m", "pytorch_distributedtraining_amd.launch", "--nproc-per-node", "2",
+                        str(ok)], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    bad = tmp_path / "bad.py"
+    bad.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ['RANK'] == '1':
+            sys.exit(7)
+        time.sleep(60)                   # the survivor must be torn down by the launcher, not hang
+    """))
+    counter = tmp_path / "restarts"
+    r = subprocess.run([sys.executable, "-m", "pytorch_distributedtraining_amd.launch", "--nproc-per-node", "2",
+                        "--max-restarts", "1", "--grace-s", "1", str(bad)], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 7
+    assert "restarting group (1/1)" in r.stderr
+
+
+def test_parse_local_rank_both_spellings(monkeypatch):
+    from pytorch_distributedtraining_amd.launch import parse_local_rank
+    assert parse_local_rank(["--local-rank", "3"]) == 3
+    assert parse_local_rank(["--local_rank=2"]) == 2
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert parse_local_rank([]) == 5
+    monkeypatch.setenv("LOCAL_RANK", "None")       # the reference's failure mode (Stoke-DDP.py:153)
+    assert parse_local_rank([]) == 0
+
+
+def test_fault_injection_raise(monkeypatch):
+    from pytorch_distributedtraining_amd.utils.fault import InjectedFault, maybe_inject_fault
+    monkeypatch.setenv("PDT_FAULT_RANK", "0")
+    monkeypatch.setenv("PDT_FAULT_STEP", "3")
+    monkeypatch.setenv("PDT_FAULT_MODE", "raise")
+    maybe_inject_fault(2)
+    with pytest.raises(InjectedFault):
+        maybe_inject_fault(3)
+
+
+def _w_consistency(rank, world, diverge):
+    from pytorch_distributedtraining_amd.parallel.comm import Comm
+    c = Comm(debug=True)
+    t = torch.ones(4)
+    c.all_reduce(t)
+    if diverge and rank == 1:
+        c._trace("all_reduce:sum", torch.ones(8))     # pretend rank 1 issued a different collective
+    else:
+        c._trace("all_reduce:sum", torch.ones(4))
+    try:
+        c.verify_consistency("step 0")
+        return "ok"
+    except RuntimeError as e:
+        return "mismatch" if "collective mismatch" in str(e) else repr(e)
+
+
+def test_collective_consistency_checker():
+    assert run_workers(_w_consistency, 2, False) == ["ok", "ok"]
+    assert run_workers(_w_consistency, 2, True) == ["mismatch", "mismatch"]
+
+
+def test_checkpoint_latest_and_atomic(tmp_path):
+    from pytorch_distributedtraining_amd.utils import checkpoint as ckpt
+    for step in (4, 12, 8):
+        ckpt.save_checkpoint(str(tmp_path), "run", model_state={"w": torch.ones(2)}, backward_step=step)
+    (tmp_path / "stoke-run-backward-step-99.pt.tmp").write_text("partial")
+    assert ckpt.latest_checkpoint(str(tmp_path)) == "stoke-run-backward-step-12"
+    p = ckpt.load_checkpoint(str(tmp_path), "stoke-run-backward-step-12")
+    assert p["backward_step"] == 12 and torch.equal(p["model_state_dict"]["w"], torch.ones(2))
+
+
+def test_device_loader_cpu_passthrough():
+    from pytorch_distributedtraining_amd.data import DeviceDataLoader, SyntheticTokenDataset
+    dl = DeviceDataLoader(SyntheticTokenDataset(n=10, seq_len=16, vocab=100), batch_size=4, device="cpu")
+    x, y = next(iter(dl))
+    assert x.shape == (4, 16) and torch.equal(x[:, 1:], y[:, :-1])
+    assert len(dl) == 3
