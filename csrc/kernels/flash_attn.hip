@@ -421,6 +421,179 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// forward v4 = v3's LDS-DMA ring + a VALU-lean tile body.  Per 64-key tile a wave issues 32 MFMAs
+// (1024 MFMA cycles); v3 spent ~3x that on VALU (address math, zero-fills, scale, rescale, masks).
+// v4: (1) every LDS fragment address is a per-lane base computed ONCE (the swizzle depends only on
+// row & 15, which tile/k-block steps never change) plus a compile-time immediate -- the loop is
+// unrolled by the 2-deep ring so the buffer offset is an immediate too; (2) the softmax scale is
+// folded into one FMA feeding v_exp (max taken on raw scores); (3) the O rescale is skipped when no
+// lane's running max moved; (4) the causal mask is one compare+select per element and only on
+// diagonal tiles.
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+struct FwdV4 {
+  static constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+
+  __device__ __forceinline__ static void tile(const bf16_t* __restrict__ lds, const int (&koff)[KS],
+                                              const int (&voff)[DT][2], const u16x8 (&qf)[KS], f32x16 (&o)[DT],
+                                              float& m, float& l, float sl2, int k0, bool diag, int lim) {
+    f32x16 s0, s1;
+    {
+      const f32x16 z = zero16();
+      s0 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[0]), qf[0], z);
+      s1 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[0] + 32 * D), qf[0], z);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) {
+        s0 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[ks]), qf[ks], s0);
+        s1 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[ks] + 32 * D), qf[ks], s1);
+      }
+    }
+    if (diag) {   // keys k0 + kt*32 + acc_row(r, h) > lim are masked (future / past Sk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        s0[r] = (k0 + rr > lim) ? -INFINITY : s0[r];
+        s1[r] = (k0 + 32 + rr > lim) ? -INFINITY : s1[r];
+      }
+    }
+    float mx = fmaxf(s0[0], s1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+    const float mn = fmaxf(m, mx);
+    const float msub = (mn == -INFINITY) ? 0.f : mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = fast_exp2(fmaf(s0[r], sl2, -msub));
+      s1[r] = fast_exp2(fmaf(s1[r], sl2, -msub));
+      ls += s0[r] + s1[r];
+    }
+    u16x8 pf[2][2];
+    pf[0][0] = pack8(s0, 0); pf[0][1] = pack8(s0, 1);
+    pf[1][0] = pack8(s1, 0); pf[1][1] = pack8(s1, 1);
+    if (!__all(mn == m)) {
+      const float alpha = fast_exp2(m - msub);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      l *= alpha;
+      m = mn;
+    }
+    l += ls;
+    const bf16_t* vs = lds + TE;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int kb = kt * 32 + 16 * ss;
+          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][0] + kb * D));
+          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][1] + kb * D));
+          const u16x8 fr = __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[dt] = mfma32(fr, pf[kt][ss], o[dt]);
+        }
+    }
+  }
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
+  using K = FwdV4<D, CAUSAL>;
+  constexpr int KS = K::KS, DT = K::DT, TE = K::TE;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
+    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+  }
+
+  // per-lane LDS element offsets (swizzle depends on row & 15 only)
+  int koff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int voff[DT][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int r1 = 4 * (g >> 1) + q;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
+      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
+    }
+  }
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+    }
+  }
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m = -INFINITY, l = 0.f;
+  // keys > lim are masked for this lane's query row; a tile needs masking if its last key > qw + off
+  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  for (int t = 0; t < ntiles; t += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tt = t + u;
+      if (tt < ntiles) {
+        __syncthreads();
+        if (tt + 1 < ntiles) {
+          bf16_t* nb = smem + (1 - u) * 2 * TE;
+          dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
+          dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
+        }
+        const int k0 = tt * TILE;
+        if (!(CAUSAL && k0 > qw + 31 + off)) {
+          const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+          K::tile(smem + u * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
+        }
+      }
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < p.Sq) {
+    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
+        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
+      }
+    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // backward (a): delta[b, h, q] = sum_d dO * O
 // ------------------------------------------------------------------------------------------------
 template <int D>
@@ -664,6 +837,9 @@ int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   if (variant == 2) {
     if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else if (variant == 4) {
+    if (causal) fa_fwd_v4_kernel<D, true><<<grid, NT, 0, st>>>(p);
+    else fa_fwd_v4_kernel<D, false><<<grid, NT, 0, st>>>(p);
   } else {
     if (causal) fa_fwd_v3_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v3_kernel<D, false><<<grid, NT, 0, st>>>(p);
@@ -703,7 +879,7 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
   static const int variant = [] {
     const char* e = getenv("PDT_FA_FWD");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 4;
   }();
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
