@@ -831,6 +831,277 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// backward v2 (dK/dV and dQ): same recipe as forward v4 -- LDS-DMA double-buffered operand tiles
+// (one barrier per tile), per-lane LDS bases + immediates (no per-read address math), scale folded
+// into an FMA ahead of v_exp, and compare/select masks only on boundary sub-tiles.  LSE and delta
+// rows travel by LDS-DMA too (4-byte pieces), so no ordinary global load sits in the loop to force
+// a vmcnt(0) drain of the prefetch.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dma_f32_row(const float* src, int row0, int nrows, float* lds, int lane) {
+  int g = row0 + lane;
+  g = g < nrows ? g : nrows - 1;
+  __builtin_amdgcn_global_load_lds((const void*)(src + g), (lds_void*)lds, 4, 0, 0);
+}
+
+// transposed-fragment offsets for a [TILE][D] swizzled image (rows kb + 4(g>>1) + q (+8), column
+// 32dt + 16(g&1) + 4p); kb must be a multiple of 16 and is added as an immediate by the caller.
+template <int D>
+__device__ __forceinline__ void tr_offsets(int lane, int (&toff)[D / 32][2]) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int r1 = 4 * (g >> 1) + q;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+    const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+    toff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
+    toff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
+  }
+}
+
+__device__ __forceinline__ u16x8 tr_pair(const bf16_t* p0, const bf16_t* p1) {
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)p0);
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)p1);
+  return __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT) void fa_bwd_dkdv_v2_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  // [buf][Q | dO] + [buf][lse | delta]
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];
+  __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x;
+  const int group = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int kw = kb * 128 + w * 32, key = kw + c32;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  u16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (key < p.Sk) {
+      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
+      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
+    }
+  }
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+
+  const int qstart = CAUSAL ? max(0, kb * 128 - off) / TILE * TILE : 0;
+  const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
+  const int total = qtiles * group;
+
+  auto issue = [&](int it, int buf) {
+    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
+    const int hq = hk * group + hi;
+    const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+    const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+    bf16_t* base = smem + buf * 2 * TE;
+    dma_tile<D>(Qp, p.q_ss, q0, p.Sq, base, w, lane);
+    dma_tile<D>(Gp, p.do_ss, q0, p.Sq, base + TE, w, lane);
+    if (w == 0) dma_f32_row(p.lse + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][0], lane);
+    if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][1], lane);
+  };
+  if (total > 0) issue(0, 0);
+
+  for (int it = 0; it < total; it += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int cur = it + u;
+      if (cur >= total) break;
+      __syncthreads();
+      if (cur + 1 < total) issue(cur + 1, 1 - u);
+      const int q0 = qstart + (cur % qtiles) * TILE;
+      const bf16_t* Qs = smem + u * 2 * TE;
+      const bf16_t* Gs = Qs + TE;
+      const float* Ls = sstat[u][0];
+      const float* Ds = sstat[u][1];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qb0 = q0 + qs * 32;
+        if (CAUSAL && qb0 + 31 + off < kw) continue;      // every query precedes these keys
+        f32x16 s, dp;
+        {
+          const f32x16 z = zero16();
+          s = mfma32(*reinterpret_cast<const u16x8*>(Qs + roff[0] + qs * 32 * D), kf[0], z);
+          dp = mfma32(*reinterpret_cast<const u16x8*>(Gs + roff[0] + qs * 32 * D), vf[0], z);
+#pragma unroll
+          for (int ks = 1; ks < KS; ++ks) {
+            s = mfma32(*reinterpret_cast<const u16x8*>(Qs + roff[ks] + qs * 32 * D), kf[ks], s);
+            dp = mfma32(*reinterpret_cast<const u16x8*>(Gs + roff[ks] + qs * 32 * D), vf[ks], dp);
+          }
+        }
+        // rows of S = queries qb0 + rr + 4h (registers), columns = keys (lanes)
+        const int tmask = CAUSAL ? key - off - qb0 - 4 * h : -1;   // masked if rr < tmask
+        const int tsq = p.Sq - qb0 - 4 * h;                          // masked if rr >= tsq
+        const bool edge = (CAUSAL && kw + 31 > qb0 + off) || (qb0 + 32 > p.Sq);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + qs * 32 + 8 * g + 4 * h);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(Ds + qs * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i, rr = i + 8 * g;
+            float pv = fast_exp2(fmaf(s[r], sl2, -l4[i] * LOG2E));
+            if (edge) pv = (rr < tmask || rr >= tsq) ? 0.f : pv;
+            s[r] = pv;
+            dp[r] = pv * (dp[r] - d4[i]);
+          }
+        }
+        const u16x8 pf0 = pack8(s, 0), pf1 = pack8(s, 1);
+        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma32(tr_pair(Gs + toff[dt][0] + qs * 32 * D, Gs + toff[dt][1] + qs * 32 * D), pf0, dv[dt]);
+          dv[dt] = mfma32(tr_pair(Gs + toff[dt][0] + (qs * 32 + 16) * D, Gs + toff[dt][1] + (qs * 32 + 16) * D),
+                          pf1, dv[dt]);
+          dk[dt] = mfma32(tr_pair(Qs + toff[dt][0] + qs * 32 * D, Qs + toff[dt][1] + qs * 32 * D), df0, dk[dt]);
+          dk[dt] = mfma32(tr_pair(Qs + toff[dt][0] + (qs * 32 + 16) * D, Qs + toff[dt][1] + (qs * 32 + 16) * D),
+                          df1, dk[dt]);
+        }
+      }
+    }
+  }
+  if (key < p.Sk) {
+    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
+    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 a, c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
+        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
+        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
+      }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT) void fa_bwd_dq_v2_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
+    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+  }
+  u16x8 qf[KS], gf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) {
+      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
+    }
+  }
+  const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
+  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  for (int t = 0; t < ntiles; t += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tt = t + u;
+      if (tt >= ntiles) break;
+      __syncthreads();
+      if (tt + 1 < ntiles) {
+        bf16_t* nb = smem + (1 - u) * 2 * TE;
+        dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
+        dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
+      }
+      const bf16_t* Ks = smem + u * 2 * TE;
+      const bf16_t* Vs = Ks + TE;
+      const int k0 = tt * TILE;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int kb0 = k0 + kt * 32;
+        if (CAUSAL && kb0 > qw + 31 + off) continue;
+        f32x16 s, dp;
+        {
+          const f32x16 z = zero16();
+          s = mfma32(*reinterpret_cast<const u16x8*>(Ks + roff[0] + kt * 32 * D), qf[0], z);
+          dp = mfma32(*reinterpret_cast<const u16x8*>(Vs + roff[0] + kt * 32 * D), gf[0], z);
+#pragma unroll
+          for (int ks = 1; ks < KS; ++ks) {
+            s = mfma32(*reinterpret_cast<const u16x8*>(Ks + roff[ks] + kt * 32 * D), qf[ks], s);
+            dp = mfma32(*reinterpret_cast<const u16x8*>(Vs + roff[ks] + kt * 32 * D), gf[ks], dp);
+          }
+        }
+        const bool edge = (kb0 + 32 > p.Sk) || (CAUSAL && kb0 + 31 > qw + off);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = (r & 3) + 8 * (r >> 2);
+          float pv = fast_exp2(fmaf(s[r], sl2, nlse2));
+          if (edge) pv = (kb0 + rr > lim) ? 0.f : pv;
+          dp[r] = pv * (dp[r] - dl);
+        }
+        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dq[dt] = mfma32(tr_pair(Ks + toff[dt][0] + kt * 32 * D, Ks + toff[dt][1] + kt * 32 * D), df0, dq[dt]);
+          dq[dt] = mfma32(tr_pair(Ks + toff[dt][0] + (kt * 32 + 16) * D, Ks + toff[dt][1] + (kt * 32 + 16) * D),
+                          df1, dq[dt]);
+        }
+      }
+    }
+  }
+  if (qrow < p.Sq) {
+    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
+        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
+      }
+  }
+}
+
 template <int D>
 int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   dim3 grid((p.Sq + 127) / 128, p.H, p.B);
@@ -853,12 +1124,26 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   fa_bwd_delta_kernel<D><<<(rows + NT - 1) / NT, NT, 0, st>>>(p);
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
-  if (causal) {
-    fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(p);
-    fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(p);
+  static const int variant = [] {
+    const char* e = getenv("PDT_FA_BWD");
+    return e ? atoi(e) : 2;
+  }();
+  if (variant == 1) {
+    if (causal) {
+      fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
   } else {
-    fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(p);
-    fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    if (causal) {
+      fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
   }
   return (int)hipGetLastError();
 }

@@ -94,11 +94,11 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
   }
 }
 
-// Backward: one wave per row, the row's x/dy held in registers as raw 16-byte vectors; dgamma/dbeta
-// are accumulated for the whole workgroup in LDS (ds_add_f32, distinct columns per lane) and written
-// as ONE partial row per workgroup (4x fewer partials than per-wave rows, and no per-lane accumulator
-// arrays: 8 waves/CU fit at N=2048 and N=8192 no longer spills).  Optional ``dres``: the gradient of
-// the fused residual sum, added into dx in the same pass.
+// Backward: one wave per row.  Pass 1 reads x, dy, w and forms the two row reductions while the
+// lane's dgamma/dbeta contributions accumulate in REGISTERS (ITERS*16 floats); pass 2 re-reads the
+// (L1/L2-resident) row to write dx (+ the fused residual gradient).  At the end the 4 waves of a
+// workgroup fold their accumulators through one [2][N] LDS buffer (wave-by-wave, so no LDS atomics)
+// and the workgroup writes ONE partial row; a 2-level column reduce finishes dgamma/dbeta.
 template <typename T, typename W, int ITERS, bool RMS>
 __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const W* __restrict__ w, const float* __restrict__ mean_in,
@@ -106,12 +106,14 @@ __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, 
                                                       T* __restrict__ dx, float* __restrict__ dw_part,
                                                       float* __restrict__ db_part, int rows, int N) {
   extern __shared__ __attribute__((aligned(16))) float sacc[];   // [2][N]
-  float* sdw = sacc;
-  float* sdb = sacc + N;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float invN = 1.f / (float)N;
-  for (int i = threadIdx.x; i < 2 * N; i += NT) sacc[i] = 0.f;
-  __syncthreads();
+  float dwa[ITERS][8], dba[ITERS][8];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; }
+
   for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
     const T* xr = x + (int64_t)row * N;
     const T* gr = dy + (int64_t)row * N;
@@ -132,24 +134,25 @@ __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, 
           const float g = dv[k] * wv[k];
           a += g * xh;
           bsum += g;
-          atomicAdd(&sdw[col + k], dv[k] * xh);
-          if (!RMS) atomicAdd(&sdb[col + k], dv[k]);
+          dwa[it][k] += dv[k] * xh;
+          dba[it][k] += dv[k];
         }
       }
     }
     a = wave_sum(a) * invN;
-    bsum = RMS ? 0.f : wave_sum(bsum) * invN;
+    if (!RMS) bsum = wave_sum(bsum) * invN;
     T* dxr = dx + (int64_t)row * N;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int col = it * 512 + lane * 8;
       if (col < N) {
         float xv[8], dv[8], wv[8], o[8];
-        Vec8<T>::load(xr + col, xv);   // L1/L2-resident re-read (keeps VGPRs low)
+        Vec8<T>::load(xr + col, xv);
         Vec8<T>::load(gr + col, dv);
         Vec8<W>::load(w + col, wv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[k] * wv[k] - bsum - (xv[k] - mean) * rstd * a);
+        for (int k = 0; k < 8; ++k)
+          o[k] = rstd * (dv[k] * wv[k] - (RMS ? 0.f : bsum) - (xv[k] - mean) * rstd * a);
         if (dres != nullptr) {
           float r8[8];
           Vec8<T>::load(dres + (int64_t)row * N + col, r8);
@@ -160,7 +163,26 @@ __global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, 
       }
     }
   }
-  __syncthreads();
+  // fold the 4 waves' accumulators: wave 0 stores, waves 1..3 add in turn (no atomics)
+  float* sdw = sacc;
+  float* sdb = sacc + N;
+#pragma unroll
+  for (int turn = 0; turn < RPB; ++turn) {
+    if (wid == turn) {
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int col = it * 512 + lane * 8;
+        if (col < N) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (turn == 0) { sdw[col + k] = dwa[it][k]; sdb[col + k] = dba[it][k]; }
+            else { sdw[col + k] += dwa[it][k]; sdb[col + k] += dba[it][k]; }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
   for (int c = threadIdx.x * 4; c < N; c += NT * 4) {
     *reinterpret_cast<f32x4*>(dw_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdw + c);
     if (db_part) *reinterpret_cast<f32x4*>(db_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdb + c);
@@ -313,7 +335,7 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
 
 // fast path: one partial row per workgroup (LDS-accumulated); fallback: one per block
 int bwd_partial_rows(int rows, int N) {
-  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, 512);
+  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, N <= 4096 ? 512 : 256);
   return grid_for(rows, 1, 512);
 }
 
