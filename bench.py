@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Flagship benchmark: GPT-2 1.3B, FSDP full-shard, bf16, fused AdamW + global grad-norm clipping,
-synthetic tokens (random-init weights), seq 1024, 8 sequences per GPU (weak scaling).
+synthetic tokens (random-init weights), seq 1024, 16 sequences per GPU (weak scaling; the MI355X's
+288 GB let the per-GPU batch grow -- larger GEMMs and the optimizer step amortised over 2x tokens).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gpt2-fsdp|gpt2-ddp|resnet50-ddp]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -24,7 +25,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp"])
+    ap.add_argument("--workload", default="gpt2-fsdp",
+                    choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp", "llama3-fsdp"])
     ap.add_argument("--model", default=None)
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--seq", type=int, default=1024)
@@ -58,7 +60,7 @@ def main():
     comm = Comm()
 
     torch.manual_seed(1234)
-    if args.workload.startswith("gpt2"):
+    if args.workload.startswith("gpt2") or args.workload.startswith("llama"):
         result = bench_gpt2(args, comm, dev, world, rank)
     else:
         result = bench_resnet(args, comm, dev, world, rank)
@@ -98,12 +100,17 @@ def bench_gpt2(args, comm, dev, world, rank):
     from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
     from pytorch_distributedtraining_amd.parallel import FullyShardedDataParallel, MixedPrecision, ShardingStrategy
 
-    fsdp = args.workload == "gpt2-fsdp"
-    name = args.model or ("gpt2-1.3b" if fsdp else "gpt2-124m")
-    mb = args.micro_batch or 8
+    fsdp = args.workload in ("gpt2-fsdp", "llama3-fsdp")
+    llama = args.workload.startswith("llama")
+    name = args.model or ("llama3-8b" if llama else "gpt2-1.3b" if fsdp else "gpt2-124m")
+    mb = args.micro_batch or (8 if llama else 16)
     S = args.seq
     with torch.device(dev):
-        model = build_gpt2(name, n_positions=max(1024, S), activation_checkpointing=bool(args.act_ckpt))
+        if llama:
+            from pytorch_distributedtraining_amd.models.llama import build_llama
+            model = build_llama(name, max_seq_len=max(S, 2048), activation_checkpointing=bool(args.act_ckpt or 1))
+        else:
+            model = build_gpt2(name, n_positions=max(1024, S), activation_checkpointing=bool(args.act_ckpt))
     nparams = model.num_params()
     flops_tok = model.flops_per_token(S)
     if fsdp:
@@ -120,10 +127,10 @@ def bench_gpt2(args, comm, dev, world, rank):
         sharded = False
         par = f"dp{world}"
     opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
-    V = model.module.config.vocab_size if hasattr(model, "module") else model.config.vocab_size
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
-    batches = [torch.randint(0, 50257, (mb, S + 1), device=dev, generator=g) for _ in range(4)]
+    vocab = 128000 if llama else 50257
+    batches = [torch.randint(0, vocab, (mb, S + 1), device=dev, generator=g) for _ in range(4)]
     state = {"i": 0, "loss": None}
 
     def step():
@@ -143,6 +150,8 @@ def bench_gpt2(args, comm, dev, world, rank):
         f"step={1000*dt/args.steps:.1f}ms MFU(bf16 2.5PF/GPU)={tps*flops_tok/world/2.5e15*100:.1f}%")
     metric = "tokens/sec GPT-2-1.3B FSDP (whole node)" if fsdp and name == "gpt2-1.3b" else \
         f"tokens/sec {name} {'FSDP' if fsdp else 'DDP'} (whole node)"
+    if llama:
+        metric = f"tokens/sec {name} FSDP + act-ckpt (whole node)"
     return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

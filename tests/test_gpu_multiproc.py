@@ -1,0 +1,87 @@
+"""Multi-process rehearsal of the sharded engines on ONE MI355X: 2 ranks share cuda:0 and talk over gloo
+(RCCL needs distinct devices).  This exercises the GPU code paths of FSDP / DDP / ZeRO at world_size 2
+(flat shards, all-gather prefetch, reduce-scatter of HIP-kernel gradients, fused AdamW on shards) and
+checks them against world_size 1 -- the 8-GPU RCCL run differs only in the transport."""
+import pytest
+import torch
+
+from dist_utils import run_workers
+
+pytestmark = pytest.mark.gpu
+
+
+def _train_fsdp(rank, world, steps, strategy):
+    import torch.distributed as dist
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel import Comm, FullyShardedDataParallel
+    from pytorch_distributedtraining_amd.parallel.fsdp import ShardingStrategy
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    with torch.device(dev):
+        m = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2)
+    comm = Comm()
+    f = FullyShardedDataParallel(m, comm=comm, device=dev, keep_low_precision_grads=True,
+                                 sharding_strategy=ShardingStrategy(strategy))
+    opt = FusedAdamW(f.flat_parameters(), lr=1e-3)
+    losses = []
+    for s in range(steps):
+        g = torch.Generator().manual_seed(s)
+        x = torch.randint(0, 512, (4, 129), generator=g).to(dev)
+        n = x.shape[0] // world
+        xs = x[rank * n:(rank + 1) * n]
+        loss = f(xs[:, :-1], labels=xs[:, 1:])
+        loss.backward()
+        _, coef, _ = clip_grad_norm_(f.flat_parameters(), 1.0, comm=comm, sharded=True, apply=False)
+        opt.step(grad_scale=coef)
+        opt.zero_grad()
+        t = loss.detach().reshape(1).clone()
+        comm.all_reduce(t, "avg")
+        losses.append(float(t.item()))
+    sd = {k: v.float().cpu() for k, v in f.state_dict().items()}
+    return losses, sd
+
+
+@pytest.mark.parametrize("strategy", ["full_shard", "shard_grad_op"])
+def test_fsdp_two_ranks_on_one_gpu_matches_one_rank(strategy):
+    (l1, sd1), = run_workers(_train_fsdp, 1, 3, strategy)
+    (l2, sd2), (l2b, _) = run_workers(_train_fsdp, 2, 3, strategy)
+    assert l2 == l2b
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 2e-2 * abs(a)
+    for k in sd1:
+        assert torch.allclose(sd1[k], sd2[k], atol=3e-3, rtol=3e-2), k
+
+
+def _train_ddp(rank, world, steps):
+    from pytorch_distributedtraining_amd.models.resnet import resnet18
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel import Comm
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributedtraining_amd.parallel.syncbn import convert_sync_batchnorm
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    comm = Comm()
+    m = convert_sync_batchnorm(resnet18(num_classes=10), comm).to(dev).to(memory_format=torch.channels_last)
+    ddp = DistributedDataParallel(m, comm=comm)
+    opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-3)
+    for s in range(steps):
+        g = torch.Generator().manual_seed(s)
+        x = torch.randn(8, 3, 32, 32, generator=g).to(dev).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (8,), generator=g).to(dev)
+        n = 8 // world
+        loss = torch.nn.functional.cross_entropy(ddp(x[rank * n:(rank + 1) * n]), y[rank * n:(rank + 1) * n])
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    return {k: v.float().cpu() for k, v in m.state_dict().items()}
+
+
+def test_ddp_syncbn_resnet_two_ranks_on_one_gpu():
+    (s1,) = run_workers(_train_ddp, 1, 2)
+    s2a, s2b = run_workers(_train_ddp, 2, 2)
+    for k in s1:
+        assert torch.equal(s2a[k], s2b[k]), k
+        assert torch.allclose(s1[k], s2a[k], atol=2e-3, rtol=1e-2), k
