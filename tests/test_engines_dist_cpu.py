@@ -178,3 +178,47 @@ def test_syncbn_matches_full_batch_bn():
         assert torch.allclose(rm, bn.running_mean, atol=1e-6)
         assert torch.allclose(rv, bn.running_var, atol=1e-5)
     assert torch.allclose(outs[0][4] + outs[1][4], bn.weight.grad, atol=1e-5)
+
+
+def _w_sharded_save(rank, world, path):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.fsdp import FullyShardedDataParallel, MixedPrecision
+    from pytorch_distributedtraining_amd.utils.sharded_checkpoint import save_sharded
+    m = _model()
+    f = FullyShardedDataParallel(m, wrap_classes=(nn.Linear,), mixed_precision=MixedPrecision(torch.float32,
+                                 torch.float32), device="cpu")
+    opt = FusedAdamW(f.parameters(), lr=1e-2)
+    x, y = _data(0, world)
+    nn.functional.mse_loss(f(_shard(x, rank, world)), _shard(y, rank, world)).backward()
+    opt.step()
+    save_sharded(path, "ck", f, opt, extras={"step": 1})
+    return f.state_dict(), f.full_optim_state_dict(opt)
+
+
+def _w_sharded_load(rank, world, path):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.fsdp import FullyShardedDataParallel, MixedPrecision
+    from pytorch_distributedtraining_amd.utils.sharded_checkpoint import load_sharded
+    m = _model(seed=123)
+    f = FullyShardedDataParallel(m, wrap_classes=(nn.Linear,), mixed_precision=MixedPrecision(torch.float32,
+                                 torch.float32), device="cpu")
+    opt = FusedAdamW(f.parameters(), lr=1e-2)
+    extras = load_sharded(path, "ck", f, opt)
+    return f.state_dict(), f.full_optim_state_dict(opt), extras
+
+
+def test_sharded_checkpoint_resharding(tmp_path):
+    """save on 2 ranks -> load on 1 rank and on 2 ranks -> identical model + optimizer state."""
+    from pytorch_distributedtraining_amd.utils.sharded_checkpoint import consolidate_to_full
+    (sd, osd), _ = run_workers(_w_sharded_save, 2, str(tmp_path))
+    for world in (1, 2):
+        (sd2, osd2, extras) = run_workers(_w_sharded_load, world, str(tmp_path))[0]
+        assert extras == {"step": 1}
+        for k in sd:
+            assert torch.equal(sd[k], sd2[k]), k
+        for i in osd["state"]:
+            assert torch.equal(osd["state"][i]["exp_avg"], osd2["state"][i]["exp_avg"])
+    full, fo = consolidate_to_full(str(tmp_path), "ck")
+    for k in sd:
+        assert torch.equal(full[k], sd[k])
+    assert torch.equal(fo["state"][0]["exp_avg_sq"], osd["state"][0]["exp_avg_sq"])
