@@ -41,6 +41,15 @@ __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f
                                                  0, 0, 0);
 }
 
+// Accumulate into an AGPR-resident tile.  Used for long-lived accumulators that only MFMAs touch until
+// the epilogue (dK/dV, dQ): the file is built with the MFMA VGPR form, which would otherwise put them in
+// the 256 arch VGPRs next to the softmax tiles and leave no room for operand prefetch.  Callers must run
+// acc_fence() before VALU reads the tile (the hazard recognizer does not see through inline asm).
+__device__ __forceinline__ void mfma32_acc(f32x16& acc, const u16x8& a, const u16x8& b) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -616,6 +625,7 @@ __global__ __launch_bounds__(NT) void fa_bwd_delta_kernel(AttnParams p) {
     for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
   }
   p.delta[idx] = acc;
+  p.delta[total + idx] = -p.lse[idx] * LOG2E;   // log2-domain lse for the v3 dK/dV kernel
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1102,6 +1112,373 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_v2_kernel(AttnParams p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// backward v3: same data flow as v2, re-shaped for intra-wave MFMA/VALU overlap.  Each 64-row tile is
+// one straight-line region: BOTH 32-row subtiles' S / dP chains are issued first, then the softmax-
+// gradient VALU work of subtile 0 runs under the MFMAs of subtile 1's chains and subtile 0's dK/dV
+// (dQ) updates, and so on -- independent work the scheduler can interleave even at one wave per SIMD.
+// Masking is resolved per tile (wave-uniform EDGE template switch) instead of per 32-row subtile, so
+// the common interior tile has no branches at all.  The file is built with the MFMA VGPR form
+// (-mllvm -amdgpu-mfma-vgpr-form): accumulators the VALU post-processes stay in arch VGPRs instead of
+// being shuttled through AGPRs with v_accvgpr_read/write.
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+struct BwdKVTile {
+  static constexpr int KS = D / 16, DT = D / 32;
+  static constexpr int EA = 16 / KS;        // softmax elements finished per stage-A step
+  static constexpr int EB = 16 / (2 * DT);  // ... per stage-B step (== EA since KS == 2 DT)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+  // Q / dO row fragment of step i (subtile i / KS, k-step i % KS)
+  __device__ __forceinline__ static u16x8 rowf(const bf16_t* base, const int (&roff)[KS], int i) {
+    return *reinterpret_cast<const u16x8*>(base + roff[i % KS] + (i / KS) * 32 * D);
+  }
+  // transposed dO / Q fragment of subtile qs, step j (dt = j / 2, 16-row half j % 2)
+  __device__ __forceinline__ static u16x8 trf(const bf16_t* base, const int (&toff)[DT][2], int qs, int j) {
+    const int o = (qs * 32 + 16 * (j & 1)) * D;
+    return tr_pair(base + toff[j >> 1][0] + o, base + toff[j >> 1][1] + o);
+  }
+  // softmax-gradient of accumulator registers [e0, e0 + N) of one 32-row subtile:
+  //   p = exp2(s * scale*log2e - lse*log2e),  dS = p * (dP - delta)
+  template <int N>
+  __device__ __forceinline__ static void smx(f32x16& sv, f32x16& dpv, int e0, const float* nl, const float* dl, float sl2,
+                                             int qs, int tmask, int tsq) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      const int r = e0 + e, rr = (r & 3) + 8 * (r >> 2) + 32 * qs;
+      float pv = fast_exp2(fmaf(sv[r], sl2, nl[e]));
+      pv = (rr < tmask || rr >= tsq) ? 0.f : pv;
+      sv[r] = pv;
+      dpv[r] = pv * (dpv[r] - dl[e]);
+    }
+  }
+  template <int N>
+  __device__ __forceinline__ static void ldstat(const float* Ls, const float* Ds, int e0, int qs, int h, float (&nl)[N],
+                                                float (&dl)[N]) {
+    const int r0 = (e0 & 3) + 8 * (e0 >> 2) + 32 * qs + 4 * h;   // N <= 4 consecutive rows
+#pragma unroll
+    for (int e = 0; e < N; ++e) { nl[e] = Ls[r0 + e]; dl[e] = Ds[r0 + e]; }
+  }
+
+  // One 64-query tile against this wave's 32 keys, software-pipelined by hand: every step is its own
+  // scheduling region (sched_barrier) holding 2 MFMAs, the LDS reads for the NEXT step and a slice of
+  // softmax VALU -- the compiler's own schedule issues each LDS read just before its MFMA, which at one
+  // wave per SIMD exposes the full LDS latency on every MFMA.
+  //   stage A (2*KS steps): S / dP chains of subtiles 0 and 1; subtile 0's softmax under subtile 1's chain
+  //   stage B (2*DT steps): dV/dK += subtile 0;                   subtile 1's softmax under it
+  //   stage C (2*DT steps): dV/dK += subtile 1
+  // Ls holds -lse*log2(e) rows, Ds delta rows.  Masking is branch-free (select) on every tile.
+  __device__ __forceinline__ static void run(const bf16_t* Qs, const bf16_t* Gs, const float* Ls, const float* Ds,
+                                             const u16x8 (&kf)[KS], const u16x8 (&vf)[KS], const int (&roff)[KS],
+                                             const int (&toff)[DT][2], f32x16 (&dk)[DT], f32x16 (&dv)[DT], float sl2,
+                                             int tmask, int tsq, int h) {
+    acc_fence();   // accumulator copies the register allocator placed before this tile have retired
+    f32x16 s[2], dp[2];
+    u16x8 pf[2][2], df[2][2];
+    const f32x16 z = zero16();
+    // ---- stage A
+    u16x8 qa = rowf(Qs, roff, 0), ga = rowf(Gs, roff, 0);
+    float nl[EA], dl[EA];
+    ldstat<EA>(Ls, Ds, 0, 0, h, nl, dl);
+    u16x8 ta, tb;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int qs = i / KS, ks = i % KS;
+      u16x8 qn, gn;
+      if (i + 1 < 2 * KS) { qn = rowf(Qs, roff, i + 1); gn = rowf(Gs, roff, i + 1); }
+      else { ta = trf(Gs, toff, 0, 0); tb = trf(Qs, toff, 0, 0); }
+      s[qs] = mfma32(qa, kf[ks], ks == 0 ? z : s[qs]);
+      dp[qs] = mfma32(ga, vf[ks], ks == 0 ? z : dp[qs]);
+      if (qs == 1) {
+        float nn[EA], dd[EA];
+        if (ks + 1 < KS) ldstat<EA>(Ls, Ds, (ks + 1) * EA, 0, h, nn, dd);
+        else ldstat<EA>(Ls, Ds, 0, 1, h, nn, dd);   // EA == EB: first stage-B slice
+        smx<EA>(s[0], dp[0], ks * EA, nl, dl, sl2, 0, tmask, tsq);
+#pragma unroll
+        for (int e = 0; e < EA; ++e) { nl[e] = nn[e]; dl[e] = dd[e]; }
+      }
+      qa = qn; ga = gn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pf[0][0] = pack8(s[0], 0); pf[0][1] = pack8(s[0], 1);
+    df[0][0] = pack8(dp[0], 0); df[0][1] = pack8(dp[0], 1);
+    // ---- stage B
+#pragma unroll
+    for (int j = 0; j < 2 * DT; ++j) {
+      u16x8 tan, tbn;
+      if (j + 1 < 2 * DT) { tan = trf(Gs, toff, 0, j + 1); tbn = trf(Qs, toff, 0, j + 1); }
+      else { tan = trf(Gs, toff, 1, 0); tbn = trf(Qs, toff, 1, 0); }
+      mfma32_acc(dv[j >> 1], ta, pf[0][j & 1]);
+      mfma32_acc(dk[j >> 1], tb, df[0][j & 1]);
+      float nn[EB], dd[EB];
+      if (j + 1 < 2 * DT) ldstat<EB>(Ls, Ds, (j + 1) * EB, 1, h, nn, dd);
+      smx<EB>(s[1], dp[1], j * EB, nl, dl, sl2, 1, tmask, tsq);
+      if (j + 1 < 2 * DT) {
+#pragma unroll
+        for (int e = 0; e < EB; ++e) { nl[e] = nn[e]; dl[e] = dd[e]; }
+      }
+      if ((j + 1) * EB == 8) { pf[1][0] = pack8(s[1], 0); df[1][0] = pack8(dp[1], 0); }
+      ta = tan; tb = tbn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pf[1][1] = pack8(s[1], 1); df[1][1] = pack8(dp[1], 1);
+    // ---- stage C
+#pragma unroll
+    for (int j = 0; j < 2 * DT; ++j) {
+      u16x8 tan, tbn;
+      if (j + 1 < 2 * DT) { tan = trf(Gs, toff, 1, j + 1); tbn = trf(Qs, toff, 1, j + 1); }
+      mfma32_acc(dv[j >> 1], ta, pf[1][j & 1]);
+      mfma32_acc(dk[j >> 1], tb, df[1][j & 1]);
+      ta = tan; tb = tbn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    acc_fence();   // inline-asm MFMA results are invisible to the hazard recognizer: retire before any copy
+  }
+};
+
+template <int D, bool CAUSAL, int OCC>
+__global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];        // [buf][Q | dO]
+  __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];    // [buf][lse | delta]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x;
+  const int group = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int kw = kb * 128 + w * 32, key = kw + c32;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  u16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (key < p.Sk) {
+      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
+      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
+    }
+  }
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+
+  const int qstart = CAUSAL ? max(0, kb * 128 - off) / TILE * TILE : 0;
+  const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
+  const int total = qtiles * group;
+
+  auto issue = [&](int it, int buf) {
+    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
+    const int hq = hk * group + hi;
+    bf16_t* base = smem + buf * 2 * TE;
+    dma_tile<D>(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w, lane);
+    dma_tile<D>(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w, lane);
+    if (w == 0) dma_f32_row(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][0], lane);
+    if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][1], lane);
+  };
+  if (total > 0) issue(0, 0);
+
+  for (int it = 0; it < total; it += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int cur = it + u;
+      if (cur >= total) break;
+      __syncthreads();
+      if (cur + 1 < total) issue(cur + 1, 1 - u);
+      const int q0 = qstart + (cur % qtiles) * TILE;
+      if (CAUSAL && q0 + TILE - 1 + off < kw) continue;         // every query of the tile precedes these keys
+      const bf16_t* Qs = smem + u * 2 * TE;
+      const float* Ls = sstat[u][0];
+      // rows of S = queries q0 + rr (+4h) with rr in [0, 64); masked if rr < tmask or rr >= tsq
+      const int tmask = CAUSAL ? key - off - q0 - 4 * h : -1;
+      const int tsq = p.Sq - q0 - 4 * h;
+      BwdKVTile<D, CAUSAL>::run(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask, tsq, h);
+    }
+  }
+  acc_fence();
+  if (key < p.Sk) {
+    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
+    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 a, c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
+        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
+        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
+      }
+  }
+}
+
+template <int D, bool CAUSAL>
+struct BwdQTile {
+  static constexpr int KS = D / 16, DT = D / 32;
+  static constexpr int EA = 16 / KS;   // softmax elements per pipeline step (KS == 2 DT)
+  // K / V row fragment of step i (subtile i / KS, k-step i % KS)
+  __device__ __forceinline__ static u16x8 rowf(const bf16_t* base, const int (&roff)[KS], int i) {
+    return *reinterpret_cast<const u16x8*>(base + roff[i % KS] + (i / KS) * 32 * D);
+  }
+  __device__ __forceinline__ static u16x8 trf(const bf16_t* base, const int (&toff)[DT][2], int kt, int j) {
+    const int o = (kt * 32 + 16 * (j & 1)) * D;
+    return tr_pair(base + toff[j >> 1][0] + o, base + toff[j >> 1][1] + o);
+  }
+  // dS^T registers [e0, e0 + EA) of key subtile kt (rows = keys, lanes = queries)
+  __device__ __forceinline__ static void smx(const f32x16& sv, f32x16& dpv, int e0, int kt, float sl2, float nlse2,
+                                             float dl, int lim) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int r = e0 + e, rr = (r & 3) + 8 * (r >> 2) + 32 * kt;
+      float pv = fast_exp2(fmaf(sv[r], sl2, nlse2));
+      pv = rr > lim ? 0.f : pv;
+      dpv[r] = pv * (dpv[r] - dl);
+    }
+  }
+  // One 64-key tile, hand-pipelined like BwdKVTile: stage A = S/dP chains of both key subtiles (subtile
+  // 0's softmax-gradient under subtile 1's chain), stage B = dQ += dS0 K0 (subtile 1's softmax under it),
+  // stage C = dQ += dS1 K1.  Masking is branch-free (lim = last valid key row of this lane's query).
+  __device__ __forceinline__ static void run(const bf16_t* Ks, const bf16_t* Vs, const u16x8 (&qf)[KS],
+                                             const u16x8 (&gf)[KS], const int (&roff)[KS], const int (&toff)[DT][2],
+                                             f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim) {
+    f32x16 s[2], dp[2];
+    u16x8 df[2][2];
+    const f32x16 z = zero16();
+    u16x8 ka = rowf(Ks, roff, 0), va = rowf(Vs, roff, 0), ta;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int kt = i / KS, ks = i % KS;
+      u16x8 kn, vn;
+      if (i + 1 < 2 * KS) { kn = rowf(Ks, roff, i + 1); vn = rowf(Vs, roff, i + 1); }
+      else ta = trf(Ks, toff, 0, 0);
+      s[kt] = mfma32(ka, qf[ks], ks == 0 ? z : s[kt]);
+      dp[kt] = mfma32(va, gf[ks], ks == 0 ? z : dp[kt]);
+      if (kt == 1) smx(s[0], dp[0], ks * EA, 0, sl2, nlse2, dl, lim);
+      ka = kn; va = vn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    df[0][0] = pack8(dp[0], 0); df[0][1] = pack8(dp[0], 1);
+#pragma unroll
+    for (int j = 0; j < 2 * DT; ++j) {
+      const u16x8 tn = j + 1 < 2 * DT ? trf(Ks, toff, 0, j + 1) : trf(Ks, toff, 1, 0);
+      dq[j >> 1] = mfma32(ta, df[0][j & 1], dq[j >> 1]);
+      smx(s[1], dp[1], j * EA, 1, sl2, nlse2, dl, lim);
+      if ((j + 1) * EA == 8) df[1][0] = pack8(dp[1], 0);
+      ta = tn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    df[1][1] = pack8(dp[1], 1);
+#pragma unroll
+    for (int j = 0; j < 2 * DT; ++j) {
+      u16x8 tn;
+      if (j + 1 < 2 * DT) tn = trf(Ks, toff, 1, j + 1);
+      dq[j >> 1] = mfma32(ta, df[1][j & 1], dq[j >> 1]);
+      ta = tn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
+    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+  }
+  u16x8 qf[KS], gf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) {
+      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
+    }
+  }
+  const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
+  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+  const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  for (int t = 0; t < ntiles; t += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tt = t + u;
+      if (tt >= ntiles) break;
+      __syncthreads();
+      if (tt + 1 < ntiles) {
+        bf16_t* nb = smem + (1 - u) * 2 * TE;
+        dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
+        dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
+      }
+      const int k0 = tt * TILE;
+      if (CAUSAL && k0 > qw + 31 + off) continue;               // every key of the tile follows these queries
+      const bf16_t* Ks = smem + u * 2 * TE;
+      BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+    }
+  }
+  if (qrow < p.Sq) {
+    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
+        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
+      }
+  }
+}
+
+// kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
+int g_fwd_variant = -1, g_bwd_variant = -1;
+int fwd_variant() {
+  if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 4; }
+  return g_fwd_variant;
+}
+int bwd_variant() {
+  if (g_bwd_variant < 0) { const char* e = getenv("PDT_FA_BWD"); g_bwd_variant = e ? atoi(e) : 3; }
+  return g_bwd_variant;
+}
+
 template <int D>
 int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   dim3 grid((p.Sq + 127) / 128, p.H, p.B);
@@ -1124,10 +1501,7 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   fa_bwd_delta_kernel<D><<<(rows + NT - 1) / NT, NT, 0, st>>>(p);
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
-  static const int variant = [] {
-    const char* e = getenv("PDT_FA_BWD");
-    return e ? atoi(e) : 2;
-  }();
+  const int variant = bwd_variant();
   if (variant == 1) {
     if (causal) {
       fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(p);
@@ -1136,13 +1510,41 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
       fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(p);
       fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(p);
     }
-  } else {
+  } else if (variant == 2) {
     if (causal) {
       fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(p);
       fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(p);
     } else {
       fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
       fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
+  } else if (variant == 5 || variant == 6) {   // mixed generations (kernel bisection in tests)
+    if (causal) {
+      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
+      else fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(p);
+      if (variant == 5) fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      else fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+    } else {
+      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
+      else fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
+      if (variant == 5) fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      else fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
+  } else if (variant == 3) {   // v3, one wave per SIMD for dK/dV (no spills)
+    if (causal) {
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
+  } else {                     // v3, two waves per SIMD for dK/dV
+    if (causal) {
+      fa_bwd_dkdv_v3_kernel<D, true, 2><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_v3_kernel<D, false, 2><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
     }
   }
   return (int)hipGetLastError();
@@ -1162,10 +1564,7 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
   p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  static const int variant = [] {
-    const char* e = getenv("PDT_FA_FWD");
-    return e ? atoi(e) : 4;
-  }();
+  const int variant = fwd_variant();
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
 
@@ -1188,4 +1587,11 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
   return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
+}
+
+// select kernel variants (<= 0 keeps the current choice); returns fwd * 16 + bwd now in effect
+PDT_API int pdt_flash_attn_set_variant(int fwd, int bwd) {
+  if (fwd > 0) g_fwd_variant = fwd;
+  if (bwd > 0) g_bwd_variant = bwd;
+  return fwd_variant() * 16 + bwd_variant();
 }

@@ -33,6 +33,11 @@ HIPCC_FLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
     "-munsafe-fp-atomics", "-ffp-contract=fast", "-Wno-unused-result",
 ]
+# MFMA kernels whose accumulators are post-processed by VALU (softmax / gradient tiles): keep the MFMA
+# results in arch VGPRs (no v_accvgpr_read/write shuttling through AGPRs).
+PER_FILE_FLAGS = {
+    "flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
 
 
 def _hipcc() -> str:
@@ -73,7 +78,8 @@ def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
     jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = [ex.submit(_run, [hipcc, *HIPCC_FLAGS, "-I", KERNEL_DIR, "-c", s, "-o", o], verbose)
+            futs = [ex.submit(_run, [hipcc, *HIPCC_FLAGS, *PER_FILE_FLAGS.get(os.path.basename(s), []),
+                                        "-I", KERNEL_DIR, "-c", s, "-o", o], verbose)
                     for s, o in todo]
             for f in futs:
                 f.result()

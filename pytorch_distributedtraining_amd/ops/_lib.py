@@ -59,6 +59,7 @@ _SIGS = {
     "pdt_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                            c_void_p],
+    "pdt_flash_attn_set_variant": [c_int, c_int],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int,

@@ -44,7 +44,7 @@ def _fwd(q, k, v, causal, scale):
 def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale):
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
-    delta = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+    delta = torch.empty((2, B, H, Sq), dtype=torch.float32, device=q.device)   # [delta | -lse*log2e]
     do = do if (do.stride(-1) == 1 and all(s % 8 == 0 for s in do.stride()[:-1])) else do.contiguous()
     strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
                            + _strides(dk) + _strides(dv), dtype=torch.int64)
@@ -121,6 +121,14 @@ def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None):
     if not qkv.is_cuda:
         return _reference(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal, scale)
     return _FlashAttnPackedFn.apply(qkv, causal, scale)
+
+
+def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:
+    """Select the flash-attention kernel generation (0 keeps the current one).  fwd: 2 register-staged,
+    3 LDS-DMA ring, 4 (default) VALU-lean LDS-DMA.  bwd: 1 baseline, 2 LDS-DMA, 3 (default) hand-pipelined
+    dK/dV (v3).  Returns the (fwd, bwd) pair now in effect."""
+    r = _lib.require().pdt_flash_attn_set_variant(int(fwd), int(bwd))
+    return r // 16, r % 16
 
 
 def supported(head_dim: int) -> bool:

@@ -59,6 +59,26 @@ def attn(B=8, S=1024, H=16, D=128, causal=True):
     report(f"flash_attn bwd {tag}", ms_b, r_b, flops=2.5 * f)
 
 
+def attn_variants(B=16, S=1024, H=16, D=128):
+    """backward kernel generations side by side (GPT-2 1.3B mb16 layer shape)."""
+    from pytorch_distributedtraining_amd.ops import flash_attn
+    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    for causal in (True, False):
+        f = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+        o = flash_attn(q, k, v, causal=causal)
+        grads = {}
+        for var in (2, 3):
+            set_kernel_variant(bwd=var)
+            ms = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
+            grads[var] = torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
+            report(f"flash_attn bwd v{var} B{B} S{S} H{H} D{D} {'causal' if causal else 'full'}", ms, flops=2.5 * f)
+        diff = max((a.float() - b.float()).abs().max().item() for a, b in zip(grads[2], grads[3]))
+        print(json.dumps({"case": "bwd v2 vs v3 max abs diff", "causal": causal, "diff": diff}), flush=True)
+    set_kernel_variant(bwd=3)
+
+
 def layernorm(rows=8192, N=2048):
     from pytorch_distributedtraining_amd.ops import layer_norm
     x = torch.randn(rows, N, device="cuda", dtype=torch.bfloat16, requires_grad=True)
@@ -120,6 +140,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     cases = {"attn": lambda: (attn(), attn(S=2048, B=4), attn(D=64, H=12, B=8, S=1024), attn(causal=False)),
+             "attnvar": attn_variants,
              "ln": layernorm, "adamw": adamw, "ce": cross_entropy, "gelu": bias_gelu}
     for k, fn in cases.items():
         if a.only and k not in a.only.split(","):

@@ -138,11 +138,22 @@ def _attn_ref(q, k, v, causal, scale):
     return (s.softmax(-1) @ vt).transpose(1, 2)
 
 
+@pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,S,H,Hkv", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 1024, 2, 1), (1, 77, 2, 2)])
-def test_flash_attn(D, causal, B, S, H, Hkv):
+def test_flash_attn(D, causal, B, S, H, Hkv, variant):
     from pytorch_distributedtraining_amd.ops import flash_attn
+    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    prev = set_kernel_variant()
+    set_kernel_variant(bwd=variant)
+    try:
+        _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv)
+    finally:
+        set_kernel_variant(*prev)
+
+
+def _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv):
     q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
