@@ -6,6 +6,7 @@
 // Llama-3 MLP (SwiGLU) and attention (RoPE, rotate-half convention), BASELINE.json north star
 // "bf16/fp8 loss-scaled cast".
 #include "common.h"
+#include "reduce.h"
 #include <hip/hip_fp8.h>
 
 using namespace pdt;
@@ -68,6 +69,54 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_kernel(const T* __restrict__
     for (int k = 0; k < 8; ++k) g[k] *= gelu_grad<TANH>(bias ? v[k] + b[k] : v[k]);
     Vec8<T>::store(dh + e, g);
   }
+}
+
+// GELU backward fused with the bias gradient: workgroups sweep (2048-column group) x (row chunk) as in
+// reduce.h; each thread keeps its 8 columns' dbias partial sums in registers while it writes dh, so the
+// bias gradient costs no second pass over the [rows, N] activation gradient.
+template <typename T, typename B, bool TANH>
+__global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restrict__ dy, const T* __restrict__ h,
+                                                              const B* __restrict__ bias, T* __restrict__ dh,
+                                                              int rows, int N, int rows_per,
+                                                              float* __restrict__ part) {
+  const int col = (blockIdx.x * NT + threadIdx.x) * 8;
+  if (col >= N) return;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(rows, r0 + rows_per);
+  float b[8], acc[8];
+  Vec8<B>::load(bias + col, b);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  int r = r0;
+  for (; r + 2 <= r1; r += 2) {
+    float v[2][8], g[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      Vec8<T>::load(h + (int64_t)(r + u) * N + col, v[u]);
+      Vec8<T>::load(dy + (int64_t)(r + u) * N + col, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[u][k] *= gelu_grad<TANH>(v[u][k] + b[k]);
+        acc[k] += g[u][k];
+      }
+      Vec8<T>::store(dh + (int64_t)(r + u) * N + col, g[u]);
+    }
+  }
+  for (; r < r1; ++r) {
+    float v[8], g[8];
+    Vec8<T>::load(h + (int64_t)r * N + col, v);
+    Vec8<T>::load(dy + (int64_t)r * N + col, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      g[k] *= gelu_grad<TANH>(v[k] + b[k]);
+      acc[k] += g[k];
+    }
+    Vec8<T>::store(dh + (int64_t)r * N + col, g);
+  }
+  Vec8<float>::store(part + (int64_t)blockIdx.y * N + col, acc);
 }
 
 // SwiGLU on a fused [rows, 2F] projection: y[r, j] = silu(x[r, j]) * x[r, F + j]
@@ -233,6 +282,27 @@ PDT_API int pdt_bias_gelu_bwd(const void* dy, const void* h, const void* bias, v
     else { if (tanh_approx) PDT_L(float, bf16_t, true); else PDT_L(float, bf16_t, false); }
   }
 #undef PDT_L
+  return (int)hipGetLastError();
+}
+
+// dh = dy * gelu'(h + bias) and dbias[N] (+= if accumulate) in one sweep; ws: pdt_colsum_ws_floats(rows, N)
+PDT_API int pdt_bias_gelu_bwd_db(const void* dy, const void* h, const void* bias, void* dh, void* dbias, float* ws,
+                                 int rows, int N, int dt, int bdt, int tanh_approx, int accumulate, hipStream_t st) {
+  if (N % 8 != 0 || bias == nullptr) return (int)hipErrorInvalidValue;
+  const red::ColPlan pl = red::col_plan(rows, N);
+  dim3 grid(pl.col_groups, pl.R);
+#define PDT_L(T, B, TH)                                                                                    \
+  bias_gelu_bwd_db_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh, rows, N, \
+                                                         pl.rows_per, ws)
+  if (dt == kBF16 && bdt == kBF16) { if (tanh_approx) PDT_L(bf16_t, bf16_t, true); else PDT_L(bf16_t, bf16_t, false); }
+  else if (dt == kBF16 && bdt == kF32) { if (tanh_approx) PDT_L(bf16_t, float, true); else PDT_L(bf16_t, float, false); }
+  else if (dt == kF32 && bdt == kF32) { if (tanh_approx) PDT_L(float, float, true); else PDT_L(float, float, false); }
+  else if (dt == kF32 && bdt == kBF16) { if (tanh_approx) PDT_L(float, bf16_t, true); else PDT_L(float, bf16_t, false); }
+  else return (int)hipErrorInvalidValue;
+#undef PDT_L
+  float* ws2 = ws + (int64_t)pl.R * N;
+  if (bdt == kBF16) red::col_reduce<bf16_t>(ws, pl.R, N, (bf16_t*)dbias, ws2, accumulate, st);
+  else red::col_reduce<float>(ws, pl.R, N, (float*)dbias, ws2, accumulate, st);
   return (int)hipGetLastError();
 }
 

@@ -607,25 +607,29 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
 // ------------------------------------------------------------------------------------------------
 template <int D>
 __global__ __launch_bounds__(NT) void fa_bwd_delta_kernel(AttnParams p) {
-  const int64_t idx = blockIdx.x * (int64_t)NT + threadIdx.x;  // over B*H*Sq
+  // delta = rowsum(dO * O) and the log2-domain lse, D/8 lanes per row (16-B coalesced loads)
+  constexpr int LPR = D / 8;
+  const int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x;
+  const int64_t idx = t / LPR;                      // row over B*H*Sq
+  const int c = (int)(t % LPR) * 8;
   const int64_t total = (int64_t)p.B * p.H * p.Sq;
-  if (idx >= total) return;
-  const int q = (int)(idx % p.Sq);
-  const int hq = (int)((idx / p.Sq) % p.H);
-  const int b = (int)(idx / ((int64_t)p.Sq * p.H));
-  const bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)q * p.o_ss;
-  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh + (int64_t)q * p.do_ss;
   float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < D; c += 8) {
+  if (idx < total) {
+    const int q = (int)(idx % p.Sq);
+    const int hq = (int)((idx / p.Sq) % p.H);
+    const int b = (int)(idx / ((int64_t)p.Sq * p.H));
     float a[8], g[8];
-    Vec8<bf16_t>::load(Op + c, a);
-    Vec8<bf16_t>::load(Gp + c, g);
+    Vec8<bf16_t>::load(p.o + b * p.o_sb + hq * p.o_sh + (int64_t)q * p.o_ss + c, a);
+    Vec8<bf16_t>::load(p.dout + b * p.do_sb + hq * p.do_sh + (int64_t)q * p.do_ss + c, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
   }
-  p.delta[idx] = acc;
-  p.delta[total + idx] = -p.lse[idx] * LOG2E;   // log2-domain lse for the v3 dK/dV kernel
+#pragma unroll
+  for (int m = LPR / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if (idx < total && c == 0) {
+    p.delta[idx] = acc;
+    p.delta[total + idx] = -p.lse[idx] * LOG2E;   // log2-domain lse for the v3 dK/dV kernel
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1498,7 +1502,7 @@ int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
 template <int D>
 int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.Sq;
-  fa_bwd_delta_kernel<D><<<(rows + NT - 1) / NT, NT, 0, st>>>(p);
+  fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
   const int variant = bwd_variant();

@@ -10,6 +10,7 @@
 // Reference parity: SwinIR LayerNorm sites (Stoke-DDP.py:206-208), GPT-2/Llama norms
 // (BASELINE.json configs 3-5); semantics of torch.nn.functional.layer_norm / rms_norm.
 #include "common.h"
+#include "reduce.h"
 
 using namespace pdt;
 
@@ -43,8 +44,11 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[it][k] += r8[k];
           Vec8<T>::store(sum_out + (int64_t)row * N + col, v[it]);
-          // normalise exactly what was stored (bf16-rounded sum)
-          Vec8<T>::load(sum_out + (int64_t)row * N + col, v[it]);
+          // normalise exactly what was stored (the T-rounded sum), rounded in registers
+          if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[it][k] = bf2f(f2bf(v[it][k]));
+          }
         }
       } else {
 #pragma unroll
@@ -268,49 +272,8 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
   }
 }
 
-// Column reduction of a [R, N] fp32 partial matrix into out[N] (type W), two levels so the
-// read of the partials is spread over many CUs (one level with N/64 blocks left most of the chip idle:
-// 7.8 ms/step at GPT-2 1.3B).  Level 1: grid (N/64, RS) blocks of 64 columns x 4 row-lanes, each
-// folding R/RS rows into part2[RS, N].  Level 2: the same kernel with RS = 1 writing out.
-// Deterministic order throughout.
-template <typename W, bool FINAL>
-__global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict__ part, int R, int N,
-                                                        W* __restrict__ out, float* __restrict__ part2,
-                                                        int accumulate) {
-  __shared__ float red[RPB][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
-  const int per = (R + gridDim.y - 1) / gridDim.y;
-  const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
-  float s = 0.f;
-  if (col < N)
-    for (int r = r0 + wid; r < r1; r += RPB) s += part[(int64_t)r * N + col];
-  red[wid][lane] = s;
-  __syncthreads();
-  if (wid == 0 && col < N) {
-    float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    if (FINAL) {
-      if (accumulate) t += to_f<W>(out[col]);
-      out[col] = from_f<W>(t);
-    } else {
-      part2[(int64_t)blockIdx.y * N + col] = t;
-    }
-  }
-}
-
-// ws2 must hold >= 64 * N floats
-template <typename W>
-void col_reduce(const float* part, int R, int N, W* out, float* ws2, int accumulate, hipStream_t st) {
-  const int cg = (N + 63) / 64;
-  int rs = 1;
-  while (rs < 64 && cg * rs < 512 && R / (rs * 2) >= 8) rs *= 2;
-  if (rs == 1) {
-    col_reduce_kernel<W, true><<<dim3(cg, 1), NT, 0, st>>>(part, R, N, out, nullptr, accumulate);
-  } else {
-    col_reduce_kernel<W, false><<<dim3(cg, rs), NT, 0, st>>>(part, R, N, out, ws2, accumulate);
-    col_reduce_kernel<W, true><<<dim3(cg, 1), NT, 0, st>>>(ws2, rs, N, out, nullptr, accumulate);
-  }
-}
+// column reductions of the [R, N] dgamma/dbeta partials: reduce.h (two-level, deterministic)
+using red::col_reduce;
 
 template <typename T, typename W, bool RMS>
 int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y, float* mean,
@@ -335,7 +298,8 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
 
 // fast path: one partial row per workgroup (LDS-accumulated); fallback: one per block
 int bwd_partial_rows(int rows, int N) {
-  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, N <= 4096 ? 512 : 256);
+  // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
+  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, N <= 2048 ? 1024 : (N <= 4096 ? 512 : 256));
   return grid_for(rows, 1, 512);
 }
 
@@ -400,19 +364,29 @@ PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const flo
   return (int)hipErrorInvalidValue;
 }
 
-// Column sums of a [rows, N] matrix (T) into out[N] (W) -- bias gradients.  ws >= R*N floats where
-// R = pdt_colsum_partial_rows(rows).
+// Column sums of a [rows, N] matrix (T) into out[N] (W) -- bias gradients.  Workspace:
+// pdt_colsum_ws_floats(rows, N) floats (reduce.h col_plan partials + second level).
 namespace {
 template <typename T>
 __global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* __restrict__ x, int rows, int N, int rows_per,
                                                             float* __restrict__ part) {
-  // block: 256 threads x 8 columns = 2048 columns per block in x; blockIdx.y = row slab
+  // blockIdx.x = 2048-column group (256 threads x 8 columns), blockIdx.y = row chunk
   const int col = (blockIdx.x * NT + threadIdx.x) * 8;
   if (col >= N) return;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(rows, r0 + rows_per);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < r1; ++r) {
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {   // 4 independent 16-B loads in flight per thread
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Vec8<T>::load(x + (int64_t)(r + u) * N + col, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[u][k];
+  }
+  for (; r < r1; ++r) {
     float v[8];
     Vec8<T>::load(x + (int64_t)r * N + col, v);
 #pragma unroll
@@ -422,20 +396,17 @@ __global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* __restrict_
 }
 }  // namespace
 
-// workspace for pdt_colsum: pdt_colsum_partial_rows(rows) * N + 64 * N floats
-PDT_API int pdt_colsum_partial_rows(int rows) { return (rows < 256 ? rows : 256) + 64; }
+PDT_API int pdt_colsum_ws_floats(int rows, int N) { return (int)red::col_ws_floats(rows, N); }
 
 PDT_API int pdt_colsum(const void* x, int rows, int N, int xdt, void* out, int odt, float* ws, int accumulate,
                        hipStream_t st) {
   if (N % 8 != 0) return (int)hipErrorInvalidValue;
-  const int R = pdt_colsum_partial_rows(rows) - 64;
-  const int rows_per = (rows + R - 1) / R;
-  const int Ruse = (rows + rows_per - 1) / rows_per;
-  dim3 grid((N / 8 + NT - 1) / NT, Ruse);
-  if (xdt == kBF16) colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, rows_per, ws);
-  else colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, rows_per, ws);
-  float* ws2 = ws + (int64_t)R * N;
-  if (odt == kBF16) col_reduce<bf16_t>(ws, Ruse, N, (bf16_t*)out, ws2, accumulate, st);
-  else col_reduce<float>(ws, Ruse, N, (float*)out, ws2, accumulate, st);
+  const red::ColPlan pl = red::col_plan(rows, N);
+  dim3 grid(pl.col_groups, pl.R);
+  if (xdt == kBF16) colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
+  else colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  float* ws2 = ws + (int64_t)pl.R * N;
+  if (odt == kBF16) red::col_reduce<bf16_t>(ws, pl.R, N, (bf16_t*)out, ws2, accumulate, st);
+  else red::col_reduce<float>(ws, pl.R, N, (float*)out, ws2, accumulate, st);
   return (int)hipGetLastError();
 }

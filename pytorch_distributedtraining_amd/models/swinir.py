@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.norms import LayerNorm
+from ..ops.window_attention import window_attention
 
 
 def window_partition(x, ws):
@@ -54,6 +55,13 @@ class WindowAttention(nn.Module):
     def forward(self, x, mask=None):
         Bw, N, C = x.shape
         h = self.num_heads
+        if x.is_cuda:
+            # fused HIP window attention: reads the qkv projection in place, never materialises the
+            # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
+            qkv = self.qkv(x)
+            bias = self.relative_position_bias_table[self.relative_position_index.view(-1)].view(N, N, h)
+            out = window_attention(qkv, bias.permute(2, 0, 1), mask, h, self.scale)
+            return self.proj(out)
         qkv = self.qkv(x).reshape(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         bias = self.relative_position_bias_table[self.relative_position_index.view(-1)].view(N, N, h)

@@ -40,7 +40,9 @@ _SIGS = {
     "pdt_norm_bwd_workspace_floats": [c_int, c_int],
     "pdt_norm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "pdt_colsum_partial_rows": [c_int],
+    "pdt_colsum_ws_floats": [c_int, c_int],
+    "pdt_bias_gelu_bwd_db": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                             c_int, c_int, c_int, c_void_p],
     "pdt_colsum": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p],
     "pdt_bias_gelu_fwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_bias_gelu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p],
@@ -60,6 +62,11 @@ _SIGS = {
                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                            c_void_p],
     "pdt_flash_attn_set_variant": [c_int, c_int],
+    "pdt_win_attn_grid": [c_int],
+    "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                         c_int, c_void_p],
+    "pdt_win_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int,

@@ -2,7 +2,8 @@
 
 ``bias_gelu(h, b)`` computes ``gelu(h + b)`` in one pass and saves only ``h`` for backward (the
 pre-activation is recomputed in the backward kernel), so the MLP keeps one [tokens, 4d] activation
-instead of two.  The bias gradient is a deterministic column reduction over the ``dh`` it produces.
+instead of two.  The backward kernel also accumulates the bias gradient (per-thread column partials +
+a deterministic two-level column reduce), so ``dh`` is written once and never re-read.
 """
 from __future__ import annotations
 
@@ -16,7 +17,7 @@ def _colsum(x2, out_dtype):
     rows, n = x2.shape
     lib = _lib.require()
     out = torch.empty(n, dtype=out_dtype, device=x2.device)
-    ws = torch.empty(lib.pdt_colsum_partial_rows(rows) * n, dtype=torch.float32, device=x2.device)
+    ws = torch.empty(lib.pdt_colsum_ws_floats(rows, n), dtype=torch.float32, device=x2.device)
     _lib.call("pdt_colsum", x2.data_ptr(), rows, n, _lib.dtype_code(x2.dtype), out.data_ptr(),
               _lib.dtype_code(out_dtype), ws.data_ptr(), 0, _lib.stream_handle(x2.device))
     return out
@@ -41,11 +42,19 @@ class _BiasGeluFn(torch.autograd.Function):
         h2, bias = ctx.saved_tensors
         dy2 = dy.reshape(h2.shape).contiguous()
         dh = torch.empty_like(h2)
-        bdt = _lib.dtype_code(bias.dtype) if bias is not None else _lib.BF16
-        _lib.call("pdt_bias_gelu_bwd", dy2.data_ptr(), h2.data_ptr(), _lib.ptr(bias), dh.data_ptr(), h2.shape[0],
-                  h2.shape[1], _lib.dtype_code(h2.dtype), bdt, 1 if ctx.tanh else 0, _lib.stream_handle(h2.device))
-        db = _colsum(dh, bias.dtype) if ctx.has_bias else None
-        return dh.view(dy.shape), db, None
+        rows, n = h2.shape
+        if ctx.has_bias:
+            # GELU backward + bias gradient in one sweep (no second pass over dh)
+            lib = _lib.require()
+            db = torch.empty_like(bias)
+            ws = torch.empty(lib.pdt_colsum_ws_floats(rows, n), dtype=torch.float32, device=h2.device)
+            _lib.call("pdt_bias_gelu_bwd_db", dy2.data_ptr(), h2.data_ptr(), bias.data_ptr(), dh.data_ptr(),
+                      db.data_ptr(), ws.data_ptr(), rows, n, _lib.dtype_code(h2.dtype), _lib.dtype_code(bias.dtype),
+                      1 if ctx.tanh else 0, 0, _lib.stream_handle(h2.device))
+            return dh.view(dy.shape), db, None
+        _lib.call("pdt_bias_gelu_bwd", dy2.data_ptr(), h2.data_ptr(), None, dh.data_ptr(), rows, n,
+                  _lib.dtype_code(h2.dtype), _lib.BF16, 1 if ctx.tanh else 0, _lib.stream_handle(h2.device))
+        return dh.view(dy.shape), None, None
 
 
 def bias_gelu(h, bias=None, approximate: str = "tanh"):

@@ -1,0 +1,97 @@
+"""Fused shifted-window attention for SwinIR / Swin blocks.
+
+``window_attention(qkv, rel_bias, mask, num_heads, scale)`` computes, for every window and head,
+``softmax(q kᵀ · scale + rel_bias[h] + mask[w]) v`` straight from the fused qkv projection
+``[Bw, N, 3C]`` and returns ``[Bw, N, C]`` ready for the output projection.  On MI355X this is one
+HIP kernel each way (``csrc/kernels/window_attn.hip``); the stock path would materialise the
+expanded bias+mask ``[Bw, h, N, N]`` and the scores in HBM.  The CPU path is the plain PyTorch
+formula (also the numerics reference in the GPU tests).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_MASK_T_CACHE: dict = {}
+
+
+def _mask_t(mask):
+    """[nw, N(i), N(j)] -> [nw, N(j), N(i)] fp32, cached per (storage, version) -- masks are buffers."""
+    key = (mask.data_ptr(), mask._version, tuple(mask.shape), mask.device)
+    hit = _MASK_T_CACHE.get(key)
+    if hit is None:
+        if len(_MASK_T_CACHE) > 64:
+            _MASK_T_CACHE.clear()
+        m = mask.float().contiguous()
+        hit = (m, m.transpose(1, 2).contiguous())
+        _MASK_T_CACHE[key] = hit
+    return hit
+
+
+def reference(qkv, rel_bias, mask, num_heads, scale):
+    Bw, N, C3 = qkv.shape
+    C = C3 // 3
+    q, k, v = qkv.float().view(Bw, N, 3, num_heads, C // num_heads).permute(2, 0, 3, 1, 4)
+    s = (q * scale) @ k.transpose(-1, -2) + rel_bias.float().unsqueeze(0)
+    if mask is not None:
+        nw = mask.shape[0]
+        s = s.view(Bw // nw, nw, num_heads, N, N) + mask.float().view(1, nw, 1, N, N)
+        s = s.view(Bw, num_heads, N, N)
+    o = s.softmax(-1) @ v
+    return o.transpose(1, 2).reshape(Bw, N, C).to(qkv.dtype)
+
+
+class _WindowAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, rel_bias, mask, num_heads, scale):
+        Bw, N, C3 = qkv.shape
+        C = C3 // 3
+        d = C // num_heads
+        qkv = qkv.contiguous()
+        bias = rel_bias.float().contiguous()
+        bias_t = bias.transpose(1, 2).contiguous()
+        m, m_t = _mask_t(mask) if mask is not None else (None, None)
+        nw = mask.shape[0] if mask is not None else 1
+        o = torch.empty((Bw, N, C), dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty((Bw, num_heads, N), dtype=torch.float32, device=qkv.device)
+        _lib.call("pdt_win_attn_fwd", qkv.data_ptr(), bias_t.data_ptr(), _lib.ptr(m_t), nw, o.data_ptr(),
+                  lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.dtype_code(qkv.dtype),
+                  _lib.stream_handle(qkv.device))
+        ctx.save_for_backward(qkv, bias, bias_t, o, lse)
+        ctx.mask = (m, m_t, nw)
+        ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, bias, bias_t, o, lse = ctx.saved_tensors
+        m, m_t, nw = ctx.mask
+        Bw, N, C3 = qkv.shape
+        d = C3 // 3 // ctx.h
+        lib = _lib.require()
+        G = lib.pdt_win_attn_grid(Bw)
+        dqkv = torch.empty_like(qkv)
+        part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
+        do = do.contiguous().to(qkv.dtype)
+        _lib.call("pdt_win_attn_bwd", qkv.data_ptr(), bias.data_ptr(), bias_t.data_ptr(), _lib.ptr(m), _lib.ptr(m_t),
+                  nw, o.data_ptr(), do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N, ctx.h,
+                  d, float(ctx.scale), _lib.dtype_code(qkv.dtype), _lib.stream_handle(qkv.device))
+        return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
+
+
+def supported(qkv, num_heads) -> bool:
+    Bw, N, C3 = qkv.shape
+    d = C3 // 3 // num_heads
+    return (qkv.is_cuda and qkv.dtype in (torch.float32, torch.bfloat16) and N <= 64 and d <= 32
+            and num_heads <= 16 and _lib.available())
+
+
+def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float):
+    """qkv [Bw, N, 3C]; rel_bias [h, N, N]; mask [nw, N, N] or None (window b uses mask b % nw)."""
+    if supported(qkv, num_heads):
+        return _WindowAttnFn.apply(qkv, rel_bias, mask, num_heads, scale)
+    if qkv.is_cuda:
+        _lib.require()          # fail loudly on a GPU box without the kernels
+    return reference(qkv, rel_bias, mask, num_heads, scale)

@@ -85,6 +85,8 @@ class DistributedDataParallel(nn.Module):
         comm: collective layer (default process group).
         bucket_cap_mb / first_bucket_mb: bucket sizes (defaults 64 / 8 MiB for xGMI; torch uses 25 / 1).
         broadcast_buffers: broadcast buffers from rank 0 every forward.
+        buffer_sync: "changed" (default) sends only buffers written since the last sync; "all" sends every
+            buffer every forward like torch DDP.
         find_unused_parameters: allow parameters that receive no gradient (flushed as zeros).
         compute_dtype: e.g. torch.bfloat16 -> the module runs in bf16, gradients are bf16 and
             all-reduced in bf16, and ``optimizer_parameters()`` returns the fp32 master flat(s)
@@ -95,6 +97,7 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, comm: Comm | None = None, device=None, bucket_cap_mb: float = 64.0,
                  first_bucket_mb: float = 8.0, broadcast_buffers: bool = True, find_unused_parameters: bool = False,
+                 buffer_sync: str = "changed",
                  compute_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
                  rebuild_buckets: bool = True, device_ids=None, **_ignored):
         super().__init__()
@@ -110,6 +113,7 @@ class DistributedDataParallel(nn.Module):
                     device = torch.device("cpu")
         self.device = torch.device(device)
         self.broadcast_buffers = broadcast_buffers
+        self.buffer_sync = buffer_sync
         self.find_unused_parameters = find_unused_parameters
         self.compute_dtype = compute_dtype
         self.reduce_dtype = reduce_dtype
@@ -262,10 +266,41 @@ class DistributedDataParallel(nn.Module):
                 g.flat_grad.zero_()
                 g.attach_grads()
         if self.broadcast_buffers and self.comm.world_size > 1 and self.module.training:
-            bufs = [b for b in self.module.buffers()]
-            if bufs:
-                self.comm.broadcast_coalesced(bufs)
+            self._sync_buffers()
         return self.module(*args, **kwargs)
+
+    def _sync_buffers(self):
+        """Broadcast rank 0's buffers -- only the ones that changed since the last sync.
+
+        torch DDP re-broadcasts every buffer every forward; SwinIR-S carries ~13 MB of constant buffers
+        (relative_position_index, shift masks) against 3.6 MB of gradients.  A buffer's autograd version
+        counter moves exactly when it is written in place (BatchNorm running stats, num_batches_tracked),
+        identically on every rank, so all ranks pick the same set without a collective.  The first sync
+        sends everything; running statistics of norm layers (updated inside the batch-norm kernels, no
+        version bump) are always sent; ``buffer_sync="all"`` restores torch's behaviour."""
+        bufs = list(self.module.buffers())
+        if not bufs:
+            return
+        seen = getattr(self, "_buf_versions", None)
+        if self.buffer_sync == "all" or seen is None or len(seen) != len(bufs):
+            send = bufs
+        else:
+            stats = self._running_stat_ids()
+            send = [b for b, v in zip(bufs, seen) if b._version != v or id(b) in stats]
+        if send:
+            self.comm.broadcast_coalesced(send)
+        self._buf_versions = [b._version for b in bufs]
+
+    def _running_stat_ids(self):
+        # norm running statistics are updated inside the batch-norm kernels without a version bump:
+        # always treat them as mutable
+        ids = set()
+        for mod in self.module.modules():
+            for name in ("running_mean", "running_var", "num_batches_tracked"):
+                b = getattr(mod, name, None)
+                if isinstance(b, torch.Tensor):
+                    ids.add(id(b))
+        return ids
 
     @contextmanager
     def no_sync(self):

@@ -222,3 +222,33 @@ def test_sharded_checkpoint_resharding(tmp_path):
     for k in sd:
         assert torch.equal(full[k], sd[k])
     assert torch.equal(fo["state"][0]["exp_avg_sq"], osd["state"][0]["exp_avg_sq"])
+
+
+def _w_ddp_buffers(rank, world):
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 8), nn.BatchNorm1d(8), nn.Linear(8, 2))
+    m.register_buffer("const_table", torch.arange(1000.0))        # never written: must not be re-sent
+    ddp = DistributedDataParallel(m)
+    sent = []
+    orig = ddp.comm.broadcast_coalesced
+
+    def spy(tensors, *a, **k):
+        sent.append(len(tensors))
+        return orig(tensors, *a, **k)
+
+    ddp.comm.broadcast_coalesced = spy
+    for step in range(3):
+        x = torch.randn(16, 8, generator=torch.Generator().manual_seed(100 * step + rank))
+        ddp(x).sum().backward()
+    bn = m[1]
+    return sent, bn.running_mean.clone(), bn.num_batches_tracked.item()
+
+
+def test_ddp_broadcasts_only_changed_buffers():
+    """first forward syncs all 4 buffers, later ones only the 3 BatchNorm buffers; rank 1's BN
+    statistics follow rank 0's each step (identical after the broadcast + identical update)."""
+    (s0, rm0, n0), (s1, rm1, n1) = run_workers(_w_ddp_buffers, 2)
+    assert s0 == s1 == [4, 3, 3]
+    assert n0 == n1 == 3
+    assert not torch.equal(rm0, rm1)   # each rank's last forward updated with its own batch
