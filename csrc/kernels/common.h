@@ -42,6 +42,14 @@ __device__ __forceinline__ bf16_t f2h(float f) {
 // Load / store 8 consecutive elements of type T as floats.
 template <typename T> struct Vec8;
 template <> struct Vec8<float> {
+  struct raw_t { f32x4 a, b; };
+  __device__ __forceinline__ static raw_t load_raw(const float* p) {
+    return raw_t{*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 4)};
+  }
+  __device__ __forceinline__ static void unpack(const raw_t& r, float* o) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = r.a[i]; o[4 + i] = r.b[i]; }
+  }
   __device__ __forceinline__ static void load(const float* p, float* o) {
     f32x4 a = *reinterpret_cast<const f32x4*>(p);
     f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
@@ -57,6 +65,12 @@ template <> struct Vec8<float> {
   }
 };
 template <> struct Vec8<bf16_t> {
+  typedef u16x8 raw_t;
+  __device__ __forceinline__ static raw_t load_raw(const bf16_t* p) { return *reinterpret_cast<const u16x8*>(p); }
+  __device__ __forceinline__ static void unpack(const raw_t& r, float* o) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = bf2f(r[i]);
+  }
   __device__ __forceinline__ static void load(const bf16_t* p, float* o) {
     u16x8 a = *reinterpret_cast<const u16x8*>(p);
 #pragma unroll

@@ -310,6 +310,37 @@ __device__ __forceinline__ void dma_tile(const bf16_t* base, int64_t row_stride,
   }
 }
 
+// LDS-DMA of a TILE-row window through a buffer resource (T8): the per-lane byte offset of this lane's
+// 16-B chunk (row-major, XOR-swizzled) is computed once per kernel; per tile only the wave-uniform
+// descriptor (base = first row of the window, num_records = bytes of the rows that exist) is rebuilt
+// in SGPRs, so `buffer_load_dwordx4 ... offen lds` issues with no VALU address math, and rows past the
+// end of the tensor come back as zeros from the range check (callers mask them) -- no clamping path.
+template <int D>
+struct DmaLane {
+  static constexpr int RPI = 1024 / (D * 2), NI = 16 / RPI, LPR = 64 / RPI;
+  uint32_t off[NI];
+  __device__ __forceinline__ void init(int64_t row_stride, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int row = 16 * w + RPI * i + lane / LPR;
+      const int c = (lane % LPR) ^ swz_f<D>(row);
+      off[i] = (uint32_t)((row * row_stride + c * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
+                                        int w) const {
+#if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
+    const int rows_left = nrows - row0;
+    const int bytes = rows_left > 0 ? (int)((int64_t)(rows_left - 1) * row_stride * 2 + D * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * row_stride), 0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off[i], 0, 0, 0);
+#endif
+  }
+};
+
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
   using IO = TileIO<D>;
@@ -528,9 +559,12 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
   int kend = p.Sk;
   if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
   const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  DmaLane<D> lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
   if (ntiles > 0) {
-    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
-    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+    lk.issue(Kp, p.k_ss, 0, p.Sk, smem, w);
+    lv.issue(Vp, p.v_ss, 0, p.Sk, smem + TE, w);
   }
 
   // per-lane LDS element offsets (swizzle depends on row & 15 only)
@@ -574,8 +608,8 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
         __syncthreads();
         if (tt + 1 < ntiles) {
           bf16_t* nb = smem + (1 - u) * 2 * TE;
-          dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
-          dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
+          lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
+          lv.issue(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w);
         }
         const int k0 = tt * TILE;
         if (!(CAUSAL && k0 > qw + 31 + off)) {
@@ -1151,7 +1185,9 @@ struct BwdKVTile {
     for (int e = 0; e < N; ++e) {
       const int r = e0 + e, rr = (r & 3) + 8 * (r >> 2) + 32 * qs;
       float pv = fast_exp2(fmaf(sv[r], sl2, nl[e]));
-      pv = (rr < tmask || rr >= tsq) ? 0.f : pv;
+      // causal mask only: query rows past Sq arrive as zero Q / dO rows (buffer range check), which
+      // contribute exactly 0 to dK (dS * q) and dV (p * dO) without masking
+      if constexpr (CAUSAL) pv = rr < tmask ? 0.f : pv;
       sv[r] = pv;
       dpv[r] = pv * (dpv[r] - dl[e]);
     }
@@ -1281,12 +1317,15 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
   const int total = qtiles * group;
 
+  DmaLane<D> lq, lg;
+  lq.init(p.q_ss, w, lane);
+  lg.init(p.do_ss, w, lane);
   auto issue = [&](int it, int buf) {
     const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
     const int hq = hk * group + hi;
     bf16_t* base = smem + buf * 2 * TE;
-    dma_tile<D>(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w, lane);
-    dma_tile<D>(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w, lane);
+    lq.issue(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w);
+    lg.issue(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w);
     if (w == 0) dma_f32_row(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][0], lane);
     if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][1], lane);
   };
@@ -1413,9 +1452,12 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int kend = p.Sk;
   if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
   const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  DmaLane<D> lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
   if (ntiles > 0) {
-    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
-    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
+    lk.issue(Kp, p.k_ss, 0, p.Sk, smem, w);
+    lv.issue(Vp, p.v_ss, 0, p.Sk, smem + TE, w);
   }
   u16x8 qf[KS], gf[KS];
 #pragma unroll
@@ -1449,8 +1491,8 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
       __syncthreads();
       if (tt + 1 < ntiles) {
         bf16_t* nb = smem + (1 - u) * 2 * TE;
-        dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
-        dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
+        lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
+        lv.issue(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w);
       }
       const int k0 = tt * TILE;
       if (CAUSAL && k0 > qw + 31 + off) continue;               // every key of the tile follows these queries

@@ -11,6 +11,7 @@
 // (BASELINE.json configs 3-5); semantics of torch.nn.functional.layer_norm / rms_norm.
 #include "common.h"
 #include "reduce.h"
+#include <stdlib.h>
 
 using namespace pdt;
 
@@ -98,73 +99,112 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
   }
 }
 
-// Backward: one wave per row.  Pass 1 reads x, dy, w and forms the two row reductions while the
-// lane's dgamma/dbeta contributions accumulate in REGISTERS (ITERS*16 floats); pass 2 re-reads the
-// (L1/L2-resident) row to write dx (+ the fused residual gradient).  At the end the 4 waves of a
-// workgroup fold their accumulators through one [2][N] LDS buffer (wave-by-wave, so no LDS atomics)
-// and the workgroup writes ONE partial row; a 2-level column reduce finishes dgamma/dbeta.
-template <typename T, typename W, int ITERS, bool RMS>
-__global__ __launch_bounds__(NT) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+// Backward: one wave per row, single pass over HBM.  The row's x and dy stay in registers between the
+// two row reductions and the dx write (no re-read), gamma is loaded once per wave, and the NEXT row's
+// x / dy / dres loads are issued before the current row's reductions so every wave keeps a full row of
+// 16-B loads in flight (the previous two-pass form was latency-bound at ~1.4 TB/s).  Per-lane
+// dgamma/dbeta partials accumulate in registers; at the end the 4 waves of a workgroup fold them
+// through one [2][N] LDS buffer (wave by wave, no atomics) and the workgroup writes ONE partial row;
+// a 2-level column reduce (reduce.h) finishes dgamma/dbeta.
+template <typename T, typename W, int ITERS, bool RMS, bool DRES, int OCC>
+__global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const W* __restrict__ w, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                       T* __restrict__ dx, float* __restrict__ dw_part,
                                                       float* __restrict__ db_part, int rows, int N) {
   extern __shared__ __attribute__((aligned(16))) float sacc[];   // [2][N]
+  typedef typename Vec8<T>::raw_t raw_t;
+  typedef typename Vec8<W>::raw_t wraw_t;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float invN = 1.f / (float)N;
-  float dwa[ITERS][8], dba[ITERS][8];
+  // loads are unconditional (column clamped into the row, row clamped into the matrix); lanes past
+  // the row end are masked at accumulate / store time
+  int cc[ITERS];
+  bool cv[ITERS];
 #pragma unroll
-  for (int it = 0; it < ITERS; ++it)
+  for (int it = 0; it < ITERS; ++it) {
+    const int col = it * 512 + lane * 8;
+    cv[it] = col < N;
+    cc[it] = cv[it] ? col : N - 8;
+  }
+  float dwa[ITERS][8], dba[ITERS][8];
+  wraw_t wr[ITERS];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; }
-
-  for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
-    const T* xr = x + (int64_t)row * N;
-    const T* gr = dy + (int64_t)row * N;
+    wr[it] = Vec8<W>::load_raw(w + cc[it]);
+  }
+  const int stride = gridDim.x * RPB;
+  int row = blockIdx.x * RPB + wid;
+  raw_t cx[ITERS], cg[ITERS], cr[DRES ? ITERS : 1];
+  {
+    const int64_t r = min(row, rows - 1);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      cx[it] = Vec8<T>::load_raw(x + r * N + cc[it]);
+      cg[it] = Vec8<T>::load_raw(dy + r * N + cc[it]);
+      if constexpr (DRES) cr[it] = Vec8<T>::load_raw(dres + r * N + cc[it]);
+    }
+  }
+  for (; row < rows; row += stride) {
+    // prefetch the next row (double buffer): in flight during this row's math and reductions
+    raw_t nx[ITERS], ng[ITERS], nr[DRES ? ITERS : 1];
+    const int64_t nrow = min(row + stride, rows - 1);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      nx[it] = Vec8<T>::load_raw(x + nrow * N + cc[it]);
+      ng[it] = Vec8<T>::load_raw(dy + nrow * N + cc[it]);
+      if constexpr (DRES) nr[it] = Vec8<T>::load_raw(dres + nrow * N + cc[it]);
+    }
     const float mean = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
     float a = 0.f, bsum = 0.f;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-      const int col = it * 512 + lane * 8;
-      if (col < N) {
-        float xv[8], dv[8], wv[8];
-        Vec8<T>::load(xr + col, xv);
-        Vec8<T>::load(gr + col, dv);
-        Vec8<W>::load(w + col, wv);
+      float xv[8], dv[8], wv[8];
+      Vec8<T>::unpack(cx[it], xv);
+      Vec8<T>::unpack(cg[it], dv);
+      Vec8<W>::unpack(wr[it], wv);
+      const float m = cv[it] ? 1.f : 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float xh = (xv[k] - mean) * rstd;
-          const float g = dv[k] * wv[k];
-          a += g * xh;
-          bsum += g;
-          dwa[it][k] += dv[k] * xh;
-          dba[it][k] += dv[k];
-        }
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[k] - mean) * rstd;
+        const float d = dv[k] * m;
+        const float g = d * wv[k];
+        a += g * xh;
+        bsum += g;
+        dwa[it][k] += d * xh;
+        dba[it][k] += d;
       }
     }
     a = wave_sum(a) * invN;
     if (!RMS) bsum = wave_sum(bsum) * invN;
+    if constexpr (sizeof(T) == 2) {
+      // re-unpack the packed row for the dx pass instead of keeping fp32 copies live across the
+      // reductions (halves the row's register footprint: 2 waves/SIMD at N = 2048)
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(cx[it]), "+v"(cg[it]));
+    }
     T* dxr = dx + (int64_t)row * N;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-      const int col = it * 512 + lane * 8;
-      if (col < N) {
-        float xv[8], dv[8], wv[8], o[8];
-        Vec8<T>::load(xr + col, xv);
-        Vec8<T>::load(gr + col, dv);
-        Vec8<W>::load(w + col, wv);
+      float xv[8], dv[8], wv[8], o[8];
+      Vec8<T>::unpack(cx[it], xv);
+      Vec8<T>::unpack(cg[it], dv);
+      Vec8<W>::unpack(wr[it], wv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          o[k] = rstd * (dv[k] * wv[k] - (RMS ? 0.f : bsum) - (xv[k] - mean) * rstd * a);
-        if (dres != nullptr) {
-          float r8[8];
-          Vec8<T>::load(dres + (int64_t)row * N + col, r8);
+      for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[k] * wv[k] - (RMS ? 0.f : bsum) - (xv[k] - mean) * rstd * a);
+      if constexpr (DRES) {
+        float rv[8];
+        Vec8<T>::unpack(cr[it], rv);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] += r8[k];
-        }
-        Vec8<T>::store(dxr + col, o);
+        for (int k = 0; k < 8; ++k) o[k] += rv[k];
       }
+      if (cv[it]) Vec8<T>::store(dxr + cc[it], o);
+      cx[it] = nx[it];
+      cg[it] = ng[it];
+      if constexpr (DRES) cr[it] = nr[it];
     }
   }
   // fold the 4 waves' accumulators: wave 0 stores, waves 1..3 add in turn (no atomics)
@@ -299,7 +339,8 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
 // fast path: one partial row per workgroup (LDS-accumulated); fallback: one per block
 int bwd_partial_rows(int rows, int N) {
   // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
-  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB, N <= 2048 ? 1024 : (N <= 4096 ? 512 : 256));
+  // a few rows per wave (so the row prefetch pays) while covering the chip: ~2 waves per SIMD
+  if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB * 4, 512);
   return grid_for(rows, 1, 512);
 }
 
@@ -315,13 +356,19 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   if (N % 8 == 0 && N <= 8192) {
     const int iters = (N + 511) / 512;
     const size_t lds = 2 * (size_t)N * sizeof(float);
-#define PDT_NB(I) norm_bwd_kernel<T, W, I, RMS><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N)
+    static const int occ2 = [] { const char* e = getenv("PDT_LN_BWD_OCC"); return e && atoi(e) == 2; }();
+#define PDT_NB1(I, O)                                                                                                 \
+  if (DR) norm_bwd_kernel<T, W, I, RMS, true, O><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N); \
+  else norm_bwd_kernel<T, W, I, RMS, false, O><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N)
+#define PDT_NB(I) \
+  do { if (occ2) { PDT_NB1(I, 2); } else { PDT_NB1(I, 1); } } while (0)
     if (iters <= 1) PDT_NB(1);
     else if (iters <= 2) PDT_NB(2);
     else if (iters <= 4) PDT_NB(4);
     else if (iters <= 8) PDT_NB(8);
     else PDT_NB(16);
 #undef PDT_NB
+#undef PDT_NB1
   } else {
     norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N);
   }

@@ -85,7 +85,20 @@ def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
                 f.result()
     if _newer(KERNEL_LIB, objs):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", KERNEL_LIB], verbose)
+        _check_no_missing_stubs(KERNEL_LIB)
     return KERNEL_LIB
+
+
+def _check_no_missing_stubs(lib: str) -> None:
+    """A kernel whose host-side stub was not emitted links fine and only fails at dlopen on the GPU box
+    ("undefined symbol: ...__device_stub__..."): catch it at build time."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-D", "--undefined-only", lib], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        os.remove(lib)
+        raise RuntimeError("kernel library has unresolved host stubs (device-only code leaked into the host "
+                           "pass?):\n  " + "\n  ".join(missing[:10]))
 
 
 def runtime_ext_path() -> str:

@@ -462,5 +462,5 @@ def test_swinir_window_attention_module_gpu():
     blk_gpu = blk.to(DEV)
     y = blk_gpu(x.to(DEV), (32, 32))
     y.sum().backward()
-    assert rel_err(y, y_cpu) < 1e-4
-    assert rel_err(blk_gpu.attn.relative_position_bias_table.grad, g_cpu) < 1e-3
+    assert rel_err(y.cpu(), y_cpu) < 1e-4
+    assert rel_err(blk_gpu.attn.relative_position_bias_table.grad.cpu(), g_cpu) < 1e-3
