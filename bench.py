@@ -26,7 +26,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="gpt2-fsdp",
-                    choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp", "llama3-fsdp"])
+                    choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp", "llama3-fsdp", "swinir-stoke"])
     ap.add_argument("--model", default=None)
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--seq", type=int, default=1024)
@@ -62,6 +62,8 @@ def main():
     torch.manual_seed(1234)
     if args.workload.startswith("gpt2") or args.workload.startswith("llama"):
         result = bench_gpt2(args, comm, dev, world, rank)
+    elif args.workload == "swinir-stoke":
+        result = bench_swinir(args, comm, dev, world, rank)
     else:
         result = bench_resnet(args, comm, dev, world, rank)
     if rank == 0:
@@ -190,6 +192,45 @@ def bench_resnet(args, comm, dev, world, rank):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": "resnet50", "global_batch": world * mb, "seq_len": None, "parallelism": f"dp{world}",
                        "image": "3x224x224"}}
+
+
+def bench_swinir(args, comm, dev, world, rank):
+    """The reference's own workload (Stoke-DDP.py:159,169-170,182-254): SwinIR-S x2 through the Stoke-style
+    Trainer with DDP + OSS (ZeRO-1) + ShardedDDP (ZeRO-2), 18 LR 128x128 -> HR 256x256 patches per device,
+    grad_accum 2, AdamW(1e-3, (0.9, 0.99), 1e-8, wd 1e-4), clip-norm 0.1, bf16 autocast; MSE loss
+    (Fairscale-DDP.py:76).  One step = one optimizer step (2 micro-batches)."""
+    import torch
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
+    from pytorch_distributedtraining_amd.trainer import ClipGradNormConfig, StokeOptimizer, Trainer
+    mb = args.micro_batch or 18
+    accum = 2
+    model = swinir_s_x2()
+    opt = StokeOptimizer(optimizer=torch.optim.AdamW,
+                         optimizer_kwargs={"lr": 1e-3, "betas": (0.9, 0.99), "eps": 1e-8, "weight_decay": 1e-4})
+    tr = Trainer(model, optimizer=opt, loss=torch.nn.functional.mse_loss, batch_size_per_device=mb,
+                 grad_accum_steps=accum, grad_clip=ClipGradNormConfig(max_norm=0.1, norm_type=2.0), gpu=True,
+                 fp16="bf16", distributed="ddp" if world > 1 else None, fairscale_oss=world > 1,
+                 fairscale_sddp=world > 1, verbose=False, comm=comm)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    data = [(torch.rand(mb, 3, 128, 128, device=dev, generator=g), torch.rand(mb, 3, 256, 256, device=dev, generator=g))
+            for _ in range(accum)]
+
+    def step():
+        for x, y in data:
+            loss = tr.loss(tr.model(x), y)
+            tr.backward(loss)
+            tr.step()
+
+    dt = timed_loop(step, args, comm, dev)
+    sps = world * mb * accum * args.steps / dt
+    return {"metric": "samples/sec SwinIR-S x2 Stoke DDP+OSS+SDDP (whole node)", "value": round(sps, 2),
+            "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "swinir-s-x2", "global_batch": world * mb * accum, "seq_len": None,
+                       "parallelism": f"dp{world}+zero2" if world > 1 else "dp1", "image": "3x128x128->3x256x256",
+                       "grad_accum": accum}}
 
 
 if __name__ == "__main__":

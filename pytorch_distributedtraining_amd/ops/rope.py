@@ -66,4 +66,12 @@ def apply_rope(x, cos, sin, pos0: int = 0):
     D = x.shape[-1]
     if not x.is_cuda or (D // 2) % 8 != 0 or x.dtype not in (torch.float32, torch.bfloat16):
         return _rope_ref(x, cos, sin, pos0, 1.0)
+    # the kernel reads fp32 [>= pos0 + S, D/2] tables (a model cast to bf16 also casts its table buffers)
+    if cos.dtype != torch.float32 or not cos.is_contiguous():
+        cos = cos.float().contiguous()
+    if sin.dtype != torch.float32 or not sin.is_contiguous():
+        sin = sin.float().contiguous()
+    if cos.shape != sin.shape or cos.dim() != 2 or cos.shape[1] != D // 2 or cos.shape[0] < pos0 + x.shape[1]:
+        raise ValueError(f"apply_rope: tables {tuple(cos.shape)} do not cover positions {pos0}..{pos0 + x.shape[1]}"
+                         f" x head_dim/2={D // 2}")
     return _RopeFn.apply(x, cos, sin, pos0)

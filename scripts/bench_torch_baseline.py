@@ -59,11 +59,59 @@ class GPT(nn.Module):
         return F.cross_entropy(logits.view(-1, logits.shape[-1]).float(), labels.reshape(-1))
 
 
+def resnet50_ddp(a, dev, world, rank):
+    """Stock torch DDP (25 MiB buckets) + bf16 autocast + torch fused AdamW + clip_grad_norm_ on the
+    same ResNet-50 / batch / synthetic data as ``bench.py --workload resnet50-ddp``."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pytorch_distributedtraining_amd.models.resnet import resnet50  # plain nn.Conv2d / nn.BatchNorm2d
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    mb = a.micro_batch or 256
+    model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    model = DDP(model, device_ids=[dev.index])
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4, fused=True)
+    x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (mb,), device=dev)
+
+    def step(i):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dt, loss = timed(step, a, dev)
+    sps = world * mb * a.steps / dt
+    if rank == 0:
+        print(f"[torch-baseline] resnet50 loss={loss.item():.4f} step={1000*dt/a.steps:.1f}ms", file=sys.stderr)
+        print(json.dumps({"metric": "samples/sec ResNet-50 DDP (whole node) -- stock PyTorch-ROCm baseline",
+                          "value": round(sps, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+                          "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_gpu": mb,
+                          "stack": "torch DDP + autocast bf16 + MIOpen + fused torch AdamW"}))
+
+
+def timed(step, a, dev):
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return float(dt.item()), loss
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "resnet50-ddp"])
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--seq", type=int, default=1024)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,6 +122,11 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if a.workload == "resnet50-ddp":
+        resnet50_ddp(a, dev, world, rank)
+        dist.destroy_process_group()
+        return
+    a.micro_batch = a.micro_batch or 16
     from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
     from torch.distributed.fsdp.wrap import ModuleWrapPolicy
     torch.manual_seed(0)
@@ -96,18 +149,7 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
-    for i in range(a.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
+    dt, loss = timed(step, a, dev)
     tps = world * a.micro_batch * a.seq * a.steps / dt
     if rank == 0:
         print(f"[torch-baseline] params={n/1e9:.3f}B loss={loss.item():.4f} step={1000*dt/a.steps:.1f}ms",

@@ -408,6 +408,29 @@ def test_llama_tiny_fsdp_step():
     assert loss.item() < l0.item()
 
 
+@pytest.mark.parametrize("family", ["llama", "gpt2"])
+def test_causal_lm_has_no_future_leak(family):
+    """Changing token t+1 must not change logits at positions <= t (whole model, multi-tile sequence,
+    GQA 4:1 with head_dim 128 on the Llama side -- the 8B's attention shape class)."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.models.llama import build_llama
+    torch.manual_seed(0)
+    with torch.device(DEV):
+        if family == "llama":
+            m = build_llama("llama3-tiny", dim=1024, n_heads=8, n_kv_heads=2, max_seq_len=1024)
+        else:
+            m = build_gpt2("gpt2-tiny", n_embd=512, n_head=4, n_positions=1024)
+    m = m.to(torch.bfloat16).eval()
+    S, t = 1024, 700
+    x = torch.randint(0, 512, (2, S), device=DEV)
+    y = x.clone()
+    y[:, t + 1:] = torch.randint(0, 512, (2, S - t - 1), device=DEV)
+    with torch.no_grad():
+        a, b = m(x).float(), m(y).float()
+    assert torch.equal(a[:, :t + 1], b[:, :t + 1])
+    assert not torch.equal(a[:, t + 1:], b[:, t + 1:])
+
+
 def test_linear_colsum_bias_grad():
     from pytorch_distributedtraining_amd.ops.linear import linear
     x = torch.randn(4, 100, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
