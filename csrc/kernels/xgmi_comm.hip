@@ -1,0 +1,281 @@
+// Peer-to-peer xGMI collectives for one node of MI355X: every rank owns one
+// symmetric buffer in HBM that the other ranks map with hipIpcOpenMemHandle, and the collectives are
+// plain HIP kernels that READ peers' buffers directly over the xGMI mesh (7 links per GPU, all used at
+// once) instead of a ring that drives one link per step.
+//
+//   symmetric buffer = [signal block 4 KB][staging slot 0][staging slot 1]
+//   signal block     = uint32 sig[NBAR][MAXW] (sig[b][p] = last epoch peer p reached barrier b at) + error word
+//
+// Protocol per call (epoch e = host call counter, identical on every rank, never 0):
+//   K1 copy-in   : the local input is stored into this rank's staging slot (e & 1), write-through at
+//                  system scope (sc0 sc1), so no peer can read a stale line from any L2.
+//   K2.. phases  : every block signals barrier b to every peer (system-scope atomic store into the PEER's
+//                  signal block) and waits until every peer signalled b for epoch e in its own block; then
+//                  it reads peers' slots with system-scope (cache-bypassing) loads, reduces in fp32 and
+//                  writes the result.  Signals are idempotent stores of the epoch, so any number of blocks
+//                  may send them and no block depends on another block of its grid (no residency
+//                  assumption).  Waits are bounded: on timeout the block records an error word and leaves.
+//   Slot reuse   : slot (e & 1) is rewritten at call e+2, whose copy-in runs after this rank passed the
+//                  first barrier of call e+1, which every peer signals only after finishing call e.
+//
+// one-shot all-reduce (latency class: scalars, grad-norm, SyncBN stats): 2 kernels, every rank reads W
+// slots.  two-shot all-reduce (bandwidth class): reduce-scatter phase (rank r reduces chunk r from all
+// peers into its own slot) + all-gather phase (every rank reads chunk p from peer p): 2(W-1)/W of the
+// payload crosses the fabric, spread over all 7 links.  all_gather / reduce_scatter: 2 kernels each.
+//
+// The scalar data cache is never written: flags and payload use vector atomics / vector buffer stores.
+#include "common.h"
+#include <string.h>
+
+using namespace pdt;
+
+namespace {
+
+constexpr int MAXW = 8;
+constexpr int NBAR = 4;
+constexpr int64_t SIG_BYTES = 4096;
+constexpr int ERR_OFF = 1024;         // byte offset of the error word in the signal block
+constexpr int NT = 256;
+constexpr int SYS = 1 | 16;           // buffer-op cache policy: sc0 | sc1 = system-scope coherent
+
+struct XArgs {
+  char* buf[MAXW];                    // symmetric buffer base of every rank (own + IPC-mapped peers)
+  int rank, world;
+  unsigned epoch;
+  unsigned spin_limit;
+  int64_t slot_bytes;
+};
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+__device__ __forceinline__ char* slot_of(const XArgs& a, int p) {
+  return a.buf[p] + SIG_BYTES + (int64_t)(a.epoch & 1u) * a.slot_bytes;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// Every block: signal barrier `b` of epoch a.epoch to all peers, then wait for all peers' signals.
+__device__ __forceinline__ void mesh_barrier(const XArgs& a, int b) {
+  const int t = threadIdx.x;
+  if (t < a.world) {
+    gu32* remote = (gu32*)(a.buf[t]) + b * MAXW + a.rank;
+    __hip_atomic_store(remote, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    gu32* mine = (gu32*)(a.buf[a.rank]) + b * MAXW + t;
+    unsigned spins = 0;
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+      if (++spins > a.spin_limit) {   // give up: record the failure, never hang the queue
+        __hip_atomic_fetch_or((gu32*)(a.buf[a.rank] + ERR_OFF), 1u << b, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system-scope acquire (one lane per peer)
+  }
+  __syncthreads();
+}
+
+template <typename T> struct Acc;
+template <> struct Acc<float> {   // 16 B = 4 fp32
+  static constexpr int N = 4;
+  __device__ static void add(float* acc, const u32x4& v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += __uint_as_float(v[i]);
+  }
+  __device__ static u32x4 pack(const float* acc, float s) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(acc[i] * s);
+    return r;
+  }
+};
+template <> struct Acc<bf16_t> {  // 16 B = 8 bf16
+  static constexpr int N = 8;
+  __device__ static void add(float* acc, const u32x4& v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[2 * i] += __uint_as_float(v[i] << 16);
+      acc[2 * i + 1] += __uint_as_float(v[i] & 0xffff0000u);
+    }
+  }
+  __device__ static u32x4 pack(const float* acc, float s) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      r[i] = (uint32_t)f2bf(acc[2 * i] * s) | ((uint32_t)f2bf(acc[2 * i + 1] * s) << 16);
+    return r;
+  }
+};
+
+// K1: local input -> own staging slot (write-through, system scope)
+__global__ __launch_bounds__(NT) void xgmi_copy_in_kernel(const u32x4* __restrict__ src, XArgs a, int64_t nvec) {
+  const __amdgpu_buffer_rsrc_t dst = rsrc_of(slot_of(a, a.rank), nvec * 16);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT)
+    __builtin_amdgcn_raw_buffer_store_b128(src[i], dst, (int)(i * 16), 0, SYS);
+}
+
+// sum over ranks of vector i of every peer slot, starting at byte offset `off`
+template <typename T>
+__device__ __forceinline__ u32x4 reduce_vec(const __amdgpu_buffer_rsrc_t* src, int world, int64_t byte, float s) {
+  float acc[Acc<T>::N];
+#pragma unroll
+  for (int k = 0; k < Acc<T>::N; ++k) acc[k] = 0.f;
+  u32x4 v[MAXW];
+#pragma unroll
+  for (int p = 0; p < MAXW; ++p)   // all W loads in flight before the first add (one xGMI round trip)
+    if (p < world) v[p] = __builtin_amdgcn_raw_buffer_load_b128(src[p], (int)byte, 0, SYS);
+#pragma unroll
+  for (int p = 0; p < MAXW; ++p)
+    if (p < world) Acc<T>::add(acc, v[p]);
+  return Acc<T>::pack(acc, s);
+}
+
+__device__ __forceinline__ void peer_rsrcs(const XArgs& a, int64_t bytes, __amdgpu_buffer_rsrc_t (&r)[MAXW]) {
+#pragma unroll
+  for (int p = 0; p < MAXW; ++p) r[p] = rsrc_of(slot_of(a, p < a.world ? p : 0), bytes);
+}
+
+// one-shot all-reduce: out[i] = s * sum_p slot_p[i]
+template <typename T>
+__global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __restrict__ out, int64_t nvec, float s) {
+  mesh_barrier(a, 0);
+  __amdgpu_buffer_rsrc_t src[MAXW];
+  peer_rsrcs(a, nvec * 16, src);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT)
+    out[i] = reduce_vec<T>(src, a.world, i * 16, s);
+}
+
+// two-shot phase 1 / reduce_scatter: chunk `rank` (cvec vectors) reduced from every peer.
+//   to_slot: write into own staging chunk (phase 1 of two-shot) instead of `out`.
+template <typename T>
+__global__ __launch_bounds__(NT) void xgmi_reduce_chunk_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, float s,
+                                                              int to_slot) {
+  mesh_barrier(a, 0);
+  const int64_t total = cvec * a.world;
+  __amdgpu_buffer_rsrc_t src[MAXW];
+  peer_rsrcs(a, total * 16, src);
+  const int64_t base = (int64_t)a.rank * cvec;
+  const __amdgpu_buffer_rsrc_t mine = rsrc_of(slot_of(a, a.rank), total * 16);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < cvec; i += (int64_t)gridDim.x * NT) {
+    const u32x4 v = reduce_vec<T>(src, a.world, (base + i) * 16, s);
+    if (to_slot) __builtin_amdgcn_raw_buffer_store_b128(v, mine, (int)((base + i) * 16), 0, SYS);
+    else out[i] = v;
+  }
+}
+
+// all-gather: out[p * cvec + i] = chunk p of peer p's slot (chunk_in_slot: peer p keeps its piece at
+// chunk p of its slot (two-shot phase 2) or at offset 0 (all_gather of a shard))
+__global__ __launch_bounds__(NT) void xgmi_gather_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, int bar,
+                                                         int chunk_in_slot) {
+  mesh_barrier(a, bar);
+  const int64_t total = cvec * a.world;
+  for (int p = 0; p < a.world; ++p) {
+    const int64_t off = chunk_in_slot ? (int64_t)p * cvec : 0;
+    const __amdgpu_buffer_rsrc_t src = rsrc_of(slot_of(a, p), (off + cvec) * 16);
+    for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < cvec; i += (int64_t)gridDim.x * NT)
+      out[(int64_t)p * cvec + i] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)((off + i) * 16), 0, SYS);
+  }
+  (void)total;
+}
+
+__global__ void xgmi_barrier_kernel(XArgs a) { mesh_barrier(a, 3); }
+
+int grid_of(int64_t nvec) {
+  int64_t g = (nvec + NT - 1) / NT;
+  if (g < 1) g = 1;
+  if (g > 512) g = 512;
+  return (int)g;
+}
+
+}  // namespace
+
+// -------------------------------------------------------------------------------------------------
+// host entry points
+// -------------------------------------------------------------------------------------------------
+PDT_API int pdt_xgmi_alloc(int64_t bytes, int uncached, void** out) {
+  // uncached fine-grained HBM: every access to the staging / signal words is coherent across devices
+  // (the kernels also use cache-bypassing sc0|sc1 accesses, so plain device memory works as well)
+  hipError_t e = uncached ? hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached)
+                          : hipMalloc(out, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*out, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
+PDT_API int pdt_xgmi_free(void* p) { return (int)hipFree(p); }
+
+PDT_API int pdt_xgmi_ipc_get(void* p, void* handle_out /* 64 B */) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e == hipSuccess) memcpy(handle_out, &h, sizeof(h));
+  return (int)e;
+}
+
+PDT_API int pdt_xgmi_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+PDT_API int pdt_xgmi_ipc_open(const void* handle_in, void** out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle_in, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+PDT_API int pdt_xgmi_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+// error word of this rank's buffer (bit b = a wait at barrier b timed out); cleared by the read
+PDT_API int pdt_xgmi_error(void* own_buf, unsigned* out) {
+  hipError_t e = hipMemcpy(out, (char*)own_buf + ERR_OFF, 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return (int)e;
+  const unsigned z = 0;
+  return (int)hipMemcpy((char*)own_buf + ERR_OFF, &z, 4, hipMemcpyHostToDevice);
+}
+
+// kind: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter, 4 barrier.
+//   in_bytes: bytes of `in` (all-gather: the local shard; reduce-scatter: the full input); multiple of 16
+//   (two-shot / reduce-scatter: multiple of 16 * world).  scale multiplies reduced values (1/world = AVG).
+PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t in_bytes, int dtype, float scale,
+                                const void* const* bufs, int rank, int world, unsigned epoch, int64_t slot_bytes,
+                                unsigned spin_limit, hipStream_t s) {
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || epoch == 0) return (int)hipErrorInvalidValue;
+  if (in_bytes % 16 != 0 || in_bytes > slot_bytes || (dtype != kF32 && dtype != kBF16)) return (int)hipErrorInvalidValue;
+  XArgs a{};
+  for (int p = 0; p < world; ++p) a.buf[p] = (char*)bufs[p];
+  a.rank = rank;
+  a.world = world;
+  a.epoch = epoch;
+  a.spin_limit = spin_limit;
+  a.slot_bytes = slot_bytes;
+  if (kind == 4) {
+    hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  const int64_t nvec = in_bytes / 16;
+  hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, (const u32x4*)in, a, nvec);
+  const bool bf = dtype == kBF16;
+  switch (kind) {
+    case 0:
+      if (bf) hipLaunchKernelGGL(xgmi_allreduce_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale);
+      else hipLaunchKernelGGL(xgmi_allreduce_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale);
+      break;
+    case 1:
+    case 3: {
+      if (nvec % world != 0) return (int)hipErrorInvalidValue;
+      const int64_t cvec = nvec / world;
+      const int to_slot = kind == 1;
+      if (bf) hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<bf16_t>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, to_slot);
+      else hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<float>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, to_slot);
+      if (kind == 1)
+        hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, 1, 1);
+      break;
+    }
+    case 2:
+      hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, 0, 0);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}

@@ -50,12 +50,13 @@ class WindowAttention(nn.Module):
         self.register_buffer("relative_position_index", rel.sum(-1), persistent=True)
         self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
         self.proj = nn.Linear(dim, dim)
+        self.native = True    # False: stock torch path (SDPA + materialised bias), see to_stock_torch()
         nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
 
     def forward(self, x, mask=None):
         Bw, N, C = x.shape
         h = self.num_heads
-        if x.is_cuda:
+        if x.is_cuda and self.native:
             # fused HIP window attention: reads the qkv projection in place, never materialises the
             # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
             qkv = self.qkv(x)
@@ -224,6 +225,20 @@ class SwinIR(nn.Module):
         x = self.upsample(x)
         x = x / self.img_range + mean
         return x[:, :, : H * self.upscale, : W * self.upscale]
+
+
+def to_stock_torch(model: nn.Module) -> nn.Module:
+    """Swap the HIP-kernel layers for stock torch ones (nn.LayerNorm, SDPA window attention) in place --
+    same parameters and state_dict keys; used by the stock PyTorch-ROCm baseline benchmark."""
+    for name, mod in list(model.named_modules()):
+        for cname, child in list(mod.named_children()):
+            if isinstance(child, LayerNorm):
+                ln = nn.LayerNorm(child.normalized_shape, eps=child.eps).to(child.weight.device)
+                ln.load_state_dict(child.state_dict())
+                setattr(mod, cname, ln)
+        if isinstance(mod, WindowAttention):
+            mod.native = False
+    return model
 
 
 def swinir_s_x2(**kw):

@@ -50,7 +50,7 @@ class Handle:
 
 
 class Comm:
-    def __init__(self, group=None, debug: bool | None = None):
+    def __init__(self, group=None, debug: bool | None = None, xgmi: bool | None = None):
         self.group = group
         self.initialized = dist.is_available() and dist.is_initialized()
         if self.initialized:
@@ -65,6 +65,24 @@ class Comm:
         self.debug = debug
         rt = runtime()
         self.tracer = rt.CollectiveTracer(4096) if rt is not None else None
+        self.xgmi = None
+        if xgmi is None:
+            xgmi = os.environ.get("PDT_XGMI", "0") == "1" and self.backend == "nccl"
+        if xgmi and self.world_size > 1 and torch.cuda.is_available():
+            self.enable_xgmi()
+
+    def enable_xgmi(self, **kw):
+        """Route eligible CUDA all_reduce / all_gather / reduce_scatter through the peer-mapped xGMI
+        kernels (parallel/xgmi.py).  Collective: every rank must call it."""
+        from .xgmi import XGMIComm
+        if self.xgmi is None and self.world_size > 1:
+            self.xgmi = XGMIComm(self, **kw)
+        return self.xgmi
+
+    def _xgmi_ok(self, t, kind="all_reduce") -> bool:
+        x = self.xgmi
+        return (x is not None and t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
+                and x.eligible(t.numel() * t.element_size(), kind))
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -79,6 +97,9 @@ class Comm:
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> Handle:
         self._trace("all_reduce:" + op, t)
         if self.world_size == 1:
+            return Handle()
+        if op in ("sum", "avg") and self._xgmi_ok(t):
+            self.xgmi.all_reduce(t, op)          # stream-ordered: complete for every later kernel
             return Handle()
         if op == "avg" and self.is_gloo:
             w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
@@ -101,6 +122,10 @@ class Comm:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp.view_as(out))
+            return Handle()
+        if op in ("sum", "avg") and out.dtype == inp.dtype and self._xgmi_ok(inp, "reduce_scatter") \
+                and out.is_contiguous():
+            self.xgmi.reduce_scatter(out, inp, op)
             return Handle()
         if self.is_gloo:
             buf = inp.clone()
@@ -125,6 +150,9 @@ class Comm:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
+            return Handle()
+        if out.dtype == inp.dtype and out.is_contiguous() and self._xgmi_ok(inp, "all_gather"):
+            self.xgmi.all_gather(out, inp)
             return Handle()
         if self.is_gloo:
             parts = list(out.view(self.world_size, -1).unbind(0))

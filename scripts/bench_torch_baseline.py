@@ -9,6 +9,7 @@ torch.distributed.fsdp.FullyShardedDataParallel (FULL_SHARD, bf16 MixedPrecision
 torch.optim.AdamW(fused=True) + torch.nn.utils.clip_grad_norm_.  Prints one JSON line like bench.py.
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -91,6 +92,43 @@ def resnet50_ddp(a, dev, world, rank):
                           "stack": "torch DDP + autocast bf16 + MIOpen + fused torch AdamW"}))
 
 
+def swinir_stoke(a, dev, world, rank):
+    """Stock torch counterpart of ``bench.py --workload swinir-stoke``: the same SwinIR-S x2 parameters with
+    nn.LayerNorm + SDPA window attention, torch DDP (no_sync on the non-boundary micro-step), bf16 autocast,
+    fused torch AdamW, clip_grad_norm_(0.1), 2 x 18 LR 128x128 patches per optimizer step."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2, to_stock_torch
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    mb, accum = a.micro_batch or 18, 2
+    model = to_stock_torch(swinir_s_x2().to(dev))
+    ddp = DDP(model, device_ids=[dev.index])
+    opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4, fused=True)
+    g = torch.Generator(device=dev).manual_seed(2000 + rank)
+    data = [(torch.rand(mb, 3, 128, 128, device=dev, generator=g), torch.rand(mb, 3, 256, 256, device=dev, generator=g))
+            for _ in range(accum)]
+
+    def step(i):
+        for j, (x, y) in enumerate(data):
+            ctx = ddp.no_sync() if j < accum - 1 else contextlib.nullcontext()
+            with ctx:
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = F.mse_loss(ddp(x).float(), y) / accum
+                loss.backward()
+        torch.nn.utils.clip_grad_norm_(ddp.parameters(), 0.1)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dt, loss = timed(step, a, dev)
+    sps = world * mb * accum * a.steps / dt
+    if rank == 0:
+        print(f"[torch-baseline] swinir loss={loss.item():.4f} step={1000*dt/a.steps:.1f}ms", file=sys.stderr)
+        print(json.dumps({"metric": "samples/sec SwinIR-S x2 DDP (whole node) -- stock PyTorch-ROCm baseline",
+                          "value": round(sps, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+                          "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_gpu": mb,
+                          "stack": "torch DDP + autocast bf16 + SDPA + nn.LayerNorm + fused torch AdamW"}))
+
+
 def timed(step, a, dev):
     for i in range(a.warmup):
         step(i)
@@ -108,7 +146,7 @@ def timed(step, a, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "resnet50-ddp"])
+    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "resnet50-ddp", "swinir-stoke"])
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--micro-batch", type=int, default=None)
@@ -122,8 +160,8 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    if a.workload == "resnet50-ddp":
-        resnet50_ddp(a, dev, world, rank)
+    if a.workload in ("resnet50-ddp", "swinir-stoke"):
+        (resnet50_ddp if a.workload == "resnet50-ddp" else swinir_stoke)(a, dev, world, rank)
         dist.destroy_process_group()
         return
     a.micro_batch = a.micro_batch or 16
