@@ -5,7 +5,8 @@
 // register copy (no Welford needed because the row never leaves the VGPRs).  Backward keeps
 // per-lane dgamma/dbeta partial sums in registers across the rows a wave visits and writes one
 // partial row per wave; a deterministic column-reduce kernel folds them.
-// Fallback (N % 8 != 0 or N > 8192): one workgroup per row streaming from global memory.
+// Narrow rows (N <= 64, N % 4 == 0, e.g. SwinIR-S C = 60): 16 lanes x 4 elements per row, 4 rows per wave.
+// Fallback (other N % 8 != 0, or N > 8192): one workgroup per row streaming from global memory.
 //
 // Reference parity: SwinIR LayerNorm sites (Stoke-DDP.py:206-208), GPT-2/Llama norms
 // (BASELINE.json configs 3-5); semantics of torch.nn.functional.layer_norm / rms_norm.
@@ -312,6 +313,163 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
   }
 }
 
+// ---- narrow rows (N <= 64, N % 4 == 0; SwinIR-S C = 60): 16 lanes x 4 elements per row, 4 rows per
+// wave.  The generic kernel would give a 60-wide row a whole 256-thread workgroup (196 idle threads and
+// two block barriers per row); here a wave normalises 4 rows per pass with shuffle-only reductions.
+constexpr int SM_LPR = 16;                 // lanes per row
+constexpr int SM_RPW = 64 / SM_LPR;        // rows per wave pass
+constexpr int SM_RPB = SM_RPW * RPB;       // rows per block pass
+
+__host__ __device__ __forceinline__ bool small_rows(int N) { return N <= 64 && N % 4 == 0; }
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  __device__ static void load(const float* p, float* o) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+  }
+  __device__ static void store(float* p, const float* o) { *reinterpret_cast<f32x4*>(p) = f32x4{o[0], o[1], o[2], o[3]}; }
+};
+template <> struct Vec4<bf16_t> {
+  __device__ static void load(const bf16_t* p, float* o) {
+    const u16x4 v = *reinterpret_cast<const u16x4*>(p);
+    o[0] = bf2f(v[0]); o[1] = bf2f(v[1]); o[2] = bf2f(v[2]); o[3] = bf2f(v[3]);
+  }
+  __device__ static void store(bf16_t* p, const float* o) {
+    *reinterpret_cast<u16x4*>(p) = u16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+  }
+};
+
+__device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes of one row
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, typename W, bool RMS>
+__global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, const T* __restrict__ res,
+                                                     T* __restrict__ sum_out, const W* __restrict__ w,
+                                                     const W* __restrict__ b, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int N, float eps) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
+  const bool col_ok = c0 < N;
+  float wr[4] = {0, 0, 0, 0}, br[4] = {0, 0, 0, 0};
+  if (col_ok) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wr[k] = to_f<W>(w[c0 + k]);
+      if (!RMS && b != nullptr) br[k] = to_f<W>(b[c0 + k]);
+    }
+  }
+  const float inv_n = 1.f / N;
+  for (int64_t base = ((int64_t)blockIdx.x * RPB + wv) * SM_RPW; base < rows; base += (int64_t)gridDim.x * SM_RPB) {
+    const int64_t row = base + sub;
+    const bool ok = col_ok && row < rows;
+    float v[4] = {0, 0, 0, 0};
+    if (ok) {
+      Vec4<T>::load(x + row * N + c0, v);
+      if (res != nullptr) {
+        float r[4];
+        Vec4<T>::load(res + row * N + c0, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = to_f<T>(from_f<T>(v[k] + r[k]));   // the stored sum, rounded
+        Vec4<T>::store(sum_out + row * N + c0, v);
+      }
+    }
+    float mean = 0.f, rstd;
+    if (RMS) {
+      rstd = rsqrtf(row16_sum(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]) * inv_n + eps);
+    } else {
+      mean = row16_sum(v[0] + v[1] + v[2] + v[3]) * inv_n;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { const float d = ok ? v[k] - mean : 0.f; q += d * d; }
+      rstd = rsqrtf(row16_sum(q) * inv_n + eps);
+    }
+    if (ok) {
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (v[k] - mean) * rstd * wr[k] + br[k];
+      Vec4<T>::store(y + row * N + c0, o);
+    }
+    if (row < rows && c0 == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename T, typename W, bool RMS>
+__global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const T* __restrict__ dres,
+                                                     T* __restrict__ dx, float* __restrict__ dw_part,
+                                                     float* __restrict__ db_part, int rows, int N) {
+  __shared__ __attribute__((aligned(16))) float sred[2][RPB][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
+  const bool col_ok = c0 < N;
+  float wr[4] = {0, 0, 0, 0};
+  if (col_ok) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wr[k] = to_f<W>(w[c0 + k]);
+  }
+  float dwa[4] = {0, 0, 0, 0}, dba[4] = {0, 0, 0, 0};
+  const float inv_n = 1.f / N;
+  for (int64_t base = ((int64_t)blockIdx.x * RPB + wv) * SM_RPW; base < rows; base += (int64_t)gridDim.x * SM_RPB) {
+    const int64_t row = base + sub;
+    const bool ok = col_ok && row < rows;
+    float xv[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0};
+    float mean = 0.f, rstd = 0.f;
+    if (ok) {
+      Vec4<T>::load(x + row * N + c0, xv);
+      Vec4<T>::load(dy + row * N + c0, g);
+      mean = RMS ? 0.f : mean_in[row];
+      rstd = rstd_in[row];
+    }
+    float xh[4], gw[4], a = 0.f, bs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xh[k] = ok ? (xv[k] - mean) * rstd : 0.f;
+      gw[k] = g[k] * wr[k];
+      a += gw[k] * xh[k];
+      bs += gw[k];
+      dwa[k] += g[k] * xh[k];
+      dba[k] += g[k];
+    }
+    a = row16_sum(a) * inv_n;
+    bs = RMS ? 0.f : row16_sum(bs) * inv_n;
+    if (ok) {
+      float o[4];
+      if (dres != nullptr) Vec4<T>::load(dres + row * N + c0, o);
+      else o[0] = o[1] = o[2] = o[3] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] += rstd * (gw[k] - bs - xh[k] * a);
+      Vec4<T>::store(dx + row * N + c0, o);
+    }
+  }
+  // fold the 4 row groups of the wave (lanes c, c+16, c+32, c+48 share columns), then the block's waves
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dwa[k] += __shfl_xor(dwa[k], 16, 64); dwa[k] += __shfl_xor(dwa[k], 32, 64);
+    dba[k] += __shfl_xor(dba[k], 16, 64); dba[k] += __shfl_xor(dba[k], 32, 64);
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { sred[0][wv][c0 + k] = dwa[k]; sred[1][wv][c0 + k] = dba[k]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += NT) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < RPB; ++q) { s0 += sred[0][q][c]; s1 += sred[1][q][c]; }
+    dw_part[(int64_t)blockIdx.x * N + c] = s0;
+    if (db_part) db_part[(int64_t)blockIdx.x * N + c] = s1;
+  }
+}
+
 // column reductions of the [R, N] dgamma/dbeta partials: reduce.h (two-level, deterministic)
 using red::col_reduce;
 
@@ -320,7 +478,10 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
                float* rstd, int rows, int N, float eps, hipStream_t st) {
   const T* X = (const T*)x; const T* R = (const T*)res; T* S = (T*)sum_out;
   const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
-  if (N % 8 == 0 && N <= 8192) {
+  if (small_rows(N)) {
+    norm_fwd_small<T, W, RMS><<<grid_for(rows, SM_RPB, 256 * 16), NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N,
+                                                                              eps);
+  } else if (N % 8 == 0 && N <= 8192) {
     const int grid = grid_for(rows, RPB, 256 * 16);
     const int iters = (N + 511) / 512;
 #define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N, eps)
@@ -340,6 +501,7 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
 int bwd_partial_rows(int rows, int N) {
   // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
   // a few rows per wave (so the row prefetch pays) while covering the chip: ~2 waves per SIMD
+  if (small_rows(N)) return grid_for(rows, SM_RPB * 8, 512);
   if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB * 4, 512);
   return grid_for(rows, 1, 512);
 }
@@ -353,7 +515,9 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   const int R = bwd_partial_rows(rows, N);
   float* dwp = ws;
   float* dbp = (db != nullptr) ? ws + (int64_t)R * N : nullptr;
-  if (N % 8 == 0 && N <= 8192) {
+  if (small_rows(N)) {
+    norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N);
+  } else if (N % 8 == 0 && N <= 8192) {
     const int iters = (N + 511) / 512;
     const size_t lds = 2 * (size_t)N * sizeof(float);
     static const int occ2 = [] { const char* e = getenv("PDT_LN_BWD_OCC"); return e && atoi(e) == 2; }();

@@ -233,10 +233,382 @@ __global__ __launch_bounds__(1024) void win_attn_bwd_kernel(const T* __restrict_
 template <int DP>
 int dp_ok(int d) { return d <= DP; }
 
+// ================================================================================================
+// MFMA path (bf16, head_dim <= 16, N <= 64; SwinIR-S: N = 64, d = 10): the window's 64 x 64 score tile
+// per head is 4 v_mfma_f32_32x32x16_bf16 (head_dim zero-padded to the K = 16 of one MFMA), with the
+// "accumulator as the next MFMA's operand" idiom of flash_attn.hip: scores are produced transposed
+// (S^T = K Q^T: lane = query, registers = keys), so the softmax is lane-local plus one xor-32 exchange
+// and the probability registers feed O^T = V^T P^T directly (keys in the permuted order
+// key = 16 s + 8 (j >> 2) + 4 hh + (j & 3), matched by the gathered V^T operand).  The backward runs a
+// lane = query pass (dQ, relative-bias gradient) and a lane = key pass (S recomputed untransposed:
+// dK, dV), 40 MFMAs per (window, head).
+//
+// Workgroup = 64 * H threads (one wave per head, H <= 8: <= 2 waves per SIMD, 256 VGPRs each), grid-strides
+// over windows.  LDS holds the window's
+// qkv rows (16-B vector staged), the output tile (written back with 16-B stores), and the dense
+// relative-position bias of all heads + the window's shift mask as bf16 rows padded to 66 elements
+// (odd dword stride: conflict-free for both row and column access) -- staged once per workgroup.
+// ================================================================================================
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16;
+
+constexpr int BP = 66;   // padded bias / mask row (bf16 elements)
+
+__device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+// accumulator register r, lane half hh -> row inside the 32 x 32 tile (column = lane & 31)
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+// token feeding k-element j of the permuted-k operand at k-step s (16 tokens per step), lane half hh
+__device__ __forceinline__ int perm_k(int s, int j, int hh) { return 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3); }
+
+// A zero the compiler cannot see through: re-derived per window so the 64+ per-register LDS addresses
+// of the bias / mask / lse lookups are not hoisted out of the window loop (that hoist spills VGPRs).
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
+// row fragment: token t, head columns [off, off + d), elements 8hh .. 8hh+7 (zero past d)
+__device__ __forceinline__ u16x8 rowfrag(const u16* s, int t, int stride, int off, int hh, int d) {
+  u16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = 8 * hh + i;
+    r[i] = e < d ? s[t * stride + off + e] : (u16)0;
+  }
+  return r;
+}
+// permuted column fragment (A operand of X^T P^T): row dd of the head slice, tokens perm_k(ks, j, hh)
+__device__ __forceinline__ u16x8 colfrag(const u16* s, int ks, int hh, int dd, int stride, int off, int d) {
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = dd < d ? s[perm_k(ks, j, hh) * stride + off + dd] : (u16)0;
+  return r;
+}
+__device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
+  return r;
+}
+
+// stage rows [0, N) of a contiguous [N, width] bf16 block into LDS [64][width], zero rows N..63
+__device__ __forceinline__ void stage_rows(const bf16_t* g, u16* s, int N, int width) {
+  const int nv = N * width / 8;
+  const u16x8* src = reinterpret_cast<const u16x8*>(g);
+  for (int i = threadIdx.x; i < nv; i += blockDim.x) reinterpret_cast<u16x8*>(s)[i] = src[i];
+  for (int i = N * width + threadIdx.x; i < 64 * width; i += blockDim.x) s[i] = 0;
+}
+__device__ __forceinline__ void zero_lds(u16* s, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = 0;
+}
+// dense fp32 [mats][N][N] -> bf16 LDS [mats][64][BP] (each matrix padded to 64 rows of BP elements)
+__device__ __forceinline__ void stage_bias(const float* g, u16* s, int mats, int N) {
+  for (int e = threadIdx.x; e < mats * N * N; e += blockDim.x) {
+    const int r = e / N, c = e - r * N;          // r = matrix * N + row
+    const int mat = r / N, row = r - mat * N;
+    s[(mat * 64 + row) * BP + c] = f2bf(g[e]);
+  }
+}
+
+__global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                         const float* __restrict__ mask, int nw, bf16_t* __restrict__ o,
+                                                         float* __restrict__ lse, int Bw, int N, int H, int d,
+                                                         float scale) {
+  extern __shared__ __attribute__((aligned(16))) u16 smf[];
+  const int C = H * d, C3 = 3 * C;
+  u16* sq = smf;                       // [64][C3]
+  u16* so = sq + 64 * C3;              // [64][C]
+  u16* sb = so + 64 * C;               // [H][64][BP]
+  u16* sm = sb + H * 64 * BP;          // [64][BP]
+  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  zero_lds(sb, (H + 1) * 64 * BP);   // bias + mask rows incl. padding (an absent mask reads zeros)
+  __syncthreads();
+  stage_bias(bias, sb, H, N);
+  for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
+    __syncthreads();
+    stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
+    if (mask) stage_bias(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
+    __syncthreads();
+    u16x8 kf[2], qf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      kf[t] = rowfrag(sq, 32 * t + l32, C3, C + h * d, hh, d);
+      qf[t] = rowfrag(sq, 32 * t + l32, C3, h * d, hh, d);
+    }
+    const int z0 = opaque_zero();
+    const u16* bh = sb + h * 64 * BP + z0;
+    const u16* smw = sm + z0;
+    f32x16 p[2][2];
+    float msum[2], mmax[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * qt + l32;
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        p[qt][kt] = mfma32(kf[kt], qf[qt], zero16());
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kt + acc_row(r, hh);
+          const float a = p[qt][kt][r] * scale + bf2f(bh[q * BP + key]) + bf2f(smw[q * BP + key]);
+          p[qt][kt][r] = (key < N && q < N) ? a : -INFINITY;
+          m = fmaxf(m, p[qt][kt][r]);
+        }
+      }
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      float l = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float a = p[qt][kt][r];
+          const float e = a == -INFINITY ? 0.f : __expf(a - m);
+          p[qt][kt][r] = e;
+          l += e;
+        }
+      l += __shfl_xor(l, 32, 64);
+      msum[qt] = l;
+      mmax[qt] = m;
+    }
+    u16x8 vt[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) vt[ks] = colfrag(sq, ks, hh, l32, C3, 2 * C + h * d, d);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma32(vt[ks], pack8(p[qt][ks >> 1], ks & 1), acc);
+      const int q = 32 * qt + l32;
+      if (q < N) {
+        const float il = 1.f / msum[qt];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dd = acc_row(r, hh);
+          if (dd < d) so[q * C + h * d + dd] = f2bf(acc[r] * il);
+        }
+        if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(msum[qt]);
+      }
+    }
+    __syncthreads();
+    u16x8* dst = reinterpret_cast<u16x8*>(o + (int64_t)bw * N * C);
+    for (int i = threadIdx.x; i < N * C / 8; i += blockDim.x) dst[i] = reinterpret_cast<const u16x8*>(so)[i];
+  }
+}
+
+__global__ __launch_bounds__(512) void win_attn_bwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                         const float* __restrict__ mask, int nw,
+                                                         const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+                                                         const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                         float* __restrict__ dbias_part, int Bw, int N, int H, int d,
+                                                         float scale) {
+  extern __shared__ __attribute__((aligned(16))) u16 smb[];
+  const int C = H * d, C3 = 3 * C;
+  u16* sq = smb;                        // [64][C3] qkv
+  u16* sd = sq + 64 * C3;               // [64][C3] dqkv tile (first [64][C] holds O while delta is formed)
+  u16* sg = sd + 64 * C3;               // [64][C] dO
+  u16* sb = sg + 64 * C;                // [H][64][BP] bias
+  u16* sm = sb + H * 64 * BP;           // [64][BP] mask
+  float* slse = reinterpret_cast<float*>(sm + 64 * BP);   // [H][64]
+  float* sdel = slse + H * 64;                            // [H][64]
+  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  zero_lds(sb, (H + 1) * 64 * BP);
+  __syncthreads();
+  stage_bias(bias, sb, H, N);
+  f32x16 dsacc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) dsacc[a][b] = zero16();
+
+  for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
+    __syncthreads();
+    stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
+    stage_rows(dout + (int64_t)bw * N * C, sg, N, C);
+    stage_rows(o + (int64_t)bw * N * C, sd, N, C);
+    if (mask) stage_bias(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
+    __syncthreads();
+    {   // delta_q = <dO_q, O_q> and lse, one lane per query
+      float dl = 0.f, ls = INFINITY;
+      if (lane < N) {
+        for (int dd = 0; dd < d; ++dd) dl += bf2f(sg[lane * C + h * d + dd]) * bf2f(sd[lane * C + h * d + dd]);
+        ls = lse[((int64_t)bw * H + h) * N + lane];
+      }
+      sdel[h * 64 + lane] = dl;
+      slse[h * 64 + lane] = ls;
+    }
+    __syncthreads();   // O consumed: sd becomes the dqkv tile
+    const int z0 = opaque_zero();
+    const float* Lh = slse + h * 64 + z0;
+    const float* Dh = sdel + h * 64 + z0;
+    const u16* bh = sb + h * 64 * BP + z0;
+    const u16* smw = sm + z0;
+    // ---- pass 1: lane = query (S^T layout) -> dS^T, dQ, relative-bias gradient
+    {
+      u16x8 ktf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) ktf[ks] = colfrag(sq, ks, hh, l32, C3, C + h * d, d);
+#pragma unroll 1
+      for (int qt = 0; qt < 2; ++qt) {
+        const int q = 32 * qt + l32;
+        const float L = Lh[q], D = Dh[q];
+        const int zq = opaque_zero();       // per-iteration: keeps the 32 bias/mask addresses local
+        const u16* bq = bh + zq;
+        const u16* mq = smw + zq;
+        const u16x8 qf = rowfrag(sq, q, C3, h * d, hh, d);
+        const u16x8 gf = rowfrag(sg, q, C, h * d, hh, d);
+        u16x8 dsk[4];   // dS^T packed to bf16 as the next MFMA's B operand
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const f32x16 s = mfma32(rowfrag(sq, 32 * kt + l32, C3, C + h * d, hh, d), qf, zero16());
+          const f32x16 dp = mfma32(rowfrag(sq, 32 * kt + l32, C3, 2 * C + h * d, hh, d), gf, zero16());
+          f32x16 ds;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = 32 * kt + acc_row(r, hh);
+            const float a = s[r] * scale + bf2f(bq[q * BP + key]) + bf2f(mq[q * BP + key]);
+            const float v = __expf(a - L) * (dp[r] - D);
+            ds[r] = (key < N && q < N) ? v : 0.f;
+          }
+          if (qt == 0) dsacc[0][kt] += ds;   // static indices only (a dynamic one sends dsacc to scratch)
+          else dsacc[1][kt] += ds;
+          dsk[2 * kt] = pack8(ds, 0);
+          dsk[2 * kt + 1] = pack8(ds, 1);
+        }
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mfma32(ktf[ks], dsk[ks], acc);
+        if (q < N) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int dd = acc_row(r, hh);
+            if (dd < d) sd[q * C3 + h * d + dd] = f2bf(acc[r] * scale);
+          }
+        }
+      }
+    }
+    // ---- pass 2: lane = key (S layout) -> dV = P^T dO (sub-pass 0), dK = dS^T Q (sub-pass 1); S and dP
+    // are recomputed per sub-pass (4 extra MFMAs) so only one packed operand set is live at a time
+#pragma unroll 1
+    for (int it = 0; it < 4; ++it) {
+      const int kt = it >> 1, part = it & 1;
+      const int key = 32 * kt + l32;
+      const int zk = opaque_zero();
+      const u16* bk = bh + zk;
+      const u16* mk = smw + zk;
+      const float* Lk = Lh + zk;
+      const float* Dk = Dh + zk;
+      const u16x8 kf = rowfrag(sq, key, C3, C + h * d, hh, d);
+      const u16x8 vf = rowfrag(sq, key, C3, 2 * C + h * d, hh, d);
+      u16x8 opk[4];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const f32x16 s = mfma32(rowfrag(sq, 32 * qt + l32, C3, h * d, hh, d), kf, zero16());
+        const f32x16 dp = mfma32(rowfrag(sg, 32 * qt + l32, C, h * d, hh, d), vf, zero16());
+        f32x16 v;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = 32 * qt + acc_row(r, hh);
+          const float a = s[r] * scale + bf2f(bk[q * BP + key]) + bf2f(mk[q * BP + key]);
+          float pv = __expf(a - Lk[q]);
+          if (part) pv *= dp[r] - Dk[q];
+          v[r] = (key < N && q < N) ? pv : 0.f;
+        }
+        opk[2 * qt] = pack8(v, 0);
+        opk[2 * qt + 1] = pack8(v, 1);
+      }
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs)
+        acc = mfma32(part ? colfrag(sq, qs, hh, l32, C3, h * d, d) : colfrag(sg, qs, hh, l32, C, h * d, d), opk[qs], acc);
+      if (key < N) {
+        const float mul = part ? scale : 1.f;
+        const int off = (part ? C : 2 * C) + h * d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dd = acc_row(r, hh);
+          if (dd < d) sd[key * C3 + off + dd] = f2bf(acc[r] * mul);
+        }
+      }
+    }
+    __syncthreads();
+    u16x8* dst = reinterpret_cast<u16x8*>(dqkv + (int64_t)bw * N * C3);
+    for (int i = threadIdx.x; i < N * C3 / 8; i += blockDim.x) dst[i] = reinterpret_cast<const u16x8*>(sd)[i];
+  }
+  // relative-position-bias gradient partial [H][N(q)][N(key)] of this workgroup
+  float* dst = dbias_part + ((int64_t)blockIdx.x * H + h) * N * N;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * qt + l32;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, hh);
+        if (q < N && key < N) dst[q * N + key] = dsacc[qt][kt][r];
+      }
+  }
+}
+
+size_t fwd_mfma_lds(int N, int H, int d) { const int C = H * d; return (size_t)2 * (64 * 3 * C + 64 * C + (H + 1) * 64 * BP); }
+size_t bwd_mfma_lds(int N, int H, int d) {
+  const int C = H * d;
+  return (size_t)2 * (2 * 64 * 3 * C + 64 * C + (H + 1) * 64 * BP) + (size_t)2 * H * 64 * sizeof(float);
+}
+bool mfma_ok(int N, int H, int d, int dt) {
+  return dt == kBF16 && d <= 16 && N <= 64 && (N * H * d) % 8 == 0 && H <= 8 && bwd_mfma_lds(N, H, d) <= 160 * 1024;
+}
+
 }  // namespace
 
 // grid size the launcher uses (also the number of dbias partials the caller must allocate)
 PDT_API int pdt_win_attn_grid(int Bw) { return Bw < 512 ? Bw : 512; }
+
+// ---- MFMA path: bias [H, N(q), N(key)] fp32 (dense relative-position bias), mask [nw, N, N] fp32 or null
+PDT_API int pdt_win_attn_mfma_ok(int N, int H, int d, int dt) { return mfma_ok(N, H, d, dt) ? 1 : 0; }
+// one workgroup per CU (LDS-bound), grid-stride over windows; also the dbias partial count
+PDT_API int pdt_win_attn_mfma_grid(int Bw) { return Bw < 256 ? Bw : 256; }
+
+PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse,
+                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = fwd_mfma_lds(N, H, d);
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void*)win_attn_fwd_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  win_attn_fwd_mfma<<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (bf16_t*)o,
+                                                                      lse, Bw, N, H, d, scale);
+  return (int)hipGetLastError();
+}
+
+// dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw), H, N, N] fp32 fully written
+PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, int nw, const void* o,
+                                  const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N,
+                                  int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = bwd_mfma_lds(N, H, d);
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void*)win_attn_bwd_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  win_attn_bwd_mfma<<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>(
+      (const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, (const bf16_t*)dout, lse, (bf16_t*)dqkv, dbias_part, Bw, N,
+      H, d, scale);
+  return (int)hipGetLastError();
+}
 
 // qkv [Bw, N, 3, H, d] (= [Bw, N, 3C]); bias_t [H, N(j), N(i)] fp32 (dense relative-position bias,
 // transposed); mask_t [nw, N(j), N(i)] fp32 or null (window bw uses mask bw % nw); o [Bw, N, C]; lse [Bw, H, N]

@@ -7,9 +7,12 @@ layers.{i}.residual_group.blocks.{j}.{norm1,attn.qkv,attn.proj,attn.relative_pos
 norm2,mlp.fc1,mlp.fc2}, layers.{i}.conv, norm, conv_after_body, upsample.0), so upstream checkpoints
 keyed 'params' load with strict=True (Stoke-DDP.py:209-213).
 
-MI355X notes: LayerNorms run on the wave-per-row HIP kernel; window attention (64 tokens/window,
-head_dim 10) goes through torch SDPA with the relative-position bias (+ shift mask) as an additive mask
--- the cyclic shift and window partition are pure reshapes/rolls.
+MI355X notes (on GPU): LayerNorms run on the narrow-row HIP kernel (C = 60); window attention (64 tokens /
+window, head_dim 10) on the fused MFMA kernels of ops/window_attention.py (relative-position bias + shift
+mask applied in-register, never materialised); the 3x3 convolutions on im2col + hipBLASLt
+(ops/conv.py; MIOpen has no bf16 implicit-GEMM solver for these channel counts); Linear weight gradients on
+the row-split batched GEMM (ops/linear.py); the MLP's bias + erf-GELU fused.  ``to_stock_torch`` swaps
+every one of them back to the stock torch module (the baseline of scripts/bench_torch_baseline.py).
 """
 from __future__ import annotations
 
@@ -19,6 +22,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.activations import bias_gelu
+from ..ops.conv import Conv2d3x3
+from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 from ..ops.window_attention import window_attention
 
@@ -48,8 +54,8 @@ class WindowAttention(nn.Module):
         rel[:, :, 1] += window_size - 1
         rel[:, :, 0] *= 2 * window_size - 1
         self.register_buffer("relative_position_index", rel.sum(-1), persistent=True)
-        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = Linear(dim, dim * 3, bias=qkv_bias)
+        self.proj = Linear(dim, dim)
         self.native = True    # False: stock torch path (SDPA + materialised bias), see to_stock_torch()
         nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
 
@@ -77,11 +83,16 @@ class WindowAttention(nn.Module):
 class Mlp(nn.Module):
     def __init__(self, dim, hidden):
         super().__init__()
-        self.fc1 = nn.Linear(dim, hidden)
+        self.fc1 = Linear(dim, hidden)
         self.act = nn.GELU()
-        self.fc2 = nn.Linear(hidden, dim)
+        self.fc2 = Linear(hidden, dim)
+        self.native = True
 
     def forward(self, x):
+        if x.is_cuda and self.native:
+            # GEMM without bias -> fused bias + erf-GELU kernel (backward also reduces the bias gradient)
+            h = linear(x, self.fc1.weight)
+            return self.fc2(bias_gelu(h, self.fc1.bias, approximate="none"))
         return self.fc2(self.act(self.fc1(x)))
 
 
@@ -150,7 +161,7 @@ class RSTB(nn.Module):
     def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio):
         super().__init__()
         self.residual_group = BasicLayer(dim, input_resolution, depth, num_heads, window_size, mlp_ratio)
-        self.conv = nn.Conv2d(dim, dim, 3, 1, 1)
+        self.conv = Conv2d3x3(dim, dim)
 
     def forward(self, x, x_size):
         B, L, C = x.shape
@@ -180,14 +191,14 @@ class SwinIR(nn.Module):
         self.img_range, self.upscale, self.window_size = img_range, upscale, window_size
         self.register_buffer("mean", torch.tensor([0.4488, 0.4371, 0.4040]).view(1, 3, 1, 1) if in_chans == 3
                              else torch.zeros(1, 1, 1, 1), persistent=False)
-        self.conv_first = nn.Conv2d(in_chans, embed_dim, 3, 1, 1)
+        self.conv_first = Conv2d3x3(in_chans, embed_dim)
         self.patch_embed = PatchEmbed(embed_dim, norm=True)
         res = (img_size, img_size)
         self.layers = nn.ModuleList([RSTB(embed_dim, res, d, h, window_size, mlp_ratio)
                                      for d, h in zip(depths, num_heads)])
         self.norm = LayerNorm(embed_dim)
-        self.conv_after_body = nn.Conv2d(embed_dim, embed_dim, 3, 1, 1)
-        self.upsample = nn.Sequential(nn.Conv2d(embed_dim, upscale ** 2 * in_chans, 3, 1, 1), nn.PixelShuffle(upscale))
+        self.conv_after_body = Conv2d3x3(embed_dim, embed_dim)
+        self.upsample = nn.Sequential(Conv2d3x3(embed_dim, upscale ** 2 * in_chans), nn.PixelShuffle(upscale))
         self.apply(self._init)
 
     @staticmethod
@@ -236,7 +247,16 @@ def to_stock_torch(model: nn.Module) -> nn.Module:
                 ln = nn.LayerNorm(child.normalized_shape, eps=child.eps).to(child.weight.device)
                 ln.load_state_dict(child.state_dict())
                 setattr(mod, cname, ln)
-        if isinstance(mod, WindowAttention):
+            elif isinstance(child, Linear):
+                li = nn.Linear(child.in_features, child.out_features, bias=child.bias is not None)
+                li = li.to(child.weight.device)
+                li.load_state_dict(child.state_dict())
+                setattr(mod, cname, li)
+            elif isinstance(child, Conv2d3x3):
+                cv = nn.Conv2d(child.in_channels, child.out_channels, 3, 1, 1).to(child.weight.device)
+                cv.load_state_dict(child.state_dict())
+                setattr(mod, cname, cv)
+        if isinstance(mod, (WindowAttention, Mlp)):
             mod.native = False
     return model
 

@@ -1,0 +1,123 @@
+"""3x3 / stride 1 / pad 1 convolution lowered to im2col (HIP kernel) + one hipBLASLt GEMM per pass.
+
+For the small-channel convolutions of SwinIR-S (3->60, 60->60, 60->12 at 18 x 128 x 128)
+MIOpen has no implicit-GEMM solver in bf16 and runs its naive direct kernels (the weight gradients alone
+cost hundreds of ms per call, profiles/r1_v5_swinir_stoke_kernel_stats.csv).  Here every pass is one GEMM
+on the matrix cores over an im2col matrix written by ``csrc/kernels/conv.hip`` (which reads any input
+strides, so NCHW images and the NHWC-strided token views SwinIR produces need no layout copy):
+
+    forward   y[P, Cout]  = cols(x)[P, Kp] @ Wm[Kp, Cout] + b
+    backward  dW          = dY[P, Cout]^T @ cols(x)        (cols recomputed: 9x smaller saved state)
+              dX          = cols(dY)[P, Kq] @ Wflip[Kq, Cin]  (3x3 conv of dY with the flipped weight)
+
+The output is returned channels_last ([N, Cout, H, W] view of an NHWC buffer): SwinIR's
+``flatten(2).transpose(1, 2)`` of it is then a free view.  ``Conv2d3x3`` subclasses nn.Conv2d, so
+parameters / state_dict keys are unchanged.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+_MAX_ELEMS = (1 << 31) - 1
+
+
+def _round8(k: int) -> int:
+    return (k + 7) // 8 * 8
+
+
+def _im2col(x: torch.Tensor, kp: int) -> torch.Tensor:
+    N, C, H, W = x.shape
+    out = torch.empty((N * H * W, kp), dtype=x.dtype, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    _lib.call("pdt_im2col3x3", x.data_ptr(), sn, sc, sh, sw, N, C, H, W, kp, out.data_ptr(),
+              _lib.dtype_code(x.dtype), _lib.stream_handle(x.device))
+    return out
+
+
+def _w_rows(w: torch.Tensor, kp: int) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> [Kp, Cout], rows ordered (kh, kw, cin), zero rows past 9*Cin."""
+    co, ci = w.shape[0], w.shape[1]
+    m = w.permute(2, 3, 1, 0).reshape(9 * ci, co)
+    return F.pad(m, (0, 0, 0, kp - 9 * ci)) if kp != 9 * ci else m.contiguous()
+
+
+def _w_flip_rows(w: torch.Tensor, kq: int) -> torch.Tensor:
+    """Data-gradient weight: rows (kh, kw, cout) of w[cout, cin, 2-kh, 2-kw] -> [Kq, Cin]."""
+    co, ci = w.shape[0], w.shape[1]
+    m = w.flip(2, 3).permute(2, 3, 0, 1).reshape(9 * co, ci)
+    return F.pad(m, (0, 0, 0, kq - 9 * co)) if kq != 9 * co else m.contiguous()
+
+
+def _nhwc_rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> [N*H*W, C] (a view when t is channels_last-contiguous)."""
+    N, C, H, W = t.shape
+    return t.permute(0, 2, 3, 1).reshape(N * H * W, C)
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, C, H, W = x.shape
+        co = weight.shape[0]
+        kp = _round8(9 * C)
+        cols = _im2col(x, kp)
+        wm = _w_rows(weight, kp)
+        y = torch.addmm(bias, cols, wm) if bias is not None else cols @ wm
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y.view(N, H, W, co).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        N, C, H, W = x.shape
+        co = weight.shape[0]
+        dym = _nhwc_rows(dy)
+        dx = dw = db = None
+        if ctx.needs_input_grad[1]:
+            kp = _round8(9 * C)
+            cols = _im2col(x, kp)
+            g = (dym.t() @ cols)[:, :9 * C]                        # [Cout, (kh, kw, c)]
+            dw = g.reshape(co, 3, 3, C).permute(0, 3, 1, 2).to(weight.dtype)
+            del cols
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dym.float().sum(0).to(weight.dtype)
+        if ctx.needs_input_grad[0]:
+            kq = _round8(9 * co)
+            dcols = _im2col(dy, kq)
+            dxm = dcols @ _w_flip_rows(weight.to(dy.dtype), kq)    # [P, Cin]
+            dx = dxm.view(N, H, W, C).permute(0, 3, 1, 2)
+        return dx, dw, db
+
+
+def conv3x3(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """3x3, stride 1, padding 1 convolution (bf16 / fp32).  Autocast-aware like F.conv2d."""
+    if not x.is_cuda:
+        return F.conv2d(x, weight, bias, 1, 1)
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return conv3x3(x.to(dt), weight.to(dt), None if bias is None else bias.to(dt))
+    if x.dtype not in (torch.float32, torch.bfloat16) or weight.dtype != x.dtype:
+        return F.conv2d(x, weight, bias, 1, 1)
+    N, C, H, W = x.shape
+    kp = max(_round8(9 * C), _round8(9 * weight.shape[0]))
+    if N * H * W * kp > _MAX_ELEMS:           # keep the im2col matrix addressable: split the batch
+        per = max(1, _MAX_ELEMS // (H * W * kp))
+        return torch.cat([conv3x3(xs, weight, bias) for xs in x.split(per)], 0)
+    _lib.require()
+    return _Conv3x3Fn.apply(x, weight, bias)
+
+
+class Conv2d3x3(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 3, 1, 1) running on im2col + hipBLASLt (same parameters / state_dict)."""
+
+    def __init__(self, in_channels, out_channels, bias=True, device=None, dtype=None):
+        super().__init__(in_channels, out_channels, 3, 1, 1, bias=bias, device=device, dtype=dtype)
+
+    def forward(self, x):
+        return conv3x3(x, self.weight, self.bias)

@@ -1,6 +1,16 @@
-"""Linear layer whose backward reduces the bias gradient with the framework's column-sum kernel
-(2x the bandwidth of the generic reduction torch uses for ``grad_output.sum(0)``; GEMMs stay on
-hipBLASLt).  ``Linear`` subclasses nn.Linear, so parameters / state_dict keys are unchanged."""
+"""Linear layer with an MI355X-shaped backward (GEMMs stay on hipBLASLt):
+
+* the bias gradient is reduced with the framework's column-sum kernel (2x the bandwidth of the generic
+  reduction torch uses for ``grad_output.sum(0)``);
+* TALL-SKINNY weight gradients -- dW = dY^T X with hundreds of thousands of rows but only tens to
+  hundreds of columns (SwinIR-S: 294,912 tokens x C = 60..180) -- are split over the row dimension into
+  a batched GEMM with fp32 output and summed: one [N x M] x [M x K] GEMM with M = 295k leaves a single
+  64x64 tile per CU walking the whole K loop (8 TFLOP/s measured, profiles/r1_v5_swinir_*), while
+  ~72 batches of 4096 rows fill the chip;
+* autocast-aware (bf16 compute with fp32 master weights) without leaving the fused path.
+
+``Linear`` subclasses nn.Linear, so parameters / state_dict keys are unchanged.
+"""
 from __future__ import annotations
 
 import torch
@@ -8,6 +18,28 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .activations import _colsum
+
+_WGRAD_CHUNK = 4096
+
+
+def _tall_skinny(m: int, n: int, k: int) -> bool:
+    return m >= 16 * _WGRAD_CHUNK and max(n, k) <= 1024
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """dW = dy2^T @ x2 ([M, N]^T [M, K] -> [N, K]) in ``out_dtype``; row-split batched GEMM for tall-skinny M."""
+    m, n = dy2.shape
+    k = x2.shape[1]
+    if not (dy2.is_cuda and _tall_skinny(m, n, k)):
+        return torch.mm(dy2.t(), x2).to(out_dtype)
+    s = m // _WGRAD_CHUNK
+    main = s * _WGRAD_CHUNK
+    a = dy2[:main].view(s, _WGRAD_CHUNK, n).transpose(1, 2)
+    b = x2[:main].view(s, _WGRAD_CHUNK, k)
+    g = torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+    if main < m:
+        g += torch.mm(dy2[main:].t(), x2[main:], out_dtype=torch.float32)
+    return g.to(out_dtype)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -27,15 +59,22 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dy2.t(), x.reshape(-1, x.shape[-1]))
+            x2 = x.reshape(-1, x.shape[-1])
+            if not x2.is_contiguous():
+                x2 = x2.contiguous()
+            dw = wgrad(dy2, x2, w.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _colsum(dy2, w.dtype) if dy2.shape[1] % 8 == 0 else dy2.sum(0).to(w.dtype)
         return dx, dw, db
 
 
 def linear(x, weight, bias=None):
-    if (x.is_cuda and bias is not None and x.dtype == weight.dtype and x.dtype in (torch.bfloat16, torch.float32)
-            and not torch.is_autocast_enabled("cuda")):
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return linear(x.to(dt), weight.to(dt), None if bias is None else bias.to(dt))
+    if x.is_cuda and x.dtype == weight.dtype and x.dtype in (torch.bfloat16, torch.float32) and \
+            (bias is None or bias.dtype == x.dtype):
         return _LinearFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
 

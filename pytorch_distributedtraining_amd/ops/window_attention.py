@@ -56,6 +56,17 @@ class _WindowAttnFn(torch.autograd.Function):
         nw = mask.shape[0] if mask is not None else 1
         o = torch.empty((Bw, N, C), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty((Bw, num_heads, N), dtype=torch.float32, device=qkv.device)
+        lib = _lib.require()
+        ctx.mfma = bool(lib.pdt_win_attn_mfma_ok(N, num_heads, d, _lib.dtype_code(qkv.dtype)))
+        if ctx.mfma:
+            # MFMA kernels: dense bias [h, N(q), N(key)] and mask [nw, N, N], no transposed copies
+            m = mask.float().contiguous() if mask is not None else None
+            _lib.call("pdt_win_attn_mfma_fwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
+                      lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.stream_handle(qkv.device))
+            ctx.save_for_backward(qkv, bias, o, lse)
+            ctx.mask = (m, None, nw)
+            ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
+            return o
         _lib.call("pdt_win_attn_fwd", qkv.data_ptr(), bias_t.data_ptr(), _lib.ptr(m_t), nw, o.data_ptr(),
                   lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.dtype_code(qkv.dtype),
                   _lib.stream_handle(qkv.device))
@@ -66,6 +77,19 @@ class _WindowAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
+        if ctx.mfma:
+            qkv, bias, o, lse = ctx.saved_tensors
+            m, _, nw = ctx.mask
+            Bw, N, C3 = qkv.shape
+            d = C3 // 3 // ctx.h
+            G = _lib.require().pdt_win_attn_mfma_grid(Bw)
+            dqkv = torch.empty_like(qkv)
+            part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
+            do = do.contiguous().to(qkv.dtype)
+            _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
+                      do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N, ctx.h, d,
+                      float(ctx.scale), _lib.stream_handle(qkv.device))
+            return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
         qkv, bias, bias_t, o, lse = ctx.saved_tensors
         m, m_t, nw = ctx.mask
         Bw, N, C3 = qkv.shape

@@ -26,7 +26,7 @@ def test_native_library_is_loaded():
     assert lib is not None and _lib.available()
 
 
-@pytest.mark.parametrize("N", [768, 2048, 4096, 100, 10000])
+@pytest.mark.parametrize("N", [768, 2048, 4096, 100, 10000, 60, 64, 12])
 @pytest.mark.parametrize("xdt,wdt", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
                                      (torch.bfloat16, torch.float32)])
 def test_layer_norm(N, xdt, wdt):
@@ -48,7 +48,7 @@ def test_layer_norm(N, xdt, wdt):
     assert rel_err(b.grad, br.grad) < tol * 2
 
 
-@pytest.mark.parametrize("N", [4096, 2048, 96])
+@pytest.mark.parametrize("N", [4096, 2048, 96, 60])
 def test_rms_norm(N):
     from pytorch_distributedtraining_amd.ops import rms_norm
     x = torch.randn(257, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -359,7 +359,7 @@ def test_ddp_bf16_engine_single_gpu_step():
 
 
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("N", [2048, 96, 4096])
+@pytest.mark.parametrize("N", [2048, 96, 4096, 60])
 def test_fused_add_norm(rms, N):
     from pytorch_distributedtraining_amd.ops.norms import add_norm
     x = torch.randn(300, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -431,6 +431,78 @@ def test_causal_lm_has_no_future_leak(family):
     assert not torch.equal(a[:, t + 1:], b[:, t + 1:])
 
 
+@pytest.mark.parametrize("cin,cout", [(3, 60), (60, 60), (60, 12), (16, 8)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("layout", ["nchw", "nhwc_view"])
+def test_conv3x3_im2col_gemm(cin, cout, dt, layout):
+    """im2col (HIP) + hipBLASLt 3x3 conv vs F.conv2d in fp32: output, input, weight and bias gradients,
+    for NCHW inputs and the NHWC-strided token views SwinIR feeds its convolutions."""
+    from pytorch_distributedtraining_amd.ops.conv import conv3x3
+    torch.manual_seed(0)
+    N, H, W = 2, 19, 23
+    if layout == "nchw":
+        x = torch.randn(N, cin, H, W, device=DEV)
+    else:
+        x = torch.randn(N, H * W, cin, device=DEV).transpose(1, 2).reshape(N, cin, H, W)
+    x = x.to(dt).requires_grad_()
+    w = (0.1 * torch.randn(cout, cin, 3, 3, device=DEV)).to(dt).requires_grad_()
+    b = (0.1 * torch.randn(cout, device=DEV)).to(dt).requires_grad_()
+    y = conv3x3(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr, wr, br, 1, 1)
+    yr.backward(dy.float())
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-4
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < tol
+    assert rel_err(x.grad, xr.grad) < tol * 2
+    assert rel_err(w.grad, wr.grad) < tol * 2
+    assert rel_err(b.grad, br.grad) < tol * 2
+
+
+def test_swinir_conv_path_matches_stock_model():
+    """SwinIR-S with the im2col convs / HIP LayerNorm / window attention vs the same weights on the stock
+    torch path (to_stock_torch), forward and parameter gradients, bf16 autocast."""
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2, to_stock_torch
+    torch.manual_seed(0)
+    m = swinir_s_x2(depths=[2, 2], num_heads=[6, 6]).to(DEV)
+    ref = swinir_s_x2(depths=[2, 2], num_heads=[6, 6]).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    to_stock_torch(ref)
+    x = torch.rand(2, 3, 32, 40, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+        yr = ref(x)
+    assert rel_err(y, yr) < 2e-2
+    y.float().square().mean().backward()
+    yr.float().square().mean().backward()
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert rel_err(p.grad, q.grad) < 6e-2, n
+
+
+@pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60)])
+def test_linear_tall_skinny_wgrad(M, K, N):
+    """Row-split batched weight gradient (SwinIR token counts) vs the fp32 product, under bf16 autocast."""
+    from pytorch_distributedtraining_amd.ops.linear import Linear, wgrad
+    torch.manual_seed(0)
+    lin = Linear(K, N).to(DEV)
+    x = torch.randn(M, K, device=DEV, requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(x)
+    assert y.dtype == torch.bfloat16
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xb = x.detach().to(torch.bfloat16).float()
+    ref_w = dy.float().t() @ xb
+    assert lin.weight.grad.dtype == torch.float32
+    assert rel_err(lin.weight.grad, ref_w) < 1e-2
+    assert rel_err(lin.bias.grad, dy.float().sum(0)) < 1e-2
+    assert rel_err(x.grad, dy.float() @ lin.weight.detach().to(torch.bfloat16).float()) < 1e-2
+    g = wgrad(dy, xb.to(torch.bfloat16), torch.float32)
+    assert rel_err(g, ref_w) < 5e-3
+
+
 def test_linear_colsum_bias_grad():
     from pytorch_distributedtraining_amd.ops.linear import linear
     x = torch.randn(4, 100, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -446,7 +518,8 @@ def test_linear_colsum_bias_grad():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("N,h,d,Bw,nw", [(64, 6, 10, 32, 16), (49, 3, 32, 8, 4), (16, 2, 4, 6, 3)])
+@pytest.mark.parametrize("N,h,d,Bw,nw", [(64, 6, 10, 32, 16), (49, 3, 32, 8, 4), (16, 2, 4, 6, 3),
+                                          (49, 4, 16, 300, 4), (64, 6, 10, 704, 64)])
 def test_window_attention(dtype, masked, N, h, d, Bw, nw):
     """Fused HIP window attention (fwd + bwd incl. relative-bias grad) vs the fp32 PyTorch formula."""
     from pytorch_distributedtraining_amd.ops.window_attention import _WindowAttnFn, reference
