@@ -119,6 +119,46 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restric
   Vec8<float>::store(part + (int64_t)blockIdx.y * N + col, acc);
 }
 
+// Narrow rows (N < 2048, e.g. the SwinIR-S MLP's 120): the column-group mapping above would leave all but
+// N/8 threads of a workgroup idle; here the workgroup covers NT / (N/8) rows per pass (coalesced: adjacent
+// rows are adjacent in memory) and folds its row groups through LDS into ONE partial row.
+template <typename T, typename B, bool TANH>
+__global__ __launch_bounds__(NT) void bias_gelu_bwd_db_narrow(const T* __restrict__ dy, const T* __restrict__ h,
+                                                              const B* __restrict__ bias, T* __restrict__ dh,
+                                                              int rows, int N, int rows_per,
+                                                              float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float sacc[NT * 8];
+  const int tpr = N >> 3, rpb = NT / tpr;
+  const int rg = threadIdx.x / tpr, col = (threadIdx.x - rg * tpr) * 8;
+  const bool act = rg < rpb;
+  float b[8], acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { acc[k] = 0.f; b[k] = 0.f; }
+  if (act) Vec8<B>::load(bias + col, b);
+  const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
+  if (act) {
+    for (int r = r0 + rg; r < r1; r += rpb) {
+      float v[8], g[8];
+      Vec8<T>::load(h + (int64_t)r * N + col, v);
+      Vec8<T>::load(dy + (int64_t)r * N + col, g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[k] *= gelu_grad<TANH>(v[k] + b[k]);
+        acc[k] += g[k];
+      }
+      Vec8<T>::store(dh + (int64_t)r * N + col, g);
+    }
+  }
+  Vec8<float>::store(sacc + threadIdx.x * 8, acc);
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += NT) {
+    const int c8 = c >> 3, k = c & 7;
+    float t = 0.f;
+    for (int g = 0; g < rpb; ++g) t += sacc[(g * tpr + c8) * 8 + k];
+    part[(int64_t)blockIdx.x * N + c] = t;
+  }
+}
+
 // SwiGLU on a fused [rows, 2F] projection: y[r, j] = silu(x[r, j]) * x[r, F + j]
 template <typename T>
 __global__ __launch_bounds__(NT) void swiglu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
@@ -291,9 +331,12 @@ PDT_API int pdt_bias_gelu_bwd_db(const void* dy, const void* h, const void* bias
   if (N % 8 != 0 || bias == nullptr) return (int)hipErrorInvalidValue;
   const red::ColPlan pl = red::col_plan(rows, N);
   dim3 grid(pl.col_groups, pl.R);
-#define PDT_L(T, B, TH)                                                                                    \
-  bias_gelu_bwd_db_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh, rows, N, \
-                                                         pl.rows_per, ws)
+  const bool narrow = N < 8 * NT;   // one column group: use the row-packed kernel (same partial layout)
+#define PDT_L(T, B, TH)                                                                                          \
+  if (narrow) bias_gelu_bwd_db_narrow<T, B, TH><<<pl.R, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias,  \
+                                                                      (T*)dh, rows, N, pl.rows_per, ws);         \
+  else bias_gelu_bwd_db_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh, \
+                                                              rows, N, pl.rows_per, ws)
   if (dt == kBF16 && bdt == kBF16) { if (tanh_approx) PDT_L(bf16_t, bf16_t, true); else PDT_L(bf16_t, bf16_t, false); }
   else if (dt == kBF16 && bdt == kF32) { if (tanh_approx) PDT_L(bf16_t, float, true); else PDT_L(bf16_t, float, false); }
   else if (dt == kF32 && bdt == kF32) { if (tanh_approx) PDT_L(float, float, true); else PDT_L(float, float, false); }

@@ -578,6 +578,33 @@ PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const flo
 // Column sums of a [rows, N] matrix (T) into out[N] (W) -- bias gradients.  Workspace:
 // pdt_colsum_ws_floats(rows, N) floats (reduce.h col_plan partials + second level).
 namespace {
+// narrow N (< 2048): rows packed NT / (N/8) per workgroup pass, one partial row per workgroup
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_partial_narrow(const T* __restrict__ x, int rows, int N, int rows_per,
+                                                            float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float sacc[NT * 8];
+  const int tpr = N >> 3, rpb = NT / tpr;
+  const int rg = threadIdx.x / tpr, col = (threadIdx.x - rg * tpr) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
+  if (rg < rpb) {
+    for (int r = r0 + rg; r < r1; r += rpb) {
+      float v[8];
+      Vec8<T>::load(x + (int64_t)r * N + col, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+  }
+  Vec8<float>::store(sacc + threadIdx.x * 8, acc);
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += NT) {
+    const int c8 = c >> 3, k = c & 7;
+    float t = 0.f;
+    for (int g = 0; g < rpb; ++g) t += sacc[(g * tpr + c8) * 8 + k];
+    part[(int64_t)blockIdx.x * N + c] = t;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* __restrict__ x, int rows, int N, int rows_per,
                                                             float* __restrict__ part) {
@@ -614,8 +641,14 @@ PDT_API int pdt_colsum(const void* x, int rows, int N, int xdt, void* out, int o
   if (N % 8 != 0) return (int)hipErrorInvalidValue;
   const red::ColPlan pl = red::col_plan(rows, N);
   dim3 grid(pl.col_groups, pl.R);
-  if (xdt == kBF16) colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
-  else colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  if (N < 8 * NT) {
+    if (xdt == kBF16) colsum_partial_narrow<bf16_t><<<pl.R, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
+    else colsum_partial_narrow<float><<<pl.R, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  } else if (xdt == kBF16) {
+    colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
+  } else {
+    colsum_partial_kernel<float><<<grid, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  }
   float* ws2 = ws + (int64_t)pl.R * N;
   if (odt == kBF16) red::col_reduce<bf16_t>(ws, pl.R, N, (bf16_t*)out, ws2, accumulate, st);
   else red::col_reduce<float>(ws, pl.R, N, (float*)out, ws2, accumulate, st);

@@ -246,14 +246,17 @@ int dp_ok(int d) { return d <= DP; }
 // Workgroup = 64 * H threads (one wave per head, H <= 8: <= 2 waves per SIMD, 256 VGPRs each), grid-strides
 // over windows.  LDS holds the window's
 // qkv rows (16-B vector staged), the output tile (written back with 16-B stores), and the dense
-// relative-position bias of all heads + the window's shift mask as bf16 rows padded to 66 elements
-// (odd dword stride: conflict-free for both row and column access) -- staged once per workgroup.
+// relative-position bias of all heads + the window's shift mask as bf16 rows padded to 68 elements
+// (34-dword stride: conflict-free 8-byte reads of 4 consecutive entries and 2-byte column reads).  The
+// forward stores them row-major ([q][key]: a lane = query reads 4 keys per ds_read_b64); the backward
+// stores them transposed ([key][q]) for its lane = key pass (4 queries per read), the pass with 2x the
+// lookups.  Masks are a template parameter: the unshifted half of the blocks does no mask lookups.
 // ================================================================================================
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16;
 
-constexpr int BP = 66;   // padded bias / mask row (bf16 elements)
+constexpr int BP = 68;   // padded bias / mask row (bf16 elements, 8-byte aligned rows)
 
 __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -312,15 +315,19 @@ __device__ __forceinline__ void stage_rows(const bf16_t* g, u16* s, int N, int w
 __device__ __forceinline__ void zero_lds(u16* s, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = 0;
 }
-// dense fp32 [mats][N][N] -> bf16 LDS [mats][64][BP] (each matrix padded to 64 rows of BP elements)
+// dense fp32 [mats][N][N] -> bf16 LDS [mats][64][BP] (each matrix padded to 64 rows of BP elements),
+// TRANSPOSE: element (row, col) stored at [col][row]
+template <bool TRANSPOSE>
 __device__ __forceinline__ void stage_bias(const float* g, u16* s, int mats, int N) {
   for (int e = threadIdx.x; e < mats * N * N; e += blockDim.x) {
     const int r = e / N, c = e - r * N;          // r = matrix * N + row
     const int mat = r / N, row = r - mat * N;
-    s[(mat * 64 + row) * BP + c] = f2bf(g[e]);
+    s[(mat * 64 + (TRANSPOSE ? c : row)) * BP + (TRANSPOSE ? row : c)] = f2bf(g[e]);
   }
 }
+__device__ __forceinline__ u16x4 ld4(const u16* p) { return *reinterpret_cast<const u16x4*>(p); }
 
+template <bool HAS_MASK>
 __global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ mask, int nw, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int Bw, int N, int H, int d,
@@ -332,13 +339,13 @@ __global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restric
   u16* sb = so + 64 * C;               // [H][64][BP]
   u16* sm = sb + H * 64 * BP;          // [64][BP]
   const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
-  zero_lds(sb, (H + 1) * 64 * BP);   // bias + mask rows incl. padding (an absent mask reads zeros)
+  zero_lds(sb, (H + 1) * 64 * BP);   // bias + mask rows incl. padding
   __syncthreads();
-  stage_bias(bias, sb, H, N);
+  stage_bias<false>(bias, sb, H, N);
   for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
     __syncthreads();
     stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
-    if (mask) stage_bias(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
+    if (HAS_MASK) stage_bias<false>(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
     __syncthreads();
     u16x8 kf[2], qf[2];
 #pragma unroll
@@ -359,11 +366,19 @@ __global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restric
       for (int kt = 0; kt < 2; ++kt) {
         p[qt][kt] = mfma32(kf[kt], qf[qt], zero16());
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = 32 * kt + acc_row(r, hh);
-          const float a = p[qt][kt][r] * scale + bf2f(bh[q * BP + key]) + bf2f(smw[q * BP + key]);
-          p[qt][kt][r] = (key < N && q < N) ? a : -INFINITY;
-          m = fmaxf(m, p[qt][kt][r]);
+        for (int i = 0; i < 4; ++i) {          // registers 4i..4i+3 = keys base..base+3
+          const int base = 32 * kt + 8 * i + 4 * hh;
+          const u16x4 bv = ld4(bh + q * BP + base);
+          u16x4 mv = {0, 0, 0, 0};
+          if (HAS_MASK) mv = ld4(smw + q * BP + base);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * i + j;
+            float a = p[qt][kt][r] * scale + bf2f(bv[j]);
+            if (HAS_MASK) a += bf2f(mv[j]);
+            p[qt][kt][r] = (base + j < N && q < N) ? a : -INFINITY;
+            m = fmaxf(m, p[qt][kt][r]);
+          }
         }
       }
       m = fmaxf(m, __shfl_xor(m, 32, 64));
@@ -406,82 +421,102 @@ __global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restric
   }
 }
 
+// Backward, split in two launches so neither holds more than one pass's registers (one kernel spilled the
+// 64-register relative-bias accumulator):
+//   PASS 1 (lane = query, S^T layout): delta = rowsum(dO o O) (written for pass 2), dS^T, dQ, and the
+//          relative-bias gradient accumulated in registers across the workgroup's windows;
+//   PASS 2 (lane = key, S layout): dV = P^T dO and dK = dS^T Q (S / dP recomputed per sub-pass).
+// Each pass writes its own column range of the [N, 3C] dqkv rows (8-byte stores).
+template <bool HAS_MASK, int PASS>
 __global__ __launch_bounds__(512) void win_attn_bwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ mask, int nw,
                                                          const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                         const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                         float* __restrict__ dbias_part, int Bw, int N, int H, int d,
-                                                         float scale) {
+                                                         const float* __restrict__ lse, float* __restrict__ delta,
+                                                         bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part,
+                                                         int Bw, int N, int H, int d, float scale) {
   extern __shared__ __attribute__((aligned(16))) u16 smb[];
   const int C = H * d, C3 = 3 * C;
   u16* sq = smb;                        // [64][C3] qkv
-  u16* sd = sq + 64 * C3;               // [64][C3] dqkv tile (first [64][C] holds O while delta is formed)
+  u16* sd = sq + 64 * C3;               // [64][C3] output tile (PASS 1: first [64][C] holds O until delta is formed)
   u16* sg = sd + 64 * C3;               // [64][C] dO
-  u16* sb = sg + 64 * C;                // [H][64][BP] bias
-  u16* sm = sb + H * 64 * BP;           // [64][BP] mask
+  u16* sb = sg + 64 * C;                // [H][64][BP] bias (PASS 1 row-major [q][key], PASS 2 transposed [key][q])
+  u16* sm = sb + H * 64 * BP;           // [64][BP] mask (same layout)
   float* slse = reinterpret_cast<float*>(sm + 64 * BP);   // [H][64]
   float* sdel = slse + H * 64;                            // [H][64]
+  constexpr bool TR = PASS == 2;
   const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
   zero_lds(sb, (H + 1) * 64 * BP);
   __syncthreads();
-  stage_bias(bias, sb, H, N);
+  stage_bias<TR>(bias, sb, H, N);
   f32x16 dsacc[2][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) dsacc[a][b] = zero16();
+    for (int y = 0; y < 2; ++y) dsacc[x][y] = zero16();
 
   for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
     __syncthreads();
     stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
     stage_rows(dout + (int64_t)bw * N * C, sg, N, C);
-    stage_rows(o + (int64_t)bw * N * C, sd, N, C);
-    if (mask) stage_bias(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
-    __syncthreads();
-    {   // delta_q = <dO_q, O_q> and lse, one lane per query
+    if (PASS == 1) stage_rows(o + (int64_t)bw * N * C, sd, N, C);
+    if (HAS_MASK) stage_bias<TR>(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
+    if (PASS == 1) __syncthreads();
+    {   // lse (both passes), delta = <dO_q, O_q> (pass 1 computes and publishes it, pass 2 reads it)
       float dl = 0.f, ls = INFINITY;
       if (lane < N) {
-        for (int dd = 0; dd < d; ++dd) dl += bf2f(sg[lane * C + h * d + dd]) * bf2f(sd[lane * C + h * d + dd]);
-        ls = lse[((int64_t)bw * H + h) * N + lane];
+        const int64_t idx = ((int64_t)bw * H + h) * N + lane;
+        ls = lse[idx];
+        if (PASS == 1) {
+          for (int dd = 0; dd < d; ++dd) dl += bf2f(sg[lane * C + h * d + dd]) * bf2f(sd[lane * C + h * d + dd]);
+          delta[idx] = dl;
+        } else {
+          dl = delta[idx];
+        }
       }
       sdel[h * 64 + lane] = dl;
       slse[h * 64 + lane] = ls;
     }
-    __syncthreads();   // O consumed: sd becomes the dqkv tile
+    __syncthreads();
     const int z0 = opaque_zero();
     const float* Lh = slse + h * 64 + z0;
     const float* Dh = sdel + h * 64 + z0;
     const u16* bh = sb + h * 64 * BP + z0;
     const u16* smw = sm + z0;
-    // ---- pass 1: lane = query (S^T layout) -> dS^T, dQ, relative-bias gradient
-    {
+    const u16* tq = sq + z0;   // per-window views: the fragment addresses are rebuilt, not kept live
+    const u16* tg = sg + z0;
+    if (PASS == 1) {
+      // ---- lane = query (S^T layout) -> dS^T, dQ, relative-bias gradient
       u16x8 ktf[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) ktf[ks] = colfrag(sq, ks, hh, l32, C3, C + h * d, d);
-#pragma unroll 1
+      for (int ks = 0; ks < 4; ++ks) ktf[ks] = colfrag(tq, ks, hh, l32, C3, C + h * d, d);
+#pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int q = 32 * qt + l32;
         const float L = Lh[q], D = Dh[q];
-        const int zq = opaque_zero();       // per-iteration: keeps the 32 bias/mask addresses local
-        const u16* bq = bh + zq;
-        const u16* mq = smw + zq;
-        const u16x8 qf = rowfrag(sq, q, C3, h * d, hh, d);
-        const u16x8 gf = rowfrag(sg, q, C, h * d, hh, d);
+        const u16x8 qf = rowfrag(tq, q, C3, h * d, hh, d);
+        const u16x8 gf = rowfrag(tg, q, C, h * d, hh, d);
         u16x8 dsk[4];   // dS^T packed to bf16 as the next MFMA's B operand
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          const f32x16 s = mfma32(rowfrag(sq, 32 * kt + l32, C3, C + h * d, hh, d), qf, zero16());
-          const f32x16 dp = mfma32(rowfrag(sq, 32 * kt + l32, C3, 2 * C + h * d, hh, d), gf, zero16());
+          const f32x16 sc = mfma32(rowfrag(tq, 32 * kt + l32, C3, C + h * d, hh, d), qf, zero16());
+          const f32x16 dp = mfma32(rowfrag(tq, 32 * kt + l32, C3, 2 * C + h * d, hh, d), gf, zero16());
           f32x16 ds;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = 32 * kt + acc_row(r, hh);
-            const float a = s[r] * scale + bf2f(bq[q * BP + key]) + bf2f(mq[q * BP + key]);
-            const float v = __expf(a - L) * (dp[r] - D);
-            ds[r] = (key < N && q < N) ? v : 0.f;
+          for (int i = 0; i < 4; ++i) {        // registers 4i..4i+3 = keys base..base+3
+            const int base = 32 * kt + 8 * i + 4 * hh;
+            const u16x4 bv = ld4(bh + q * BP + base);
+            u16x4 mv = {0, 0, 0, 0};
+            if (HAS_MASK) mv = ld4(smw + q * BP + base);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * i + j;
+              float a = sc[r] * scale + bf2f(bv[j]);
+              if (HAS_MASK) a += bf2f(mv[j]);
+              const float v = __expf(a - L) * (dp[r] - D);
+              ds[r] = (base + j < N && q < N) ? v : 0.f;
+            }
           }
-          if (qt == 0) dsacc[0][kt] += ds;   // static indices only (a dynamic one sends dsacc to scratch)
-          else dsacc[1][kt] += ds;
+          dsacc[qt][kt] += ds;
           dsk[2 * kt] = pack8(ds, 0);
           dsk[2 * kt + 1] = pack8(ds, 1);
         }
@@ -496,67 +531,86 @@ __global__ __launch_bounds__(512) void win_attn_bwd_mfma(const bf16_t* __restric
           }
         }
       }
-    }
-    // ---- pass 2: lane = key (S layout) -> dV = P^T dO (sub-pass 0), dK = dS^T Q (sub-pass 1); S and dP
-    // are recomputed per sub-pass (4 extra MFMAs) so only one packed operand set is live at a time
+    } else {
+      // ---- lane = key (S layout) -> dV = P^T dO (sub-pass 0), dK = dS^T Q (sub-pass 1)
 #pragma unroll 1
-    for (int it = 0; it < 4; ++it) {
-      const int kt = it >> 1, part = it & 1;
-      const int key = 32 * kt + l32;
-      const int zk = opaque_zero();
-      const u16* bk = bh + zk;
-      const u16* mk = smw + zk;
-      const float* Lk = Lh + zk;
-      const float* Dk = Dh + zk;
-      const u16x8 kf = rowfrag(sq, key, C3, C + h * d, hh, d);
-      const u16x8 vf = rowfrag(sq, key, C3, 2 * C + h * d, hh, d);
-      u16x8 opk[4];
+      for (int it = 0; it < 4; ++it) {
+        const int kt = it >> 1, part = it & 1;
+        const int key = 32 * kt + l32;
+        const int zk = opaque_zero();
+        const u16* bk = bh + zk;
+        const u16* mk = smw + zk;
+        const float* Lk = Lh + zk;
+        const float* Dk = Dh + zk;
+        const u16* uq = tq + zk;
+        const u16* ug = tg + zk;
+        const u16x8 kf = rowfrag(uq, key, C3, C + h * d, hh, d);
+        const u16x8 vf = rowfrag(uq, key, C3, 2 * C + h * d, hh, d);
+        u16x8 opk[4];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const f32x16 s = mfma32(rowfrag(sq, 32 * qt + l32, C3, h * d, hh, d), kf, zero16());
-        const f32x16 dp = mfma32(rowfrag(sg, 32 * qt + l32, C, h * d, hh, d), vf, zero16());
-        f32x16 v;
+        for (int qt = 0; qt < 2; ++qt) {
+          const f32x16 sc = mfma32(rowfrag(uq, 32 * qt + l32, C3, h * d, hh, d), kf, zero16());
+          const f32x16 dp = mfma32(rowfrag(ug, 32 * qt + l32, C, h * d, hh, d), vf, zero16());
+          f32x16 v;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = 32 * qt + acc_row(r, hh);
-          const float a = s[r] * scale + bf2f(bk[q * BP + key]) + bf2f(mk[q * BP + key]);
-          float pv = __expf(a - Lk[q]);
-          if (part) pv *= dp[r] - Dk[q];
-          v[r] = (key < N && q < N) ? pv : 0.f;
+          for (int i = 0; i < 4; ++i) {        // registers 4i..4i+3 = queries base..base+3
+            const int base = 32 * qt + 8 * i + 4 * hh;
+            const u16x4 bv = ld4(bk + key * BP + base);
+            u16x4 mv = {0, 0, 0, 0};
+            if (HAS_MASK) mv = ld4(mk + key * BP + base);
+            const f32x4 L4 = *reinterpret_cast<const f32x4*>(Lk + base);
+            const f32x4 D4 = *reinterpret_cast<const f32x4*>(Dk + base);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * i + j;
+              float a = sc[r] * scale + bf2f(bv[j]);
+              if (HAS_MASK) a += bf2f(mv[j]);
+              float pv = __expf(a - L4[j]);
+              if (part) pv *= dp[r] - D4[j];
+              v[r] = (key < N && base + j < N) ? pv : 0.f;
+            }
+          }
+          opk[2 * qt] = pack8(v, 0);
+          opk[2 * qt + 1] = pack8(v, 1);
         }
-        opk[2 * qt] = pack8(v, 0);
-        opk[2 * qt + 1] = pack8(v, 1);
-      }
-      f32x16 acc = zero16();
+        f32x16 acc = zero16();
 #pragma unroll
-      for (int qs = 0; qs < 4; ++qs)
-        acc = mfma32(part ? colfrag(sq, qs, hh, l32, C3, h * d, d) : colfrag(sg, qs, hh, l32, C, h * d, d), opk[qs], acc);
-      if (key < N) {
-        const float mul = part ? scale : 1.f;
-        const int off = (part ? C : 2 * C) + h * d;
+        for (int qs = 0; qs < 4; ++qs)
+          acc = mfma32(part ? colfrag(uq, qs, hh, l32, C3, h * d, d) : colfrag(ug, qs, hh, l32, C, h * d, d), opk[qs], acc);
+        if (key < N) {
+          const float mul = part ? scale : 1.f;
+          const int off = (part ? C : 2 * C) + h * d;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int dd = acc_row(r, hh);
-          if (dd < d) sd[key * C3 + off + dd] = f2bf(acc[r] * mul);
+          for (int r = 0; r < 16; ++r) {
+            const int dd = acc_row(r, hh);
+            if (dd < d) sd[key * C3 + off + dd] = f2bf(acc[r] * mul);
+          }
         }
       }
     }
     __syncthreads();
-    u16x8* dst = reinterpret_cast<u16x8*>(dqkv + (int64_t)bw * N * C3);
-    for (int i = threadIdx.x; i < N * C3 / 8; i += blockDim.x) dst[i] = reinterpret_cast<const u16x8*>(sd)[i];
+    // write this pass's column range [c0, c1) of the window's dqkv rows (8-byte stores; C % 4 == 0)
+    const int c0 = PASS == 1 ? 0 : C, w4 = (PASS == 1 ? C : 2 * C) / 4;
+    bf16_t* dst = dqkv + (int64_t)bw * N * C3;
+    for (int i = threadIdx.x; i < N * w4; i += blockDim.x) {
+      const int t = i / w4, c = c0 + (i - t * w4) * 4;
+      *reinterpret_cast<u16x4*>(dst + t * C3 + c) = *reinterpret_cast<const u16x4*>(sd + t * C3 + c);
+    }
   }
-  // relative-position-bias gradient partial [H][N(q)][N(key)] of this workgroup
-  float* dst = dbias_part + ((int64_t)blockIdx.x * H + h) * N * N;
+  if (PASS == 1) {
+    // relative-position-bias gradient partial [H][N(q)][N(key)] of this workgroup
+    float* dstb = dbias_part + ((int64_t)blockIdx.x * H + h) * N * N;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = 32 * qt + l32;
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * qt + l32;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = 32 * kt + acc_row(r, hh);
-        if (q < N && key < N) dst[q * N + key] = dsacc[qt][kt][r];
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kt + acc_row(r, hh);
+          if (q < N && key < N) dstb[q * N + key] = dsacc[qt][kt][r];
+        }
+    }
   }
 }
 
@@ -566,7 +620,8 @@ size_t bwd_mfma_lds(int N, int H, int d) {
   return (size_t)2 * (2 * 64 * 3 * C + 64 * C + (H + 1) * 64 * BP) + (size_t)2 * H * 64 * sizeof(float);
 }
 bool mfma_ok(int N, int H, int d, int dt) {
-  return dt == kBF16 && d <= 16 && N <= 64 && (N * H * d) % 8 == 0 && H <= 8 && bwd_mfma_lds(N, H, d) <= 160 * 1024;
+  return dt == kBF16 && d <= 16 && N <= 64 && (N * H * d) % 8 == 0 && (H * d) % 4 == 0 && H <= 8 &&
+         bwd_mfma_lds(N, H, d) <= 160 * 1024;
 }
 
 }  // namespace
@@ -584,29 +639,44 @@ PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const floa
   if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
   const size_t lds = fwd_mfma_lds(N, H, d);
   static bool attr = [] {
-    return hipFuncSetAttribute((const void*)win_attn_fwd_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+    return hipFuncSetAttribute((const void*)win_attn_fwd_mfma<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024) == hipSuccess &&
+           hipFuncSetAttribute((const void*)win_attn_fwd_mfma<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  win_attn_fwd_mfma<<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (bf16_t*)o,
-                                                                      lse, Bw, N, H, d, scale);
+  if (mask)
+    win_attn_fwd_mfma<true><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw,
+                                                                             (bf16_t*)o, lse, Bw, N, H, d, scale);
+  else
+    win_attn_fwd_mfma<false><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw,
+                                                                              (bf16_t*)o, lse, Bw, N, H, d, scale);
   return (int)hipGetLastError();
 }
 
-// dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw), H, N, N] fp32 fully written
+// dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw), H, N, N] fp32 fully written;
+// delta_ws [Bw, H, N] fp32 scratch (pass 1 -> pass 2)
 PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, int nw, const void* o,
-                                  const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N,
-                                  int H, int d, float scale, hipStream_t st) {
+                                  const void* dout, const float* lse, float* delta_ws, void* dqkv, float* dbias_part,
+                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
   if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
   const size_t lds = bwd_mfma_lds(N, H, d);
   static bool attr = [] {
-    return hipFuncSetAttribute((const void*)win_attn_bwd_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024) == hipSuccess;
+    bool ok = true;
+    const void* fns[4] = {(const void*)win_attn_bwd_mfma<true, 1>, (const void*)win_attn_bwd_mfma<true, 2>,
+                          (const void*)win_attn_bwd_mfma<false, 1>, (const void*)win_attn_bwd_mfma<false, 2>};
+    for (const void* f : fns)
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
   }();
   (void)attr;
-  win_attn_bwd_mfma<<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>(
-      (const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, (const bf16_t*)dout, lse, (bf16_t*)dqkv, dbias_part, Bw, N,
-      H, d, scale);
+#define PDT_WB(M, P)                                                                                        \
+  win_attn_bwd_mfma<M, P><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>(                                 \
+      (const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, \
+      dbias_part, Bw, N, H, d, scale)
+  if (mask) { PDT_WB(true, 1); PDT_WB(true, 2); }
+  else { PDT_WB(false, 1); PDT_WB(false, 2); }
+#undef PDT_WB
   return (int)hipGetLastError();
 }
 

@@ -68,11 +68,20 @@ _SIGS = {
     "pdt_win_attn_mfma_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_float, c_void_p],
     "pdt_win_attn_mfma_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_int, c_int, c_int, c_int, c_float, c_void_p],
+                              c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
     "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                          c_int, c_void_p],
     "pdt_win_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
+    "pdt_xgmi_alloc": [c_int64, c_int, c_void_p],
+    "pdt_xgmi_free": [c_void_p],
+    "pdt_xgmi_ipc_get": [c_void_p, c_void_p],
+    "pdt_xgmi_ipc_handle_bytes": [],
+    "pdt_xgmi_ipc_open": [c_void_p, c_void_p],
+    "pdt_xgmi_ipc_close": [c_void_p],
+    "pdt_xgmi_error": [c_void_p, c_void_p],
+    "pdt_xgmi_collective": [c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_int, c_int,
+                            ctypes.c_uint, c_int64, ctypes.c_uint, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,
                       c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],

@@ -85,10 +85,11 @@ class _WindowAttnFn(torch.autograd.Function):
             G = _lib.require().pdt_win_attn_mfma_grid(Bw)
             dqkv = torch.empty_like(qkv)
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
+            delta = torch.empty_like(lse)
             do = do.contiguous().to(qkv.dtype)
             _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
-                      do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N, ctx.h, d,
-                      float(ctx.scale), _lib.stream_handle(qkv.device))
+                      do.data_ptr(), lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
+                      ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
             return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
         qkv, bias, bias_t, o, lse = ctx.saved_tensors
         m, m_t, nw = ctx.mask

@@ -33,22 +33,6 @@ SIG_BYTES = 4096
 MAX_WORLD = 8
 
 
-def _sig(lib):
-    c = ctypes
-    lib.pdt_xgmi_alloc.argtypes = [c.c_int64, c.c_int, c.POINTER(c.c_void_p)]
-    lib.pdt_xgmi_free.argtypes = [c.c_void_p]
-    lib.pdt_xgmi_ipc_get.argtypes = [c.c_void_p, c.c_void_p]
-    lib.pdt_xgmi_ipc_handle_bytes.argtypes = []
-    lib.pdt_xgmi_ipc_open.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
-    lib.pdt_xgmi_ipc_close.argtypes = [c.c_void_p]
-    lib.pdt_xgmi_error.argtypes = [c.c_void_p, c.POINTER(c.c_uint)]
-    lib.pdt_xgmi_collective.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int64, c.c_int, c.c_float,
-                                        c.c_void_p, c.c_int, c.c_int, c.c_uint, c.c_int64, c.c_uint, c.c_void_p]
-    for n in ("pdt_xgmi_alloc", "pdt_xgmi_free", "pdt_xgmi_ipc_get", "pdt_xgmi_ipc_handle_bytes",
-              "pdt_xgmi_ipc_open", "pdt_xgmi_ipc_close", "pdt_xgmi_error", "pdt_xgmi_collective"):
-        getattr(lib, n).restype = c.c_int
-
-
 class XGMIComm:
     """Peer-mapped collectives for ``comm``'s ranks (one process per GPU of one node)."""
 
@@ -62,8 +46,7 @@ class XGMIComm:
         self.oneshot_max_bytes = int(oneshot_max_bytes)
         self.spin_limit = int(spin_limit)
         self.device = torch.device("cuda", torch.cuda.current_device())
-        lib = _lib.require()
-        _sig(lib)
+        lib = _lib.require()   # ctypes signatures: ops/_lib.py _SIGS (checked against the C sources)
         self._lib = lib
         nbytes = SIG_BYTES + 2 * self.slot_bytes
         own = ctypes.c_void_p()

@@ -13,6 +13,6 @@ echo "=== swinir ours"
 timeout -k 10 300 python bench.py --workload swinir-stoke --steps 10 --warmup 3 2> $OUT/swinir.err || exit $?
 tail -n 2 $OUT/swinir.err
 echo "=== swinir profile"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof_swinir3 -o swinir --output-format csv -- \
-  python3 bench.py --workload swinir-stoke --steps 3 --warmup 1 > $OUT/prof_swinir3.log 2>&1 || exit $?
-python3 scripts/trace_kernels.py $(find $OUT/prof_swinir3 -name "*kernel_trace.csv" | head -1) --top 25
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof_swinir4 -o swinir --output-format csv -- \
+  python3 bench.py --workload swinir-stoke --steps 3 --warmup 1 > $OUT/prof_swinir4.log 2>&1 || exit $?
+python3 scripts/trace_kernels.py $(find $OUT/prof_swinir4 -name "*kernel_trace.csv" | head -1) --top 25
