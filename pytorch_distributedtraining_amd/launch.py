@@ -106,7 +106,13 @@ def main(argv=None):
     ap.add_argument("-m", dest="module", default=None, help="run a module instead of a script")
     ap.add_argument("script", nargs="?")
     ap.add_argument("script_args", nargs=argparse.REMAINDER)
-    a = ap.parse_args(argv)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if "-m" in argv:   # like python -m: everything after the module name belongs to the child
+        i = argv.index("-m")
+        a = ap.parse_args(argv[:i])
+        a.module, a.script, a.script_args = argv[i + 1], None, argv[i + 2:]
+    else:
+        a = ap.parse_args(argv)
     if a.nnodes != 1:
         raise SystemExit("this launcher is single-node (use torch.distributed.run for multi-node rendezvous)")
     if a.module:

@@ -69,7 +69,8 @@ class Comm:
         if xgmi is None:
             xgmi = os.environ.get("PDT_XGMI", "0") == "1" and self.backend == "nccl"
         if xgmi and self.world_size > 1 and torch.cuda.is_available():
-            self.enable_xgmi()
+            from ..run_config import xgmi_kwargs
+            self.enable_xgmi(**xgmi_kwargs())
 
     def enable_xgmi(self, **kw):
         """Route eligible CUDA all_reduce / all_gather / reduce_scatter through the peer-mapped xGMI

@@ -16,3 +16,5 @@ echo "=== swinir profile"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof_swinir4 -o swinir --output-format csv -- \
   python3 bench.py --workload swinir-stoke --steps 3 --warmup 1 > $OUT/prof_swinir4.log 2>&1 || exit $?
 python3 scripts/trace_kernels.py $(find $OUT/prof_swinir4 -name "*kernel_trace.csv" | head -1) --top 25
+echo "=== gemm layouts"
+timeout -k 10 300 python scripts/bench_gemm_layouts.py 2>&1 | tee $OUT/gemm_layouts.jsonl | grep -v amdgpu.ids
