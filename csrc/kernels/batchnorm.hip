@@ -1,0 +1,340 @@
+// Fused BatchNorm (+ residual add) (+ ReLU) for channels-last (NHWC) activations on gfx950 -- the
+// ResNet-50 DDP config (BASELINE.json config 2).  A bf16 ResNet-50 step spends ~35 % of
+// its time in BatchNorm and another ~8 % in ReLU (scripts/resnet_breakdown.py: 42.2 ms -> 27.3 ms without
+// BN, -> 24.0 ms without BN and ReLU); stock PyTorch runs BN, the residual add and ReLU as separate
+// passes over HBM.  Here:
+//
+//   forward   stats  : per-channel (sum, sum^2) partials over row chunks (fp32) -> fp64 combine
+//             apply  : y = relu(x * scale[c] + shift[c] (+ res))         ONE pass (reads x (+res), writes y)
+//   backward  reduce : (sum dy', sum dy' * xhat) with dy' = dy * (y > 0)  (ReLU mask from the saved output)
+//             apply  : dx = (dy' - s1/M - xhat * s2/M) * invstd * w ; dres = dy' (residual branch)
+//
+// x is [R rows, C] contiguous (R = N*H*W), C % 8 == 0.  A thread owns 8 consecutive channels for the
+// whole launch (scale / shift / mean / invstd live in registers, no per-element channel index math) and
+// walks rows; a workgroup covers 256 / (C/8) rows per pass (coalesced 16-byte accesses).  Cross-rank
+// SyncBN = one all-reduce of the fp64 sums between the combine and finalize kernels (caller).
+#include "common.h"
+
+using namespace pdt;
+
+namespace {
+
+constexpr int NT = 256;
+
+struct Tile {
+  int G, rpb, rl, cg;   // channel groups, rows per block pass, this thread's row lane, channel group
+  bool act;
+  __device__ Tile(int C) {
+    G = C >> 3;
+    rpb = NT / G;
+    rl = threadIdx.x / G;
+    cg = threadIdx.x - rl * G;
+    act = rl < rpb;
+  }
+};
+
+// MODE 0: (x, x^2)  MODE 1: (dy', dy' * xhat), dy' = dy * (y > 0) if RELU
+template <int MODE, bool RELU>
+__global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                       const bf16_t* __restrict__ y, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, int64_t R, int C,
+                                                       float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float sa[NT * 8];
+  __shared__ __attribute__((aligned(16))) float sb[NT * 8];
+  const Tile t(C);
+  float a[8], b[8], mu[8], is[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; is[k] = 0.f; }
+  if (t.act) {
+    if (MODE == 1) {
+      Vec8<float>::load(mean + t.cg * 8, mu);
+      Vec8<float>::load(invstd + t.cg * 8, is);
+    }
+    const int64_t stride = (int64_t)gridDim.x * t.rpb;
+    int64_t r = (int64_t)blockIdx.x * t.rpb + t.rl;
+    // two rows in flight per thread (all loads issued before the first use)
+    for (; r + stride < R; r += 2 * stride) {
+      const int64_t off0 = r * C + t.cg * 8, off1 = (r + stride) * C + t.cg * 8;
+      typename Vec8<bf16_t>::raw_t x0 = Vec8<bf16_t>::load_raw(x + off0), x1 = Vec8<bf16_t>::load_raw(x + off1);
+      typename Vec8<bf16_t>::raw_t g0, g1, y0, y1;
+      if (MODE == 1) { g0 = Vec8<bf16_t>::load_raw(dy + off0); g1 = Vec8<bf16_t>::load_raw(dy + off1); }
+      if (MODE == 1 && RELU) { y0 = Vec8<bf16_t>::load_raw(y + off0); y1 = Vec8<bf16_t>::load_raw(y + off1); }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float xv[8];
+        Vec8<bf16_t>::unpack(u ? x1 : x0, xv);
+        if (MODE == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
+        } else {
+          float g[8];
+          Vec8<bf16_t>::unpack(u ? g1 : g0, g);
+          if (RELU) {
+            float yv[8];
+            Vec8<bf16_t>::unpack(u ? y1 : y0, yv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
+        }
+      }
+    }
+    for (; r < R; r += stride) {
+      const int64_t off = r * C + t.cg * 8;
+      float xv[8];
+      Vec8<bf16_t>::load(x + off, xv);
+      if (MODE == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
+      } else {
+        float g[8];
+        Vec8<bf16_t>::load(dy + off, g);
+        if (RELU) {
+          float yv[8];
+          Vec8<bf16_t>::load(y + off, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
+      }
+    }
+  }
+  Vec8<float>::store(sa + threadIdx.x * 8, a);
+  Vec8<float>::store(sb + threadIdx.x * 8, b);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int g = c >> 3, k = c & 7;
+    float s1 = 0.f, s2 = 0.f;
+    for (int q = 0; q < t.rpb; ++q) { s1 += sa[(q * t.G + g) * 8 + k]; s2 += sb[(q * t.G + g) * 8 + k]; }
+    part[(int64_t)blockIdx.x * 2 * C + c] = s1;
+    part[(int64_t)blockIdx.x * 2 * C + C + c] = s2;
+  }
+}
+
+// [P, 2C] fp32 partials -> out[2C] fp64.  Workgroup = 64 outputs x 4 waves; each wave sums a quarter of
+// the P partial rows (lanes read consecutive outputs: coalesced), folded through LDS.
+//   count > 0: out[2C] = count (forward);  dw / db (nullable): fp32 copies of the two halves (backward)
+__global__ __launch_bounds__(256) void bn_combine_kernel(const float* __restrict__ part, int P, int C, double count,
+                                                         double* __restrict__ out, float* __restrict__ dw,
+                                                         float* __restrict__ db) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (i < 2 * C) {
+    const int per = (P + 3) / 4, j0 = wv * per, j1 = min(P, j0 + per);
+    int j = j0;
+    for (; j + 4 <= j1; j += 4) {
+      const float a0 = part[(int64_t)j * 2 * C + i], a1 = part[(int64_t)(j + 1) * 2 * C + i];
+      const float a2 = part[(int64_t)(j + 2) * 2 * C + i], a3 = part[(int64_t)(j + 3) * 2 * C + i];
+      s += (double)a0 + (double)a1 + (double)a2 + (double)a3;
+    }
+    for (; j < j1; ++j) s += (double)part[(int64_t)j * 2 * C + i];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && i < 2 * C) {
+    const double t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[i] = t;
+    if (i < C) { if (db) db[i] = (float)t; }
+    else if (dw) dw[i - C] = (float)t;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && count > 0) out[2 * C] = count;
+}
+
+// stats (global sums + count) -> mean, invstd, scale = invstd * w, shift = b - mean * scale; running stats
+__global__ void bn_finalize_kernel(const double* __restrict__ stats, int C, float eps, float momentum,
+                                   const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ mean,
+                                   float* __restrict__ invstd, float* __restrict__ scale, float* __restrict__ shift,
+                                   float* __restrict__ rmean, float* __restrict__ rvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double n = stats[2 * C];
+  const double mu = stats[c] / n;
+  double var = stats[C + c] / n - mu * mu;
+  if (var < 0) var = 0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  scale[c] = is * wc;
+  shift[c] = bc - (float)mu * is * wc;
+  if (rmean) {
+    const double unbiased = n > 1 ? var * n / (n - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mu);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unbiased);
+  }
+}
+
+// eval mode: scale / shift from the running statistics
+__global__ void bn_eval_coef_kernel(const float* __restrict__ rmean, const float* __restrict__ rvar, int C, float eps,
+                                    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ scale,
+                                    float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = rsqrtf(rvar[c] + eps), wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+  scale[c] = is * wc;
+  shift[c] = bc - rmean[c] * is * wc;
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      bf16_t* __restrict__ y, int64_t R, int C) {
+  const Tile t(C);
+  if (!t.act) return;
+  float sc[8], sh[8];
+  Vec8<float>::load(scale + t.cg * 8, sc);
+  Vec8<float>::load(shift + t.cg * 8, sh);
+  const int64_t stride = (int64_t)gridDim.x * t.rpb;
+#pragma unroll 2
+  for (int64_t r = (int64_t)blockIdx.x * t.rpb + t.rl; r < R; r += stride) {
+    const int64_t off = r * C + t.cg * 8;
+    float v[8];
+    Vec8<bf16_t>::load(x + off, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc[k] + sh[k];
+    if (RES) {
+      float rv[8];
+      Vec8<bf16_t>::load(res + off, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += rv[k];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+    }
+    Vec8<bf16_t>::store(y + off, v);
+  }
+}
+
+// dx = (dy' - s1 / M - xhat * s2 / M) * invstd * w ; dres = dy'
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ x, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, const float* __restrict__ w,
+                                                          const double* __restrict__ sums, const double* __restrict__ count,
+                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t R,
+                                                          int C) {
+  const Tile t(C);
+  if (!t.act) return;
+  const double inv_m = 1.0 / count[0];
+  float mu[8], is[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = t.cg * 8 + k;
+    mu[k] = mean[c];
+    is[k] = invstd[c];
+    const float wc = w ? w[c] : 1.f;
+    k1[k] = is[k] * wc;                               // dy' coefficient
+    k2[k] = (float)(sums[c] * inv_m) * k1[k];         // mean(dy') term
+    k3[k] = (float)(sums[C + c] * inv_m) * k1[k];     // mean(dy' xhat) term (times xhat)
+  }
+  const int64_t stride = (int64_t)gridDim.x * t.rpb;
+#pragma unroll 2
+  for (int64_t r = (int64_t)blockIdx.x * t.rpb + t.rl; r < R; r += stride) {
+    const int64_t off = r * C + t.cg * 8;
+    float g[8], xv[8], o[8];
+    Vec8<bf16_t>::load(dy + off, g);
+    Vec8<bf16_t>::load(x + off, xv);
+    if (RELU) {
+      float yv[8];
+      Vec8<bf16_t>::load(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (DRES) Vec8<bf16_t>::store(dres + off, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = g[k] * k1[k] - k2[k] - (xv[k] - mu[k]) * is[k] * k3[k];
+    Vec8<bf16_t>::store(dx + off, o);
+  }
+}
+
+int reduce_grid(int64_t R, int C) {
+  const int rpb = NT / (C >> 3);
+  int64_t g = (R + (int64_t)rpb * 16 - 1) / ((int64_t)rpb * 16);   // >= 16 rows per thread
+  if (g < 1) g = 1;
+  if (g > 512) g = 512;
+  return (int)g;
+}
+int apply_grid(int64_t R, int C) {
+  const int rpb = NT / (C >> 3);
+  int64_t g = (R + (int64_t)rpb * 8 - 1) / ((int64_t)rpb * 8);
+  if (g < 1) g = 1;
+  if (g > 256 * 8) g = 256 * 8;
+  return (int)g;
+}
+
+}  // namespace
+
+// workspace (fp32) for the partial sums: 2 * C * 1024 floats
+PDT_API int pdt_bn_ws_floats(int C) { return 2 * C * 1024; }
+
+PDT_API int pdt_bn_ok(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 : 0; }
+
+// forward statistics: out[0:2C] = (sum, sum^2) fp64, out[2C] = R (count)
+PDT_API int pdt_bn_stats(const void* x, int64_t R, int C, float* ws, double* out, hipStream_t st) {
+  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+  const int P = reduce_grid(R, C);
+  bn_reduce_kernel<0, false><<<P, NT, 0, st>>>((const bf16_t*)x, nullptr, nullptr, nullptr, nullptr, R, C, ws);
+  bn_combine_kernel<<<(2 * C + 63) / 64, 256, 0, st>>>(ws, P, C, (double)R, out, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_bn_finalize(const double* stats, int C, float eps, float momentum, const float* w, const float* b,
+                            float* mean, float* invstd, float* scale, float* shift, float* rmean, float* rvar,
+                            hipStream_t st) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(stats, C, eps, momentum, w, b, mean, invstd, scale, shift, rmean,
+                                                      rvar);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_bn_eval_coef(const float* rmean, const float* rvar, int C, float eps, const float* w, const float* b,
+                             float* scale, float* shift, hipStream_t st) {
+  bn_eval_coef_kernel<<<(C + 255) / 256, 256, 0, st>>>(rmean, rvar, C, eps, w, b, scale, shift);
+  return (int)hipGetLastError();
+}
+
+// y = act(x * scale + shift (+ res)); act: 0 none, 1 relu
+PDT_API int pdt_bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t R,
+                         int C, int relu, hipStream_t st) {
+  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+  const int g = apply_grid(R, C);
+#define PDT_L(RS, RL) bn_apply_kernel<RS, RL><<<g, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)res, scale, shift, \
+                                                                (bf16_t*)y, R, C)
+  if (res) { if (relu) PDT_L(true, true); else PDT_L(true, false); }
+  else { if (relu) PDT_L(false, true); else PDT_L(false, false); }
+#undef PDT_L
+  return (int)hipGetLastError();
+}
+
+// backward sums: out[0:2C] = (sum dy', sum dy' * xhat) fp64 (local; caller all-reduces for SyncBN);
+// dw / db (fp32, nullable) receive the local parameter gradients
+PDT_API int pdt_bn_bwd_reduce(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
+                              int64_t R, int C, int relu, float* ws, double* out, float* dw, float* db,
+                              hipStream_t st) {
+  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+  const int P = reduce_grid(R, C);
+  if (relu) bn_reduce_kernel<1, true><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)y, mean,
+                                                        invstd, R, C, ws);
+  else bn_reduce_kernel<1, false><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, nullptr, mean, invstd, R, C,
+                                                     ws);
+  bn_combine_kernel<<<(2 * C + 63) / 64, 256, 0, st>>>(ws, P, C, 0.0, out, dw, db);
+  return (int)hipGetLastError();
+}
+
+// dx (and dres = masked dy when dres != null); sums = global (sum dy', sum dy' xhat); count = global M
+PDT_API int pdt_bn_bwd_apply(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
+                             const float* w, const double* sums, const double* count, void* dx, void* dres, int64_t R,
+                             int C, int relu, hipStream_t st) {
+  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+  const int g = apply_grid(R, C);
+#define PDT_L(RL, DR) bn_bwd_apply_kernel<RL, DR><<<g, NT, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, \
+      (const bf16_t*)x, mean, invstd, w, sums, count, (bf16_t*)dx, (bf16_t*)dres, R, C)
+  if (relu) { if (dres) PDT_L(true, true); else PDT_L(true, false); }
+  else { if (dres) PDT_L(false, true); else PDT_L(false, false); }
+#undef PDT_L
+  return (int)hipGetLastError();
+}

@@ -2,14 +2,23 @@
 
 Parameter / buffer names match torchvision's ResNet (conv1, bn1, layer{1-4}.{i}.conv{1,2,3}, bn*,
 downsample.{0,1}, fc) so torchvision checkpoints load with ``strict=True``.  Convolutions run on
-MIOpen (framework layer); use ``channels_last`` + bf16 autocast on MI355X.  BatchNorm layers are
-plain nn.BatchNorm2d -- ``parallel.syncbn.convert_sync_batchnorm`` swaps in the HIP SyncBN.
+MIOpen (framework layer); use ``channels_last`` + bf16 autocast on MI355X.  With ``fused_bn=True`` (default)
+every BatchNorm is an ``ops.batchnorm.BatchNormAct2d`` (an nn.BatchNorm2d subclass) that fuses the
+following ReLU and, at the end of a block, the residual add into one channels-last HIP pass
+(``relu(bn3(conv3(h)) + identity)``); ``fused_bn=False`` builds the plain nn.BatchNorm2d / nn.ReLU model
+(the stock-torch baseline).  ``parallel.syncbn.convert_sync_batchnorm`` makes either cross-rank.
 Written from the published architecture (He et al. 2015), random init.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
+
+from ..ops.batchnorm import BatchNormAct2d
+
+
+def _bn(c, act, fused):
+    return BatchNormAct2d(c, act=act) if fused else nn.BatchNorm2d(c)
 
 
 def conv3x3(cin, cout, stride=1):
@@ -23,17 +32,20 @@ def conv1x1(cin, cout, stride=1):
 class BasicBlock(nn.Module):
     expansion = 1
 
-    def __init__(self, cin, planes, stride=1, downsample=None):
+    def __init__(self, cin, planes, stride=1, downsample=None, fused=True):
         super().__init__()
+        self.fused = fused
         self.conv1 = conv3x3(cin, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = _bn(planes, "relu", fused)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = _bn(planes, "relu", fused)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
+        if self.fused:
+            return self.bn2(self.conv2(self.bn1(self.conv1(x))), residual=idt)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + idt)
@@ -42,19 +54,23 @@ class BasicBlock(nn.Module):
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, cin, planes, stride=1, downsample=None):
+    def __init__(self, cin, planes, stride=1, downsample=None, fused=True):
         super().__init__()
+        self.fused = fused
         self.conv1 = conv1x1(cin, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = _bn(planes, "relu", fused)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = _bn(planes, "relu", fused)
         self.conv3 = conv1x1(planes, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.bn3 = _bn(planes * 4, "relu", fused)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
+        if self.fused:
+            out = self.bn2(self.conv2(self.bn1(self.conv1(x))))
+            return self.bn3(self.conv3(out), residual=idt)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -62,11 +78,12 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, block, layers, num_classes=1000, zero_init_residual=True):
+    def __init__(self, block, layers, num_classes=1000, zero_init_residual=True, fused_bn=True):
         super().__init__()
+        self.fused = fused_bn
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = _bn(64, "relu", fused_bn)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])
@@ -92,14 +109,15 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                 nn.BatchNorm2d(planes * block.expansion))
-        layers = [block(self.inplanes, planes, stride, down)]
+                                 _bn(planes * block.expansion, None, self.fused))
+        layers = [block(self.inplanes, planes, stride, down, fused=self.fused)]
         self.inplanes = planes * block.expansion
-        layers += [block(self.inplanes, planes) for _ in range(1, n)]
+        layers += [block(self.inplanes, planes, fused=self.fused) for _ in range(1, n)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.bn1(self.conv1(x))
+        x = self.maxpool(x if self.fused else self.relu(x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

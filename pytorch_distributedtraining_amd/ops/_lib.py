@@ -82,6 +82,17 @@ _SIGS = {
     "pdt_xgmi_error": [c_void_p, c_void_p],
     "pdt_xgmi_collective": [c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_int, c_int,
                             ctypes.c_uint, c_int64, ctypes.c_uint, c_void_p],
+    "pdt_bn_ws_floats": [c_int],
+    "pdt_bn_ok": [c_int],
+    "pdt_bn_stats": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "pdt_bn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_bn_eval_coef": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_bn_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_bn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_bn_bwd_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,
                       c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],

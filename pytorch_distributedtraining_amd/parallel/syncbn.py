@@ -171,7 +171,11 @@ class SyncBatchNorm(nn.modules.batchnorm._BatchNorm):
 def convert_sync_batchnorm(module: nn.Module, comm: Comm | None = None) -> nn.Module:
     """Recursively replace BatchNorm layers by SyncBatchNorm, keeping parameters and buffers
     (semantics of torch.nn.SyncBatchNorm.convert_sync_batchnorm, batchnorm.py:842)."""
+    from ..ops.batchnorm import BatchNormAct2d
     out = module
+    if isinstance(module, BatchNormAct2d):
+        module.comm = comm if comm is not None else default_comm()   # fused kernels all-reduce their stats
+        return module
     if isinstance(module, nn.modules.batchnorm._BatchNorm) and not isinstance(module, SyncBatchNorm):
         out = SyncBatchNorm(module.num_features, module.eps, module.momentum, module.affine,
                             module.track_running_stats, comm=comm)

@@ -67,7 +67,7 @@ def resnet50_ddp(a, dev, world, rank):
     from pytorch_distributedtraining_amd.models.resnet import resnet50  # plain nn.Conv2d / nn.BatchNorm2d
     from torch.nn.parallel import DistributedDataParallel as DDP
     mb = a.micro_batch or 256
-    model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    model = resnet50(fused_bn=False).to(dev).to(memory_format=torch.channels_last)   # nn.BatchNorm2d + nn.ReLU
     model = DDP(model, device_ids=[dev.index])
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4, fused=True)
     x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)

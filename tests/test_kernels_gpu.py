@@ -560,3 +560,69 @@ def test_swinir_window_attention_module_gpu():
     y.sum().backward()
     assert rel_err(y.cpu(), y_cpu) < 1e-4
     assert rel_err(blk_gpu.attn.relative_position_bias_table.grad.cpu(), g_cpu) < 1e-3
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048, 24])
+@pytest.mark.parametrize("act,res", [("relu", False), ("relu", True), (None, False)])
+def test_fused_batchnorm_act(C, act, res):
+    """BatchNormAct2d (fused BN [+ residual] [+ ReLU], channels-last bf16) vs nn.BatchNorm2d + add + ReLU in fp32:
+    output, input / residual / weight / bias gradients and running statistics."""
+    from pytorch_distributedtraining_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(0)
+    N, H, W = 4, 9, 7
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    r = torch.randn(N, C, H, W, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_() \
+        if res else None
+    bn = BatchNormAct2d(C, act=act).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).to(DEV)
+    ref.load_state_dict({k: v for k, v in bn.state_dict().items()})
+    y = bn(x, residual=r)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    yr = ref(xr)
+    if res:
+        yr = yr + rr
+    if act == "relu":
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    if res:
+        assert rel_err(r.grad, rr.grad) < 1e-2
+    assert rel_err(bn.weight.grad, ref.weight.grad) < 1e-2
+    assert rel_err(bn.bias.grad, ref.bias.grad) < 1e-2
+    assert torch.allclose(bn.running_mean, ref.running_mean, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+
+
+def test_resnet50_fused_bn_matches_plain_model():
+    """bf16 ResNet-50 with the fused BN kernels vs the plain nn.BatchNorm2d model, both measured against the
+    fp32 model: the fused model's error must be of the same order as stock bf16 autocast's (deep BN
+    backward amplifies rounding, so the two bf16 models are compared through the fp32 reference)."""
+    from pytorch_distributedtraining_amd.models.resnet import resnet50
+    torch.manual_seed(0)
+    a = resnet50(num_classes=10).to(DEV).to(memory_format=torch.channels_last)
+    b = resnet50(num_classes=10, fused_bn=False).to(DEV).to(memory_format=torch.channels_last)
+    r = resnet50(num_classes=10, fused_bn=False).to(DEV).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    r.load_state_dict(a.state_dict())
+    x = torch.randn(8, 3, 96, 96, device=DEV).to(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya, yb = a(x), b(x)
+    yr = r(x)
+    assert rel_err(ya, yr) < 2 * rel_err(yb, yr) + 2e-2
+    for m, y in ((a, ya), (b, yb), (r, yr)):
+        y.float().square().sum().backward()
+    for name in ("conv1.weight", "layer1.0.conv1.weight", "layer4.2.conv3.weight", "fc.weight"):
+        ga = dict(a.named_parameters())[name].grad
+        gb = dict(b.named_parameters())[name].grad
+        gr = dict(r.named_parameters())[name].grad
+        assert rel_err(ga, gr) < 2 * rel_err(gb, gr) + 5e-2, name
