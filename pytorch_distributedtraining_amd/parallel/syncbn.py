@@ -162,6 +162,14 @@ class SyncBatchNorm(nn.modules.batchnorm._BatchNorm):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         if not use_batch:
             return torch.nn.functional.batch_norm(x, rm, rv, self.weight, self.bias, False, 0.0, self.eps)
+        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and self.num_features % 8 == 0
+                and self.num_features <= 2048 and x.is_contiguous(memory_format=torch.channels_last)
+                and (not self.affine or self.weight.dtype == torch.float32)
+                and (rm is None or rm.dtype == torch.float32)):
+            # channels-last bf16: the fused BN kernels (ops/batchnorm.py) with cross-rank statistics
+            from ..ops.batchnorm import _BNActFn
+            return _BNActFn.apply(x, None, self.weight, self.bias, rm if self.training else None,
+                                  rv if self.training else None, self.eps, momentum, False, comm)
         if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16):
             return _SyncBNFn.apply(x, self.weight, self.bias, rm if self.training else None,
                                    rv if self.training else None, self.eps, momentum, comm)
