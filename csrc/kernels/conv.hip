@@ -72,3 +72,72 @@ PDT_API int pdt_im2col3x3(const void* x, int64_t sn, int64_t sc, int64_t sh, int
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Shifted-window partition / reverse as ONE row permutation (SwinIR's torch.roll +
+// window_partition + window_reverse + torch.roll + residual add are 3-5 passes over the activation; here
+// partition is one gather pass and reverse (+ residual) one pass).  x is [B, H, W, C] (row = one token,
+// C contiguous elements); windows are [B * nWh * nWw, ws * ws, C].  Window token (b, wh, ww, i, j) takes
+// image token (b, (wh*ws + i + s) mod H, (ww*ws + j + s) mod W) -- torch.roll(x, (-s, -s), (1, 2)) then
+// partition.  REVERSE maps back (inverse permutation) and optionally adds the residual.
+// ------------------------------------------------------------------------------------------------
+namespace {
+template <bool REVERSE, bool RES>
+__global__ __launch_bounds__(256) void window_perm_kernel(const bf16_t* __restrict__ src, const bf16_t* __restrict__ res,
+                                                          bf16_t* __restrict__ dst, int64_t rows, int C, int H, int W,
+                                                          int ws, int shift) {
+  const int cpr = C / 4;                      // 8-byte chunks per row
+  const int nww = W / ws, per_img = H * W;
+  const int64_t total = rows * cpr;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cpr;
+    const int ch = (int)(e - r * cpr);
+    int64_t img_row, win_row;
+    if (!REVERSE) {                           // r = window-order row
+      win_row = r;
+      const int64_t b = r / per_img;
+      const int t = (int)(r - b * per_img);
+      const int wi = t / (ws * ws), k = t - wi * ws * ws;
+      const int wh = wi / nww, ww = wi - wh * nww, i = k / ws, j = k - i * ws;
+      int h = wh * ws + i + shift, w = ww * ws + j + shift;
+      if (h >= H) h -= H;
+      if (w >= W) w -= W;
+      img_row = b * per_img + (int64_t)h * W + w;
+    } else {                                  // r = image-order row
+      img_row = r;
+      const int64_t b = r / per_img;
+      const int t = (int)(r - b * per_img);
+      int h = t / W - shift, w = t % W - shift;
+      if (h < 0) h += H;
+      if (w < 0) w += W;
+      const int wh = h / ws, i = h - wh * ws, ww = w / ws, j = w - ww * ws;
+      win_row = b * per_img + (int64_t)(wh * nww + ww) * ws * ws + i * ws + j;
+    }
+    const int64_t so = (REVERSE ? win_row : img_row) * C + ch * 4;
+    const int64_t dof = (REVERSE ? img_row : win_row) * C + ch * 4;
+    u16x4 v = *reinterpret_cast<const u16x4*>(src + so);
+    if (RES) {
+      const u16x4 a = *reinterpret_cast<const u16x4*>(res + dof);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = f2bf(bf2f(v[k]) + bf2f(a[k]));
+    }
+    *reinterpret_cast<u16x4*>(dst + dof) = v;
+  }
+}
+}  // namespace
+
+// reverse = 0: windows = partition(roll(x, -shift)); reverse = 1: x = roll(reverse(windows), +shift) (+ res).
+// bf16, C % 4 == 0, H % ws == 0, W % ws == 0, 0 <= shift < ws.
+PDT_API int pdt_window_perm(const void* src, const void* res, void* dst, int64_t rows, int C, int H, int W, int ws,
+                            int shift, int reverse, hipStream_t st) {
+  if (C % 4 || H % ws || W % ws || shift < 0 || shift >= ws || rows % ((int64_t)H * W)) return (int)hipErrorInvalidValue;
+  const int64_t total = rows * (C / 4);
+  const int grid = grid_for(total, 256, 256 * 16);
+  if (reverse) {
+    if (res) window_perm_kernel<true, true><<<grid, 256, 0, st>>>((const bf16_t*)src, (const bf16_t*)res, (bf16_t*)dst, rows, C, H, W, ws, shift);
+    else window_perm_kernel<true, false><<<grid, 256, 0, st>>>((const bf16_t*)src, nullptr, (bf16_t*)dst, rows, C, H, W, ws, shift);
+  } else {
+    window_perm_kernel<false, false><<<grid, 256, 0, st>>>((const bf16_t*)src, nullptr, (bf16_t*)dst, rows, C, H, W, ws, shift);
+  }
+  return (int)hipGetLastError();
+}

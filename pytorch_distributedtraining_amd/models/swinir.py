@@ -26,7 +26,8 @@ from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3
 from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
-from ..ops.window_attention import window_attention
+from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
+                                    window_reverse_shifted_add)
 
 
 def window_partition(x, ws):
@@ -126,6 +127,17 @@ class SwinTransformerBlock(nn.Module):
     def forward(self, x, x_size):
         H, W = x_size
         B, L, C = x.shape
+        if self.attn.native and fused_window_ok(x, H, W, self.window_size, self.shift_size):
+            # roll + partition and reverse + roll + residual add as one permutation pass each
+            if self.shift_size > 0:
+                mask = self.attn_mask if (H, W) == tuple(self.input_resolution) else self._mask((H, W)).to(x.device)
+            else:
+                mask = None
+            h = self.norm1(x).to(torch.bfloat16)
+            win = window_partition_shifted(h, H, W, self.window_size, self.shift_size)
+            a = self.attn(win, mask=mask).to(torch.bfloat16)
+            x = window_reverse_shifted_add(a, x, H, W, self.window_size, self.shift_size)
+            return x + self.mlp(self.norm2(x))
         sc = x
         x = self.norm1(x).view(B, H, W, C)
         if self.shift_size > 0:

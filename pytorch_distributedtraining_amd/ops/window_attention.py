@@ -120,3 +120,61 @@ def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float):
     if qkv.is_cuda:
         _lib.require()          # fail loudly on a GPU box without the kernels
     return reference(qkv, rel_bias, mask, num_heads, scale)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fused shifted-window partition / reverse (+ residual): one row-permutation pass each way
+# (csrc/kernels/conv.hip window_perm_kernel; SURVEY.md K6).
+# ------------------------------------------------------------------------------------------------
+def _perm(src, res, out_shape, H, W, ws, shift, reverse):
+    C = src.shape[-1]
+    if src.dtype != torch.bfloat16 or (res is not None and res.dtype != torch.bfloat16):
+        raise TypeError("fused window permutation takes bf16 tensors")
+    out = torch.empty(out_shape, dtype=src.dtype, device=src.device)
+    rows = src.numel() // C
+    _lib.call("pdt_window_perm", src.data_ptr(), _lib.ptr(res), out.data_ptr(), rows, C, H, W, ws, shift,
+              1 if reverse else 0, _lib.stream_handle(src.device))
+    return out
+
+
+class _PartitionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, H, W, ws, shift):
+        B, L, C = x.shape
+        ctx.geom = (B, H, W, ws, shift)
+        return _perm(x.contiguous(), None, (B * (H // ws) * (W // ws), ws * ws, C), H, W, ws, shift, False)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, H, W, ws, shift = ctx.geom
+        return _perm(g.contiguous(), None, (B, H * W, g.shape[-1]), H, W, ws, shift, True), None, None, None, None
+
+
+class _ReverseAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, win, res, H, W, ws, shift):
+        ctx.geom = (H, W, ws, shift)
+        return _perm(win.contiguous(), res.contiguous(), res.shape, H, W, ws, shift, True)
+
+    @staticmethod
+    def backward(ctx, g):
+        H, W, ws, shift = ctx.geom
+        g = g.contiguous()
+        B, L, C = g.shape
+        dwin = _perm(g, None, (B * (H // ws) * (W // ws), ws * ws, C), H, W, ws, shift, False)
+        return dwin, g, None, None, None, None
+
+
+def fused_window_ok(x, H, W, ws, shift) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.shape[1] == H * W and
+            x.shape[2] % 4 == 0 and H % ws == 0 and W % ws == 0 and 0 <= shift < ws)
+
+
+def window_partition_shifted(x, H, W, ws, shift):
+    """[B, H*W, C] -> windows [B*nW, ws*ws, C] of torch.roll(x, (-shift, -shift)) in ONE pass."""
+    return _PartitionFn.apply(x, H, W, ws, shift)
+
+
+def window_reverse_shifted_add(windows, res, H, W, ws, shift):
+    """res + roll(window_reverse(windows), (shift, shift)) as [B, H*W, C] in ONE pass."""
+    return _ReverseAddFn.apply(windows, res, H, W, ws, shift)

@@ -60,6 +60,124 @@ class GPT(nn.Module):
         return F.cross_entropy(logits.view(-1, logits.shape[-1]).float(), labels.reshape(-1))
 
 
+class LlamaBlock(nn.Module):
+    """Stock-torch Llama-3 block: nn.RMSNorm, fused qkv nn.Linear, torch RoPE, SDPA with GQA, SwiGLU."""
+
+    def __init__(self, d=4096, h=32, hkv=8, ffn=14336):
+        super().__init__()
+        self.h, self.hkv, self.hd = h, hkv, d // h
+        self.attention_norm = nn.RMSNorm(d, eps=1e-5)
+        self.wqkv = nn.Linear(d, (h + 2 * hkv) * self.hd, bias=False)
+        self.wo = nn.Linear(d, d, bias=False)
+        self.ffn_norm = nn.RMSNorm(d, eps=1e-5)
+        self.w13 = nn.Linear(d, 2 * ffn, bias=False)
+        self.w2 = nn.Linear(ffn, d, bias=False)
+
+    @staticmethod
+    def rope(x, cos, sin):
+        d = x.shape[-1] // 2
+        a, b = x[..., :d], x[..., d:]
+        return torch.cat([a * cos - b * sin, b * cos + a * sin], -1)
+
+    def forward(self, x, cos, sin):
+        B, S, D = x.shape
+        qkv = self.wqkv(self.attention_norm(x)).view(B, S, self.h + 2 * self.hkv, self.hd)
+        q = self.rope(qkv[:, :, :self.h], cos, sin).transpose(1, 2)
+        k = self.rope(qkv[:, :, self.h:self.h + self.hkv], cos, sin).transpose(1, 2)
+        v = qkv[:, :, self.h + self.hkv:].transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
+        x = x + self.wo(o.transpose(1, 2).reshape(B, S, D))
+        g, u = self.w13(self.ffn_norm(x)).chunk(2, -1)
+        return x + self.w2(F.silu(g) * u)
+
+
+class Llama(nn.Module):
+    def __init__(self, V=128256, d=4096, L=32, S=1024):
+        super().__init__()
+        self.tok_embeddings = nn.Embedding(V, d)
+        self.layers = nn.ModuleList([LlamaBlock(d) for _ in range(L)])
+        self.norm = nn.RMSNorm(d, eps=1e-5)
+        self.output = nn.Linear(d, V, bias=False)
+        inv = 1.0 / (500000.0 ** (torch.arange(0, 128, 2, dtype=torch.float64) / 128))
+        f = torch.outer(torch.arange(S, dtype=torch.float64), inv)
+        self.register_buffer("cos", f.cos().float().view(1, S, 1, 64), persistent=False)
+        self.register_buffer("sin", f.sin().float().view(1, S, 1, 64), persistent=False)
+        for p in self.parameters():
+            if p.dim() == 2:
+                nn.init.normal_(p, 0, 0.02)
+
+    def forward(self, idx, labels):
+        x = self.tok_embeddings(idx)
+        S = idx.shape[1]
+        cos, sin = self.cos[:, :S].to(x.dtype), self.sin[:, :S].to(x.dtype)
+        for b in self.layers:
+            x = torch.utils.checkpoint.checkpoint(b, x, cos, sin, use_reentrant=False)
+        logits = self.output(self.norm(x))
+        return F.cross_entropy(logits.view(-1, logits.shape[-1]).float(), labels.reshape(-1))
+
+
+def lm_fsdp(a, dev, world, rank, kind):
+    """Stock torch FSDP (FULL_SHARD, bf16 MixedPrecision) + fused torch AdamW + clip_grad_norm_ for the
+    GPT-2 1.3B (``gpt2-fsdp``) and Llama-3 8B + activation checkpointing (``llama3-fsdp``) configs;
+    ``gpt2-ddp`` = GPT-2 124M under stock DDP."""
+    from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
+    from torch.distributed.fsdp.wrap import ModuleWrapPolicy
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    torch.manual_seed(0)
+    if kind == "llama3-fsdp":
+        mb, vocab, name = a.micro_batch or 8, 128000, "Llama-3 8B FSDP + act-ckpt"
+        with torch.device(dev):
+            model = Llama(S=a.seq)
+        wrap = {LlamaBlock}
+        opt_kw = dict(lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    elif kind == "gpt2-ddp":
+        mb, vocab, name = a.micro_batch or 16, 50257, "GPT-2 124M DDP"
+        with torch.device(dev):
+            model = GPT(S=a.seq, d=768, L=12, h=12)
+        wrap = None
+        opt_kw = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    else:
+        mb, vocab, name = a.micro_batch or 32, 50257, "GPT-2-1.3B FSDP"
+        with torch.device(dev):
+            model = GPT(S=a.seq)
+        wrap = {Block}
+        opt_kw = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    n = sum(p.numel() for p in model.parameters())
+    if wrap is None:
+        model = DDP(model, device_ids=[dev.index])              # fp32 params + bf16 autocast
+        opt = torch.optim.AdamW(model.parameters(), fused=True, **opt_kw)
+    else:
+        model = FSDP(model, sharding_strategy=ShardingStrategy.FULL_SHARD, auto_wrap_policy=ModuleWrapPolicy(wrap),
+                     mixed_precision=MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16), device_id=dev,
+                     use_orig_params=False, limit_all_gathers=True)
+        opt = torch.optim.AdamW(model.parameters(), fused=True, **opt_kw)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    batches = [torch.randint(0, vocab, (mb, a.seq + 1), device=dev, generator=g) for _ in range(4)]
+
+    def step(i):
+        b = batches[i % 4]
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=wrap is None):
+            loss = model(b[:, :-1], b[:, 1:])
+        loss.backward()
+        if wrap is None:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        else:
+            model.clip_grad_norm_(1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dt, loss = timed(step, a, dev)
+    tps = world * mb * a.seq * a.steps / dt
+    if rank == 0:
+        print(f"[torch-baseline] {name} params={n/1e9:.3f}B loss={loss.item():.4f} step={1000*dt/a.steps:.1f}ms",
+              file=sys.stderr)
+        print(json.dumps({"metric": f"tokens/sec {name} (whole node) -- stock PyTorch-ROCm baseline",
+                          "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
+                          "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_gpu": mb,
+                          "seq_len": a.seq}))
+
+
 def resnet50_ddp(a, dev, world, rank):
     """Stock torch DDP (25 MiB buckets) + bf16 autocast + torch fused AdamW + clip_grad_norm_ on the
     same ResNet-50 / batch / synthetic data as ``bench.py --workload resnet50-ddp``."""
@@ -146,7 +264,8 @@ def timed(step, a, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="gpt2-fsdp", choices=["gpt2-fsdp", "resnet50-ddp", "swinir-stoke"])
+    ap.add_argument("--workload", default="gpt2-fsdp",
+                    choices=["gpt2-fsdp", "gpt2-ddp", "llama3-fsdp", "resnet50-ddp", "swinir-stoke"])
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--micro-batch", type=int, default=None)
@@ -162,6 +281,10 @@ def main():
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     if a.workload in ("resnet50-ddp", "swinir-stoke"):
         (resnet50_ddp if a.workload == "resnet50-ddp" else swinir_stoke)(a, dev, world, rank)
+        dist.destroy_process_group()
+        return
+    if a.workload in ("llama3-fsdp", "gpt2-ddp"):
+        lm_fsdp(a, dev, world, rank, a.workload)
         dist.destroy_process_group()
         return
     a.micro_batch = a.micro_batch or 16

@@ -22,7 +22,9 @@ def _entry(rank, world, port, fn, args, outdir):
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # file rendezvous: no TCP port to race for when many suites spawn workers back to back
+        dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "rdzv"), rank=rank,
+                                world_size=world)
         res = fn(rank, world, *args)
         err = None
     except Exception:

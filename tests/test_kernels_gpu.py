@@ -461,6 +461,36 @@ def test_conv3x3_im2col_gemm(cin, cout, dt, layout):
     assert rel_err(b.grad, br.grad) < tol * 2
 
 
+@pytest.mark.parametrize("H,W,ws,shift,C", [(16, 24, 8, 4, 60), (14, 21, 7, 0, 12), (16, 16, 8, 3, 96)])
+def test_window_perm_fused(H, W, ws, shift, C):
+    """Fused shifted-window partition / reverse(+residual) vs torch.roll + view/permute, values and grads."""
+    from pytorch_distributedtraining_amd.ops.window_attention import (window_partition_shifted,
+                                                                       window_reverse_shifted_add)
+    from pytorch_distributedtraining_amd.models.swinir import window_partition, window_reverse
+    torch.manual_seed(0)
+    B = 3
+    x = torch.randn(B, H * W, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    win = window_partition_shifted(x, H, W, ws, shift)
+    wr = window_partition(torch.roll(xr.view(B, H, W, C), (-shift, -shift), (1, 2)), ws).view(-1, ws * ws, C)
+    assert torch.equal(win, wr)
+    a = torch.randn_like(win, requires_grad=True)
+    ar = a.detach().clone().requires_grad_(True)
+    res = torch.randn(B, H * W, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    resr = res.detach().clone().requires_grad_(True)
+    out = window_reverse_shifted_add(a, res, H, W, ws, shift)
+    outr = resr + torch.roll(window_reverse(ar.view(-1, ws, ws, C), ws, H, W), (shift, shift), (1, 2)).view(B, H * W, C)
+    assert torch.equal(out, outr)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    (outr * g).sum().backward()
+    assert torch.equal(a.grad, ar.grad) and torch.equal(res.grad, resr.grad)
+    gw = torch.randn_like(win)
+    (win * gw).sum().backward()
+    (wr * gw).sum().backward()
+    assert torch.equal(x.grad, xr.grad)
+
+
 def test_swinir_conv_path_matches_stock_model():
     """SwinIR-S with the im2col convs / HIP LayerNorm / window attention vs the same weights on the stock
     torch path (to_stock_torch), forward and parameter gradients, bf16 autocast."""
