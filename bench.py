@@ -27,7 +27,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="gpt2-fsdp",
-                    choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp", "llama3-fsdp", "swinir-stoke"])
+                    choices=["gpt2-fsdp", "gpt2-ddp", "resnet50-ddp", "llama3-fsdp", "swinir-stoke", "resnet18-cpu"])
     ap.add_argument("--model", default=None)
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--seq", type=int, default=1024)
@@ -50,13 +50,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    from pytorch_distributedtraining_amd.ops import _lib
-    _lib.require()  # fail loudly if the HIP kernels are missing
+    if args.workload == "resnet18-cpu":      # BASELINE.json config 1: CPU / gloo plumbing run
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        from pytorch_distributedtraining_amd.ops import _lib
+        _lib.require()  # fail loudly if the HIP kernels are missing
     from pytorch_distributedtraining_amd.parallel import Comm
     comm = Comm()
 
@@ -76,21 +80,27 @@ def main():
 
 def timed_loop(step_fn, args, comm, dev):
     import torch
+
+    class _NoSync:
+        @staticmethod
+        def synchronize(_dev=None):
+            pass
+    torch_cuda = torch.cuda if dev.type == "cuda" else _NoSync
     for i in range(args.warmup):
         step_fn()
         if i == 0:
-            torch.cuda.synchronize(dev)
+            torch_cuda.synchronize(dev)
             log(f"[bench] warmup step 0 done")
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    torch_cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step_fn()
         if (i + 1) % 10 == 0:
             log(f"[bench] step {i + 1}/{args.steps}")
-    torch.cuda.synchronize(dev)
+    torch_cuda.synchronize(dev)
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    torch_cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     comm.all_reduce(t, "max")
@@ -169,9 +179,14 @@ def bench_resnet(args, comm, dev, world, rank):
     from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
 
-    mb = args.micro_batch or 256
-    model = resnet50().to(dev).to(memory_format=torch.channels_last)
-    model = DistributedDataParallel(model, comm=comm, reduce_dtype=torch.bfloat16)
+    cpu = dev.type == "cpu"
+    mb = args.micro_batch or (16 if cpu else 256)
+    if cpu:
+        from pytorch_distributedtraining_amd.models.resnet import resnet18
+        model = resnet18().to(memory_format=torch.channels_last)
+    else:
+        model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    model = DistributedDataParallel(model, comm=comm, reduce_dtype=None if cpu else torch.bfloat16)
     params = model.optimizer_parameters()
     opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
     x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
@@ -179,7 +194,7 @@ def bench_resnet(args, comm, dev, world, rank):
     crit = torch.nn.CrossEntropyLoss()
 
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not cpu):
             loss = crit(model(x), y)
         loss.backward()
         _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
@@ -188,11 +203,13 @@ def bench_resnet(args, comm, dev, world, rank):
 
     dt = timed_loop(step, args, comm, dev)
     sps = world * mb * args.steps / dt
-    return {"metric": "samples/sec ResNet-50 DDP (whole node)", "value": round(sps, 2), "unit": "samples/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"model": "resnet50", "global_batch": world * mb, "seq_len": None, "parallelism": f"dp{world}",
-                       "image": "3x224x224"}}
+    name = "ResNet-18 DDP CPU/gloo" if cpu else "ResNet-50 DDP"
+    return {"metric": f"samples/sec {name} (whole node)", "value": round(sps, 2), "unit": "samples/s",
+            "n_gpus": 0 if cpu else world, "n_ranks": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32" if cpu else "bf16", "data": "synthetic",
+            "config": {"model": "resnet18" if cpu else "resnet50", "global_batch": world * mb, "seq_len": None,
+                       "parallelism": f"dp{world}", "image": "3x224x224"}}
 
 
 def bench_swinir(args, comm, dev, world, rank):

@@ -178,6 +178,33 @@ def lm_fsdp(a, dev, world, rank, kind):
                           "seq_len": a.seq}))
 
 
+def resnet18_cpu(a, dev, world, rank):
+    """Stock torch DDP over gloo on CPU, ResNet-18 fp32 (BASELINE.json config 1), same shapes as
+    ``bench.py --workload resnet18-cpu``."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pytorch_distributedtraining_amd.models.resnet import resnet18
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    mb = a.micro_batch or 16
+    model = DDP(resnet18(fused_bn=False).to(memory_format=torch.channels_last))
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    x = torch.randn(mb, 3, 224, 224).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (mb,))
+
+    def step(i):
+        loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dt, loss = timed(step, a, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "samples/sec ResNet-18 DDP CPU/gloo (whole node) -- stock PyTorch baseline",
+                          "value": round(world * mb * a.steps / dt, 2), "unit": "samples/s", "n_ranks": world,
+                          "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_rank": mb}))
+
+
 def resnet50_ddp(a, dev, world, rank):
     """Stock torch DDP (25 MiB buckets) + bf16 autocast + torch fused AdamW + clip_grad_norm_ on the
     same ResNet-50 / batch / synthetic data as ``bench.py --workload resnet50-ddp``."""
@@ -250,12 +277,13 @@ def swinir_stoke(a, dev, world, rank):
 def timed(step, a, dev):
     for i in range(a.warmup):
         step(i)
-    torch.cuda.synchronize()
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
@@ -265,7 +293,8 @@ def timed(step, a, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="gpt2-fsdp",
-                    choices=["gpt2-fsdp", "gpt2-ddp", "llama3-fsdp", "resnet50-ddp", "swinir-stoke"])
+                    choices=["gpt2-fsdp", "gpt2-ddp", "llama3-fsdp", "resnet50-ddp", "swinir-stoke",
+                             "resnet18-cpu"])
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--micro-batch", type=int, default=None)
@@ -274,10 +303,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     lr = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(lr)
-    dev = torch.device("cuda", lr)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
+    if a.workload == "resnet18-cpu":
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        resnet18_cpu(a, torch.device("cpu"), world, rank)
+        dist.destroy_process_group()
+        return
+    torch.cuda.set_device(lr)
+    dev = torch.device("cuda", lr)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     if a.workload in ("resnet50-ddp", "swinir-stoke"):
         (resnet50_ddp if a.workload == "resnet50-ddp" else swinir_stoke)(a, dev, world, rank)
