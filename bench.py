@@ -20,6 +20,11 @@ import os
 import sys
 import time
 
+# MIOpen find / perf database for the ResNet-50 (batch 256, NHWC bf16) convolutions, recorded on MI355X
+# (scripts/gpu_miopen.sh): without it the first step of a fresh box spends minutes in MIOpen's find.
+os.environ.setdefault("MIOPEN_USER_DB_PATH",
+                      os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "miopen"))
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -180,6 +185,10 @@ def bench_resnet(args, comm, dev, world, rank):
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
 
     cpu = dev.type == "cpu"
+    if not cpu and os.environ.get("PDT_CONV_BENCHMARK", "1") == "1":
+        # MIOpen find per conv shape in the first (untimed) step instead of its immediate-mode heuristic:
+        # 7,133 -> 7,999 samples/s (profiles/r1_v9_miopen_modes.log; exhaustive search adds nothing)
+        torch.backends.cudnn.benchmark = True
     mb = args.micro_batch or (16 if cpu else 256)
     if cpu:
         from pytorch_distributedtraining_amd.models.resnet import resnet18

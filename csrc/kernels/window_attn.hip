@@ -8,8 +8,9 @@
 // materialises the expanded bias+mask [Bw, h, N, N] and the score matrix in HBM; here nothing of
 // size N×N leaves the CU.
 //
-// Shape regime: N ≤ 64 tokens per window, head_dim d ≤ 32 (SwinIR-S: N = 64, d = 10).  With d = 10 an
-// MFMA tile would be > 60% padding, so the math runs on the VALU in fp32: one wave per head, one
+// Two implementations.  bf16 with an even head_dim <= 16 (SwinIR-S: N = 64, d = 10) runs the MFMA kernels
+// at the end of this file (one wave per (window, head), see the comment there).  Everything else
+// (fp32, odd or > 16 head dims, d <= 32) runs the VALU kernels below in fp32: one wave per head, one
 // lane per query (forward / dQ) or per key (dK/dV); the window's K/V (and Q/dO in backward) are staged
 // in LDS as fp32 rows padded to DP floats and read as wave-uniform broadcasts (conflict-free).
 // A workgroup = one window × all heads (64·H threads) and walks windows grid-stride.
@@ -234,29 +235,36 @@ template <int DP>
 int dp_ok(int d) { return d <= DP; }
 
 // ================================================================================================
-// MFMA path (bf16, head_dim <= 16, N <= 64; SwinIR-S: N = 64, d = 10): the window's 64 x 64 score tile
-// per head is 4 v_mfma_f32_32x32x16_bf16 (head_dim zero-padded to the K = 16 of one MFMA), with the
-// "accumulator as the next MFMA's operand" idiom of flash_attn.hip: scores are produced transposed
-// (S^T = K Q^T: lane = query, registers = keys), so the softmax is lane-local plus one xor-32 exchange
-// and the probability registers feed O^T = V^T P^T directly (keys in the permuted order
-// key = 16 s + 8 (j >> 2) + 4 hh + (j & 3), matched by the gathered V^T operand).  The backward runs a
-// lane = query pass (dQ, relative-bias gradient) and a lane = key pass (S recomputed untransposed:
-// dK, dV), 40 MFMAs per (window, head).
-//
-// Workgroup = 64 * H threads (one wave per head, H <= 8: <= 2 waves per SIMD, 256 VGPRs each), grid-strides
-// over windows.  LDS holds the window's
-// qkv rows (16-B vector staged), the output tile (written back with 16-B stores), and the dense
-// relative-position bias of all heads + the window's shift mask as bf16 rows padded to 68 elements
-// (34-dword stride: conflict-free 8-byte reads of 4 consecutive entries and 2-byte column reads).  The
-// forward stores them row-major ([q][key]: a lane = query reads 4 keys per ds_read_b64); the backward
-// stores them transposed ([key][q]) for its lane = key pass (4 queries per read), the pass with 2x the
-// lookups.  Masks are a template parameter: the unshifted half of the blocks does no mask lookups.
+// MFMA path (bf16, even head_dim D <= 16, N <= 64; SwinIR-S: N = 64, D = 10).  ONE WAVE PER (window, head):
+// a workgroup is 4 waves working on the same head h (its relative-position bias staged once in LDS, as
+// bf16 rows padded to BP), each wave grid-strides over windows on its own -- no workgroup barrier in the
+// window loop, so one wave's global loads overlap the other waves' MFMA/softmax work.  Per window a lane
+// = token stages its d-wide Q/K/V(/dO) slices (dword loads straight from the fused [Bw, N, 3C] rows) into
+// the wave's private LDS tiles:
+//   row tiles  R[64][16] (dims >= D zero)          -> one ds_read_b128 per MFMA operand fragment
+//   transposed T[17][TP] (rows D..16 zero)          -> two ds_read_b64 per permuted-k X^T fragment
+// The 64 x 64 score tile is 4 v_mfma_f32_32x32x16_bf16 (head dim zero-padded to the MFMA K = 16), computed
+// transposed (S^T = K Q^T: lane = query, registers = keys) so the softmax is lane-local plus one xor-32
+// exchange and the probability registers feed O^T = V^T P^T directly (keys in the permuted order
+// key = 16 s + 8 (j >> 2) + 4 hh + (j & 3), matched by the transposed-tile fragment).  Outputs go straight
+// from the accumulators to global memory (4 consecutive head dims per register group = 2 dword stores).
+// Backward, per (window, head) in one wave: delta = rowsum(dO o O) at staging time; pass 1 (lane = query):
+// dS^T, dQ, dS accumulated in registers for the relative-bias gradient; pass 2 (lane = key): S / dP
+// recomputed untransposed, P and dS packed in one sweep, dV = P^T dO and dK = dS^T Q.  40 MFMAs per
+// (window, head).  The shift mask ([nw, N, N] fp32, shared by every head and image) is read from global
+// memory (L2-resident) only by the masked half of the blocks (template parameter).
 // ================================================================================================
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
-constexpr int BP = 68;   // padded bias / mask row (bf16 elements, 8-byte aligned rows)
+constexpr int BP = 68;       // padded bias row (bf16): conflict-free 8-byte reads of 4 consecutive entries
+constexpr int TP = 68;       // transposed-tile row pitch (tokens)
+constexpr int TT = 17 * TP;  // transposed tile: rows 0..15 = head dims, row 16 = zeros for lanes dd >= 16
+constexpr int WA_NT = 256;   // 4 waves per workgroup
+constexpr int FWD_WAVE = 2 * 1024 + TT + 4;                   // QR, KR, VT (u16, padded to 16 B)
+constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4;         // QR KR VR GR, SL SD (fp32), 2 transposed
 
 __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -270,97 +278,127 @@ __device__ __forceinline__ f32x16 zero16() {
 }
 // accumulator register r, lane half hh -> row inside the 32 x 32 tile (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
-// token feeding k-element j of the permuted-k operand at k-step s (16 tokens per step), lane half hh
-__device__ __forceinline__ int perm_k(int s, int j, int hh) { return 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3); }
-
-// A zero the compiler cannot see through: re-derived per window so the 64+ per-register LDS addresses
-// of the bias / mask / lse lookups are not hoisted out of the window loop (that hoist spills VGPRs).
-__device__ __forceinline__ int opaque_zero() {
-  int z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return z;
-}
-
-// row fragment: token t, head columns [off, off + d), elements 8hh .. 8hh+7 (zero past d)
-__device__ __forceinline__ u16x8 rowfrag(const u16* s, int t, int stride, int off, int hh, int d) {
-  u16x8 r;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int e = 8 * hh + i;
-    r[i] = e < d ? s[t * stride + off + e] : (u16)0;
-  }
-  return r;
-}
-// permuted column fragment (A operand of X^T P^T): row dd of the head slice, tokens perm_k(ks, j, hh)
-__device__ __forceinline__ u16x8 colfrag(const u16* s, int ks, int hh, int dd, int stride, int off, int d) {
-  u16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = dd < d ? s[perm_k(ks, j, hh) * stride + off + dd] : (u16)0;
-  return r;
-}
 __device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
   u16x8 r;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
   return r;
 }
-
-// stage rows [0, N) of a contiguous [N, width] bf16 block into LDS [64][width], zero rows N..63
-__device__ __forceinline__ void stage_rows(const bf16_t* g, u16* s, int N, int width) {
-  const int nv = N * width / 8;
-  const u16x8* src = reinterpret_cast<const u16x8*>(g);
-  for (int i = threadIdx.x; i < nv; i += blockDim.x) reinterpret_cast<u16x8*>(s)[i] = src[i];
-  for (int i = N * width + threadIdx.x; i < 64 * width; i += blockDim.x) s[i] = 0;
-}
-__device__ __forceinline__ void zero_lds(u16* s, int n) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = 0;
-}
-// dense fp32 [mats][N][N] -> bf16 LDS [mats][64][BP] (each matrix padded to 64 rows of BP elements),
-// TRANSPOSE: element (row, col) stored at [col][row]
-template <bool TRANSPOSE>
-__device__ __forceinline__ void stage_bias(const float* g, u16* s, int mats, int N) {
-  for (int e = threadIdx.x; e < mats * N * N; e += blockDim.x) {
-    const int r = e / N, c = e - r * N;          // r = matrix * N + row
-    const int mat = r / N, row = r - mat * N;
-    s[(mat * 64 + (TRANSPOSE ? c : row)) * BP + (TRANSPOSE ? row : c)] = f2bf(g[e]);
-  }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 __device__ __forceinline__ u16x4 ld4(const u16* p) { return *reinterpret_cast<const u16x4*>(p); }
+// order this wave's LDS writes before its (cross-lane) reads: LDS executes a wave's instructions in order,
+// so only the compiler has to be stopped from moving them
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
-template <bool HAS_MASK>
-__global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
-                                                         const float* __restrict__ mask, int nw, bf16_t* __restrict__ o,
-                                                         float* __restrict__ lse, int Bw, int N, int H, int d,
-                                                         float scale) {
+template <int D>
+struct Slice {
+  uint32_t v[D / 2];
+  __device__ __forceinline__ void load(const bf16_t* p) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) v[i] = s[i];
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) v[i] = 0u;
+  }
+  __device__ __forceinline__ float f(int e) const { return bf2f((u16)(v[e >> 1] >> (16 * (e & 1)))); }
+  // row tile R[64][16]: token t's 16 dims (zero past D) as two 16-byte stores
+  __device__ __forceinline__ void put_row(u16* R, int t) const {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = i < D / 2 ? v[i] : 0u;
+    u32x4* dst = reinterpret_cast<u32x4*>(R + t * 16);
+    dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+    dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+  }
+  // transposed tile T[dd][t]
+  __device__ __forceinline__ void put_col(u16* T, int t) const {
+#pragma unroll
+    for (int dd = 0; dd < D; ++dd) T[dd * TP + t] = (u16)(v[dd >> 1] >> (16 * (dd & 1)));
+  }
+};
+
+// B/A operand fragment of a row tile: token t, dims 8hh .. 8hh+7
+__device__ __forceinline__ u16x8 rfrag(const u16* R, int t, int hh) {
+  return *reinterpret_cast<const u16x8*>(R + t * 16 + 8 * hh);
+}
+// A operand X^T for k-step ks: lane row = head dim dd (dd >= 16 -> zero row 16), k = permuted tokens
+__device__ __forceinline__ u16x8 tfrag(const u16* T, int ks, int hh, int dd) {
+  const u16* row = T + (dd < 16 ? dd : 16) * TP + 16 * ks + 4 * hh;
+  const u16x4 a = ld4(row), b = ld4(row + 8);
+  return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// D-wide output row from an O^T-layout accumulator (register r = dim acc_row(r, hh), lane = token)
+template <int D>
+__device__ __forceinline__ void store_dims(bf16_t* row, const f32x16& acc, float mul, int hh) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int dim = 8 * g + 4 * hh + 2 * pr;
+      if (dim < D)
+        *reinterpret_cast<uint32_t*>(row + dim) = pack2(acc[4 * g + 2 * pr] * mul, acc[4 * g + 2 * pr + 1] * mul);
+    }
+}
+// bias [N][N] fp32 of one head -> bf16 LDS [64][BP] (TRANSPOSE: [key][q]), zero padded
+template <bool TRANSPOSE>
+__device__ __forceinline__ void stage_bias(const float* g, u16* s, int N) {
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+    const int r = e >> 6, c = e & 63;
+    const u16 v = (r < N && c < N) ? f2bf(g[r * N + c]) : (u16)0;
+    s[(TRANSPOSE ? c : r) * BP + (TRANSPOSE ? r : c)] = v;
+  }
+}
+
+template <int D, bool HAS_MASK, bool FULL>
+__global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __restrict__ qkv,
+                                                               const float* __restrict__ bias,
+                                                               const float* __restrict__ mask, int nw,
+                                                               bf16_t* __restrict__ o, float* __restrict__ lse, int Bw,
+                                                               int N, int H, float scale, int P) {
   extern __shared__ __attribute__((aligned(16))) u16 smf[];
-  const int C = H * d, C3 = 3 * C;
-  u16* sq = smf;                       // [64][C3]
-  u16* so = sq + 64 * C3;              // [64][C]
-  u16* sb = so + 64 * C;               // [H][64][BP]
-  u16* sm = sb + H * 64 * BP;          // [64][BP]
-  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
-  zero_lds(sb, (H + 1) * 64 * BP);   // bias + mask rows incl. padding
+  const int C = H * D, C3 = 3 * C;
+  const int h = blockIdx.x % H, pb = blockIdx.x / H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  u16* BR = smf;                                    // [64][BP] bias of head h, [q][key]
+  u16* QR = smf + 64 * BP + wv * FWD_WAVE;          // this wave's tiles
+  u16* KR = QR + 1024;
+  u16* VT = KR + 1024;
+  stage_bias<false>(bias + (int64_t)h * N * N, BR, N);
+  for (int e = lane; e < TT; e += 64) VT[e] = 0;
   __syncthreads();
-  stage_bias<false>(bias, sb, H, N);
-  for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
-    __syncthreads();
-    stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
-    if (HAS_MASK) stage_bias<false>(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
-    __syncthreads();
+
+  for (int bw = pb * 4 + wv; bw < Bw; bw += P * 4) {
+    {
+      Slice<D> q, k, v;
+      if (lane < N) {
+        const bf16_t* row = qkv + ((int64_t)bw * N + lane) * C3 + h * D;
+        q.load(row); k.load(row + C); v.load(row + 2 * C);
+      } else {
+        q.zero(); k.zero(); v.zero();
+      }
+      q.put_row(QR, lane); k.put_row(KR, lane); v.put_col(VT, lane);
+    }
+    wave_sync();
+    const float* mw = HAS_MASK ? mask + (int64_t)(bw % nw) * N * N : nullptr;
     u16x8 kf[2], qf[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      kf[t] = rowfrag(sq, 32 * t + l32, C3, C + h * d, hh, d);
-      qf[t] = rowfrag(sq, 32 * t + l32, C3, h * d, hh, d);
+      kf[t] = rfrag(KR, 32 * t + l32, hh);
+      qf[t] = rfrag(QR, 32 * t + l32, hh);
     }
-    const int z0 = opaque_zero();
-    const u16* bh = sb + h * 64 * BP + z0;
-    const u16* smw = sm + z0;
     f32x16 p[2][2];
-    float msum[2], mmax[2];
+    float lsum[2], mmax[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int q = 32 * qt + l32;
+      const int qc = FULL ? q : min(q, N - 1);
       float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -368,152 +406,156 @@ __global__ __launch_bounds__(512) void win_attn_fwd_mfma(const bf16_t* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) {          // registers 4i..4i+3 = keys base..base+3
           const int base = 32 * kt + 8 * i + 4 * hh;
-          const u16x4 bv = ld4(bh + q * BP + base);
-          u16x4 mv = {0, 0, 0, 0};
-          if (HAS_MASK) mv = ld4(smw + q * BP + base);
+          const u16x4 bv = ld4(BR + q * BP + base);
+          f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+          if (HAS_MASK) {
+            if (FULL) {
+              mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) mv[j] = base + j < N ? mw[qc * N + base + j] : 0.f;
+            }
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * i + j;
-            float a = p[qt][kt][r] * scale + bf2f(bv[j]);
-            if (HAS_MASK) a += bf2f(mv[j]);
-            p[qt][kt][r] = (base + j < N && q < N) ? a : -INFINITY;
-            m = fmaxf(m, p[qt][kt][r]);
+            float a = fmaf(p[qt][kt][r], scale, bf2f(bv[j]) + mv[j]);
+            if (!FULL) a = (base + j < N && q < N) ? a : -INFINITY;
+            p[qt][kt][r] = a;
+            m = fmaxf(m, a);
           }
         }
       }
       m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const float msub = m == -INFINITY ? 0.f : m;
       float l = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float a = p[qt][kt][r];
-          const float e = a == -INFINITY ? 0.f : __expf(a - m);
+          const float e = __expf(p[qt][kt][r] - msub);
           p[qt][kt][r] = e;
           l += e;
         }
       l += __shfl_xor(l, 32, 64);
-      msum[qt] = l;
-      mmax[qt] = m;
+      lsum[qt] = l;
+      mmax[qt] = msub;
     }
     u16x8 vt[4];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) vt[ks] = colfrag(sq, ks, hh, l32, C3, 2 * C + h * d, d);
+    for (int ks = 0; ks < 4; ++ks) vt[ks] = tfrag(VT, ks, hh, l32);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) acc = mfma32(vt[ks], pack8(p[qt][ks >> 1], ks & 1), acc);
       const int q = 32 * qt + l32;
-      if (q < N) {
-        const float il = 1.f / msum[qt];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int dd = acc_row(r, hh);
-          if (dd < d) so[q * C + h * d + dd] = f2bf(acc[r] * il);
-        }
-        if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(msum[qt]);
+      if (FULL || q < N) {
+        store_dims<D>(o + ((int64_t)bw * N + q) * C + h * D, acc, 1.f / lsum[qt], hh);
+        if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(lsum[qt]);
       }
     }
-    __syncthreads();
-    u16x8* dst = reinterpret_cast<u16x8*>(o + (int64_t)bw * N * C);
-    for (int i = threadIdx.x; i < N * C / 8; i += blockDim.x) dst[i] = reinterpret_cast<const u16x8*>(so)[i];
+    wave_sync();
   }
 }
 
-// Backward, split in two launches so neither holds more than one pass's registers (one kernel spilled the
-// 64-register relative-bias accumulator):
-//   PASS 1 (lane = query, S^T layout): delta = rowsum(dO o O) (written for pass 2), dS^T, dQ, and the
-//          relative-bias gradient accumulated in registers across the workgroup's windows;
-//   PASS 2 (lane = key, S layout): dV = P^T dO and dK = dS^T Q (S / dP recomputed per sub-pass).
-// Each pass writes its own column range of the [N, 3C] dqkv rows (8-byte stores).
-template <bool HAS_MASK, int PASS>
-__global__ __launch_bounds__(512) void win_attn_bwd_mfma(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
-                                                         const float* __restrict__ mask, int nw,
-                                                         const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                         const float* __restrict__ lse, float* __restrict__ delta,
-                                                         bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part,
-                                                         int Bw, int N, int H, int d, float scale) {
+// Backward pass PASS (1: dQ + relative-bias gradient, lane = query; 2: dK, dV, lane = key).  Two launches
+// rather than one so neither holds the other's registers (the 64-register bias-gradient accumulator of
+// pass 1 next to pass 2's P / dS tiles spilled).  Both recompute delta = rowsum(dO o O) while staging.
+template <int D, bool HAS_MASK, bool FULL, int PASS>
+__global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
+    const bf16_t* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask, int nw,
+    const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P) {
   extern __shared__ __attribute__((aligned(16))) u16 smb[];
-  const int C = H * d, C3 = 3 * C;
-  u16* sq = smb;                        // [64][C3] qkv
-  u16* sd = sq + 64 * C3;               // [64][C3] output tile (PASS 1: first [64][C] holds O until delta is formed)
-  u16* sg = sd + 64 * C3;               // [64][C] dO
-  u16* sb = sg + 64 * C;                // [H][64][BP] bias (PASS 1 row-major [q][key], PASS 2 transposed [key][q])
-  u16* sm = sb + H * 64 * BP;           // [64][BP] mask (same layout)
-  float* slse = reinterpret_cast<float*>(sm + 64 * BP);   // [H][64]
-  float* sdel = slse + H * 64;                            // [H][64]
-  constexpr bool TR = PASS == 2;
-  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
-  zero_lds(sb, (H + 1) * 64 * BP);
+  const int C = H * D, C3 = 3 * C;
+  const int h = blockIdx.x % H, pb = blockIdx.x / H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  u16* BB = smb;                        // [64][BP] bias: pass 1 [q][key], pass 2 [key][q]
+  u16* QR = BB + 64 * BP + wv * BWD_WAVE;
+  u16* KR = QR + 1024;
+  u16* VR = KR + 1024;
+  u16* GR = VR + 1024;
+  float* SL = reinterpret_cast<float*>(GR + 1024);   // [64] lse
+  float* SD = SL + 64;                               // [64] delta
+  u16* T0 = GR + 1024 + 256;                         // pass 1: K^T; pass 2: Q^T
+  u16* T1 = T0 + TT;                                 // pass 2: dO^T
+  stage_bias<PASS == 2>(bias + (int64_t)h * N * N, BB, N);
+  for (int e = lane; e < 2 * TT; e += 64) T0[e] = 0;
   __syncthreads();
-  stage_bias<TR>(bias, sb, H, N);
   f32x16 dsacc[2][2];
+  if (PASS == 1) {
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) dsacc[x][y] = zero16();
+      for (int y = 0; y < 2; ++y) dsacc[x][y] = zero16();
+  }
 
-  for (int bw = blockIdx.x; bw < Bw; bw += gridDim.x) {
-    __syncthreads();
-    stage_rows(qkv + (int64_t)bw * N * C3, sq, N, C3);
-    stage_rows(dout + (int64_t)bw * N * C, sg, N, C);
-    if (PASS == 1) stage_rows(o + (int64_t)bw * N * C, sd, N, C);
-    if (HAS_MASK) stage_bias<TR>(mask + (int64_t)(bw % nw) * N * N, sm, 1, N);
-    if (PASS == 1) __syncthreads();
-    {   // lse (both passes), delta = <dO_q, O_q> (pass 1 computes and publishes it, pass 2 reads it)
-      float dl = 0.f, ls = INFINITY;
+  for (int bw = pb * 4 + wv; bw < Bw; bw += P * 4) {
+    {
+      Slice<D> q, k, v, g, oo;
+      float L = 0.f, dl = 0.f;
       if (lane < N) {
-        const int64_t idx = ((int64_t)bw * H + h) * N + lane;
-        ls = lse[idx];
-        if (PASS == 1) {
-          for (int dd = 0; dd < d; ++dd) dl += bf2f(sg[lane * C + h * d + dd]) * bf2f(sd[lane * C + h * d + dd]);
-          delta[idx] = dl;
-        } else {
-          dl = delta[idx];
-        }
+        const int64_t tok = (int64_t)bw * N + lane;
+        const bf16_t* row = qkv + tok * C3 + h * D;
+        q.load(row); k.load(row + C); v.load(row + 2 * C);
+        g.load(dout + tok * C + h * D);
+        oo.load(o + tok * C + h * D);
+        L = lse[((int64_t)bw * H + h) * N + lane];
+#pragma unroll
+        for (int e = 0; e < D; ++e) dl = fmaf(g.f(e), oo.f(e), dl);
+      } else {
+        q.zero(); k.zero(); v.zero(); g.zero();
       }
-      sdel[h * 64 + lane] = dl;
-      slse[h * 64 + lane] = ls;
+      q.put_row(QR, lane); k.put_row(KR, lane); v.put_row(VR, lane); g.put_row(GR, lane);
+      if (PASS == 1) {
+        k.put_col(T0, lane);
+      } else {
+        q.put_col(T0, lane);
+        g.put_col(T1, lane);
+      }
+      SL[lane] = L;
+      SD[lane] = dl;
     }
-    __syncthreads();
-    const int z0 = opaque_zero();
-    const float* Lh = slse + h * 64 + z0;
-    const float* Dh = sdel + h * 64 + z0;
-    const u16* bh = sb + h * 64 * BP + z0;
-    const u16* smw = sm + z0;
-    const u16* tq = sq + z0;   // per-window views: the fragment addresses are rebuilt, not kept live
-    const u16* tg = sg + z0;
+    wave_sync();
+    const float* mw = HAS_MASK ? mask + (int64_t)(bw % nw) * N * N : nullptr;
     if (PASS == 1) {
-      // ---- lane = query (S^T layout) -> dS^T, dQ, relative-bias gradient
+      // lane = query (S^T layout): dS^T, dQ = dS K * scale, dS summed for the bias gradient
       u16x8 ktf[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) ktf[ks] = colfrag(tq, ks, hh, l32, C3, C + h * d, d);
+      for (int ks = 0; ks < 4; ++ks) ktf[ks] = tfrag(T0, ks, hh, l32);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int q = 32 * qt + l32;
-        const float L = Lh[q], D = Dh[q];
-        const u16x8 qf = rowfrag(tq, q, C3, h * d, hh, d);
-        const u16x8 gf = rowfrag(tg, q, C, h * d, hh, d);
-        u16x8 dsk[4];   // dS^T packed to bf16 as the next MFMA's B operand
+        const int qc = FULL ? q : min(q, N - 1);
+        const float Lq = SL[q], Dq = SD[q];
+        const u16x8 qf = rfrag(QR, q, hh), gf = rfrag(GR, q, hh);
+        u16x8 dsk[4];
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          const f32x16 sc = mfma32(rowfrag(tq, 32 * kt + l32, C3, C + h * d, hh, d), qf, zero16());
-          const f32x16 dp = mfma32(rowfrag(tq, 32 * kt + l32, C3, 2 * C + h * d, hh, d), gf, zero16());
+          const f32x16 sc = mfma32(rfrag(KR, 32 * kt + l32, hh), qf, zero16());
+          const f32x16 dp = mfma32(rfrag(VR, 32 * kt + l32, hh), gf, zero16());
           f32x16 ds;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {        // registers 4i..4i+3 = keys base..base+3
+          for (int i = 0; i < 4; ++i) {
             const int base = 32 * kt + 8 * i + 4 * hh;
-            const u16x4 bv = ld4(bh + q * BP + base);
-            u16x4 mv = {0, 0, 0, 0};
-            if (HAS_MASK) mv = ld4(smw + q * BP + base);
+            const u16x4 bv = ld4(BB + q * BP + base);
+            f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+            if (HAS_MASK) {
+              if (FULL) {
+                mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
+              } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) mv[j] = base + j < N ? mw[qc * N + base + j] : 0.f;
+              }
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int r = 4 * i + j;
-              float a = sc[r] * scale + bf2f(bv[j]);
-              if (HAS_MASK) a += bf2f(mv[j]);
-              const float v = __expf(a - L) * (dp[r] - D);
-              ds[r] = (base + j < N && q < N) ? v : 0.f;
+              const float a = fmaf(sc[r], scale, bf2f(bv[j]) + mv[j]);
+              float v = __expf(a - Lq) * (dp[r] - Dq);
+              if (!FULL) v = (base + j < N && q < N) ? v : 0.f;
+              ds[r] = v;
             }
           }
           dsacc[qt][kt] += ds;
@@ -523,105 +565,86 @@ __global__ __launch_bounds__(512) void win_attn_bwd_mfma(const bf16_t* __restric
         f32x16 acc = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) acc = mfma32(ktf[ks], dsk[ks], acc);
-        if (q < N) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int dd = acc_row(r, hh);
-            if (dd < d) sd[q * C3 + h * d + dd] = f2bf(acc[r] * scale);
-          }
-        }
+        if (FULL || q < N) store_dims<D>(dqkv + ((int64_t)bw * N + q) * C3 + h * D, acc, scale, hh);
       }
     } else {
-      // ---- lane = key (S layout) -> dV = P^T dO (sub-pass 0), dK = dS^T Q (sub-pass 1)
+      // lane = key (S layout): P and dS in one sweep; dV = P^T dO, dK = dS^T Q * scale
 #pragma unroll 1
-      for (int it = 0; it < 4; ++it) {
-        const int kt = it >> 1, part = it & 1;
+      for (int kt = 0; kt < 2; ++kt) {
         const int key = 32 * kt + l32;
-        const int zk = opaque_zero();
-        const u16* bk = bh + zk;
-        const u16* mk = smw + zk;
-        const float* Lk = Lh + zk;
-        const float* Dk = Dh + zk;
-        const u16* uq = tq + zk;
-        const u16* ug = tg + zk;
-        const u16x8 kf = rowfrag(uq, key, C3, C + h * d, hh, d);
-        const u16x8 vf = rowfrag(uq, key, C3, 2 * C + h * d, hh, d);
-        u16x8 opk[4];
+        const int kc = FULL ? key : min(key, N - 1);
+        const u16x8 kf = rfrag(KR, key, hh), vf = rfrag(VR, key, hh);
+        f32x16 av = zero16(), ak = zero16();
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-          const f32x16 sc = mfma32(rowfrag(uq, 32 * qt + l32, C3, h * d, hh, d), kf, zero16());
-          const f32x16 dp = mfma32(rowfrag(ug, 32 * qt + l32, C, h * d, hh, d), vf, zero16());
-          f32x16 v;
+          const f32x16 sc = mfma32(rfrag(QR, 32 * qt + l32, hh), kf, zero16());
+          const f32x16 dp = mfma32(rfrag(GR, 32 * qt + l32, hh), vf, zero16());
+          f32x16 pv, dv;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {        // registers 4i..4i+3 = queries base..base+3
             const int base = 32 * qt + 8 * i + 4 * hh;
-            const u16x4 bv = ld4(bk + key * BP + base);
-            u16x4 mv = {0, 0, 0, 0};
-            if (HAS_MASK) mv = ld4(mk + key * BP + base);
-            const f32x4 L4 = *reinterpret_cast<const f32x4*>(Lk + base);
-            const f32x4 D4 = *reinterpret_cast<const f32x4*>(Dk + base);
+            const u16x4 bv = ld4(BB + key * BP + base);
+            const f32x4 L4 = *reinterpret_cast<const f32x4*>(SL + base);
+            const f32x4 D4 = *reinterpret_cast<const f32x4*>(SD + base);
+            float mv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (HAS_MASK) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) mv[j] = (FULL || base + j < N) ? mw[(base + j) * N + kc] : 0.f;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int r = 4 * i + j;
-              float a = sc[r] * scale + bf2f(bv[j]);
-              if (HAS_MASK) a += bf2f(mv[j]);
-              float pv = __expf(a - L4[j]);
-              if (part) pv *= dp[r] - D4[j];
-              v[r] = (key < N && base + j < N) ? pv : 0.f;
+              const float a = fmaf(sc[r], scale, bf2f(bv[j]) + mv[j]);
+              float e = __expf(a - L4[j]);
+              if (!FULL) e = (key < N && base + j < N) ? e : 0.f;
+              pv[r] = e;
+              dv[r] = e * (dp[r] - D4[j]);
             }
           }
-          opk[2 * qt] = pack8(v, 0);
-          opk[2 * qt + 1] = pack8(v, 1);
-        }
-        f32x16 acc = zero16();
 #pragma unroll
-        for (int qs = 0; qs < 4; ++qs)
-          acc = mfma32(part ? colfrag(uq, qs, hh, l32, C3, h * d, d) : colfrag(ug, qs, hh, l32, C, h * d, d), opk[qs], acc);
-        if (key < N) {
-          const float mul = part ? scale : 1.f;
-          const int off = (part ? C : 2 * C) + h * d;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int dd = acc_row(r, hh);
-            if (dd < d) sd[key * C3 + off + dd] = f2bf(acc[r] * mul);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            av = mfma32(tfrag(T1, 2 * qt + s2, hh, l32), pack8(pv, s2), av);
+            ak = mfma32(tfrag(T0, 2 * qt + s2, hh, l32), pack8(dv, s2), ak);
           }
+        }
+        if (FULL || key < N) {
+          bf16_t* row = dqkv + ((int64_t)bw * N + key) * C3 + h * D;
+          store_dims<D>(row + C, ak, scale, hh);
+          store_dims<D>(row + 2 * C, av, 1.f, hh);
         }
       }
     }
-    __syncthreads();
-    // write this pass's column range [c0, c1) of the window's dqkv rows (8-byte stores; C % 4 == 0)
-    const int c0 = PASS == 1 ? 0 : C, w4 = (PASS == 1 ? C : 2 * C) / 4;
-    bf16_t* dst = dqkv + (int64_t)bw * N * C3;
-    for (int i = threadIdx.x; i < N * w4; i += blockDim.x) {
-      const int t = i / w4, c = c0 + (i - t * w4) * 4;
-      *reinterpret_cast<u16x4*>(dst + t * C3 + c) = *reinterpret_cast<const u16x4*>(sd + t * C3 + c);
-    }
+    wave_sync();
   }
   if (PASS == 1) {
-    // relative-position-bias gradient partial [H][N(q)][N(key)] of this workgroup
-    float* dstb = dbias_part + ((int64_t)blockIdx.x * H + h) * N * N;
+    // relative-position-bias gradient of this workgroup's windows: the 4 waves' tiles summed in LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(BB + 64 * BP);    // [64][64] over the wave tiles
+    for (int e = threadIdx.x; e < 64 * 64; e += WA_NT) red[e] = 0.f;
+    __syncthreads();
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = 32 * qt + l32;
+    for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = 32 * kt + acc_row(r, hh);
-          if (q < N && key < N) dstb[q * N + key] = dsacc[qt][kt][r];
-        }
-    }
+        for (int r = 0; r < 16; ++r)
+          atomicAdd(red + (32 * qt + l32) * 64 + 32 * kt + acc_row(r, hh), dsacc[qt][kt][r]);
+    __syncthreads();
+    float* dst = dbias_part + ((int64_t)pb * H + h) * N * N;
+    for (int e = threadIdx.x; e < N * N; e += WA_NT) dst[e] = red[(e / N) * 64 + e % N];
   }
 }
 
-size_t fwd_mfma_lds(int N, int H, int d) { const int C = H * d; return (size_t)2 * (64 * 3 * C + 64 * C + (H + 1) * 64 * BP); }
-size_t bwd_mfma_lds(int N, int H, int d) {
-  const int C = H * d;
-  return (size_t)2 * (2 * 64 * 3 * C + 64 * C + (H + 1) * 64 * BP) + (size_t)2 * H * 64 * sizeof(float);
-}
+size_t fwd_mfma_lds() { return (size_t)2 * (64 * BP + 4 * FWD_WAVE); }
+size_t bwd_mfma_lds() { return (size_t)2 * (64 * BP + 4 * BWD_WAVE); }
 bool mfma_ok(int N, int H, int d, int dt) {
-  return dt == kBF16 && d <= 16 && N <= 64 && (N * H * d) % 8 == 0 && (H * d) % 4 == 0 && H <= 8 &&
-         bwd_mfma_lds(N, H, d) <= 160 * 1024;
+  return dt == kBF16 && d >= 2 && d <= 16 && d % 2 == 0 && N >= 1 && N <= 64 && H >= 1;
+}
+// workgroups per head: 4 waves each, ~`per_cu` workgroups per CU over all heads
+int mfma_blocks_per_head(int Bw, int H, int per_cu) {
+  const int want = (256 * per_cu) / H;
+  const int need = (Bw + 3) / 4;
+  return need < want ? need : (want > 0 ? want : 1);
 }
 
 }  // namespace
@@ -631,54 +654,88 @@ PDT_API int pdt_win_attn_grid(int Bw) { return Bw < 512 ? Bw : 512; }
 
 // ---- MFMA path: bias [H, N(q), N(key)] fp32 (dense relative-position bias), mask [nw, N, N] fp32 or null
 PDT_API int pdt_win_attn_mfma_ok(int N, int H, int d, int dt) { return mfma_ok(N, H, d, dt) ? 1 : 0; }
-// one workgroup per CU (LDS-bound), grid-stride over windows; also the dbias partial count
-PDT_API int pdt_win_attn_mfma_grid(int Bw) { return Bw < 256 ? Bw : 256; }
+// number of relative-bias-gradient partials [P, H, N, N] the backward writes
+PDT_API int pdt_win_attn_mfma_grid(int Bw, int H) { return mfma_blocks_per_head(Bw, H, 2); }
 
-PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse,
-                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
-  const size_t lds = fwd_mfma_lds(N, H, d);
-  static bool attr = [] {
-    return hipFuncSetAttribute((const void*)win_attn_fwd_mfma<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024) == hipSuccess &&
-           hipFuncSetAttribute((const void*)win_attn_fwd_mfma<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024) == hipSuccess;
-  }();
-  (void)attr;
-  if (mask)
-    win_attn_fwd_mfma<true><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw,
-                                                                             (bf16_t*)o, lse, Bw, N, H, d, scale);
-  else
-    win_attn_fwd_mfma<false><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>((const bf16_t*)qkv, bias, mask, nw,
-                                                                              (bf16_t*)o, lse, Bw, N, H, d, scale);
+#define PDT_WA_DISPATCH_D(d, CALL) \
+  switch (d) {                      \
+    case 2: CALL(2); break;         \
+    case 4: CALL(4); break;         \
+    case 6: CALL(6); break;         \
+    case 8: CALL(8); break;         \
+    case 10: CALL(10); break;       \
+    case 12: CALL(12); break;       \
+    case 14: CALL(14); break;       \
+    default: CALL(16); break;       \
+  }
+
+namespace {
+template <int D>
+int wa_fwd_launch(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse, int Bw, int N,
+                  int H, float scale, hipStream_t st) {
+  const int P = mfma_blocks_per_head(Bw, H, 4);
+  const size_t lds = fwd_mfma_lds();
+  const bool full = N == 64;
+#define PDT_WF(M, F)                                                                                            \
+  win_attn_fwd_mfma<D, M, F><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (bf16_t*)o, lse, Bw, N, \
+                                                        H, scale, P)
+  if (mask) { if (full) PDT_WF(true, true); else PDT_WF(true, false); }
+  else { if (full) PDT_WF(false, true); else PDT_WF(false, false); }
+#undef PDT_WF
   return (int)hipGetLastError();
 }
-
-// dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw), H, N, N] fp32 fully written;
-// delta_ws [Bw, H, N] fp32 scratch (pass 1 -> pass 2)
-PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, int nw, const void* o,
-                                  const void* dout, const float* lse, float* delta_ws, void* dqkv, float* dbias_part,
-                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || N <= 0 || Bw <= 0) return (int)hipErrorInvalidValue;
-  const size_t lds = bwd_mfma_lds(N, H, d);
+template <int D>
+int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, int nw, const void* o, const void* dout,
+                  const float* lse, void* dqkv, float* dbias_part, int Bw, int N, int H, float scale, hipStream_t st) {
+  const int P = mfma_blocks_per_head(Bw, H, 2);
+  const size_t lds = bwd_mfma_lds();
   static bool attr = [] {
     bool ok = true;
-    const void* fns[4] = {(const void*)win_attn_bwd_mfma<true, 1>, (const void*)win_attn_bwd_mfma<true, 2>,
-                          (const void*)win_attn_bwd_mfma<false, 1>, (const void*)win_attn_bwd_mfma<false, 2>};
+    const void* fns[8] = {
+        (const void*)win_attn_bwd_mfma<D, true, true, 1>,   (const void*)win_attn_bwd_mfma<D, true, false, 1>,
+        (const void*)win_attn_bwd_mfma<D, false, true, 1>,  (const void*)win_attn_bwd_mfma<D, false, false, 1>,
+        (const void*)win_attn_bwd_mfma<D, true, true, 2>,   (const void*)win_attn_bwd_mfma<D, true, false, 2>,
+        (const void*)win_attn_bwd_mfma<D, false, true, 2>,  (const void*)win_attn_bwd_mfma<D, false, false, 2>};
     for (const void* f : fns)
-      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_mfma_lds()) == hipSuccess;
     return ok;
   }();
-  (void)attr;
-#define PDT_WB(M, P)                                                                                        \
-  win_attn_bwd_mfma<M, P><<<pdt_win_attn_mfma_grid(Bw), 64 * H, lds, st>>>(                                 \
-      (const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, \
-      dbias_part, Bw, N, H, d, scale)
-  if (mask) { PDT_WB(true, 1); PDT_WB(true, 2); }
-  else { PDT_WB(false, 1); PDT_WB(false, 2); }
+  if (!attr) return (int)hipErrorInvalidValue;
+  const bool full = N == 64;
+#define PDT_WB(M, F, PS)                                                                                       \
+  win_attn_bwd_mfma<D, M, F, PS><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, \
+                                                            (const bf16_t*)dout, lse, (bf16_t*)dqkv, dbias_part, Bw, N, \
+                                                            H, scale, P)
+  if (mask) {
+    if (full) { PDT_WB(true, true, 1); PDT_WB(true, true, 2); }
+    else { PDT_WB(true, false, 1); PDT_WB(true, false, 2); }
+  } else {
+    if (full) { PDT_WB(false, true, 1); PDT_WB(false, true, 2); }
+    else { PDT_WB(false, false, 1); PDT_WB(false, false, 2); }
+  }
 #undef PDT_WB
   return (int)hipGetLastError();
 }
+}  // namespace
+
+PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse,
+                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || (mask && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D) return wa_fwd_launch<D>(qkv, bias, mask, nw, o, lse, Bw, N, H, scale, st)
+  PDT_WA_DISPATCH_D(d, PDT_C)
+#undef PDT_C
+}
+
+// dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw, H), H, N, N] fp32 fully written
+PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, int nw, const void* o,
+                                  const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N,
+                                  int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || (mask && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D) return wa_bwd_launch<D>(qkv, bias, mask, nw, o, dout, lse, dqkv, dbias_part, Bw, N, H, scale, st)
+  PDT_WA_DISPATCH_D(d, PDT_C)
+#undef PDT_C
+}
+#undef PDT_WA_DISPATCH_D
 
 // qkv [Bw, N, 3, H, d] (= [Bw, N, 3C]); bias_t [H, N(j), N(i)] fp32 (dense relative-position bias,
 // transposed); mask_t [nw, N(j), N(i)] fp32 or null (window bw uses mask bw % nw); o [Bw, N, C]; lse [Bw, H, N]

@@ -51,8 +51,6 @@ class _WindowAttnFn(torch.autograd.Function):
         d = C // num_heads
         qkv = qkv.contiguous()
         bias = rel_bias.float().contiguous()
-        bias_t = bias.transpose(1, 2).contiguous()
-        m, m_t = _mask_t(mask) if mask is not None else (None, None)
         nw = mask.shape[0] if mask is not None else 1
         o = torch.empty((Bw, N, C), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty((Bw, num_heads, N), dtype=torch.float32, device=qkv.device)
@@ -67,6 +65,8 @@ class _WindowAttnFn(torch.autograd.Function):
             ctx.mask = (m, None, nw)
             ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
             return o
+        bias_t = bias.transpose(1, 2).contiguous()
+        m, m_t = _mask_t(mask) if mask is not None else (None, None)
         _lib.call("pdt_win_attn_fwd", qkv.data_ptr(), bias_t.data_ptr(), _lib.ptr(m_t), nw, o.data_ptr(),
                   lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.dtype_code(qkv.dtype),
                   _lib.stream_handle(qkv.device))
@@ -82,13 +82,12 @@ class _WindowAttnFn(torch.autograd.Function):
             m, _, nw = ctx.mask
             Bw, N, C3 = qkv.shape
             d = C3 // 3 // ctx.h
-            G = _lib.require().pdt_win_attn_mfma_grid(Bw)
+            G = _lib.require().pdt_win_attn_mfma_grid(Bw, ctx.h)
             dqkv = torch.empty_like(qkv)
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
-            delta = torch.empty_like(lse)
             do = do.contiguous().to(qkv.dtype)
             _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
-                      do.data_ptr(), lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
+                      do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
                       ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
             return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
         qkv, bias, bias_t, o, lse = ctx.saved_tensors

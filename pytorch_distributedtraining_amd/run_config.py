@@ -42,6 +42,7 @@ class RunConfig:
     bucket_cap_mb: float = 64.0
     first_bucket_mb: float = 8.0
     sync_batchnorm: bool = False
+    conv_benchmark: bool = True             # MIOpen find per conv shape (torch.backends.cudnn.benchmark)
     steps: int = 10
     warmup: int = 2
     log_every: int = 10

@@ -80,6 +80,8 @@ def run(cfg: RunConfig) -> dict:
 
     gpu = cfg.gpu and torch.cuda.is_available()
     torch.manual_seed(cfg.seed)
+    if cfg.gpu and cfg.conv_benchmark:
+        torch.backends.cudnn.benchmark = True   # MIOpen find: +12 % on ResNet-50 (profiles/r1_v9_miopen_modes.log)
     model, kind = build_model(cfg)
     if gpu and kind == "cls":
         model = model.to(memory_format=torch.channels_last)

@@ -312,6 +312,8 @@ def main():
         return
     torch.cuda.set_device(lr)
     dev = torch.device("cuda", lr)
+    # same MIOpen find mode as bench.py for the convolution workloads (fair comparison)
+    torch.backends.cudnn.benchmark = os.environ.get("PDT_CONV_BENCHMARK", "1") == "1"
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     if a.workload in ("resnet50-ddp", "swinir-stoke"):
         (resnet50_ddp if a.workload == "resnet50-ddp" else swinir_stoke)(a, dev, world, rank)

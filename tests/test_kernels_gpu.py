@@ -549,7 +549,8 @@ def test_linear_colsum_bias_grad():
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("N,h,d,Bw,nw", [(64, 6, 10, 32, 16), (49, 3, 32, 8, 4), (16, 2, 4, 6, 3),
-                                          (49, 4, 16, 300, 4), (64, 6, 10, 704, 64)])
+                                          (49, 4, 16, 300, 4), (64, 6, 10, 704, 64), (64, 12, 8, 40, 8),
+                                          (64, 4, 9, 12, 4), (36, 2, 14, 9, 3)])
 def test_window_attention(dtype, masked, N, h, d, Bw, nw):
     """Fused HIP window attention (fwd + bwd incl. relative-bias grad) vs the fp32 PyTorch formula."""
     from pytorch_distributedtraining_amd.ops.window_attention import _WindowAttnFn, reference
