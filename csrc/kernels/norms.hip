@@ -578,29 +578,47 @@ PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const flo
 // Column sums of a [rows, N] matrix (T) into out[N] (W) -- bias gradients.  Workspace:
 // pdt_colsum_ws_floats(rows, N) floats (reduce.h col_plan partials + second level).
 namespace {
-// narrow N (< 2048): rows packed NT / (N/8) per workgroup pass, one partial row per workgroup
-template <typename T>
+// narrow N (< VEC * NT): rows packed NT / (N / VEC) per workgroup pass, one partial row per workgroup.
+// VEC = 8 (16-B bf16 loads) when N % 8 == 0, else 4 (SwinIR's C = 60 / 180 bias gradients).
+template <typename T, int VEC>
+__device__ __forceinline__ void load_vec(const T* p, float* v) {
+  if constexpr (VEC == 8) {
+    Vec8<T>::load(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    const u16x4 a = *reinterpret_cast<const u16x4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = bf2f(a[k]);
+  } else {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = a[k];
+  }
+}
+template <typename T, int VEC>
 __global__ __launch_bounds__(NT) void colsum_partial_narrow(const T* __restrict__ x, int rows, int N, int rows_per,
                                                             float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sacc[NT * 8];
-  const int tpr = N >> 3, rpb = NT / tpr;
-  const int rg = threadIdx.x / tpr, col = (threadIdx.x - rg * tpr) * 8;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __shared__ __attribute__((aligned(16))) float sacc[NT * VEC];
+  const int tpr = N / VEC, rpb = NT / tpr;
+  const int rg = threadIdx.x / tpr, col = (threadIdx.x - rg * tpr) * VEC;
+  float acc[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
   const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
   if (rg < rpb) {
     for (int r = r0 + rg; r < r1; r += rpb) {
-      float v[8];
-      Vec8<T>::load(x + (int64_t)r * N + col, v);
+      float v[VEC];
+      load_vec<T, VEC>(x + (int64_t)r * N + col, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      for (int k = 0; k < VEC; ++k) acc[k] += v[k];
     }
   }
-  Vec8<float>::store(sacc + threadIdx.x * 8, acc);
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) sacc[threadIdx.x * VEC + k] = acc[k];
   __syncthreads();
   for (int c = threadIdx.x; c < N; c += NT) {
-    const int c8 = c >> 3, k = c & 7;
+    const int cv = c / VEC, k = c % VEC;
     float t = 0.f;
-    for (int g = 0; g < rpb; ++g) t += sacc[(g * tpr + c8) * 8 + k];
+    for (int g = 0; g < rpb; ++g) t += sacc[(g * tpr + cv) * VEC + k];
     part[(int64_t)blockIdx.x * N + c] = t;
   }
 }
@@ -638,12 +656,15 @@ PDT_API int pdt_colsum_ws_floats(int rows, int N) { return (int)red::col_ws_floa
 
 PDT_API int pdt_colsum(const void* x, int rows, int N, int xdt, void* out, int odt, float* ws, int accumulate,
                        hipStream_t st) {
-  if (N % 8 != 0) return (int)hipErrorInvalidValue;
+  if (N % 8 != 0 && !(N % 4 == 0 && N < 4 * NT)) return (int)hipErrorInvalidValue;
   const red::ColPlan pl = red::col_plan(rows, N);
   dim3 grid(pl.col_groups, pl.R);
-  if (N < 8 * NT) {
-    if (xdt == kBF16) colsum_partial_narrow<bf16_t><<<pl.R, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
-    else colsum_partial_narrow<float><<<pl.R, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  if (N % 8 != 0) {
+    if (xdt == kBF16) colsum_partial_narrow<bf16_t, 4><<<pl.R, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
+    else colsum_partial_narrow<float, 4><<<pl.R, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
+  } else if (N < 8 * NT) {
+    if (xdt == kBF16) colsum_partial_narrow<bf16_t, 8><<<pl.R, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
+    else colsum_partial_narrow<float, 8><<<pl.R, NT, 0, st>>>((const float*)x, rows, N, pl.rows_per, ws);
   } else if (xdt == kBF16) {
     colsum_partial_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, rows, N, pl.rows_per, ws);
   } else {

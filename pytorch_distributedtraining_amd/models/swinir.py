@@ -42,6 +42,25 @@ def window_reverse(w, ws, H, W):
     return x.permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, -1)
 
 
+class _RelBiasGather(torch.autograd.Function):
+    """table[idx] whose backward is one atomic index_add_ into the (225 x heads) table instead of the
+    sort-based index backward (5-6 small kernels per block per micro-step on the GPU)."""
+
+    @staticmethod
+    def forward(ctx, table, idx):
+        ctx.save_for_backward(idx)
+        ctx.rows = table.shape[0]
+        return table.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        if torch.are_deterministic_algorithms_enabled():
+            gt = torch.zeros((ctx.rows, g.shape[1]), dtype=g.dtype, device=g.device)
+            return gt.index_put_((idx,), g, accumulate=True), None
+        return torch.zeros((ctx.rows, g.shape[1]), dtype=g.dtype, device=g.device).index_add_(0, idx, g), None
+
+
 class WindowAttention(nn.Module):
     def __init__(self, dim, window_size, num_heads, qkv_bias=True):
         super().__init__()
@@ -67,7 +86,8 @@ class WindowAttention(nn.Module):
             # fused HIP window attention: reads the qkv projection in place, never materialises the
             # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
             qkv = self.qkv(x)
-            bias = self.relative_position_bias_table[self.relative_position_index.view(-1)].view(N, N, h)
+            bias = _RelBiasGather.apply(self.relative_position_bias_table, self.relative_position_index.view(-1))
+            bias = bias.view(N, N, h)
             out = window_attention(qkv, bias.permute(2, 0, 1), mask, h, self.scale)
             return self.proj(out)
         qkv = self.qkv(x).reshape(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4)

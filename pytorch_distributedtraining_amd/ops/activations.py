@@ -13,6 +13,11 @@ import torch.nn.functional as F
 from . import _lib
 
 
+def colsum_ok(n: int) -> bool:
+    """Widths the HIP column-sum kernel takes: N % 8 == 0, or N % 4 == 0 below 1024 columns."""
+    return n % 8 == 0 or (n % 4 == 0 and n < 1024)
+
+
 def _colsum(x2, out_dtype):
     rows, n = x2.shape
     lib = _lib.require()

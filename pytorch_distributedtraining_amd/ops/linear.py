@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .activations import _colsum
+from .activations import _colsum, colsum_ok
 
 _WGRAD_CHUNK = 4096
 
@@ -64,7 +64,7 @@ class _LinearFn(torch.autograd.Function):
                 x2 = x2.contiguous()
             dw = wgrad(dy2, x2, w.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _colsum(dy2, w.dtype) if dy2.shape[1] % 8 == 0 else dy2.sum(0).to(w.dtype)
+            db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
         return dx, dw, db
 
 

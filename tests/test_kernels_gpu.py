@@ -657,3 +657,28 @@ def test_resnet50_fused_bn_matches_plain_model():
         gb = dict(b.named_parameters())[name].grad
         gr = dict(r.named_parameters())[name].grad
         assert rel_err(ga, gr) < 2 * rel_err(gb, gr) + 5e-2, name
+
+
+@pytest.mark.parametrize("n", [60, 180, 12, 1020, 64, 2056])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_colsum_widths(n, dt):
+    """HIP column sum (bias gradients) for 16-B and 8-B column chunks vs the fp32 torch sum."""
+    from pytorch_distributedtraining_amd.ops.activations import _colsum, colsum_ok
+    assert colsum_ok(n)
+    torch.manual_seed(0)
+    x = torch.randn(30011, n, device=DEV).to(dt)
+    out = _colsum(x, torch.float32)
+    assert rel_err(out, x.float().sum(0)) < 1e-4
+
+
+def test_swinir_rel_bias_gather_grad():
+    """Atomic index_add_ backward of the relative-position-bias gather equals the torch index backward."""
+    from pytorch_distributedtraining_amd.models.swinir import _RelBiasGather
+    torch.manual_seed(0)
+    table = torch.randn(225, 6, device=DEV, requires_grad=True)
+    idx = torch.randint(0, 225, (4096,), device=DEV)
+    g = torch.randn(4096, 6, device=DEV)
+    (_RelBiasGather.apply(table, idx) * g).sum().backward()
+    t2 = table.detach().clone().requires_grad_()
+    (t2[idx] * g).sum().backward()
+    assert rel_err(table.grad, t2.grad) < 1e-5
