@@ -55,6 +55,30 @@ __global__ __launch_bounds__(NT) void im2col3x3_kernel(const T* __restrict__ x, 
   }
 }
 
+// channels-contiguous bf16 input (sc == 1, C % 4 == 0: SwinIR's [B, L, C] token tensors viewed as NHWC):
+// every K run of one (kh, kw) tap is C contiguous input elements, so each thread moves 4 channels with
+// one 8-byte load and one 8-byte store (coalesced both ways) instead of 8 two-byte gathers.
+__global__ __launch_bounds__(NT) void im2col3x3_c4_kernel(const bf16_t* __restrict__ x, int64_t sn, int64_t sh,
+                                                          int64_t sw, int C, int H, int W, int Kp, int64_t total4,
+                                                          bf16_t* __restrict__ out) {
+  const int kp4 = Kp >> 2, c4n = C >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total4; i += (int64_t)gridDim.x * NT) {
+    const int64_t p = i / kp4;
+    const int j = (int)(i - p * kp4);
+    const int kk = j / c4n, c = (j - kk * c4n) * 4;
+    const int w = (int)(p % W);
+    const int64_t t = p / W;
+    const int h = (int)(t % H);
+    const int64_t n = t / H;
+    u16x4 v = {0, 0, 0, 0};
+    if (kk < 9) {
+      const int ih = h + kk / 3 - 1, iw = w + kk % 3 - 1;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = *reinterpret_cast<const u16x4*>(x + n * sn + ih * sh + iw * sw + c);
+    }
+    *reinterpret_cast<u16x4*>(out + i * 4) = v;
+  }
+}
+
 }  // namespace
 
 // x: logical [N, C, H, W] with element strides (sn, sc, sh, sw); out: [N*H*W, Kp] row-major, Kp % 8 == 0,
@@ -62,6 +86,13 @@ __global__ __launch_bounds__(NT) void im2col3x3_kernel(const T* __restrict__ x, 
 PDT_API int pdt_im2col3x3(const void* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int N, int C, int H, int W,
                           int Kp, void* out, int dt, hipStream_t st) {
   if (Kp % 8 != 0 || Kp < 9 * C || N <= 0 || C <= 0 || H <= 0 || W <= 0) return (int)hipErrorInvalidValue;
+  if (dt == kBF16 && sc == 1 && C % 4 == 0 && sn % 4 == 0 && sh % 4 == 0 && sw % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(x) & 7) == 0) {
+    const int64_t total4 = (int64_t)N * H * W * (Kp / 4);
+    im2col3x3_c4_kernel<<<grid_for(total4, NT, 256 * 16), NT, 0, st>>>((const bf16_t*)x, sn, sh, sw, C, H, W, Kp,
+                                                                        total4, (bf16_t*)out);
+    return (int)hipGetLastError();
+  }
   const int64_t total8 = (int64_t)N * H * W * (Kp / 8);
   const int grid = grid_for(total8, NT, 256 * 16);
   if (dt == kBF16)
