@@ -48,9 +48,14 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 template <typename G>
 __global__ __launch_bounds__(MT_THREADS) void adamw_mt_kernel(
     const int64_t* __restrict__ meta, const int* __restrict__ blk, int chunk, AdamHyper h,
-    const float* __restrict__ gscale, const int* __restrict__ found_inf) {
+    const float* __restrict__ gscale, const int* __restrict__ found_inf, const float* __restrict__ dstep) {
   if (found_inf != nullptr && *found_inf != 0) return;  // GradScaler semantics: skip the step
   const float gs = gscale ? *gscale : 1.f;
+  if (dstep != nullptr) {   // graph-capturable: the step count lives on the device, bias corrections here
+    const float t = *dstep;
+    h.step_size = h.lr / (1.f - powf(h.beta1, t));
+    h.bc2_sqrt = sqrtf(1.f - powf(h.beta2, t));
+  }
   const int t = blk[2 * blockIdx.x], c = blk[2 * blockIdx.x + 1];
   const int64_t* mt = meta + (int64_t)t * MT_META;
   float* __restrict__ P = reinterpret_cast<float*>(mt[0]);
@@ -202,13 +207,14 @@ __global__ __launch_bounds__(MT_THREADS) void cast_f32_bf16_mt_kernel(const int6
 
 PDT_API int pdt_adamw_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, int grad_dtype, float lr,
                          float beta1, float beta2, float eps, float wd, float step_size, float bc2_sqrt,
-                         int decoupled, const float* gscale, const int* found_inf, hipStream_t stream) {
+                         int decoupled, const float* gscale, const int* found_inf, const float* dstep,
+                         hipStream_t stream) {
   AdamHyper h{lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, decoupled};
   if (nblocks <= 0) return 0;
   if (grad_dtype == kF32)
-    adamw_mt_kernel<float><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk, h, gscale, found_inf);
+    adamw_mt_kernel<float><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk, h, gscale, found_inf, dstep);
   else
-    adamw_mt_kernel<bf16_t><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk, h, gscale, found_inf);
+    adamw_mt_kernel<bf16_t><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk, h, gscale, found_inf, dstep);
   return (int)hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ c_float = ctypes.c_float
 # name -> argtypes (restype is always c_int)
 _SIGS = {
     "pdt_adamw_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float,
-                     c_float, c_float, c_int, c_void_p, c_void_p, c_void_p],
+                     c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_l2norm_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],

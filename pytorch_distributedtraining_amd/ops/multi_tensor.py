@@ -177,13 +177,18 @@ def scale_(tensors: Sequence[torch.Tensor], s: torch.Tensor) -> None:
 
 def adamw_step(params, grads, exp_avgs, exp_avg_sqs, *, lr: float, beta1: float, beta2: float, eps: float,
                weight_decay: float, step: int, decoupled: bool = True, grad_scale: torch.Tensor | None = None,
-               found_inf: torch.Tensor | None = None, out_bf16=None, table: TensorTable | None = None) -> None:
+               found_inf: torch.Tensor | None = None, out_bf16=None, table: TensorTable | None = None,
+               dstep: torch.Tensor | None = None) -> None:
     """One fused (multi-tensor) AdamW update.  fp32 params/state; grads fp32 or bf16.
 
     grad_scale: optional device scalar multiplied into every gradient (unscale x clip coefficient).
     found_inf: optional device int32 flag; non-zero skips the update (GradScaler semantics).
     out_bf16: optional list of bf16 tensors receiving the updated params (low-precision compute copy /
-    all-gather input for the sharded engines)."""
+    all-gather input for the sharded engines).
+    dstep: optional device fp32 step count (already incremented): the kernel derives the bias corrections
+    from it, so the launch replays correctly inside a captured HIP graph (``step`` is then ignored)."""
+    if dstep is not None and params and params[0].device.type != "cuda":
+        step = int(dstep.item())
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     step_size = lr / bc1
@@ -219,7 +224,7 @@ def adamw_step(params, grads, exp_avgs, exp_avg_sqs, *, lr: float, beta1: float,
     _lib.call("pdt_adamw_mt", table.meta.data_ptr(), table.blk.data_ptr(), table.nblocks, table.chunk,
               _lib.dtype_code(gdt), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
               float(step_size), float(bc2_sqrt), 1 if decoupled else 0, _lib.ptr(grad_scale), _lib.ptr(found_inf),
-              _lib.stream_handle(dev))
+              _lib.ptr(dstep), _lib.stream_handle(dev))
 
 
 def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:

@@ -6,6 +6,10 @@
   so LR schedulers (OneCycleLR cycling betas, Stoke-DDP.py:300) and checkpoints interoperate.
 * Sync-free mixed precision: ``step(grad_scale=t, found_inf=f)`` takes device scalars produced by the
   fused clip / unscale kernels; no host round trip between backward and the update.
+* Graph capture (``capturable=True``): the step count of each param group lives in a device tensor that a
+  captured kernel increments, and the AdamW kernel derives its bias corrections from it, so a training step
+  captured into a HIP graph (``utils.graphs.GraphedStep``) replays with the right step every time.  The
+  learning rate is read when the step is captured (a schedule needs a re-capture).
 * Sharded engines: a parameter carrying ``_pdt_lp_shard`` (FSDP / ZeRO flat shards) gets its bf16
   compute copy written by the same kernel (fused cast epilogue = the all-gather input).
 
@@ -30,14 +34,41 @@ def _like(g, p):
 
 class FusedAdamW(Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
-                 decoupled=True, **_ignored):
+                 decoupled=True, capturable=False, **_ignored):
         if amsgrad:
             raise ValueError("FusedAdamW: amsgrad is not supported")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
-                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                        maximize=False, foreach=None, capturable=capturable, differentiable=False, fused=None,
                         decoupled=decoupled)
         super().__init__(params, defaults)
         self._tables = mt.TableCache()
+        self._dsteps: dict = {}
+
+    def _device_step(self, gi, group, dev):
+        """The group's shared device step tensor (created eagerly, before any capture, from the state)."""
+        ds = self._dsteps.get(gi)
+        if ds is None or ds.device != dev:
+            start = 0.0
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    start = max(start, float(st["step"]))
+            ds = self._dsteps[gi] = torch.full((), start, dtype=torch.float32, device=dev)
+        return ds
+
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics for ``.grad``; engine-owned flat gradients (``_pdt_zero_grad``: DDP's
+        compute-dtype mode, where autograd accumulates into the bucket views) are zeroed in place."""
+        super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                zero = getattr(p, "_pdt_zero_grad", None)
+                if zero is not None:
+                    zero()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dsteps.clear()     # device step counters are rebuilt from the loaded per-param steps
 
     def _init_state(self, p):
         st = self.state[p]
@@ -57,6 +88,8 @@ class FusedAdamW(Optimizer):
             beta1, beta2 = group["betas"]
             lr = float(group["lr"]) if not torch.is_tensor(group["lr"]) else float(group["lr"].item())
             buckets = {}
+            cap = bool(group.get("capturable", False))
+            dstep = None
             for p in group["params"]:
                 g = grad_of(p)
                 if g is None:
@@ -67,8 +100,15 @@ class FusedAdamW(Optimizer):
                     raise TypeError("FusedAdamW keeps fp32 master params; wrap low-precision models with an "
                                     "engine (FSDP/ZeRO) or keep params fp32 and use autocast")
                 st = self._init_state(p)
-                st["step"] += 1
-                key = (g.dtype, int(st["step"].item()), p.device)
+                if cap and p.device.type == "cuda":
+                    if dstep is None:
+                        dstep = self._device_step(gi, group, p.device)
+                        dstep.add_(1.0)          # one device increment per group (captured with the step)
+                    st["step"] = dstep
+                    key = (g.dtype, -1, p.device)
+                else:
+                    st["step"] += 1
+                    key = (g.dtype, int(st["step"].item()), p.device)
                 buckets.setdefault(key, []).append(p)
             for (gdt, step, dev), ps in buckets.items():
                 grads = [_like(grad_of(p), p) for p in ps]
@@ -81,9 +121,9 @@ class FusedAdamW(Optimizer):
                     cols = [ps, grads, ms, vs, lps if has_lp else [None] * len(ps)]
                     table = self._tables.get((gi, gdt, step > 0), cols)
                 mt.adamw_step(ps, grads, ms, vs, lr=lr, beta1=beta1, beta2=beta2, eps=group["eps"],
-                              weight_decay=group["weight_decay"], step=step, decoupled=group.get("decoupled", True),
-                              grad_scale=grad_scale, found_inf=found_inf, out_bf16=lps if has_lp else None,
-                              table=table)
+                              weight_decay=group["weight_decay"], step=max(step, 1),
+                              decoupled=group.get("decoupled", True), grad_scale=grad_scale, found_inf=found_inf,
+                              out_bf16=lps if has_lp else None, table=table, dstep=dstep if step < 0 else None)
                 for p in ps:
                     if getattr(p, "_pdt_lp_shard", None) is not None:
                         p._pdt_lp_version = p._version   # compute copy already refreshed by the kernel

@@ -68,6 +68,7 @@ class _FlatGroup:
             m._pdt_lp_shard = self.flat_param
             m._pdt_lp_version = m._version
             m._pdt_grad = self.flat_grad
+            m._pdt_zero_grad = self.flat_grad.zero_   # optimizer.zero_grad() clears the accumulated flat grad
             self.master = m
 
     def attach_grads(self):
@@ -205,6 +206,7 @@ class DistributedDataParallel(nn.Module):
                 om.data = new
                 om._pdt_lp_shard = g.flat_param
                 om._pdt_grad = g.flat_grad
+                om._pdt_zero_grad = g.flat_grad.zero_
                 om._pdt_lp_version = om._version
                 g.master = om
 

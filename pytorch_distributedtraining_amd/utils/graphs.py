@@ -1,0 +1,67 @@
+"""HIP-graph capture of a whole training step ("HIP streams and graphs instead of a tracing
+compiler").  A step of a fixed-shape model -- forward, backward, gradient clipping coefficient, fused AdamW
+-- is a few hundred to a few thousand kernel launches; replaying it as one graph removes the per-launch
+host cost (Python dispatch + HIP launch, 5-10 us each), which is what bounds small-batch and many-small-
+kernel steps (SwinIR: ~4,600 launches per step).
+
+Requirements on ``step_fn`` (the usual graph-capture rules): static input buffers, no host synchronisation
+(``.item()``, ``.cpu()``, data-dependent Python control flow), an optimizer that is capture-safe
+(``FusedAdamW(capturable=True)``: device step counter, device clip coefficient), and gradients zeroed in
+place (``zero_grad(set_to_none=False)``) so they keep their addresses.
+
+    step = GraphedStep(train_step, x_static, y_static, warmup=3)
+    for x, y in loader:
+        loss = step(x, y)        # copies into the static buffers, replays the graph
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+
+class GraphedStep:
+    """Capture ``step_fn(*static_inputs)`` into a HIP graph on first call and replay it afterwards.
+
+    The first call runs ``warmup`` eager iterations on a side stream (allocator / workspace / kernel-table
+    warm-up: these ARE training steps on the first batch), captures one iteration, then replays it -- so the
+    first call advances training by ``warmup + 1`` steps and every later call by exactly one."""
+
+    def __init__(self, step_fn: Callable, *static_inputs: torch.Tensor, warmup: int = 3,
+                 pool: Optional[tuple] = None):
+        if warmup < 1:
+            raise ValueError("GraphedStep needs at least one eager warm-up iteration before capture")
+        self.fn = step_fn
+        self.inputs = static_inputs
+        self.warmup = warmup
+        self.pool = pool
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.out = None
+        self.eager_steps = 0
+
+    def _capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                self.fn(*self.inputs)
+                self.eager_steps += 1
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=self.pool):
+            self.out = self.fn(*self.inputs)
+
+    def __call__(self, *inputs: torch.Tensor):
+        for dst, src in zip(self.inputs, inputs):
+            if src is not dst:
+                dst.copy_(src, non_blocking=True)
+        if self.graph is None:
+            self._capture()
+        self.graph.replay()
+        return self.out
+
+    def reset(self):
+        """Drop the captured graph (e.g. after changing the learning rate); the next call re-captures."""
+        self.graph = None
+        self.out = None

@@ -72,6 +72,31 @@ def test_ddp_matches_single_process(accum):
         assert torch.allclose(outs[0][k], ref[k], atol=2e-5), k
 
 
+def _w_ddp_master(rank, world):
+    """DDP compute-dtype mode (flat compute copies + fp32 master per group): only FusedAdamW.zero_grad()
+    clears the accumulated flat gradient between steps."""
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    m = _model()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.001, first_bucket_mb=0.0005, compute_dtype=torch.float32)
+    opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    for s in range(STEPS):
+        x, y = _data(s, world)
+        loss = nn.functional.mse_loss(ddp(_shard(x, rank, world)), _shard(y, rank, world))
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    return {k: v.detach().clone() for k, v in ddp.full_state_dict().items()}
+
+
+def test_ddp_compute_dtype_master_matches_single_process():
+    ref = _reference(2)
+    outs = run_workers(_w_ddp_master, 2)
+    for k in ref:
+        assert torch.allclose(outs[0][k], outs[1][k], atol=0)
+        assert torch.allclose(outs[0][k], ref[k], atol=2e-5), k
+
+
 def _w_zero(rank, world, sddp, bcast16):
     from pytorch_distributedtraining_amd.optim import FusedAdamW
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
