@@ -40,8 +40,6 @@ def parse():
     ap.add_argument("--reshard", type=int, default=1, help="FSDP reshard after forward (FULL_SHARD)")
     ap.add_argument("--act-ckpt", type=int, default=0)
     ap.add_argument("--profile-steps", type=int, default=0)
-    ap.add_argument("--graph", type=int, default=0,
-                    help="replay the whole training step as a captured HIP graph (gpt2-ddp, single rank)")
     return ap.parse_args()
 
 
@@ -146,8 +144,7 @@ def bench_gpt2(args, comm, dev, world, rank):
         params = model.optimizer_parameters()
         sharded = False
         par = f"dp{world}"
-    use_graph = bool(args.graph) and not fsdp and world == 1
-    opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, capturable=use_graph)
+    opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     vocab = 128000 if llama else 50257
@@ -163,24 +160,6 @@ def bench_gpt2(args, comm, dev, world, rank):
         opt.step(grad_scale=coef)
         opt.zero_grad(set_to_none=True)
         state["loss"] = loss
-
-    if use_graph:
-        from pytorch_distributedtraining_amd.utils.graphs import GraphedStep
-
-        def captured(x):
-            opt.zero_grad(set_to_none=False)
-            loss = model(x[:, :-1], labels=x[:, 1:])
-            loss.backward()
-            _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=sharded, apply=False)
-            opt.step(grad_scale=coef)
-            return loss.detach()
-
-        graphed = GraphedStep(captured, batches[0].clone(), warmup=2)
-
-        def step():  # noqa: F811 -- graph replay of the same step
-            b = batches[state["i"] % len(batches)]
-            state["i"] += 1
-            state["loss"] = graphed(b)
 
     dt = timed_loop(step, args, comm, dev)
     tokens = world * mb * S * args.steps

@@ -9,6 +9,11 @@ Requirements on ``step_fn`` (the usual graph-capture rules): static input buffer
 (``FusedAdamW(capturable=True)``: device step counter, device clip coefficient), and gradients zeroed in
 place (``zero_grad(set_to_none=False)``) so they keep their addresses.
 
+Status: tested on a plain bf16-autocast GPT-2 (tests/test_kernels_gpu.py::test_graphed_training_step_matches_eager,
+losses and weights match the eager run).  Replaying a DistributedDataParallel-wrapped GPT-2 124M step
+(vocab 50,257) faulted with an illegal address in a rocprim partition kernel, so bench.py does not use
+graphs and engine-wrapped models are not supported yet.
+
     step = GraphedStep(train_step, x_static, y_static, warmup=3)
     for x, y in loader:
         loss = step(x, y)        # copies into the static buffers, replays the graph
