@@ -56,7 +56,6 @@ def test_fsdp_two_ranks_on_one_gpu_matches_one_rank(strategy):
 
 def _train_ddp(rank, world, steps):
     from pytorch_distributedtraining_amd.models.resnet import resnet18
-    from pytorch_distributedtraining_amd.optim import FusedAdamW
     from pytorch_distributedtraining_amd.parallel import Comm
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
     from pytorch_distributedtraining_amd.parallel.syncbn import convert_sync_batchnorm
@@ -66,7 +65,9 @@ def _train_ddp(rank, world, steps):
     comm = Comm()
     m = convert_sync_batchnorm(resnet18(num_classes=10), comm).to(dev).to(memory_format=torch.channels_last)
     ddp = DistributedDataParallel(m, comm=comm)
-    opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-3)
+    # SGD: the update is linear in the gradient, so world-1 vs world-2 rounding differences stay at rounding
+    # level (Adam turns near-zero BN-bias gradients into +-lr sign flips and made this comparison flaky)
+    opt = torch.optim.SGD(ddp.optimizer_parameters(), lr=0.05)
     for s in range(steps):
         g = torch.Generator().manual_seed(s)
         x = torch.randn(8, 3, 32, 32, generator=g).to(dev).to(memory_format=torch.channels_last)
