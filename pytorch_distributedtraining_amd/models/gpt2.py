@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
-from ..ops.linear import Linear
+from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 
 
@@ -77,7 +77,7 @@ class MLP(nn.Module):
         self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        h = F.linear(x, self.c_fc.weight)            # hipBLASLt GEMM, bias folded into the GELU kernel
+        h = linear(x, self.c_fc.weight)              # hipBLASLt GEMM, bias folded into the GELU kernel
         h = bias_gelu(h, self.c_fc.bias, approximate="tanh")
         return self.c_proj(h)
 

@@ -2,6 +2,8 @@
 
 * the bias gradient is reduced with the framework's column-sum kernel (2x the bandwidth of the generic
   reduction torch uses for ``grad_output.sum(0)``);
+* SMALL weight gradients (GPT-2 124M: N x K <= 2.5M outputs) are split 4-8 ways over the tokens into one
+  batched GEMM with fp32 output (1.4-2x, see ``_split_k``);
 * TALL-SKINNY weight gradients -- dW = dY^T X with hundreds of thousands of rows but only tens to
   hundreds of columns (SwinIR-S: 294,912 tokens x C = 60..180) -- are split over the row dimension into
   a batched GEMM with fp32 output and summed: one [N x M] x [M x K] GEMM with M = 295k leaves a single
@@ -26,12 +28,33 @@ def _tall_skinny(m: int, n: int, k: int) -> bool:
     return m >= 16 * _WGRAD_CHUNK and max(n, k) <= 1024
 
 
+def _split_k(m: int, n: int, k: int) -> int:
+    """Token-dimension split for SMALL weight gradients (N x K <= 2.5M outputs: a few dozen 256 x 256
+    output tiles for 256 CUs).  GPT-2 124M at 16 x 1024 tokens (profiles/r1_v10_gemm_small.jsonl):
+    2304x768 134 -> 91 us (8-way), 768x768 95 -> 49 us (8-way), 3072x768 / 768x3072 151 -> 95 us (4-way);
+    the 1.3B flagship's >= 2048x2048 gradients gain nothing and stay one GEMM."""
+    nk = n * k
+    if m < 8192 or nk > 2_500_000:
+        return 1
+    s = 8 if nk < 2_000_000 else 4
+    while s > 1 and (m % s or m // s < 1024):
+        s //= 2
+    return s
+
+
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
     """dW = dy2^T @ x2 ([M, N]^T [M, K] -> [N, K]) in ``out_dtype``; row-split batched GEMM for tall-skinny M."""
     m, n = dy2.shape
     k = x2.shape[1]
-    if not (dy2.is_cuda and _tall_skinny(m, n, k)):
+    if not dy2.is_cuda:
         return torch.mm(dy2.t(), x2).to(out_dtype)
+    if not _tall_skinny(m, n, k):
+        sk = _split_k(m, n, k)
+        if sk == 1:
+            return torch.mm(dy2.t(), x2).to(out_dtype)
+        c = m // sk
+        g = torch.bmm(dy2.view(sk, c, n).transpose(1, 2), x2.view(sk, c, k), out_dtype=torch.float32).sum(0)
+        return g.to(out_dtype)
     s = m // _WGRAD_CHUNK
     main = s * _WGRAD_CHUNK
     a = dy2[:main].view(s, _WGRAD_CHUNK, n).transpose(1, 2)

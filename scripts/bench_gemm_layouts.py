@@ -2,10 +2,17 @@
 dW[N, K] = dY[T, N]^T X[T, K].  Prints ms and TFLOP/s per formulation (hipBLASLt / rocBLAS choices differ
 by operand layout).  Usage: python scripts/bench_gemm_layouts.py"""
 import json
+import sys
+
 import torch
 
-T = 32768
-SHAPES = [(6144, 2048), (2048, 2048), (8192, 2048), (2048, 8192), (50304, 2048)]
+# default: flagship (GPT-2 1.3B, 32 x 1024 tokens); "small": GPT-2 124M DDP (16 x 1024 tokens)
+if len(sys.argv) > 1 and sys.argv[1] == "small":
+    T = 16384
+    SHAPES = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (50304, 768)]
+else:
+    T = 32768
+    SHAPES = [(6144, 2048), (2048, 2048), (8192, 2048), (2048, 8192), (50304, 2048)]
 
 
 def timeit(fn, iters=10):
@@ -36,6 +43,13 @@ def main():
                                                  out_dtype=torch.float32).sum(0),
             "dyT contiguous + mm": lambda: torch.mm(dy.t().contiguous(), x),
         }
+        for sp in (4, 8):
+            cands[f"bmm split{sp} fp32"] = (lambda sp=sp: torch.bmm(dy.view(sp, T // sp, n).transpose(1, 2),
+                                                                    x.view(sp, T // sp, k),
+                                                                    out_dtype=torch.float32).sum(0))
+            cands[f"bmm split{sp} xT fp32"] = (lambda sp=sp: torch.bmm(x.view(sp, T // sp, k).transpose(1, 2),
+                                                                       dy.view(sp, T // sp, n),
+                                                                       out_dtype=torch.float32).sum(0).t())
         for name, fn in cands.items():
             try:
                 out = fn()

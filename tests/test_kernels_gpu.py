@@ -511,7 +511,8 @@ def test_swinir_conv_path_matches_stock_model():
         assert rel_err(p.grad, q.grad) < 6e-2, n
 
 
-@pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60)])
+@pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60), (16384, 768, 768), (16384, 768, 3072),
+                                   (8192 + 512, 3072, 768)])
 def test_linear_tall_skinny_wgrad(M, K, N):
     """Row-split batched weight gradient (SwinIR token counts) vs the fp32 product, under bf16 autocast."""
     from pytorch_distributedtraining_amd.ops.linear import Linear, wgrad
