@@ -470,6 +470,26 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
 // lane's running max moved; (4) the causal mask is one compare+select per element and only on
 // diagonal tiles.
 // ------------------------------------------------------------------------------------------------
+// Causal blocks carry work proportional to their distance from the diagonal.  Workgroups dispatch in
+// flattened-id order, so with the natural (tile, head, batch) grid every (head, batch) group ends with its
+// light tiles and the heaviest tiles of the LAST groups start last (a long tail: causal ran at 80-86 % of
+// the full-attention time, scripts/attn_causal_probe.py).  Decoding the flattened id tile-major instead
+// dispatches the heaviest tile of every (head, batch) first (longest-processing-time order).
+struct BlockCoord {
+  int t, h, b;
+};
+__device__ __forceinline__ BlockCoord heavy_first(bool heavy_is_high) {
+  const int nt = gridDim.x, nh = gridDim.y;
+  const int lin = blockIdx.x + nt * (blockIdx.y + nh * blockIdx.z);
+  const int hb = nh * gridDim.z;
+  const int rank = lin / hb, rem = lin - rank * hb;
+  BlockCoord c;
+  c.h = rem % nh;
+  c.b = rem / nh;
+  c.t = heavy_is_high ? nt - 1 - rank : rank;
+  return c;
+}
+
 template <int D, bool CAUSAL>
 struct FwdV4 {
   static constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
@@ -546,8 +566,9 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const BlockCoord bc = heavy_first(true);
+  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
+  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
   const int hk = hq / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
@@ -1283,7 +1304,9 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];    // [buf][lse | delta]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x;
+  const BlockCoord bc = heavy_first(false);   // causal: low key blocks see the most queries
+  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hk = CAUSAL ? bc.h : (int)blockIdx.y;
+  const int kb = CAUSAL ? bc.t : (int)blockIdx.x;
   const int group = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   const int kw = kb * 128 + w * 32, key = kw + c32;
@@ -1438,8 +1461,9 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const BlockCoord bc = heavy_first(true);
+  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
+  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
   const int hk = hq / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
