@@ -17,7 +17,6 @@ from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
 from ..ops.linear import Linear, linear
@@ -153,7 +152,7 @@ class GPT2LMHeadModel(nn.Module):
             else:
                 x, pending = blk(x, pending)
         x, _ = self.ln_f.forward_add(x, pending)
-        logits = F.linear(x, self.wte.weight)   # tied head
+        logits = linear(x, self.wte.weight)     # tied head (framework linear: transposed-layout dgrad)
         if labels is None:
             return logits
         return cross_entropy(logits, labels, inplace_backward=True)

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import apply_rope, cross_entropy, flash_attn, rope_tables, swiglu
+from ..ops.linear import Linear
 from ..ops.norms import RMSNorm
 
 
@@ -55,8 +56,8 @@ class Attention(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.h, self.hkv, self.d = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
-        self.wqkv = nn.Linear(cfg.dim, (self.h + 2 * self.hkv) * self.d, bias=False)
-        self.wo = nn.Linear(self.h * self.d, cfg.dim, bias=False)
+        self.wqkv = Linear(cfg.dim, (self.h + 2 * self.hkv) * self.d, bias=False)
+        self.wo = Linear(self.h * self.d, cfg.dim, bias=False)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
@@ -71,8 +72,8 @@ class Attention(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)
-        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
+        self.w13 = Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)
+        self.w2 = Linear(cfg.ffn_dim, cfg.dim, bias=False)
 
     def forward(self, x):
         return self.w2(swiglu(self.w13(x)))
@@ -105,7 +106,7 @@ class Llama(nn.Module):
         self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList([LlamaBlock(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
-        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self.output = Linear(cfg.dim, cfg.vocab_size, bias=False)
         cos, sin = rope_tables(cfg.head_dim, cfg.max_seq_len, cfg.rope_theta)
         self.register_buffer("rope_cos", cos, persistent=False)
         self.register_buffer("rope_sin", sin, persistent=False)

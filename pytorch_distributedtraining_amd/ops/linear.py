@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
 from .activations import _colsum, colsum_ok
 
 _WGRAD_CHUNK = 4096
@@ -65,6 +66,23 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.
     return g.to(out_dtype)
 
 
+def transpose16(w: torch.Tensor) -> torch.Tensor:
+    """w.t().contiguous() for a contiguous 16-bit GPU matrix with both dims % 64 == 0 (HIP LDS-tiled kernel)."""
+    r, c = w.shape
+    out = torch.empty(c, r, dtype=w.dtype, device=w.device)
+    _lib.call("pdt_transpose16", w.data_ptr(), out.data_ptr(), r, c, _lib.stream_handle(w.device))
+    return out
+
+
+def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
+    """dX = dY W ([M, N] x [N, K]) as F.linear(dY, W^T): hipBLASLt's NN-layout kernels for this product ran
+    10-25 % below the forward's x W^T layout on the flagship shapes (qkv 0.79 -> 0.59 ms, fc2 0.89 -> 0.75 ms,
+    tied LM head 4.97 -> 4.36 ms at 32 x 1024 tokens, profiles/r1_v11_gemm_dgrad_layout.jsonl); the weight
+    transpose costs ~1 % of the GEMM.  Small weights (GPT-2 124M, SwinIR) keep the single mm."""
+    return (w.dtype in (torch.bfloat16, torch.float16) and w.is_contiguous() and m >= 4096
+            and n % 64 == 0 and k % 64 == 0 and n * k >= 4_000_000 and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -80,7 +98,11 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
+                dx = F.linear(dy2, transpose16(w))
+            else:
+                dx = torch.mm(dy2, w)
+            dx = dx.view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             if not x2.is_contiguous():

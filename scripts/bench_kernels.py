@@ -120,7 +120,7 @@ def cross_entropy(rows=8192, V=50304):
     report(f"cross_entropy fwd+bwd {rows}x{V}", timeit(ours, iters=10), timeit(ref, iters=10), bytes_=3 * rows * V * 2)
 
 
-def bias_gelu(rows=8192, N=8192):
+def bias_gelu(rows=32768, N=8192):
     from pytorch_distributedtraining_amd.ops import bias_gelu
     h = torch.randn(rows, N, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     b = torch.randn(N, device="cuda", dtype=torch.bfloat16, requires_grad=True)

@@ -534,6 +534,28 @@ def test_linear_tall_skinny_wgrad(M, K, N):
     assert rel_err(g, ref_w) < 5e-3
 
 
+@pytest.mark.parametrize("R,C", [(64, 64), (6144, 2048), (2048, 8192), (50304, 768), (192, 4096)])
+def test_transpose16(R, C):
+    from pytorch_distributedtraining_amd.ops.linear import transpose16
+    x = torch.randn(R, C, device=DEV).to(torch.bfloat16)
+    assert torch.equal(transpose16(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("M,K,N", [(8192, 2048, 6144), (4096 + 64, 1024, 4096)])
+def test_linear_transposed_dgrad(M, K, N):
+    """Large data gradients go through F.linear on the HIP-transposed weight: compare with fp32 math."""
+    from pytorch_distributedtraining_amd.ops.linear import _dgrad_via_transpose, linear
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (0.02 * torch.randn(N, K, device=DEV)).to(torch.bfloat16).requires_grad_()
+    assert _dgrad_via_transpose(M, N, K, w)
+    y = linear(x, w)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert rel_err(x.grad, dy.float() @ w.detach().float()) < 1e-2
+    assert rel_err(w.grad, dy.float().t() @ x.detach().float()) < 1e-2
+
+
 def test_linear_colsum_bias_grad():
     from pytorch_distributedtraining_amd.ops.linear import linear
     x = torch.randn(4, 100, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
