@@ -47,8 +47,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def self_launch(args) -> int | None:
+    """``--gpus N`` without a torchrun environment: start N ranks of this script as child processes (one per
+    GPU, env:// rendezvous on 127.0.0.1) -- the reference's own launch patterns (Stoke-DDP.py:2
+    ``torch.distributed.launch --nproc_per_node``, Fairscale-DDP.py:125-132 ``mp.spawn``).  The parent never
+    touches the GPU and never re-execs; it waits for the group and returns its exit code.  Returns None
+    when this process is itself a rank (torchrun / our launcher set WORLD_SIZE)."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled run")
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    from pytorch_distributedtraining_amd.launch import _launch_once
+    from pytorch_distributedtraining_amd.utils.dist import find_free_port
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    return _launch_once(cmd, args.gpus, int(find_free_port()), 0, False, 10.0)
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
 
@@ -98,6 +121,7 @@ def timed_loop(step_fn, args, comm, dev):
             log(f"[bench] warmup step 0 done")
     comm.barrier()
     torch_cuda.synchronize(dev)
+    comm.reset_stats()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step_fn()
@@ -107,9 +131,18 @@ def timed_loop(step_fn, args, comm, dev):
     comm.barrier()
     torch_cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    # collectives issued by the engines inside the timed steps (the two barriers excluded)
+    calls, nbytes = comm.stats["calls"], comm.stats["bytes"]
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     comm.all_reduce(t, "max")
+    timed_loop.comm = {"collectives_per_step": round(calls / args.steps, 2),
+                       "comm_bytes_per_step": int(nbytes / args.steps)}
     return float(t.item())
+
+
+def comm_fields(world):
+    """Traffic of the engines per timed step, for the JSON line (zero collectives at world 1)."""
+    return dict(n_ranks=world, **getattr(timed_loop, "comm", {}))
 
 
 def bench_gpt2(args, comm, dev, world, rank):
@@ -172,7 +205,7 @@ def bench_gpt2(args, comm, dev, world, rank):
         metric = f"tokens/sec {name} FSDP + act-ckpt (whole node)"
     return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": "weak", **comm_fields(world), "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
                        "micro_batch_per_gpu": mb, "params": nparams, "sharding": "full_shard" if args.reshard else
                        "shard_grad_op", "optimizer": "fused AdamW + global-norm clip"}}
@@ -214,9 +247,9 @@ def bench_resnet(args, comm, dev, world, rank):
     sps = world * mb * args.steps / dt
     name = "ResNet-18 DDP CPU/gloo" if cpu else "ResNet-50 DDP"
     return {"metric": f"samples/sec {name} (whole node)", "value": round(sps, 2), "unit": "samples/s",
-            "n_gpus": 0 if cpu else world, "n_ranks": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": 0 if cpu else world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32" if cpu else "bf16", "data": "synthetic",
+            **comm_fields(world), "vs_baseline": None, "dtype": "fp32" if cpu else "bf16", "data": "synthetic",
             "config": {"model": "resnet18" if cpu else "resnet50", "global_batch": world * mb, "seq_len": None,
                        "parallelism": f"dp{world}", "image": "3x224x224"}}
 
@@ -254,7 +287,7 @@ def bench_swinir(args, comm, dev, world, rank):
     return {"metric": "samples/sec SwinIR-S x2 Stoke DDP+OSS+SDDP (whole node)", "value": round(sps, 2),
             "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            **comm_fields(world), "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": "swinir-s-x2", "global_batch": world * mb * accum, "seq_len": None,
                        "parallelism": f"dp{world}+zero2" if world > 1 else "dp1", "image": "3x128x128->3x256x256",
                        "grad_accum": accum}}

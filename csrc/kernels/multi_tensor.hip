@@ -203,7 +203,18 @@ __global__ __launch_bounds__(MT_THREADS) void cast_f32_bf16_mt_kernel(const int6
   for (int64_t j = beg + threadIdx.x; j < end; j += MT_THREADS) D[j] = f2bf(S[j]);
 }
 
+// Device step counter of a param group: +1 unless the (all-reduced) found_inf flag says the step is skipped
+// (torch.amp.GradScaler skips optimizer.step() on overflow, so Adam's bias-correction step must not move).
+__global__ void step_inc_kernel(float* __restrict__ dstep, const int* __restrict__ found_inf) {
+  if (threadIdx.x == 0 && (found_inf == nullptr || *found_inf == 0)) dstep[0] = dstep[0] + 1.f;
+}
+
 }  // namespace
+
+PDT_API int pdt_step_inc(float* dstep, const int* found_inf, hipStream_t stream) {
+  step_inc_kernel<<<1, 64, 0, stream>>>(dstep, found_inf);
+  return (int)hipGetLastError();
+}
 
 PDT_API int pdt_adamw_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, int grad_dtype, float lr,
                          float beta1, float beta2, float eps, float wd, float step_size, float bc2_sqrt,

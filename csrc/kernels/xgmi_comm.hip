@@ -23,6 +23,16 @@
 // peers into its own slot) + all-gather phase (every rank reads chunk p from peer p): 2(W-1)/W of the
 // payload crosses the fabric, spread over all 7 links.  all_gather / reduce_scatter: 2 kernels each.
 //
+// Every collective of a rank runs on that rank's dedicated communication stream (parallel/xgmi.py), so
+// the per-rank kernel order -- which the slot-reuse argument above relies on -- is the issue order.
+// Payloads larger than a slot are chunked by the host, one epoch per chunk; reduce-scatter inputs and
+// all-gather outputs are addressed with a per-peer pitch so a chunk is a strided window of the tensor.
+//
+// A wait that exceeds the spin budget is an error, never a silent result: the block poisons its part
+// of the output with NaN (all-ones bits, NaN in fp32 and bf16) instead of reading possibly stale peer
+// slots, and sets the error word in device memory AND in a host-mapped word that the engines poll at
+// their synchronisation points without a device sync (XGMIComm.raise_if_failed).
+//
 // The scalar data cache is never written: flags and payload use vector atomics / vector buffer stores.
 #include "common.h"
 #include <string.h>
@@ -40,6 +50,7 @@ constexpr int SYS = 1 | 16;           // buffer-op cache policy: sc0 | sc1 = sys
 
 struct XArgs {
   char* buf[MAXW];                    // symmetric buffer base of every rank (own + IPC-mapped peers)
+  unsigned* host_err;                 // host-mapped error word (may be null)
   int rank, world;
   unsigned epoch;
   unsigned spin_limit;
@@ -58,8 +69,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t
 }
 
 // Every block: signal barrier `b` of epoch a.epoch to all peers, then wait for all peers' signals.
-__device__ __forceinline__ void mesh_barrier(const XArgs& a, int b) {
+// Returns false (for the whole block) if any wait ran out of budget.
+__device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
+  __shared__ int timed_out;
   const int t = threadIdx.x;
+  if (t == 0) timed_out = 0;
+  __syncthreads();
   if (t < a.world) {
     gu32* remote = (gu32*)(a.buf[t]) + b * MAXW + a.rank;
     __hip_atomic_store(remote, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -69,6 +84,9 @@ __device__ __forceinline__ void mesh_barrier(const XArgs& a, int b) {
       if (++spins > a.spin_limit) {   // give up: record the failure, never hang the queue
         __hip_atomic_fetch_or((gu32*)(a.buf[a.rank] + ERR_OFF), 1u << b, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.host_err != nullptr)   // plain system-scope store (no PCIe atomics needed): any bit = failure
+          __hip_atomic_store(a.host_err, 0x100u | (1u << b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        atomicOr(&timed_out, 1);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -76,7 +94,10 @@ __device__ __forceinline__ void mesh_barrier(const XArgs& a, int b) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system-scope acquire (one lane per peer)
   }
   __syncthreads();
+  return timed_out == 0;
 }
+
+__device__ __forceinline__ u32x4 poison() { return u32x4{~0u, ~0u, ~0u, ~0u}; }
 
 template <typename T> struct Acc;
 template <> struct Acc<float> {   // 16 B = 4 fp32
@@ -110,11 +131,14 @@ template <> struct Acc<bf16_t> {  // 16 B = 8 bf16
   }
 };
 
-// K1: local input -> own staging slot (write-through, system scope)
-__global__ __launch_bounds__(NT) void xgmi_copy_in_kernel(const u32x4* __restrict__ src, XArgs a, int64_t nvec) {
-  const __amdgpu_buffer_rsrc_t dst = rsrc_of(slot_of(a, a.rank), nvec * 16);
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT)
-    __builtin_amdgcn_raw_buffer_store_b128(src[i], dst, (int)(i * 16), 0, SYS);
+// K1: local input -> own staging slot (write-through, system scope).  `pieces` windows of `pvec` vectors,
+// window p read at src + p * pitch (reduce-scatter chunk), stored back to back in the slot.
+__global__ __launch_bounds__(NT) void xgmi_copy_in_kernel(const u32x4* __restrict__ src, XArgs a, int64_t pvec,
+                                                          int pieces, int64_t pitch) {
+  const __amdgpu_buffer_rsrc_t dst = rsrc_of(slot_of(a, a.rank), pvec * pieces * 16);
+  for (int p = 0; p < pieces; ++p)
+    for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < pvec; i += (int64_t)gridDim.x * NT)
+      __builtin_amdgcn_raw_buffer_store_b128(src[p * pitch + i], dst, (int)((p * pvec + i) * 16), 0, SYS);
 }
 
 // sum over ranks of vector i of every peer slot, starting at byte offset `off`
@@ -140,12 +164,15 @@ __device__ __forceinline__ void peer_rsrcs(const XArgs& a, int64_t bytes, __amdg
 
 // one-shot all-reduce: out[i] = s * sum_p slot_p[i]
 template <typename T>
-__global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __restrict__ out, int64_t nvec, float s) {
-  mesh_barrier(a, 0);
+// root >= 0: reduce to one rank (ZeRO-2 reduce-to-owner): the others only take part in the barrier.
+__global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __restrict__ out, int64_t nvec, float s,
+                                                            int root) {
+  const bool ok = mesh_barrier(a, 0);
+  if (root >= 0 && a.rank != root) return;
   __amdgpu_buffer_rsrc_t src[MAXW];
   peer_rsrcs(a, nvec * 16, src);
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT)
-    out[i] = reduce_vec<T>(src, a.world, i * 16, s);
+    out[i] = ok ? reduce_vec<T>(src, a.world, i * 16, s) : poison();
 }
 
 // two-shot phase 1 / reduce_scatter: chunk `rank` (cvec vectors) reduced from every peer.
@@ -153,40 +180,42 @@ __global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __re
 template <typename T>
 __global__ __launch_bounds__(NT) void xgmi_reduce_chunk_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, float s,
                                                               int to_slot) {
-  mesh_barrier(a, 0);
+  const bool ok = mesh_barrier(a, 0);
   const int64_t total = cvec * a.world;
   __amdgpu_buffer_rsrc_t src[MAXW];
   peer_rsrcs(a, total * 16, src);
   const int64_t base = (int64_t)a.rank * cvec;
   const __amdgpu_buffer_rsrc_t mine = rsrc_of(slot_of(a, a.rank), total * 16);
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < cvec; i += (int64_t)gridDim.x * NT) {
-    const u32x4 v = reduce_vec<T>(src, a.world, (base + i) * 16, s);
+    const u32x4 v = ok ? reduce_vec<T>(src, a.world, (base + i) * 16, s) : poison();
     if (to_slot) __builtin_amdgcn_raw_buffer_store_b128(v, mine, (int)((base + i) * 16), 0, SYS);
     else out[i] = v;
   }
 }
 
-// all-gather: out[p * cvec + i] = chunk p of peer p's slot (chunk_in_slot: peer p keeps its piece at
+// all-gather: out[p * pitch + i] = chunk p of peer p's slot (chunk_in_slot: peer p keeps its piece at
 // chunk p of its slot (two-shot phase 2) or at offset 0 (all_gather of a shard))
-__global__ __launch_bounds__(NT) void xgmi_gather_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, int bar,
-                                                         int chunk_in_slot) {
-  mesh_barrier(a, bar);
-  const int64_t total = cvec * a.world;
+__global__ __launch_bounds__(NT) void xgmi_gather_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, int64_t pitch,
+                                                         int bar, int chunk_in_slot) {
+  const bool ok = mesh_barrier(a, bar);
   for (int p = 0; p < a.world; ++p) {
     const int64_t off = chunk_in_slot ? (int64_t)p * cvec : 0;
     const __amdgpu_buffer_rsrc_t src = rsrc_of(slot_of(a, p), (off + cvec) * 16);
     for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < cvec; i += (int64_t)gridDim.x * NT)
-      out[(int64_t)p * cvec + i] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)((off + i) * 16), 0, SYS);
+      out[(int64_t)p * pitch + i] = ok ? __builtin_amdgcn_raw_buffer_load_b128(src, (int)((off + i) * 16), 0, SYS)
+                                       : poison();
   }
-  (void)total;
 }
 
-__global__ void xgmi_barrier_kernel(XArgs a) { mesh_barrier(a, 3); }
+__global__ void xgmi_barrier_kernel(XArgs a) { (void)mesh_barrier(a, 3); }
 
+// Communication kernels share the GPU with the compute stream: a modest grid (<= 128 blocks of 256
+// lanes, half a block per CU) keeps enough 16-B loads in flight to saturate the links while leaving most
+// of every CU to the GEMMs it overlaps with.
 int grid_of(int64_t nvec) {
   int64_t g = (nvec + NT - 1) / NT;
   if (g < 1) g = 1;
-  if (g > 512) g = 512;
+  if (g > 128) g = 128;
   return (int)g;
 }
 
@@ -233,16 +262,35 @@ PDT_API int pdt_xgmi_error(void* own_buf, unsigned* out) {
   return (int)hipMemcpy((char*)own_buf + ERR_OFF, &z, 4, hipMemcpyHostToDevice);
 }
 
-// kind: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter, 4 barrier.
-//   in_bytes: bytes of `in` (all-gather: the local shard; reduce-scatter: the full input); multiple of 16
-//   (two-shot / reduce-scatter: multiple of 16 * world).  scale multiplies reduced values (1/world = AVG).
-PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t in_bytes, int dtype, float scale,
-                                const void* const* bufs, int rank, int world, unsigned epoch, int64_t slot_bytes,
-                                unsigned spin_limit, hipStream_t s) {
+// Host-mapped error word (pinned, coherent): the kernels OR timeout bits into it, the host reads it
+// without synchronising the device.
+PDT_API int pdt_xgmi_host_flag_alloc(void** host_ptr, void** dev_ptr) {
+  hipError_t e = hipHostMalloc(host_ptr, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  memset(*host_ptr, 0, 64);
+  return (int)hipHostGetDevicePointer(dev_ptr, *host_ptr, 0);
+}
+
+PDT_API int pdt_xgmi_host_flag_free(void* host_ptr) { return (int)hipHostFree(host_ptr); }
+
+// kind: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter, 4 barrier,
+//       5 reduce to root (root rank passed as pitch_bytes / 16).
+//   bytes: all-reduce: the whole payload (two-shot: multiple of 16 * world); all-gather / reduce-scatter:
+//          ONE rank's piece (a multiple of 16).
+//   pitch_bytes: all-gather: distance between consecutive peers' pieces in `out`; reduce-scatter: distance
+//          between consecutive pieces in `in` (both = bytes for a contiguous tensor).
+//   scale multiplies reduced values (1/world = AVG).
+PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t bytes, int64_t pitch_bytes, int dtype,
+                                float scale, const void* const* bufs, int rank, int world, unsigned epoch,
+                                int64_t slot_bytes, unsigned spin_limit, unsigned* host_err, hipStream_t s) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || epoch == 0) return (int)hipErrorInvalidValue;
-  if (in_bytes % 16 != 0 || in_bytes > slot_bytes || (dtype != kF32 && dtype != kBF16)) return (int)hipErrorInvalidValue;
+  if (bytes % 16 != 0 || pitch_bytes % 16 != 0 || (dtype != kF32 && dtype != kBF16)) return (int)hipErrorInvalidValue;
+  if (slot_bytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;   // 32-bit buffer offsets
+  const int64_t staged = kind == 3 ? bytes * world : bytes;
+  if (staged > slot_bytes) return (int)hipErrorInvalidValue;
   XArgs a{};
   for (int p = 0; p < world; ++p) a.buf[p] = (char*)bufs[p];
+  a.host_err = host_err;
   a.rank = rank;
   a.world = world;
   a.epoch = epoch;
@@ -252,27 +300,36 @@ PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t in_
     hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, s, a);
     return (int)hipGetLastError();
   }
-  const int64_t nvec = in_bytes / 16;
-  hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, (const u32x4*)in, a, nvec);
+  const int64_t nvec = bytes / 16, pitch = pitch_bytes / 16;
+  if (kind == 3)
+    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec * world)), dim3(NT), 0, s, (const u32x4*)in, a, nvec,
+                       world, pitch);
+  else
+    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, (const u32x4*)in, a, nvec, 1,
+                       (int64_t)0);
   const bool bf = dtype == kBF16;
   switch (kind) {
     case 0:
-      if (bf) hipLaunchKernelGGL(xgmi_allreduce_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale);
-      else hipLaunchKernelGGL(xgmi_allreduce_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale);
-      break;
-    case 1:
-    case 3: {
-      if (nvec % world != 0) return (int)hipErrorInvalidValue;
-      const int64_t cvec = nvec / world;
-      const int to_slot = kind == 1;
-      if (bf) hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<bf16_t>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, to_slot);
-      else hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<float>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, to_slot);
-      if (kind == 1)
-        hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, 1, 1);
+    case 5: {
+      const int root = kind == 5 ? (int)(pitch_bytes / 16) : -1;   // reduce: pitch carries the root rank
+      if (bf) hipLaunchKernelGGL(xgmi_allreduce_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, root);
+      else hipLaunchKernelGGL(xgmi_allreduce_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, root);
       break;
     }
+    case 1: {
+      if (nvec % world != 0) return (int)hipErrorInvalidValue;
+      const int64_t cvec = nvec / world;
+      if (bf) hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<bf16_t>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, 1);
+      else hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<float>, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, scale, 1);
+      hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(cvec)), dim3(NT), 0, s, a, (u32x4*)out, cvec, cvec, 1, 1);
+      break;
+    }
+    case 3:
+      if (bf) hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, 0);
+      else hipLaunchKernelGGL(xgmi_reduce_chunk_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, 0);
+      break;
     case 2:
-      hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, 0, 0);
+      hipLaunchKernelGGL(xgmi_gather_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, pitch, 0, 0);
       break;
     default:
       return (int)hipErrorInvalidValue;

@@ -241,6 +241,85 @@ class FlatLayout {
 };
 
 // ------------------------------------------------------------------------------------------------
+// ZeRO-1 / ZeRO-2 owner-contiguous layout (parallel/zero.py).  Each owner's parameters (greedy partition)
+// are packed into ONE segment and every segment is padded to a common length, so
+//   * the post-step parameter exchange is ONE all-gather of [seg_0 | seg_1 | ... ] (not world broadcasts),
+//   * a rank's optimizer state, fp32 master and (ZeRO-2) gradient are one contiguous slice,
+// and inside a segment parameters run in DESCENDING index order (~ the order backward produces their
+// gradients), so the reduction buckets -- windows of <= cap elements of one segment -- fill in order.
+// Buckets are returned in launch order: descending smallest parameter index (the bucket whose last
+// gradient arrives first is released first).
+// ------------------------------------------------------------------------------------------------
+struct ZeroBucket {
+  int owner;
+  int64_t start;   // absolute element offset in the flat buffer
+  int64_t numel;
+  std::vector<int> params;
+};
+
+class ZeroLayout {
+ public:
+  ZeroLayout(std::vector<int64_t> numels, std::vector<int> owners, int world, int64_t align, int64_t cap)
+      : offsets_(numels.size(), 0), world_(world) {
+    if (world <= 0) throw std::invalid_argument("ZeroLayout: world must be > 0");
+    if (owners.size() != numels.size()) throw std::invalid_argument("ZeroLayout: owners/numels size mismatch");
+    if (align < 1) align = 1;
+    if (cap < 1) cap = 1;
+    std::vector<std::vector<int>> mine(world);
+    for (int i = (int)numels.size() - 1; i >= 0; --i) {
+      if (owners[i] < 0 || owners[i] >= world) throw std::out_of_range("ZeroLayout: bad owner");
+      mine[owners[i]].push_back(i);
+    }
+    std::vector<int64_t> used(world, 0);
+    std::vector<std::vector<int64_t>> local(world);
+    for (int r = 0; r < world; ++r) {
+      int64_t off = 0;
+      for (int i : mine[r]) {
+        off = align_up(off, align);
+        local[r].push_back(off);
+        off += numels[i];
+      }
+      used[r] = off;
+    }
+    seg_ = align_up(std::max<int64_t>(1, *std::max_element(used.begin(), used.end())), align);
+    for (int r = 0; r < world; ++r) {
+      ZeroBucket cur{r, -1, 0, {}};
+      int64_t end = 0;
+      for (size_t k = 0; k < mine[r].size(); ++k) {
+        const int i = mine[r][k];
+        const int64_t abs = (int64_t)r * seg_ + local[r][k];
+        offsets_[i] = abs;
+        if (cur.start >= 0 && abs + numels[i] - cur.start > cap) {
+          cur.numel = align_up(end, align) - cur.start;   // whole 16-element granules (16-B collectives)
+          buckets_.push_back(cur);
+          cur = ZeroBucket{r, -1, 0, {}};
+        }
+        if (cur.start < 0) cur.start = abs;
+        cur.params.push_back(i);
+        end = abs + numels[i];
+      }
+      if (cur.start >= 0) {
+        cur.numel = align_up(end, align) - cur.start;
+        buckets_.push_back(cur);
+      }
+    }
+    std::stable_sort(buckets_.begin(), buckets_.end(), [](const ZeroBucket& a, const ZeroBucket& b) {
+      return *std::min_element(a.params.begin(), a.params.end()) > *std::min_element(b.params.begin(), b.params.end());
+    });
+  }
+  int64_t seg() const { return seg_; }
+  int64_t total() const { return seg_ * world_; }
+  const std::vector<int64_t>& offsets() const { return offsets_; }
+  const std::vector<ZeroBucket>& buckets() const { return buckets_; }
+
+ private:
+  std::vector<int64_t> offsets_;
+  std::vector<ZeroBucket> buckets_;
+  int world_;
+  int64_t seg_ = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
 // Collective tracer (debug consistency checking across ranks).
 // ------------------------------------------------------------------------------------------------
 class CollectiveTracer {
@@ -331,6 +410,20 @@ PYBIND11_MODULE(_pdt_runtime, m) {
       .def_property_readonly("offsets", &FlatLayout::offsets)
       .def("shard_range", &FlatLayout::shard_range)
       .def("pieces", &FlatLayout::pieces);
+
+  py::class_<ZeroBucket>(m, "ZeroBucket")
+      .def_readonly("owner", &ZeroBucket::owner)
+      .def_readonly("start", &ZeroBucket::start)
+      .def_readonly("numel", &ZeroBucket::numel)
+      .def_readonly("params", &ZeroBucket::params);
+
+  py::class_<ZeroLayout>(m, "ZeroLayout")
+      .def(py::init<std::vector<int64_t>, std::vector<int>, int, int64_t, int64_t>(), py::arg("numels"),
+           py::arg("owners"), py::arg("world"), py::arg("align"), py::arg("bucket_cap"))
+      .def_property_readonly("seg", &ZeroLayout::seg)
+      .def_property_readonly("total", &ZeroLayout::total)
+      .def_property_readonly("offsets", &ZeroLayout::offsets)
+      .def_property_readonly("buckets", &ZeroLayout::buckets);
 
   py::class_<CollectiveTracer>(m, "CollectiveTracer")
       .def(py::init<size_t>(), py::arg("capacity") = 4096)

@@ -31,6 +31,7 @@ c_float = ctypes.c_float
 _SIGS = {
     "pdt_adamw_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float,
                      c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_step_inc": [c_void_p, c_void_p, c_void_p],
     "pdt_l2norm_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
@@ -81,8 +82,10 @@ _SIGS = {
     "pdt_xgmi_ipc_open": [c_void_p, c_void_p],
     "pdt_xgmi_ipc_close": [c_void_p],
     "pdt_xgmi_error": [c_void_p, c_void_p],
-    "pdt_xgmi_collective": [c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_int, c_int,
-                            ctypes.c_uint, c_int64, ctypes.c_uint, c_void_p],
+    "pdt_xgmi_collective": [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int, c_float, c_void_p, c_int, c_int,
+                            ctypes.c_uint, c_int64, ctypes.c_uint, c_void_p, c_void_p],
+    "pdt_xgmi_host_flag_alloc": [c_void_p, c_void_p],
+    "pdt_xgmi_host_flag_free": [c_void_p],
     "pdt_bn_ws_floats": [c_int],
     "pdt_bn_ok": [c_int],
     "pdt_bn_stats": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],

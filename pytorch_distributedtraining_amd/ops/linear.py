@@ -15,8 +15,6 @@
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,7 +23,6 @@ from . import _lib
 from .activations import _colsum, colsum_ok
 
 _WGRAD_CHUNK = 4096
-_WGRAD_STREAM = os.environ.get("PDT_WGRAD_STREAM", "0") == "1"
 
 
 def _tall_skinny(m: int, n: int, k: int) -> bool:
@@ -86,23 +83,6 @@ def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
             and n % 64 == 0 and k % 64 == 0 and n * k >= 4_000_000 and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
 
 
-_SIDE_STREAMS: dict = {}
-
-
-def _wgrad_side_stream(dy2: torch.Tensor, w: torch.Tensor, need_dx: bool):
-    """The per-device side stream for a concurrent weight gradient, or None (PDT_WGRAD_STREAM=1 enables;
-    only for large GEMMs with both gradients wanted, never inside a HIP-graph capture)."""
-    if not (_WGRAD_STREAM and need_dx and dy2.is_cuda) or torch.cuda.is_current_stream_capturing():
-        return None
-    if dy2.shape[0] * w.shape[0] * w.shape[1] < (1 << 33):
-        return None
-    idx = dy2.device.index
-    s = _SIDE_STREAMS.get(idx)
-    if s is None:
-        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=dy2.device)
-    return s
-
-
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -117,31 +97,19 @@ class _LinearFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = db = None
-        side = None
         if ctx.needs_input_grad[1]:
+            # (a concurrent dW on a second HIP stream measured 1 % slower on the flagship shapes,
+            # profiles/r1_v11_wgrad_side_stream.log, and was removed)
             x2 = x.reshape(-1, x.shape[-1])
             if not x2.is_contiguous():
                 x2 = x2.contiguous()
-            side = _wgrad_side_stream(dy2, w, ctx.needs_input_grad[0])
-            if side is not None:
-                # dW on a second HIP stream, concurrent with dX: a weight gradient with few output tiles
-                # (GPT-2 1.3B proj: 64 tiles of 256^2) leaves most of the 256 CUs idle for its long K loop.
-                # The main stream waits for the side stream before returning, so every tensor touched
-                # there is consumed in stream order (no record_stream needed).
-                main = torch.cuda.current_stream(dy2.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    dw = wgrad(dy2, x2, w.dtype)
-            else:
-                dw = wgrad(dy2, x2, w.dtype)
+            dw = wgrad(dy2, x2, w.dtype)
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
                 dx = F.linear(dy2, transpose16(w))
             else:
                 dx = torch.mm(dy2, w)
             dx = dx.view(*dy.shape[:-1], w.shape[1])
-        if side is not None:
-            main.wait_stream(side)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
         return dx, dw, db

@@ -227,6 +227,15 @@ def adamw_step(params, grads, exp_avgs, exp_avg_sqs, *, lr: float, beta1: float,
               _lib.ptr(dstep), _lib.stream_handle(dev))
 
 
+def step_inc_(dstep: torch.Tensor, found_inf: torch.Tensor | None = None) -> None:
+    """dstep += 1 unless ``found_inf`` (device int32 flag) is set -- on the device, no host sync."""
+    if dstep.device.type != "cuda":
+        if found_inf is None or int(found_inf.reshape(-1)[0]) == 0:
+            dstep.add_(1.0)
+        return
+    _lib.call("pdt_step_inc", dstep.data_ptr(), _lib.ptr(found_inf), _lib.stream_handle(dstep.device))
+
+
 def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
     assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() == dst.numel()
     if src.device.type != "cuda":

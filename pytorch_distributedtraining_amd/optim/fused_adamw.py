@@ -6,6 +6,9 @@
   so LR schedulers (OneCycleLR cycling betas, Stoke-DDP.py:300) and checkpoints interoperate.
 * Sync-free mixed precision: ``step(grad_scale=t, found_inf=f)`` takes device scalars produced by the
   fused clip / unscale kernels; no host round trip between backward and the update.
+* fp16 overflow: a step whose ``found_inf`` flag is set changes nothing -- parameters, moments and the
+  step count (torch.amp.GradScaler skips ``optimizer.step()``, grad_scaler.py:360); the device count
+  advances only when the flag is clear.
 * Graph capture (``capturable=True``): the step count of each param group lives in a device tensor that a
   captured kernel increments, and the AdamW kernel derives its bias corrections from it, so a training step
   captured into a HIP graph (``utils.graphs.GraphedStep``) replays with the right step every time.  The
@@ -69,6 +72,8 @@ class FusedAdamW(Optimizer):
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._dsteps.clear()     # device step counters are rebuilt from the loaded per-param steps
+        for p in self.state:
+            p._pdt_opt_state = True   # engines must not re-lay-out this parameter any more (DDP rebuild)
 
     def _init_state(self, p):
         st = self.state[p]
@@ -76,6 +81,7 @@ class FusedAdamW(Optimizer):
             st["step"] = torch.tensor(0.0, dtype=torch.float32)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format, dtype=torch.float32)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format, dtype=torch.float32)
+            p._pdt_opt_state = True
         return st
 
     @torch.no_grad()
@@ -89,6 +95,13 @@ class FusedAdamW(Optimizer):
             lr = float(group["lr"]) if not torch.is_tensor(group["lr"]) else float(group["lr"].item())
             buckets = {}
             cap = bool(group.get("capturable", False))
+            # An overflowed fp16 step (found_inf != 0) must leave params, moments AND the step count alone:
+            # torch.amp.GradScaler skips optimizer.step() entirely.  With a device flag the count lives on the
+            # device and advances conditionally (pdt_step_inc), so no host sync is needed; once a group has a
+            # device count it keeps it (mixing the two counters would double-count).
+            dev_step = cap or gi in self._dsteps or (found_inf is not None and found_inf.device.type == "cuda")
+            if found_inf is not None and found_inf.device.type != "cuda" and int(found_inf.reshape(-1)[0]) != 0:
+                continue
             dstep = None
             for p in group["params"]:
                 g = grad_of(p)
@@ -100,10 +113,10 @@ class FusedAdamW(Optimizer):
                     raise TypeError("FusedAdamW keeps fp32 master params; wrap low-precision models with an "
                                     "engine (FSDP/ZeRO) or keep params fp32 and use autocast")
                 st = self._init_state(p)
-                if cap and p.device.type == "cuda":
+                if dev_step and p.device.type == "cuda":
                     if dstep is None:
                         dstep = self._device_step(gi, group, p.device)
-                        dstep.add_(1.0)          # one device increment per group (captured with the step)
+                        mt.step_inc_(dstep, found_inf)   # one device increment per group (graph-capturable)
                     st["step"] = dstep
                     key = (g.dtype, -1, p.device)
                 else:

@@ -29,24 +29,39 @@ _DT_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 
 
 
 class Handle:
-    """Async work handle; ``wait()`` orders the current stream after the collective."""
+    """Async work handle; ``wait()`` orders the current stream after the collective (no host sync for
+    device collectives: a c10d work's wait, or a stream wait on the xGMI comm stream's event)."""
 
-    def __init__(self, work=None, post=None):
+    def __init__(self, work=None, post=None, event=None):
         self._work = work
         self._post = post
-        self._done = work is None and post is None
+        self._event = event
+        self._done = work is None and post is None and event is None
 
     def wait(self):
         if self._done:
             return
         if self._work is not None:
             self._work.wait()
+        if self._event is not None:
+            torch.cuda.current_stream().wait_event(self._event)
         if self._post is not None:
             self._post()
         self._done = True
 
     def is_completed(self) -> bool:
-        return self._done or (self._work is not None and self._work.is_completed())
+        if self._done:
+            return True
+        if self._event is not None:
+            return self._event.query()
+        return self._work is not None and self._work.is_completed()
+
+
+def _xgmi_handle(ev, async_op: bool) -> Handle:
+    h = Handle(event=ev)
+    if not async_op:
+        h.wait()          # stream-ordered for the caller, still no host sync
+    return h
 
 
 class Comm:
@@ -63,6 +78,7 @@ class Comm:
             debug = os.environ.get("PDT_COMM_DEBUG", "0") == "1" or \
                 os.environ.get("TORCH_DISTRIBUTED_DEBUG", "").upper() == "DETAIL"
         self.debug = debug
+        self.stats = {"calls": 0, "bytes": 0}
         rt = runtime()
         self.tracer = rt.CollectiveTracer(4096) if rt is not None else None
         self.xgmi = None
@@ -90,9 +106,16 @@ class Comm:
     def is_gloo(self) -> bool:
         return self.backend == "gloo"
 
-    def _trace(self, op, t):
+    def _trace(self, op, t, nbytes=None):
+        """Sequence/shape record for the consistency checker plus per-process traffic counters
+        (``stats``: collective calls and full-payload bytes, read by bench.py per step)."""
+        self.stats["calls"] += 1
+        self.stats["bytes"] += t.numel() * t.element_size() if nbytes is None else nbytes
         if self.tracer is not None:
             self.tracer.record(op, list(t.shape), _DT_CODE.get(t.dtype, 99))
+
+    def reset_stats(self):
+        self.stats = {"calls": 0, "bytes": 0}
 
     # ------------------------------------------------------------------ collectives
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> Handle:
@@ -100,8 +123,7 @@ class Comm:
         if self.world_size == 1:
             return Handle()
         if op in ("sum", "avg") and self._xgmi_ok(t):
-            self.xgmi.all_reduce(t, op)          # stream-ordered: complete for every later kernel
-            return Handle()
+            return _xgmi_handle(self.xgmi.all_reduce(t, op, async_op=True), async_op)
         if op == "avg" and self.is_gloo:
             w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
             ws = self.world_size
@@ -126,8 +148,7 @@ class Comm:
             return Handle()
         if op in ("sum", "avg") and out.dtype == inp.dtype and self._xgmi_ok(inp, "reduce_scatter") \
                 and out.is_contiguous():
-            self.xgmi.reduce_scatter(out, inp, op)
-            return Handle()
+            return _xgmi_handle(self.xgmi.reduce_scatter(out, inp, op, async_op=True), async_op)
         if self.is_gloo:
             buf = inp.clone()
             w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
@@ -147,14 +168,13 @@ class Comm:
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Handle:
         """out (world * inp numel) = concat over ranks of inp."""
-        self._trace("all_gather", inp)
+        self._trace("all_gather", inp, out.numel() * out.element_size())
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
             return Handle()
         if out.dtype == inp.dtype and out.is_contiguous() and self._xgmi_ok(inp, "all_gather"):
-            self.xgmi.all_gather(out, inp)
-            return Handle()
+            return _xgmi_handle(self.xgmi.all_gather(out, inp, async_op=True), async_op)
         if self.is_gloo:
             parts = list(out.view(self.world_size, -1).unbind(0))
             w = dist.all_gather(parts, inp.view(-1).contiguous(), group=self.group, async_op=async_op)
@@ -174,6 +194,8 @@ class Comm:
         self._trace("reduce", t)
         if self.world_size == 1:
             return Handle()
+        if op in ("sum", "avg") and self._xgmi_ok(t, "reduce"):
+            return _xgmi_handle(self.xgmi.reduce(t, dst, op, async_op=True), async_op)
         gdst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
         w = dist.reduce(t, dst=gdst, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
         if op == "avg":
@@ -234,7 +256,13 @@ class Comm:
                         t.copy_(flat[off:off + n].view_as(t))
                     off += n
 
-    # ------------------------------------------------------------------ debug
+    # ------------------------------------------------------------------ failure detection / debug
+    def check_errors(self):
+        """Raise if a device collective of this rank failed (xGMI timeout word, read without a device sync).
+        Called by the engines at their end-of-backward sync points."""
+        if self.xgmi is not None:
+            self.xgmi.raise_if_failed()
+
     def verify_consistency(self, tag: str = "") -> None:
         """Cross-rank check that every rank issued the same collective sequence (debug mode)."""
         if self.tracer is None or self.world_size == 1:

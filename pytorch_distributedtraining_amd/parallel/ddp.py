@@ -31,6 +31,42 @@ from .comm import Comm, default_comm
 _DT_ID = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
 
 
+def sync_buffers(module: nn.Module, comm: Comm, holder, mode: str = "changed") -> None:
+    """Broadcast rank 0's buffers -- only the ones that changed since the last sync.
+
+    torch DDP re-broadcasts every buffer every forward; SwinIR-S carries ~13 MB of constant buffers
+    (relative_position_index, shift masks) against 3.6 MB of gradients.  A buffer's autograd version
+    counter moves exactly when it is written in place (BatchNorm running stats, num_batches_tracked),
+    identically on every rank, so all ranks pick the same set without a collective.  The first sync
+    sends everything; running statistics of norm layers (updated inside the batch-norm kernels, no
+    version bump) are always sent; ``mode="all"`` restores torch's behaviour.  ``holder`` keeps the
+    version snapshot between calls (DDP and ShardedDataParallel both use this)."""
+    bufs = list(module.buffers())
+    if not bufs:
+        return
+    seen = getattr(holder, "_buf_versions", None)
+    if mode == "all" or seen is None or len(seen) != len(bufs):
+        send = bufs
+    else:
+        stats = _running_stat_ids(module)
+        send = [b for b, v in zip(bufs, seen) if b._version != v or id(b) in stats]
+    if send:
+        comm.broadcast_coalesced(send)
+    holder._buf_versions = [b._version for b in bufs]
+
+
+def _running_stat_ids(module):
+    # norm running statistics are updated inside the batch-norm kernels without a version bump:
+    # always treat them as mutable
+    ids = set()
+    for mod in module.modules():
+        for name in ("running_mean", "running_var", "num_batches_tracked"):
+            b = getattr(mod, name, None)
+            if isinstance(b, torch.Tensor):
+                ids.add(id(b))
+    return ids
+
+
 class _FlatGroup:
     """All parameters of one storage dtype, laid out bucket after bucket."""
 
@@ -181,6 +217,11 @@ class DistributedDataParallel(nn.Module):
         order += [i for i in reversed(range(len(self.params))) if i not in seen]
         if order == list(reversed(range(len(self.params)))):
             return
+        if any(getattr(g.master, "_pdt_opt_state", False) for g in self.groups):
+            # the optimizer already holds moments in the current master layout (e.g. restored from a
+            # checkpoint before the first step): a new element order would misalign them -- keep the layout
+            warnings.warn("DDP: optimizer state already attached to the flat masters; skipping the bucket rebuild")
+            return
         old_master = {id(g): g.master for g in self.groups}
         grads = [p.grad.detach().clone() if p.grad is not None else None for p in self.params]
         masters = {}
@@ -243,6 +284,7 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._callback_queued = False
+        self.comm.check_errors()
         if not self.tracker.all_launched():
             if not self.find_unused_parameters and not self._warned_unused:
                 warnings.warn("DDP: some parameters received no gradient this iteration; their buckets were "
@@ -272,37 +314,7 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def _sync_buffers(self):
-        """Broadcast rank 0's buffers -- only the ones that changed since the last sync.
-
-        torch DDP re-broadcasts every buffer every forward; SwinIR-S carries ~13 MB of constant buffers
-        (relative_position_index, shift masks) against 3.6 MB of gradients.  A buffer's autograd version
-        counter moves exactly when it is written in place (BatchNorm running stats, num_batches_tracked),
-        identically on every rank, so all ranks pick the same set without a collective.  The first sync
-        sends everything; running statistics of norm layers (updated inside the batch-norm kernels, no
-        version bump) are always sent; ``buffer_sync="all"`` restores torch's behaviour."""
-        bufs = list(self.module.buffers())
-        if not bufs:
-            return
-        seen = getattr(self, "_buf_versions", None)
-        if self.buffer_sync == "all" or seen is None or len(seen) != len(bufs):
-            send = bufs
-        else:
-            stats = self._running_stat_ids()
-            send = [b for b, v in zip(bufs, seen) if b._version != v or id(b) in stats]
-        if send:
-            self.comm.broadcast_coalesced(send)
-        self._buf_versions = [b._version for b in bufs]
-
-    def _running_stat_ids(self):
-        # norm running statistics are updated inside the batch-norm kernels without a version bump:
-        # always treat them as mutable
-        ids = set()
-        for mod in self.module.modules():
-            for name in ("running_mean", "running_var", "num_batches_tracked"):
-                b = getattr(mod, name, None)
-                if isinstance(b, torch.Tensor):
-                    ids.add(id(b))
-        return ids
+        sync_buffers(self.module, self.comm, self, self.buffer_sync)
 
     @contextmanager
     def no_sync(self):
@@ -339,6 +351,70 @@ class DistributedDataParallel(nn.Module):
                 o = g.offset_of[li]
                 sd[name_of[id(p)]] = g.master.detach()[o:o + p.numel()].view(p.shape).clone()
         return sd
+
+    def full_optim_state_dict(self, optimizer):
+        """compute_dtype mode: the optimizer steps flat fp32 masters; return its state in torch's
+        per-parameter layout ({state: {param_idx: {step, exp_avg, exp_avg_sq}}, param_groups}) keyed by the
+        module's parameter order, so checkpoints match a plain torch.optim.AdamW over ``module``."""
+        if self.compute_dtype is None:
+            return optimizer.state_dict()
+        idx_of = {id(p): i for i, p in enumerate(self.module.parameters())}
+        state = {}
+        for g in self.groups:
+            st = optimizer.state.get(g.master)
+            if not st:
+                continue
+            for li, gi in enumerate(g.idxs):
+                p = self.params[gi]
+                o = g.offset_of[li]
+                ent = {}
+                for k, v in st.items():
+                    if torch.is_tensor(v) and v.dim() == 1 and v.numel() == g.master.numel():
+                        ent[k] = v.detach()[o:o + p.numel()].view(p.shape).clone()
+                    else:
+                        ent[k] = v.detach().clone() if torch.is_tensor(v) else v
+                state[idx_of[id(p)]] = ent
+        groups = []
+        for pg in optimizer.param_groups:
+            d = {k: v for k, v in pg.items() if k != "params"}
+            d["params"] = sorted(idx_of[id(self.params[gi])] for g in self.groups if any(m is g.master for m in
+                                                                                        pg["params"])
+                                 for gi in g.idxs)
+            groups.append(d)
+        return {"state": state, "param_groups": groups}
+
+    def load_full_optim_state_dict(self, optimizer, sd):
+        if self.compute_dtype is None:
+            optimizer.load_state_dict(sd)
+            return
+        idx_of = {id(p): i for i, p in enumerate(self.module.parameters())}
+        if sd.get("param_groups"):
+            hp = {k: v for k, v in sd["param_groups"][0].items() if k != "params"}
+            for pg in optimizer.param_groups:
+                pg.update(hp)
+        st_all = sd["state"]
+        for g in self.groups:
+            new, step = {}, None
+            for li, gi in enumerate(g.idxs):
+                p = self.params[gi]
+                e = st_all.get(idx_of[id(p)], st_all.get(str(idx_of[id(p)])))
+                if e is None:
+                    continue
+                o = g.offset_of[li]
+                for k, v in e.items():
+                    if torch.is_tensor(v) and v.dim() > 0:
+                        if k not in new:
+                            new[k] = torch.zeros_like(g.master, dtype=torch.float32)
+                        new[k][o:o + p.numel()].copy_(v.reshape(-1))
+                    elif k == "step":
+                        step = v
+            if new:
+                if step is not None:
+                    new["step"] = step.clone() if torch.is_tensor(step) else torch.tensor(float(step))
+                optimizer.state[g.master] = new
+                g.master._pdt_opt_state = True
+        if hasattr(optimizer, "_dsteps"):
+            optimizer._dsteps.clear()
 
     def load_full_state_dict(self, sd, strict=True):
         res = self.module.load_state_dict(sd, strict=strict)

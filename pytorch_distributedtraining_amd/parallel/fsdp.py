@@ -394,6 +394,7 @@ class FullyShardedDataParallel(nn.Module):
         def cb():
             self._callback_queued = False
             self._order_frozen = True
+            self.comm.check_errors()
             if self._no_sync:
                 return
             for u in self.all_units():

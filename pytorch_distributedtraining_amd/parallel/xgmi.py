@@ -9,16 +9,23 @@ collectives are HIP kernels in ``csrc/kernels/xgmi_comm.hip`` that read peers' s
   * ``all_reduce``   one-shot (<= ``oneshot_max_bytes``: grad-norm / found_inf scalars, loss sync,
                      SyncBN statistics -- latency class) or two-shot (reduce-scatter + all-gather phases:
                      2(W-1)/W of the payload over all 7 links at once -- bandwidth class);
-  * ``all_gather`` / ``reduce_scatter`` of one staging slot.
+  * ``all_gather`` / ``reduce_scatter`` of flat shards (FSDP units, ZeRO-2 buckets).
 
-They run on the caller's current HIP stream (stream-ordered like every other kernel: no host sync, no
-separate communication stream), so a ``Handle`` returned to the engines is already complete from the
-host's point of view.  A wait that exceeds ``spin_limit`` never hangs the queue: the kernel records an
-error bit that ``check()`` raises on.
+Asynchronous like c10d: each collective runs on this rank's dedicated communication stream after an
+event wait on the caller's stream, the tensors are ``record_stream``-ed so the caching allocator cannot
+recycle them early, and the returned event is what ``Handle.wait()`` makes the *waiting* stream wait on
+(no host sync).  FSDP prefetch all-gathers and DDP / ZeRO-2 bucket reductions therefore overlap the GEMMs
+of the compute stream.  Payloads larger than a staging slot are chunked (one epoch per chunk); the
+kernels address reduce-scatter inputs and all-gather outputs with a per-peer pitch, so a chunk is a
+strided window of the caller's tensor (no extra copy).
 
-``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes eligible CUDA collectives here (sizes that are a multiple
-of 16 B, world <= 8, payload <= one staging slot); everything else stays on RCCL.  Ranks must issue
-collectives in the same order (the same contract as RCCL).
+Failure is loud: a mesh wait that exceeds ``spin_limit`` makes the kernel poison its output with NaN and
+set a host-mapped error word; ``raise_if_failed()`` (called by every engine at its end-of-backward and
+optimizer sync points through ``Comm.check_errors``) reads that word without synchronising and raises.
+
+``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes eligible CUDA collectives here (fp32/bf16, sizes a multiple
+of 16 B, world <= 8); everything else stays on RCCL.  Ranks must issue collectives in the same order (the
+same contract as RCCL).
 """
 from __future__ import annotations
 
@@ -28,7 +35,7 @@ import torch
 
 from ..ops import _lib
 
-_KIND = {"allreduce1": 0, "allreduce2": 1, "all_gather": 2, "reduce_scatter": 3, "barrier": 4}
+_KIND = {"allreduce1": 0, "allreduce2": 1, "all_gather": 2, "reduce_scatter": 3, "barrier": 4, "reduce": 5}
 SIG_BYTES = 4096
 MAX_WORLD = 8
 
@@ -36,13 +43,16 @@ MAX_WORLD = 8
 class XGMIComm:
     """Peer-mapped collectives for ``comm``'s ranks (one process per GPU of one node)."""
 
-    def __init__(self, comm, slot_bytes: int = 64 << 20, oneshot_max_bytes: int = 256 << 10,
+    def __init__(self, comm, slot_bytes: int = 256 << 20, oneshot_max_bytes: int = 256 << 10,
                  spin_limit: int = 1 << 24, uncached: bool = True):
         if comm.world_size > MAX_WORLD:
             raise ValueError(f"XGMIComm spans one node (<= {MAX_WORLD} GPUs), got world_size={comm.world_size}")
         self.comm = comm
         self.rank, self.world = comm.rank, comm.world_size
         self.slot_bytes = int(slot_bytes)
+        if not 0 < self.slot_bytes < (1 << 31) or self.slot_bytes % 4096:
+            # the kernels address a slot with 32-bit buffer-resource offsets
+            raise ValueError(f"xGMI slot_bytes must be a positive multiple of 4 KiB below 2 GiB, got {slot_bytes}")
         self.oneshot_max_bytes = int(oneshot_max_bytes)
         self.spin_limit = int(spin_limit)
         self.device = torch.device("cuda", torch.cuda.current_device())
@@ -52,6 +62,9 @@ class XGMIComm:
         own = ctypes.c_void_p()
         _lib.check(lib.pdt_xgmi_alloc(nbytes, 1 if uncached else 0, ctypes.byref(own)), "pdt_xgmi_alloc")
         self._own = own
+        hp, dp = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.pdt_xgmi_host_flag_alloc(ctypes.byref(hp), ctypes.byref(dp)), "pdt_xgmi_host_flag_alloc")
+        self._host_flag, self._dev_flag = hp, dp
         hb = lib.pdt_xgmi_ipc_handle_bytes()
         handle = ctypes.create_string_buffer(hb)
         _lib.check(lib.pdt_xgmi_ipc_get(own, handle), "pdt_xgmi_ipc_get")
@@ -67,26 +80,41 @@ class XGMIComm:
             ptrs.append(q.value)
         self._bufs = (ctypes.c_void_p * MAX_WORLD)(*(ptrs + [None] * (MAX_WORLD - len(ptrs))))
         self.epoch = 0
+        self.calls = 0           # collectives issued through the mesh (tests assert the engines used it)
+        # high priority: a collective that peers are spinning on should not queue behind GEMMs
+        self.stream = torch.cuda.Stream(device=self.device, priority=-1)
         comm.barrier()
 
     # ------------------------------------------------------------------ eligibility
     def eligible(self, nbytes: int, kind: str = "all_reduce") -> bool:
-        if nbytes <= 0 or nbytes % 16 or nbytes > self.slot_bytes:
-            return False
-        if kind in ("reduce_scatter", "allreduce2") and nbytes % (16 * self.world):
-            return False
-        return True
+        """Any fp32/bf16 payload that is a multiple of 16 B (larger ones are chunked)."""
+        return nbytes > 0 and nbytes % 16 == 0
 
     # ------------------------------------------------------------------ launch
-    def _run(self, kind: str, inp, out, in_bytes: int, dtype: torch.dtype, scale: float):
+    def _run(self, kind: str, inp: int, out: int, nbytes: int, pitch: int, dtype, scale: float):
         self.epoch += 1
         if self.epoch >= 1 << 32:
             self.epoch = 1
         code = _lib.dtype_code(dtype) if dtype is not None else 0
-        err = self._lib.pdt_xgmi_collective(_KIND[kind], _lib.ptr(inp), _lib.ptr(out), int(in_bytes), code,
-                                            float(scale), self._bufs, self.rank, self.world, self.epoch,
-                                            self.slot_bytes, self.spin_limit, _lib.stream_handle(self.device))
+        err = self._lib.pdt_xgmi_collective(_KIND[kind], inp, out, int(nbytes), int(pitch), code, float(scale),
+                                            self._bufs, self.rank, self.world, self.epoch, self.slot_bytes,
+                                            self.spin_limit, self._dev_flag, self.stream.cuda_stream)
         _lib.check(err, f"pdt_xgmi_collective[{kind}]")
+
+    def _issue(self, tensors, launch, async_op: bool = False) -> torch.cuda.Event:
+        """Run ``launch`` on the comm stream after the caller's pending work; return the completion event
+        (``async_op=False``: the caller's stream also waits for it -- stream-ordered, no host sync)."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        self.calls += 1
+        launch()
+        for t in tensors:
+            t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        if not async_op:
+            cur.wait_event(ev)
+        return ev
 
     @staticmethod
     def _flat(t):
@@ -94,45 +122,105 @@ class XGMIComm:
             raise ValueError("xGMI collectives need contiguous tensors")
         return t.view(-1)
 
-    def all_reduce(self, t: torch.Tensor, op: str = "sum", out: torch.Tensor | None = None) -> torch.Tensor:
-        """In place (or into ``out``): sum / avg over ranks.  fp32 or bf16 (fp32 accumulation)."""
+    def _two_shot_chunk(self) -> int:
+        q = 16 * self.world
+        return (self.slot_bytes // q) * q
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> torch.cuda.Event:
+        """In place: sum / avg over ranks.  fp32 or bf16 (fp32 accumulation).  Returns the completion event."""
         if op not in ("sum", "avg"):
             raise ValueError(f"xGMI all_reduce supports sum/avg, got {op}")
+        t = self._flat(t)
         nbytes = t.numel() * t.element_size()
         if not self.eligible(nbytes):
             raise ValueError(f"xGMI all_reduce: {nbytes} B not eligible")
-        out = t if out is None else out
         scale = 1.0 / self.world if op == "avg" else 1.0
-        two_shot = nbytes > self.oneshot_max_bytes and nbytes % (16 * self.world) == 0
-        self._run("allreduce2" if two_shot else "allreduce1", self._flat(t), self._flat(out), nbytes, t.dtype, scale)
-        return out
+        base = t.data_ptr()
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        def launch():
+            if nbytes <= self.oneshot_max_bytes:
+                self._run("allreduce1", base, base, nbytes, 0, t.dtype, scale)
+                return
+            q = 16 * self.world
+            main = (nbytes // q) * q
+            step = self._two_shot_chunk()
+            for o in range(0, main, step):
+                c = min(step, main - o)
+                self._run("allreduce2", base + o, base + o, c, 0, t.dtype, scale)
+            if main < nbytes:    # < 16 * world bytes left: latency-class one-shot
+                self._run("allreduce1", base + main, base + main, nbytes - main, 0, t.dtype, scale)
+        return self._issue([t], launch, async_op)
+
+    def reduce(self, t: torch.Tensor, dst: int, op: str = "sum", async_op: bool = False) -> torch.cuda.Event:
+        """In place on ``dst`` (ZeRO-2 reduce-to-owner): the owner reads every peer's slot, the others only
+        stage their contribution.  Other ranks' ``t`` is left unchanged."""
+        if op not in ("sum", "avg"):
+            raise ValueError(f"xGMI reduce supports sum/avg, got {op}")
+        t = self._flat(t)
+        nbytes = t.numel() * t.element_size()
+        if not self.eligible(nbytes) or not 0 <= dst < self.world:
+            raise ValueError(f"xGMI reduce: {nbytes} B / dst {dst} not eligible")
+        scale = 1.0 / self.world if op == "avg" else 1.0
+        base = t.data_ptr()
+
+        def launch():
+            for o in range(0, nbytes, self.slot_bytes):
+                c = min(self.slot_bytes, nbytes - o)
+                self._run("reduce", base + o, base + o, c, 16 * dst, t.dtype, scale)
+        return self._issue([t], launch, async_op)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> torch.cuda.Event:
+        inp, out = self._flat(inp), self._flat(out)
         nbytes = inp.numel() * inp.element_size()
-        if out.numel() != inp.numel() * self.world or not self.eligible(nbytes):
+        if out.numel() != inp.numel() * self.world or out.dtype != inp.dtype or not self.eligible(nbytes):
             raise ValueError("xGMI all_gather: bad sizes")
-        self._run("all_gather", self._flat(inp), self._flat(out), nbytes, inp.dtype, 1.0)
-        return out
+        src, dst = inp.data_ptr(), out.data_ptr()
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        nbytes = inp.numel() * inp.element_size()
-        if inp.numel() != out.numel() * self.world or not self.eligible(nbytes, "reduce_scatter"):
+        def launch():
+            for o in range(0, nbytes, self.slot_bytes):
+                c = min(self.slot_bytes, nbytes - o)
+                self._run("all_gather", src + o, dst + o, c, nbytes, inp.dtype, 1.0)
+        return self._issue([inp, out], launch, async_op)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum",
+                       async_op: bool = False) -> torch.cuda.Event:
+        inp, out = self._flat(inp), self._flat(out)
+        nbytes = out.numel() * out.element_size()          # one rank's piece
+        if inp.numel() != out.numel() * self.world or out.dtype != inp.dtype or not self.eligible(nbytes):
             raise ValueError("xGMI reduce_scatter: bad sizes")
         scale = 1.0 / self.world if op == "avg" else 1.0
-        self._run("reduce_scatter", self._flat(inp), self._flat(out), nbytes, inp.dtype, scale)
-        return out
+        src, dst = inp.data_ptr(), out.data_ptr()
+        step = (self.slot_bytes // self.world) // 16 * 16
 
-    def barrier(self):
-        self._run("barrier", None, None, 0, None, 1.0)
+        def launch():
+            for o in range(0, nbytes, step):
+                c = min(step, nbytes - o)
+                self._run("reduce_scatter", src + o, dst + o, c, nbytes, inp.dtype, scale)
+        return self._issue([inp, out], launch, async_op)
+
+    def barrier(self) -> torch.cuda.Event:
+        return self._issue([], lambda: self._run("barrier", 0, 0, 0, 0, None, 1.0), False)
+
+    # ------------------------------------------------------------------ failure detection
+    def failed(self) -> int:
+        """Timeout bits recorded by the kernels so far (host-mapped word: no device sync)."""
+        return ctypes.c_uint.from_address(self._host_flag.value).value
+
+    def raise_if_failed(self):
+        v = self.failed()
+        if v:
+            raise RuntimeError(f"xGMI collective timed out on rank {self.rank} (flag {v:#x}): a peer did not reach "
+                               "the same collective in time; its outputs were poisoned with NaN")
 
     def check(self):
-        """Raise if any mesh wait on this rank timed out since the last check (synchronises the device)."""
-        torch.cuda.synchronize(self.device)
+        """Synchronise the comm stream, then raise if any mesh wait timed out (tests / teardown)."""
+        self.stream.synchronize()
         v = ctypes.c_uint(0)
         _lib.check(self._lib.pdt_xgmi_error(self._own, ctypes.byref(v)), "pdt_xgmi_error")
         if v.value:
             raise RuntimeError(f"xGMI collective timed out on rank {self.rank} (barrier bits {v.value:#x}): "
                                "a peer did not reach the same collective")
+        self.raise_if_failed()
 
     def close(self):
         if getattr(self, "_own", None) is None:
@@ -143,4 +231,5 @@ class XGMIComm:
             self._lib.pdt_xgmi_ipc_close(q)
         self._opened = []
         self._lib.pdt_xgmi_free(self._own)
+        self._lib.pdt_xgmi_host_flag_free(self._host_flag)
         self._own = None

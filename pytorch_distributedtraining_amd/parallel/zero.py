@@ -8,16 +8,28 @@ API-compatible with what the reference drives from Fairscale:
     (Stoke-DDP.py:300-301).
   * ``ShardedDataParallel(model, optimizer)``, ``.zero_grad()``, ``no_sync()`` (Fairscale-DDP.py:89,97).
 Semantics reference: greedy partition of torch/distributed/optim/zero_redundancy_optimizer.py:680-700
-(here done by the native ``greedy_partition``), owner broadcast after step (:758-810).
+(native ``greedy_partition``); owners update their parameters and the rest receive them (:758-810).
 
-MI355X-first design:
-  * Each rank's parameters are re-pointed into ONE contiguous flat buffer per (owner rank, dtype), so
-    the post-step parameter exchange is one broadcast per owner (world_size collectives per step,
-    not one per tensor), optionally in bf16/fp16 (``broadcast_fp16``) through a persistent staging
-    buffer.
-  * ShardedDataParallel lays the gradients out the same way (``param.grad`` = view of the owner's flat
-    gradient), so the reduce-to-owner is bucketed with no copy-in, launched asynchronously from the
-    grad hooks in the order buckets complete, and averaged inside RCCL.
+MI355X-first design (not Fairscale's per-rank broadcasts and per-parameter reduces):
+  * ONE owner-contiguous flat buffer per (dtype, device) -- the native ``ZeroLayout``: every rank's owned
+    parameters packed into one segment, segments padded to a common length.  The module parameters are
+    views into it, so the post-step exchange is ONE all-gather of the owners' segments (world_size
+    broadcasts before), and a rank's optimizer state / fp32 master / gradient shard is one contiguous
+    slice.
+  * ``broadcast_fp16``: the all-gather payload is a bf16 (fp16 on CPU) flat; the fused AdamW writes the
+    owner's slice of it in its epilogue (no cast pass), receivers cast only the peers' slices back.
+  * ``compute_dtype=torch.bfloat16``: the module itself runs on bf16 parameters (views of the bf16 flat)
+    while each rank keeps fp32 masters for its OWN segment only; the fused AdamW updates the masters and
+    writes the bf16 parameters in its epilogue, the all-gather then moves bf16.  No per-forward fp32->bf16
+    weight casts and no bf16->fp32 gradient casts (the autocast "cast storm").
+  * ``ShardedDataParallel`` (ZeRO-2, ``reduce_mode="reduce"``): a rank keeps a persistent gradient buffer
+    for its own segment only; gradients of other owners' parameters are produced by autograd, packed per
+    bucket (a window of one owner's segment) into a transient buffer, reduced (AVG) to the owner
+    asynchronously from the grad hooks, and freed -- per-rank gradient memory is ~1/world of the model.
+    ``reduce_mode="all_reduce"`` is the ZeRO-1 gradient path (DDP + OSS): full gradients, bucketed
+    all-reduces over the same flat.
+  * Optimizer-state consolidation gathers flat per-key state slices (tensors, no pickled state), plus one
+    tiny all-reduce of the per-parameter step counts.
 """
 from __future__ import annotations
 
@@ -30,61 +42,121 @@ from torch.optim import Optimizer
 from ..optim.clip import clip_grad_norm_
 from ..utils.native import require_runtime
 from .comm import Comm, default_comm
+from .ddp import sync_buffers
+
+ALIGN = 16
+
+
+class _Bank:
+    """Parameters of one (storage dtype, device): owner-contiguous flat + views + (optional) payload/masters."""
+
+    def __init__(self, params, idxs, owners, world, rank, flat_dtype, device):
+        self.params, self.idxs, self.owners = params, idxs, owners
+        self.world, self.rank, self.device, self.dtype = world, rank, device, flat_dtype
+        lay = self.layout(1 << 62)
+        self.seg, self.total = int(lay.seg), int(lay.total)
+        self.offsets = list(lay.offsets)
+        self.flat = torch.zeros(self.total, dtype=flat_dtype, device=device)
+        self.lp = None          # broadcast_fp16 payload
+        self.master_flat = None  # compute-dtype mode: fp32 masters of this rank's segment
+        self.masters = {}       # local param index -> fp32 master Parameter
+
+    def layout(self, bucket_elems):
+        """Native owner-contiguous layout; offsets do not depend on the bucket cap."""
+        return require_runtime().ZeroLayout([p.numel() for p in self.params], self.owners, self.world, ALIGN,
+                                            max(1, int(bucket_elems)))
+
+    def own(self, t):
+        return t[self.rank * self.seg:(self.rank + 1) * self.seg]
+
+    def view(self, t, li):
+        p = self.params[li]
+        o = self.offsets[li]
+        return t[o:o + p.numel()].view(p.shape)
 
 
 class OSS(Optimizer):
     """Optimizer state sharding wrapper (ZeRO-1)."""
 
-    def __init__(self, params, optim=None, comm: Comm | None = None, broadcast_fp16: bool = False,
-                 group=None, **defaults):
+    def __init__(self, params, optim=None, comm: Comm | None = None, broadcast_fp16: bool = False, group=None,
+                 compute_dtype: torch.dtype | None = None, **defaults):
         from ..optim import FusedAdamW
 
         self.comm = comm or (Comm(group) if group is not None else default_comm())
         self.optim_cls = optim or FusedAdamW
         self.broadcast_fp16 = broadcast_fp16
+        self.compute_dtype = compute_dtype
         super().__init__(params, defaults)
         world, rank = self.comm.world_size, self.comm.rank
         self._all_params = [p for g in self.param_groups for p in g["params"]]
-        numels = [p.numel() for p in self._all_params]
-        self.owner = list(require_runtime().greedy_partition(numels, world))
+        self._index = {id(p): i for i, p in enumerate(self._all_params)}
+        self.owner = list(require_runtime().greedy_partition([p.numel() for p in self._all_params], world))
         self._owner_of = {id(p): r for p, r in zip(self._all_params, self.owner)}
-        # local optimizer over owned params, one local group per wrapper group
+        if self.comm.world_size > 1:      # identical start everywhere (rank 0 wins), before the re-layout
+            self.comm.broadcast_coalesced([p.data for p in self._all_params])
+        self._build_banks()
+        # local optimizer over what this rank owns: the module parameters themselves, or (compute-dtype
+        # mode) the fp32 masters shadowing them -- one local group per wrapper group
         local_groups = []
         for g in self.param_groups:
             lg = {k: v for k, v in g.items() if k != "params"}
-            lg["params"] = [p for p in g["params"] if self._owner_of[id(p)] == rank]
+            lg["params"] = [self._opt_param(p) for p in g["params"] if self._owner_of[id(p)] == rank]
             local_groups.append(lg)
-        nonempty = [g for g in local_groups if g["params"]]
         self._local_group_idx = [i for i, g in enumerate(local_groups) if g["params"]]
-        self.optim = self.optim_cls(nonempty if nonempty else [{"params": []}], **defaults) if nonempty else None
-        self._flatten_by_owner()
+        nonempty = [g for g in local_groups if g["params"]]
+        self.optim = self.optim_cls(nonempty, **defaults) if nonempty else None
+        self._fused = isinstance(self.optim, FusedAdamW)
         self._state_cache = None
-        if self.comm.world_size > 1:
-            self.comm.broadcast_coalesced([p.data for p in self._all_params])
 
     # ---------------------------------------------------------------- layout
-    def _flatten_by_owner(self):
-        """Re-point every parameter into a contiguous flat buffer per (owner, dtype, device)."""
-        self._flats = []   # (owner, flat tensor, [params])
+    def _build_banks(self):
+        world, rank = self.comm.world_size, self.comm.rank
         by = {}
-        for p, r in zip(self._all_params, self.owner):
-            by.setdefault((r, p.dtype, p.device), []).append(p)
-        for (r, dt, dev), ps in sorted(by.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
-            n = sum(p.numel() for p in ps)
-            flat = torch.empty(n, dtype=dt, device=dev)
-            off = 0
-            for p in ps:
-                flat[off:off + p.numel()].copy_(p.detach().reshape(-1))
-                p.data = flat[off:off + p.numel()].view(p.shape)
-                off += p.numel()
-            lp = None
-            if self.broadcast_fp16 and dt == torch.float32:
-                lp = torch.empty(n, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float16, device=dev)
-            self._flats.append((r, flat, ps, lp))
+        for i, p in enumerate(self._all_params):
+            dt = self.compute_dtype if (self.compute_dtype is not None and p.dtype == torch.float32) else p.dtype
+            by.setdefault((dt, p.device), []).append(i)
+        self._banks = []
+        self._bank_of = {}
+        for (dt, dev), idxs in by.items():
+            ps = [self._all_params[i] for i in idxs]
+            bank = _Bank(ps, idxs, [self.owner[i] for i in idxs], world, rank, dt, dev)
+            mixed = dt != ps[0].dtype
+            if mixed:
+                bank.master_flat = torch.zeros(bank.seg, dtype=torch.float32, device=dev)
+            with torch.no_grad():
+                for li, p in enumerate(ps):
+                    v = bank.view(bank.flat, li)
+                    v.copy_(p.detach())
+                    if mixed and bank.owners[li] == rank:
+                        o = bank.offsets[li] - rank * bank.seg
+                        mv = bank.master_flat[o:o + p.numel()].view(p.shape)
+                        mv.copy_(p.detach())                 # exact fp32 values, not the rounded bf16 copy
+                        m = nn.Parameter(mv)
+                        m._pdt_grad_src = p                  # the optimizer reads the module parameter's grad
+                        m._pdt_lp_shard = v                  # ... and writes its bf16 value in the epilogue
+                        bank.masters[li] = m
+                    p.data = v
+            if self.broadcast_fp16 and not mixed and dt == torch.float32:
+                bank.lp = torch.zeros(bank.total, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float16,
+                                      device=dev)
+                for li, p in enumerate(ps):
+                    if bank.owners[li] == rank:
+                        p._pdt_lp_shard = bank.view(bank.lp, li)   # AdamW epilogue writes the payload
+            for li, i in enumerate(idxs):
+                self._bank_of[i] = (bank, li)
+            self._banks.append(bank)
+
+    def _opt_param(self, p):
+        bank, li = self._bank_of[self._index[id(p)]]
+        return bank.masters.get(li, p)
 
     def owned_params(self):
+        """The tensors this rank's optimizer steps (fp32 masters in compute-dtype mode)."""
         r = self.comm.rank
-        return [p for p in self._all_params if self._owner_of[id(p)] == r]
+        return [self._opt_param(p) for p in self._all_params if self._owner_of[id(p)] == r]
+
+    def banks(self):
+        return self._banks
 
     # ---------------------------------------------------------------- step
     def _sync_hparams(self):
@@ -103,64 +175,139 @@ class OSS(Optimizer):
                 loss = closure()
         self._sync_hparams()
         if self.optim is not None:
-            self.optim.step(**kw)
-        self._broadcast_params()
+            if self._fused:
+                self.optim.step(**kw)
+            else:
+                found = kw.get("found_inf")
+                if found is None or int(found.reshape(-1)[0]) == 0:
+                    self.optim.step()
+        self._exchange()
         return loss
 
-    def _broadcast_params(self):
-        if self.comm.world_size == 1:
-            return
-        handles = []
-        for (r, flat, _ps, lp) in self._flats:
-            if lp is not None:
-                if self.comm.rank == r:
-                    lp.copy_(flat)
-                handles.append((self.comm.broadcast(lp, src=r, async_op=True), flat, lp, r))
-            else:
-                handles.append((self.comm.broadcast(flat, src=r, async_op=True), None, None, r))
-        for h, flat, lp, r in handles:
-            h.wait()
-            if lp is not None and self.comm.rank != r:
-                flat.copy_(lp)
+    def _exchange(self):
+        """Owners -> everyone: ONE all-gather per bank of the owners' (payload) segments."""
+        for bank in self._banks:
+            if bank.master_flat is not None and not self._fused:
+                for li, m in bank.masters.items():          # non-fused optimizer: write the compute copy here
+                    bank.view(bank.flat, li).copy_(m.detach())
+            src = bank.lp if bank.lp is not None else bank.flat
+            if bank.lp is not None and not self._fused:
+                bank.own(bank.lp).copy_(bank.own(bank.flat))
+            if self.comm.world_size == 1:
+                continue
+            self.comm.all_gather(src, bank.own(src))
+            if bank.lp is not None:        # receivers: fp32 params from the compressed payload (peers only)
+                r, s = self.comm.rank, bank.seg
+                if r > 0:
+                    bank.flat[:r * s].copy_(bank.lp[:r * s])
+                if r + 1 < self.comm.world_size:
+                    bank.flat[(r + 1) * s:].copy_(bank.lp[(r + 1) * s:])
 
     def zero_grad(self, set_to_none: bool = True):
         for p in self._all_params:
             if p.grad is not None:
-                if set_to_none and getattr(p, "_pdt_keep_grad_view", False) is False:
+                if getattr(p, "_pdt_keep_grad_view", False):
+                    p.grad.zero_()
+                elif set_to_none:
                     p.grad = None
                 else:
                     p.grad.zero_()
 
     def clip_grad_norm(self, max_norm: float, norm_type: float = 2.0):
-        """Global norm over the owned (already reduced) gradients: one 1-float all-reduce."""
+        """Global norm over the owned gradients (each parameter counted once): one 1-float all-reduce."""
         norm, _, _ = clip_grad_norm_(self.owned_params(), max_norm, norm_type=norm_type, comm=self.comm,
                                      sharded=True)
         return norm
 
-    # ---------------------------------------------------------------- checkpointing
-    def _local_state_by_global_index(self):
+    # ---------------------------------------------------------------- full parameters
+    @torch.no_grad()
+    def full_parameters(self):
+        """{module parameter: full fp32 value} on every rank (compute-dtype mode gathers the fp32 masters;
+        otherwise the module parameters already hold full values)."""
         out = {}
-        if self.optim is None:
-            return out
-        idx_of = {id(p): i for i, p in enumerate(self._all_params)}
-        for p, st in self.optim.state.items():
-            out[idx_of[id(p)]] = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in st.items()}
+        for bank in self._banks:
+            if bank.master_flat is None:
+                for p in bank.params:
+                    out[p] = p.detach()
+                continue
+            full = torch.empty(bank.total, dtype=torch.float32, device=bank.device)
+            self.comm.all_gather(full, bank.master_flat)
+            for li, p in enumerate(bank.params):
+                out[p] = bank.view(full, li).clone()
         return out
 
+    @torch.no_grad()
+    def load_full_parameters(self, values):
+        """Set module parameters (and this rank's masters) from full fp32 values {param: tensor}."""
+        for bank in self._banks:
+            for li, p in enumerate(bank.params):
+                if p not in values:
+                    continue
+                v = values[p].to(device=bank.device)
+                bank.view(bank.flat, li).copy_(v)
+                if li in bank.masters:
+                    bank.masters[li].copy_(v)
+                    bank.masters[li]._pdt_lp_version = bank.masters[li]._version
+
+    # ---------------------------------------------------------------- checkpointing
+    def _state_keys(self):
+        keys = set()
+        if self.optim is not None:
+            for st in self.optim.state.values():
+                keys.update(k for k, v in st.items() if torch.is_tensor(v) and v.dim() > 0)
+        allk = self.comm.all_gather_object(sorted(keys))     # key NAMES only -- the state moves as tensors
+        return sorted(set(k for ks in allk for k in ks))
+
+    @torch.no_grad()
     def consolidate_state_dict(self, recipient_rank: int = 0):
-        """Gather every rank's optimizer state shard on ``recipient_rank`` (Stoke/Fairscale save path)."""
-        mine = self._local_state_by_global_index()
-        if self.comm.world_size == 1:
-            self._state_cache = mine
-            return
-        gathered = self.comm.all_gather_object(mine)
-        if self.comm.rank == recipient_rank:
-            full = {}
-            for part in gathered:
-                full.update(part)
-            self._state_cache = full
-        else:
+        """Gather the optimizer state on ``recipient_rank`` (Stoke/Fairscale save path):
+        per bank and state key, every owner's flat segment moves in one all-gather; step counts in one
+        tiny all-reduce."""
+        rank, world = self.comm.rank, self.comm.world_size
+        keys = self._state_keys() if world > 1 else sorted(
+            {k for st in (self.optim.state.values() if self.optim else []) for k, v in st.items()
+             if torch.is_tensor(v) and v.dim() > 0})
+        dev = self._banks[0].device if self._banks else torch.device("cpu")
+        n = len(self._all_params)
+        steps = torch.zeros(n, dtype=torch.float64, device=dev)
+        has = torch.zeros(n, dtype=torch.float64, device=dev)
+        full = {}
+        for bank in self._banks:
+            for k in keys:
+                seg = torch.zeros(bank.seg, dtype=torch.float32, device=bank.device)
+                for li, p in enumerate(bank.params):
+                    if bank.owners[li] != rank:
+                        continue
+                    st = self.optim.state.get(self._opt_param(p), {}) if self.optim is not None else {}
+                    if k in st:
+                        o = bank.offsets[li] - rank * bank.seg
+                        seg[o:o + p.numel()].copy_(st[k].reshape(-1))
+                g = torch.empty(bank.total, dtype=torch.float32, device=bank.device)
+                self.comm.all_gather(g, seg)
+                full[(id(bank), k)] = g
+            for li, p in enumerate(bank.params):
+                if bank.owners[li] == rank and self.optim is not None:
+                    st = self.optim.state.get(self._opt_param(p))
+                    if st and "step" in st:
+                        steps[bank.idxs[li]] = float(st["step"])
+                        has[bank.idxs[li]] = 1.0
+        self.comm.all_reduce(steps, "sum")
+        self.comm.all_reduce(has, "sum")
+        if rank != recipient_rank:
             self._state_cache = None
+            return
+        steps, has = steps.cpu(), has.cpu()
+        state = {}
+        for bank in self._banks:
+            for li, p in enumerate(bank.params):
+                gi = bank.idxs[li]
+                if not has[gi]:
+                    continue
+                ent = {"step": torch.tensor(float(steps[gi]))}
+                for k in keys:
+                    ent[k] = bank.view(full[(id(bank), k)], li).detach().to("cpu", copy=True).view(p.shape)
+                state[gi] = ent
+        self._state_cache = state
 
     def state_dict(self):
         """torch layout: {state: {global_idx: {...}}, param_groups: [...]} (call consolidate first)."""
@@ -170,16 +317,14 @@ class OSS(Optimizer):
             else:
                 raise RuntimeError("OSS.state_dict(): call consolidate_state_dict(recipient_rank) first "
                                    "(only the recipient holds the full state)")
-        groups, start = [], 0
-        idx_of = {id(p): i for i, p in enumerate(self._all_params)}
+        groups = []
         for g in self.param_groups:
             d = {k: v for k, v in g.items() if k != "params"}
-            d["params"] = [idx_of[id(p)] for p in g["params"]]
+            d["params"] = [self._index[id(p)] for p in g["params"]]
             groups.append(d)
         return {"state": dict(self._state_cache), "param_groups": groups}
 
     def load_state_dict(self, sd):
-        idx_of = {id(p): i for i, p in enumerate(self._all_params)}
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for k, v in sg.items():
                 if k != "params":
@@ -189,11 +334,13 @@ class OSS(Optimizer):
         local = {"state": {}, "param_groups": []}
         lidx = 0
         for li, gi in enumerate(self._local_group_idx):
-            lg = {k: v for k, v in self.param_groups[gi].items() if k != "params"}
+            lg = {k: v for k, v in self.optim.param_groups[li].items() if k != "params"}
+            lg.update({k: v for k, v in self.param_groups[gi].items() if k != "params"})
             ps = self.optim.param_groups[li]["params"]
             lg["params"] = list(range(lidx, lidx + len(ps)))
-            for j, p in enumerate(ps):
-                gidx = idx_of[id(p)]
+            owned = [p for p in self.param_groups[gi]["params"] if self._owner_of[id(p)] == self.comm.rank]
+            for j, p in enumerate(owned):
+                gidx = self._index[id(p)]
                 st = sd["state"].get(gidx, sd["state"].get(str(gidx)))
                 if st is not None:
                     local["state"][lidx + j] = st
@@ -203,47 +350,88 @@ class OSS(Optimizer):
 
 
 class ShardedDataParallel(nn.Module):
-    """ZeRO-2: each gradient is reduced (averaged) only to the rank that owns its optimizer shard."""
+    """ZeRO-2: each gradient is reduced (averaged) only to the rank that owns its optimizer shard, and
+    non-owners drop it.  ``reduce_mode="all_reduce"``: ZeRO-1 (full gradients all-reduced, DDP + OSS)."""
 
     def __init__(self, module: nn.Module, sharded_optimizer: OSS, comm: Comm | None = None,
                  broadcast_buffers: bool = True, sync_models_at_startup: bool = True,
-                 reduce_buffer_size: int = 2 ** 23, reduce_fp16: bool = False, **_ignored):
+                 reduce_buffer_size: int = 2 ** 23, reduce_fp16: bool = False, reduce_mode: str = "reduce",
+                 buffer_sync: str = "changed", **_ignored):
         super().__init__()
+        if reduce_mode not in ("reduce", "all_reduce"):
+            raise ValueError(f"reduce_mode must be 'reduce' or 'all_reduce', got {reduce_mode}")
         self.module = module
         self.optimizer = sharded_optimizer
         self.comm = comm or sharded_optimizer.comm
         self.broadcast_buffers = broadcast_buffers
+        self.buffer_sync = buffer_sync
         self.reduce_fp16 = reduce_fp16
+        self.reduce_mode = reduce_mode
         self._no_sync = False
         self._callback_queued = False
         self._handles = []
         if sync_models_at_startup and self.comm.world_size > 1:
-            self.comm.broadcast_coalesced([p.data for p in module.parameters()] + list(module.buffers()))
-        # gradient flats mirror the optimizer's parameter flats; split into <= reduce_buffer_size buckets
+            # parameters were already synced by OSS (before its re-layout); buffers here
+            bufs = list(module.buffers())
+            if bufs:
+                self.comm.broadcast_coalesced(bufs)
         self.params = sharded_optimizer._all_params
-        self._param_index = {id(p): i for i, p in enumerate(self.params)}
-        self._buckets = []       # (owner, grad view, [param idx])
-        elem_cap = max(1, reduce_buffer_size)
-        for (r, flat, ps, _lp) in sharded_optimizer._flats:
-            g = torch.zeros_like(flat)
-            off, cur, cur_start = 0, [], 0
-            for p in ps:
-                n = p.numel()
-                p.grad = g[off:off + n].view(p.shape)
-                p._pdt_keep_grad_view = True
-                cur.append(self._param_index[id(p)])
-                off += n
-                if (off - cur_start) * g.element_size() >= elem_cap:
-                    self._buckets.append((r, g[cur_start:off], cur))
-                    cur, cur_start = [], off
-            if cur:
-                self._buckets.append((r, g[cur_start:off], cur))
-        # launch order = expected completion order under reverse-order backward
-        self._buckets.sort(key=lambda b: -min(b[2]))
-        self.tracker = require_runtime().ReadyTracker([b[2] for b in self._buckets], len(self.params))
+        self._pad = {}
+        # gradient storage: own segment only (ZeRO-2) or the full flat (ZeRO-1); buckets from the layout
+        self._buckets = []          # (bank, owner, start, numel, [local idx])
+        self._grad = {}             # bank id -> gradient flat
+        for bank in sharded_optimizer.banks():
+            if reduce_mode == "reduce":
+                self._grad[id(bank)] = torch.zeros(bank.seg, dtype=bank.dtype, device=bank.device)
+            else:
+                self._grad[id(bank)] = torch.zeros(bank.total, dtype=bank.dtype, device=bank.device)
+            esz = torch.tensor([], dtype=bank.dtype).element_size()
+            for b in bank.layout(reduce_buffer_size // esz).buckets:
+                self._buckets.append((bank, int(b.owner), int(b.start), int(b.numel), list(b.params)))
+        self._buckets.sort(key=lambda b: -min(b[0].idxs[li] for li in b[4]))
+        self._attach()
+        gidx = {}
+        for bi, (bank, _o, _s, _n, lidx) in enumerate(self._buckets):
+            for li in lidx:
+                gidx.setdefault(bi, []).append(bank.idxs[li])
+        self.tracker = require_runtime().ReadyTracker([gidx[b] for b in range(len(self._buckets))], len(self.params))
+        self._bank_li = {}
+        for bank in sharded_optimizer.banks():
+            for li, gi in enumerate(bank.idxs):
+                self._bank_li[gi] = (bank, li)
         for i, p in enumerate(self.params):
-            p.register_post_accumulate_grad_hook(self._make_hook(i))
+            if p.requires_grad:       # frozen parameters: their buckets are released at the end of backward
+                p.register_post_accumulate_grad_hook(self._make_hook(i))
 
+    # ------------------------------------------------------------------ gradient storage
+    def _grad_view(self, bank, li):
+        p = bank.params[li]
+        o = bank.offsets[li] - (bank.rank * bank.seg if self.reduce_mode == "reduce" else 0)
+        return self._grad[id(bank)][o:o + p.numel()].view(p.shape)
+
+    def _persistent(self, bank, li) -> bool:
+        return self.reduce_mode == "all_reduce" or bank.owners[li] == bank.rank
+
+    def _attach(self):
+        """Persistent gradients are views of the flat (autograd accumulates in place, no copy-in)."""
+        for bank in self.optimizer.banks():
+            for li, p in enumerate(bank.params):
+                if self._persistent(bank, li):
+                    v = self._grad_view(bank, li)
+                    if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                        p.grad = v
+                    p._pdt_keep_grad_view = True
+
+    def grad_bytes(self) -> int:
+        """Gradient bytes this rank currently holds (persistent flat + any live non-owned .grad)."""
+        n = sum(t.numel() * t.element_size() for t in self._grad.values())
+        for bank in self.optimizer.banks():
+            for li, p in enumerate(bank.params):
+                if not self._persistent(bank, li) and p.grad is not None:
+                    n += p.grad.numel() * p.grad.element_size()
+        return n
+
+    # ------------------------------------------------------------------ hooks / reduction
     def _make_hook(self, idx):
         def hook(_p):
             if self._no_sync or self.comm.world_size == 1:
@@ -253,14 +441,47 @@ class ShardedDataParallel(nn.Module):
                 self._launch(b)
         return hook
 
+    def _zeros(self, n, dtype, device):
+        z = self._pad.get((n, dtype, device))
+        if z is None:
+            z = self._pad[(n, dtype, device)] = torch.zeros(n, dtype=dtype, device=device)
+        return z
+
+    def _pack(self, bank, start, n, lidx):
+        """Non-owner: this bucket's gradients in the owner's segment layout, one cat (gaps = zeros)."""
+        pieces, cur = [], start
+        for li in sorted(lidx, key=lambda i: bank.offsets[i]):
+            p = bank.params[li]
+            o = bank.offsets[li]
+            if o > cur:
+                pieces.append(self._zeros(o - cur, bank.dtype, bank.device))
+            g = p.grad
+            pieces.append(g.reshape(-1) if g is not None else self._zeros(p.numel(), bank.dtype, bank.device))
+            p.grad = None                                # ZeRO-2: a non-owner drops the gradient
+            cur = o + p.numel()
+        if start + n > cur:
+            pieces.append(self._zeros(start + n - cur, bank.dtype, bank.device))
+        return torch.cat(pieces) if len(pieces) > 1 else pieces[0].clone()
+
     def _launch(self, b):
-        owner, view, _ = self._buckets[b]
-        if self.reduce_fp16 and view.dtype == torch.float32:
-            payload = view.to(torch.bfloat16 if view.is_cuda else torch.float16)
-            h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
-            self._handles.append((h, view, payload, owner))
+        bank, owner, start, n, lidx = self._buckets[b]
+        if self.reduce_mode == "all_reduce":
+            buf = self._grad[id(bank)][start:start + n]
+        elif owner == bank.rank:
+            o = start - bank.rank * bank.seg
+            buf = self._grad[id(bank)][o:o + n]
         else:
-            self._handles.append((self.comm.reduce(view, dst=owner, op="avg", async_op=True), None, None, owner))
+            buf = self._pack(bank, start, n, lidx)
+        payload = buf
+        if self.reduce_fp16 and buf.dtype == torch.float32:
+            payload = buf.to(torch.bfloat16 if buf.is_cuda else torch.float16)
+        if self.reduce_mode == "all_reduce":
+            h = self.comm.all_reduce(payload, "avg", async_op=True)
+            keep = True
+        else:
+            h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
+            keep = owner == bank.rank
+        self._handles.append((h, buf if (keep and payload is not buf) else None, payload))
 
     def _queue_finalize(self):
         if self._callback_queued:
@@ -270,39 +491,30 @@ class ShardedDataParallel(nn.Module):
 
     def _finalize(self):
         self._callback_queued = False
-        for b in self.tracker.flush():
+        self.comm.check_errors()
+        for b in self.tracker.flush():      # buckets with parameters that got no gradient
             self._launch(b)
-        for h, view, payload, owner in self._handles:
+        for h, dst, payload in self._handles:
             h.wait()
-            if view is not None and self.comm.rank == owner:
-                view.copy_(payload)
+            if dst is not None:
+                dst.copy_(payload)
         self._handles.clear()
         self.tracker.reset()
 
+    # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
-        for p in self.params:
-            if p.grad is None:      # a torch-style zero_grad(set_to_none) dropped the views: re-attach
-                self._reattach()
-                break
+        self._attach()        # a torch-style zero_grad(set_to_none) may have dropped the views
         if self.broadcast_buffers and self.comm.world_size > 1 and self.module.training:
-            bufs = list(self.module.buffers())
-            if bufs:
-                self.comm.broadcast_coalesced(bufs)
+            sync_buffers(self.module, self.comm, self, self.buffer_sync)
         return self.module(*args, **kwargs)
 
-    def _reattach(self):
-        # grads are views of the bucket storage; zero and re-attach them from the bucket list
-        for (r, view, idxs) in self._buckets:
-            view.zero_()
-            off = 0
-            for i in idxs:
-                p = self.params[i]
-                p.grad = view[off:off + p.numel()].view(p.shape)
-                off += p.numel()
-
     def zero_grad(self, set_to_none: bool = False):
-        for (_r, view, _i) in self._buckets:
-            view.zero_()
+        for g in self._grad.values():
+            g.zero_()
+        for bank in self.optimizer.banks():
+            for li, p in enumerate(bank.params):
+                if not self._persistent(bank, li):
+                    p.grad = None
 
     @contextmanager
     def no_sync(self):
@@ -312,3 +524,26 @@ class ShardedDataParallel(nn.Module):
             yield
         finally:
             self._no_sync = old
+
+    # ------------------------------------------------------------------ checkpoint helpers
+    def full_state_dict(self):
+        """Module state dict with full fp32 parameter values (no 'module.' prefix)."""
+        sd = self.module.state_dict()
+        name_of = {id(p): n for n, p in self.module.named_parameters()}
+        for p, v in self.optimizer.full_parameters().items():
+            if id(p) in name_of:
+                sd[name_of[id(p)]] = v.to(torch.float32)
+        return sd
+
+    def load_full_state_dict(self, sd, strict=True):
+        name_of = {id(p): n for n, p in self.module.named_parameters()}
+        vals = {p: sd[name_of[id(p)]] for p in self.params if id(p) in name_of and name_of[id(p)] in sd}
+        rest = {k: v for k, v in sd.items() if k not in set(name_of.values())}
+        res = self.module.load_state_dict(rest, strict=False)
+        self.optimizer.load_full_parameters(vals)
+        if strict:
+            missing = [n for n in name_of.values() if n not in sd] + list(res.missing_keys)
+            missing = [k for k in missing if k not in sd]
+            if missing or res.unexpected_keys:
+                raise RuntimeError(f"load_full_state_dict: missing={missing} unexpected={res.unexpected_keys}")
+        return res

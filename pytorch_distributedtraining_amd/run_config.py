@@ -47,6 +47,8 @@ class RunConfig:
     warmup: int = 2
     log_every: int = 10
     checkpoint_dir: Optional[str] = None
+    checkpoint_every: int = 0               # optimizer steps between checkpoints (0: only at the end)
+    resume: bool = True                     # continue from the newest checkpoint in checkpoint_dir
     metrics_path: Optional[str] = None
     seed: int = 0
 

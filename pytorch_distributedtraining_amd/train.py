@@ -7,8 +7,10 @@ through the Stoke-style ``Trainer`` on synthetic data of the workload's shape.
 
 Accepts both ``--local-rank`` and ``--local_rank`` (the reference's parser only knew the latter while
 torch.distributed.launch passes the former).  Prints rank-0 progress lines with the
-synced loss and whole-job throughput, writes JSONL metrics when ``metrics_path`` is set, and saves a
-Stoke-layout checkpoint at the end when ``checkpoint_dir`` is set.
+synced loss and whole-job throughput, writes JSONL metrics when ``metrics_path`` is set, saves Stoke-layout
+checkpoints every ``checkpoint_every`` optimizer steps and at the end when ``checkpoint_dir`` is set, and
+resumes from the newest one found there (``resume``, default on) -- which is what makes a launcher restart
+(``launch --max-restarts``) after a rank failure continue the run instead of starting over.
 """
 from __future__ import annotations
 
@@ -115,36 +117,57 @@ def run(cfg: RunConfig) -> dict:
             tr.step()
         return loss
 
-    for _ in range(cfg.warmup):
+    # auto-resume: continue from the newest Stoke-layout checkpoint in checkpoint_dir --
+    # after a launcher restart (--max-restarts) the group picks up where the last save left it
+    start = 0
+    if cfg.checkpoint_dir and cfg.resume:
+        from .utils.checkpoint import latest_checkpoint
+        tag = latest_checkpoint(cfg.checkpoint_dir) if os.path.isdir(cfg.checkpoint_dir) else None
+        if tag is not None:
+            extras = tr.load(cfg.checkpoint_dir, tag) or {}
+            start = int(extras.get("step", 0))
+            tr.print(f"[train] resumed from {tag} at step {start}")
+    total = cfg.warmup + cfg.steps
+
+    def maybe_save(step):
+        if cfg.checkpoint_dir and cfg.checkpoint_every and step % cfg.checkpoint_every == 0 and step < total:
+            tr.save(cfg.checkpoint_dir, name=f"{cfg.name}-s{step}", extras={"step": step})
+
+    for step in range(start, min(cfg.warmup, total)):
         opt_step()
+        maybe_save(step + 1)
     if gpu:
         torch.cuda.synchronize(dev)
     tr.barrier()
     t0 = time.perf_counter()
-    last = None
-    for i in range(cfg.steps):
+    last, loss = None, None
+    first = max(start, cfg.warmup)
+    for step in range(first, total):
         loss = opt_step()
-        if (i + 1) % cfg.log_every == 0 or i + 1 == cfg.steps:
+        i = step - cfg.warmup
+        maybe_save(step + 1)
+        if (i + 1) % cfg.log_every == 0 or step + 1 == total:
             last = tr.detach_and_sync_loss(loss)       # one host sync per log line only
             el = time.perf_counter() - t0
-            samples = (i + 1) * cfg.batch_size_per_device * cfg.grad_accum_steps * tr.world_size
-            rec = {"step": i + 1, "loss": last, "samples_per_s": samples / el}
+            samples = (step + 1 - first) * cfg.batch_size_per_device * cfg.grad_accum_steps * tr.world_size
+            rec = {"step": step + 1, "loss": last, "samples_per_s": samples / el}
             if kind == "lm":
                 rec["tokens_per_s"] = samples * cfg.seq_len / el
             tr.print(json.dumps(rec))
             if sink:
-                sink.log(rec, step=i + 1)
+                sink.log(rec, step=step + 1)
     if gpu:
         torch.cuda.synchronize(dev)
     tr.barrier()
     dt = time.perf_counter() - t0
-    samples = cfg.steps * cfg.batch_size_per_device * cfg.grad_accum_steps * tr.world_size
+    n = max(1, total - first)
+    samples = n * cfg.batch_size_per_device * cfg.grad_accum_steps * tr.world_size
     result = {"name": cfg.name, "model": cfg.model, "world_size": tr.world_size, "steps": cfg.steps,
-              "ms_per_step": 1000 * dt / max(1, cfg.steps), "samples_per_s": samples / dt, "loss": last}
+              "resumed_from": start, "ms_per_step": 1000 * dt / n, "samples_per_s": samples / dt, "loss": last}
     if kind == "lm":
         result["tokens_per_s"] = samples * cfg.seq_len / dt
     if cfg.checkpoint_dir:
-        result["checkpoint"] = tr.save(cfg.checkpoint_dir, name=cfg.name)
+        result["checkpoint"] = tr.save(cfg.checkpoint_dir, name=f"{cfg.name}-final", extras={"step": total})
     if sink:
         sink.log({"final": result})
         sink.close()

@@ -17,6 +17,7 @@ Same method names and semantics as the reference exercises them:
 from __future__ import annotations
 
 import contextlib
+import os
 import uuid
 
 import torch
@@ -26,7 +27,9 @@ from ..data.loader import DeviceDataLoader
 from ..optim import FusedAdamW, GradScaler, clip_grad_norm_
 from ..parallel.comm import Comm
 from ..utils import checkpoint as ckpt
+from ..utils import profiling as prof
 from ..utils.dist import init_distributed
+from ..utils.fault import maybe_inject_fault
 from ..utils.logging import RankLogger
 from .configs import (AMPConfig, ClipGradConfig, ClipGradNormConfig, DDPConfig, DeepspeedConfig, DistributedOptions,
                       FairscaleFSDPConfig, FairscaleOSSConfig, FairscaleSDDPConfig, FP16Options, StokeOptimizer,
@@ -108,6 +111,7 @@ class Trainer:
         opt_cls = self._fused_equivalent(opt_spec.optimizer)
         kw = dict(opt_spec.optimizer_kwargs)
         self._sharded_grads = False
+        self.compute_dtype = None
         if fairscale_fsdp:
             from ..parallel.fsdp import FullyShardedDataParallel, MixedPrecision, ShardingStrategy
             c = self.fsdp_config
@@ -125,29 +129,32 @@ class Trainer:
             self._sharded_grads = True
         else:
             model.to(self.device)
+            # bf16 compute copy: with the fused optimizer the module itself runs on bf16 parameters that the
+            # AdamW epilogue rewrites from fp32 masters, instead of autocast casting every fp32 weight to bf16
+            # in every forward and every bf16 gradient back to fp32 (thousands of cast kernels per step)
+            cdt = torch.bfloat16 if (self.gpu and self.fp16 == "bf16" and opt_cls is FusedAdamW) else None
+            self.compute_dtype = cdt
             if fairscale_oss:
-                from ..parallel.zero import OSS
-                if fairscale_sddp:
-                    self._optimizer = OSS(model.parameters(), optim=opt_cls, comm=self.comm,
-                                          broadcast_fp16=self.oss_config.broadcast_fp16, **kw)
-                    from ..parallel.zero import ShardedDataParallel
-                    s = self.sddp_config
-                    self._engine = ShardedDataParallel(model, self._optimizer, comm=self.comm,
-                                                       broadcast_buffers=s.broadcast_buffers,
-                                                       sync_models_at_startup=s.sync_models_at_startup,
-                                                       reduce_buffer_size=s.reduce_buffer_size,
-                                                       reduce_fp16=s.reduce_fp16)
-                    self._clip_params = self._optimizer.owned_params
-                    self._sharded_grads = True
-                else:
-                    self._engine = self._make_ddp(model, rebuild=False)
-                    self._optimizer = OSS(model.parameters(), optim=opt_cls, comm=self.comm,
-                                          broadcast_fp16=self.oss_config.broadcast_fp16, **kw)
-                    self._clip_params = lambda: list(self._module.parameters())
-            elif self.distributed is not None:
-                self._engine = self._make_ddp(model, rebuild=True)
-                self._optimizer = opt_cls(model.parameters(), **kw)
-                self._clip_params = lambda: list(self._module.parameters())
+                from ..parallel.zero import OSS, ShardedDataParallel
+                self._optimizer = OSS(model.parameters(), optim=opt_cls, comm=self.comm,
+                                      broadcast_fp16=self.oss_config.broadcast_fp16, compute_dtype=cdt, **kw)
+                s = self.sddp_config
+                # ZeRO-2 (reduce each bucket to its owner, drop the rest) with SDDP, else ZeRO-1 gradients
+                # (bucketed all-reduce over the same owner-contiguous flat) under DDP + OSS
+                self._engine = ShardedDataParallel(model, self._optimizer, comm=self.comm,
+                                                   broadcast_buffers=s.broadcast_buffers if fairscale_sddp else
+                                                   self.ddp_config.broadcast_buffers,
+                                                   sync_models_at_startup=s.sync_models_at_startup,
+                                                   reduce_buffer_size=s.reduce_buffer_size if fairscale_sddp else
+                                                   int(self.ddp_config.bucket_cap_mb * (1 << 20)),
+                                                   reduce_fp16=s.reduce_fp16,
+                                                   reduce_mode="reduce" if fairscale_sddp else "all_reduce")
+                self._clip_params = self._optimizer.owned_params
+                self._sharded_grads = True
+            elif self.distributed is not None or cdt is not None:
+                self._engine = self._make_ddp(model, rebuild=self.distributed is not None, compute_dtype=cdt)
+                self._optimizer = opt_cls(self._engine.optimizer_parameters(), **kw)
+                self._clip_params = self._engine.optimizer_parameters
             else:
                 self._engine = model
                 self._optimizer = opt_cls(model.parameters(), **kw)
@@ -161,6 +168,8 @@ class Trainer:
         self._ema = None           # device tensor
         self._last_loss = None
         self._training = True
+        # PDT_COMM_DEBUG=1: cross-rank collective-sequence check every K optimizer steps
+        self._verify_every = max(1, int(os.environ.get("PDT_VERIFY_EVERY", "50")))
         if verbose:
             self.logger.print(f"[Trainer] {self.status.as_dict()} device={self.device}")
 
@@ -173,13 +182,13 @@ class Trainer:
             return lambda params, **kw: FusedAdamW(params, decoupled=False, **kw)
         return cls
 
-    def _make_ddp(self, model, rebuild):
+    def _make_ddp(self, model, rebuild, compute_dtype=None):
         from ..parallel.ddp import DistributedDataParallel
         c = self.ddp_config
         return DistributedDataParallel(model, comm=self.comm, device=self.device, bucket_cap_mb=c.bucket_cap_mb,
                                        first_bucket_mb=c.first_bucket_mb, broadcast_buffers=c.broadcast_buffers,
                                        find_unused_parameters=c.find_unused_parameters, reduce_dtype=c.reduce_dtype,
-                                       rebuild_buckets=rebuild)
+                                       rebuild_buckets=rebuild, compute_dtype=compute_dtype)
 
     # ------------------------------------------------------------------ properties
     @property
@@ -229,7 +238,7 @@ class Trainer:
         return torch.autocast(self.device.type, dtype=self.autocast_dtype)
 
     def model(self, *args, **kwargs):
-        with self._autocast():
+        with prof.range("pdt.forward"), self._autocast():
             return self._engine(*args, **kwargs)
 
     __call__ = model
@@ -253,7 +262,7 @@ class Trainer:
         boundary = self._is_boundary()
         scaled = self.scaler.scale(loss) if self.scaler is not None else loss
         use_no_sync = (not boundary) and self.ddp_config.no_sync and hasattr(self._engine, "no_sync")
-        with (self._engine.no_sync() if use_no_sync else contextlib.nullcontext()):
+        with prof.range("pdt.backward"), (self._engine.no_sync() if use_no_sync else contextlib.nullcontext()):
             scaled.backward()
         self._backward_steps += 1
         self._grad_accum_counter = (self._grad_accum_counter + 1) % self.grad_accum
@@ -261,6 +270,15 @@ class Trainer:
     def step(self):
         if self._grad_accum_counter != 0:
             return False   # not an accumulation boundary
+        maybe_inject_fault(self._optimizer_steps)     # env-driven fault injection (tests of restart/resume)
+        with prof.range("pdt.optimizer_step"):
+            self._step()
+        self._optimizer_steps += 1
+        if self.comm.debug and self._optimizer_steps % self._verify_every == 0:
+            self.comm.verify_consistency(f"after optimizer step {self._optimizer_steps}")
+        return True
+
+    def _step(self):
         params = self._clip_params() if callable(self._clip_params) else self._clip_params
         opt = self._optimizer
         fused = isinstance(opt, FusedAdamW) or (hasattr(opt, "optim") and isinstance(getattr(opt, "optim", None),
@@ -290,8 +308,6 @@ class Trainer:
         if self.scaler is not None:
             self.scaler.update()
         self.zero_grads()
-        self._optimizer_steps += 1
-        return True
 
     def zero_grads(self):
         if hasattr(self._engine, "zero_grad") and self._engine is not self._module:

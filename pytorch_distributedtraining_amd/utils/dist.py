@@ -45,6 +45,8 @@ def init_distributed(backend: str | None = None, timeout_s: float = 1800.0, rank
     if use_gpu and device_bind:
         torch.cuda.set_device(device)
     if world_size > 1 and not dist.is_initialized():
+        from .fault import configure_watchdog
+        configure_watchdog(timeout_s)    # RCCL async error handling: a dead peer ends the job, never a hang
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if use_gpu else "gloo"

@@ -15,6 +15,7 @@ import torch.distributed as dist
 
 
 def configure_watchdog(timeout_s: float = 600.0):
+    """Called by ``init_distributed`` before the process group exists (the NCCL/RCCL env is read then)."""
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "1")
     os.environ.setdefault("TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC", str(int(timeout_s)))
@@ -26,9 +27,13 @@ class InjectedFault(RuntimeError):
 
 
 def maybe_inject_fault(step: int):
+    """Called by ``Trainer.step`` before optimizer step ``step`` (0-based).  Fires only in the launch attempt
+    ``PDT_FAULT_RESTART`` (default 0, from TORCHELASTIC_RESTART_COUNT), so a restarted group runs clean."""
     fr = os.environ.get("PDT_FAULT_RANK")
     fs = os.environ.get("PDT_FAULT_STEP")
     if fr is None or fs is None:
+        return
+    if os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != os.environ.get("PDT_FAULT_RESTART", "0"):
         return
     rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
     if rank != int(fr) or step != int(fs):

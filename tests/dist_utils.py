@@ -16,6 +16,8 @@ def _free_port():
 
 
 def _entry(rank, world, port, fn, args, outdir):
+    import faulthandler
+    faulthandler.enable()       # a native crash in a worker prints its Python stack instead of vanishing
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -44,18 +46,27 @@ def run_workers(fn, world=2, *args, timeout=240):
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.start_processes(_entry, args=(world, _free_port(), fn, args, d), nprocs=world, join=False,
                                  start_method="spawn")
-        ctx.join(timeout)
+        import time
+        deadline = time.time() + timeout
+        # ProcessContext.join returns as soon as ONE process exits cleanly: keep joining until all are done
+        while not ctx.join(max(0.0, deadline - time.time())):
+            if time.time() >= deadline:
+                break
         for p in ctx.processes:
             if p.is_alive():
                 p.kill()
-        out = []
+        out, errs = [], []
         for r in range(world):
             path = os.path.join(d, f"r{r}.pkl")
             if not os.path.exists(path):
-                raise RuntimeError(f"rank {r} produced no result (crashed or timed out)")
+                codes = [p.exitcode for p in ctx.processes]
+                errs.append(f"rank {r} produced no result (crashed or timed out); exit codes {codes}")
+                continue
             with open(path, "rb") as f:
                 res, err = pickle.load(f)
             if err:
-                raise RuntimeError(f"rank {r} failed:\n{err}")
+                errs.append(f"rank {r} failed:\n{err}")
             out.append(res)
+        if errs:
+            raise RuntimeError("\n".join(errs))
         return out

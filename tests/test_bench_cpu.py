@@ -1,0 +1,38 @@
+"""bench.py contract on CPU: ``--gpus N`` launches N ranks itself (no torchrun), rank 0 prints ONE JSON
+line that reports the real world size and the engines' collective traffic; a WORLD_SIZE that disagrees
+with ``--gpus`` is refused (reference launch patterns: Stoke-DDP.py:2, Fairscale-DDP.py:125-132)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", **kw)
+    return env
+
+
+def test_bench_self_launches_two_gloo_ranks():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--workload", "resnet18-cpu", "--steps", "1",
+                        "--warmup", "1", "--micro-batch", "2"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_ranks"] == 2
+    assert res["config"]["parallelism"] == "dp2"
+    assert res["config"]["global_batch"] == 4
+    # DDP gradient buckets + the clip-norm scalar cross the wire every step
+    assert res["collectives_per_step"] >= 2
+    assert res["comm_bytes_per_step"] >= 4 * 11_000_000
+
+
+def test_bench_refuses_mismatched_world_size():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--workload", "resnet18-cpu"], cwd=ROOT,
+                       env=_env(WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr

@@ -277,3 +277,116 @@ def test_ddp_broadcasts_only_changed_buffers():
     assert s0 == s1 == [4, 3, 3]
     assert n0 == n1 == 3
     assert not torch.equal(rm0, rm1)   # each rank's last forward updated with its own batch
+
+
+def _w_zero2(rank, world, mode, accum, compute_bf16):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel.zero import OSS, ShardedDataParallel
+    m = _model()
+    model_bytes = sum(p.numel() * 4 for p in m.parameters())
+    opt = OSS(m.parameters(), optim=FusedAdamW, lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4,
+              compute_dtype=torch.bfloat16 if compute_bf16 else None)
+    model = ShardedDataParallel(m, opt, reduce_buffer_size=512, reduce_mode=mode)
+    gbytes = []
+    for s in range(STEPS):
+        for a in range(accum):
+            x, y = _data(s * accum + a, world)
+            ctx = model.no_sync() if a < accum - 1 else torch.enable_grad()
+            with ctx:
+                out = model(_shard(x, rank, world).to(torch.bfloat16 if compute_bf16 else torch.float32))
+                loss = nn.functional.mse_loss(out.float(), _shard(y, rank, world)) / accum
+                loss.backward()
+        gbytes.append(model.grad_bytes())
+        clip_grad_norm_(opt.owned_params(), 1e9, comm=opt.comm, sharded=True)
+        opt.step()
+        model.zero_grad()
+        opt.zero_grad()
+    full = model.full_state_dict()
+    opt.consolidate_state_dict(0)
+    osd = opt.state_dict() if rank == 0 else None
+    masters = sum(mm.numel() for b in opt.banks() for mm in b.masters.values())
+    return ({k: v.detach().float().clone() for k, v in full.items()}, osd, gbytes, model_bytes, masters,
+            [p.dtype for p in m.parameters()])
+
+
+@pytest.mark.parametrize("mode,accum", [("reduce", 1), ("reduce", 2), ("all_reduce", 1)])
+def test_zero2_reduce_to_owner_matches_and_shards_gradients(mode, accum):
+    ref = _reference(2, accum=accum)
+    (s0, osd, gb0, mbytes, _, _), (s1, _, gb1, _, _, _) = run_workers(_w_zero2, 2, mode, accum, False)
+    for k in ref:
+        assert torch.equal(s0[k], s1[k])
+        assert torch.allclose(s0[k], ref[k], atol=2e-5), k
+    if mode == "reduce":
+        # ZeRO-2: after backward a rank holds only its own segment of the gradients (this 6-tensor model
+        # partitions 1024 : 708 elements; see test_zero2_gradient_memory for a balanced model)
+        assert max(gb1) <= 0.6 * mbytes and max(gb0) <= 0.6 * mbytes, (gb0, gb1, mbytes)
+    else:
+        assert min(gb1) >= mbytes        # ZeRO-1 keeps full gradients
+    assert sorted(osd["state"].keys()) == list(range(6))
+    assert all(float(e["step"]) == STEPS for e in osd["state"].values())
+
+
+def test_zero2_bf16_compute_copy_masters_are_sharded():
+    ref = _reference(2)
+    (s0, osd, _, mbytes, mast0, dts), (s1, _, _, _, mast1, _) = run_workers(_w_zero2, 2, "reduce", 1, True)
+    assert all(dt == torch.bfloat16 for dt in dts)           # the module runs on the bf16 compute copy
+    assert mast0 + mast1 == mbytes // 4                      # fp32 masters: each parameter on one rank only
+    assert 0 < mast0 < mbytes // 4 and 0 < mast1 < mbytes // 4
+    for k in ref:
+        assert torch.equal(s0[k], s1[k])                     # full_state_dict gathers the fp32 masters
+        assert torch.allclose(s0[k], ref[k], atol=3e-2), k
+
+
+def _w_zero_roundtrip(rank, world):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.zero import OSS, ShardedDataParallel
+
+    def build():
+        m = _model()
+        opt = OSS(m.parameters(), optim=FusedAdamW, lr=1e-2)
+        return m, opt, ShardedDataParallel(m, opt)
+
+    m, opt, model = build()
+    for s in range(2):
+        x, y = _data(s, world)
+        nn.functional.mse_loss(model(_shard(x, rank, world)), _shard(y, rank, world)).backward()
+        opt.step()
+        model.zero_grad()
+    opt.consolidate_state_dict(0)
+    sd = opt.state_dict() if rank == 0 else None
+    sd = opt.comm.broadcast_object(sd, 0)
+    full = model.full_state_dict()
+    m2, opt2, model2 = build()
+    model2.load_full_state_dict(full)
+    opt2.load_state_dict(sd)
+    for mm, oo, md in ((m, opt, model), (m2, opt2, model2)):
+        x, y = _data(7, world)
+        nn.functional.mse_loss(md(_shard(x, rank, world)), _shard(y, rank, world)).backward()
+        oo.step()
+        md.zero_grad()
+    return [torch.equal(a, b) for a, b in zip(m.parameters(), m2.parameters())]
+
+
+def test_zero_state_roundtrip_continues_identically():
+    for r in run_workers(_w_zero_roundtrip, 2):
+        assert all(r)
+
+
+def _w_zero2_mem(rank, world):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.zero import OSS, ShardedDataParallel
+    torch.manual_seed(0)
+    m = nn.Sequential(*[nn.Linear(64, 64) for _ in range(8)])
+    opt = OSS(m.parameters(), optim=FusedAdamW, lr=1e-3)
+    model = ShardedDataParallel(m, opt, reduce_buffer_size=8192)
+    x = torch.randn(4, 64)
+    model(x).square().mean().backward()
+    held = model.grad_bytes()
+    live = sum(p.grad.numel() * 4 for p in m.parameters() if p.grad is not None)
+    return held, live, sum(p.numel() * 4 for p in m.parameters())
+
+
+def test_zero2_gradient_memory():
+    for held, live, total in run_workers(_w_zero2_mem, 2):
+        assert held <= 0.55 * total, (held, total)
+        assert live <= 0.55 * total, (live, total)

@@ -66,3 +66,76 @@ def test_xgmi_collectives_two_ranks_on_one_gpu():
         rs_ref = sum(t[r * 4096:(r + 1) * 4096] for t in rs_in) / world
         assert torch.allclose(res[r]["rs"], rs_ref, atol=1e-6)
         assert torch.equal(res[r]["comm_sum"], torch.full((4,), 3.0))
+
+
+def _chunked_worker(rank, world):
+    from pytorch_distributedtraining_amd.parallel import Comm
+    torch.cuda.set_device(0)
+    comm = Comm(xgmi=False)
+    x = comm.enable_xgmi(slot_bytes=1 << 20, oneshot_max_bytes=16 << 10)
+    out = {}
+    t = _data(rank, 3 * (1 << 18) + 40, torch.float32, 11).cuda()      # 3 MiB + 160 B: chunks + one-shot tail
+    x.all_reduce(t, "sum")
+    out["ar"] = t.cpu()
+    shard = _data(rank, 5 * (1 << 18) // 2, torch.bfloat16, 12).cuda()  # 1.25 MiB shard, 1 MiB slot
+    full = torch.empty(shard.numel() * world, dtype=shard.dtype, device="cuda")
+    ev = x.all_gather(full, shard, async_op=True)
+    torch.cuda.current_stream().wait_event(ev)
+    out["ag"] = full.float().cpu()
+    inp = _data(rank, 3 * (1 << 17) * world, torch.float32, 13).cuda()   # 1.5 MiB pieces -> 3 windows
+    rs = torch.empty(3 * (1 << 17), device="cuda")
+    x.reduce_scatter(rs, inp, "avg")
+    out["rs"] = rs.cpu()
+    r = _data(rank, (1 << 18) + 64, torch.bfloat16, 14).cuda()
+    keep = r.clone()
+    comm.reduce(r, dst=1, op="sum")
+    out["red"] = r.float().cpu()
+    out["red_keep"] = keep.float().cpu()
+    x.check()
+    x.close()
+    return out
+
+
+def test_xgmi_chunked_collectives_and_reduce():
+    world = 2
+    res = run_workers(_chunked_worker, world)
+    ar = sum(_data(r, 3 * (1 << 18) + 40, torch.float32, 11) for r in range(world))
+    ag = torch.cat([_data(r, 5 * (1 << 18) // 2, torch.bfloat16, 12).float() for r in range(world)])
+    rs_in = [_data(r, 3 * (1 << 17) * world, torch.float32, 13) for r in range(world)]
+    red = sum(_data(r, (1 << 18) + 64, torch.bfloat16, 14).float() for r in range(world))
+    n = 3 * (1 << 17)
+    for r in range(world):
+        assert torch.allclose(res[r]["ar"], ar, atol=1e-5)
+        assert torch.equal(res[r]["ag"], ag)
+        assert torch.allclose(res[r]["rs"], sum(t[r * n:(r + 1) * n] for t in rs_in) / world, atol=1e-6)
+    assert torch.allclose(res[1]["red"], red, atol=3e-2, rtol=1e-2)       # the root holds the sum ...
+    assert torch.equal(res[0]["red"], res[0]["red_keep"])                 # ... the others keep their input
+
+
+def _timeout_worker(rank, world):
+    import time
+    from pytorch_distributedtraining_amd.parallel import Comm
+    torch.cuda.set_device(0)
+    comm = Comm(xgmi=False)
+    x = comm.enable_xgmi(slot_bytes=1 << 20, spin_limit=2000)
+    if rank == 1:
+        time.sleep(3.0)                      # rank 1 is late: rank 0's mesh wait runs out of budget
+    t = torch.ones(4096, device="cuda")
+    x.all_reduce(t, "sum")
+    torch.cuda.synchronize()
+    failed = x.failed()
+    raised = False
+    try:
+        comm.check_errors()
+    except RuntimeError:
+        raised = True
+    nan = bool(torch.isnan(t).any())
+    comm.barrier()
+    x.close()
+    return failed, raised, nan
+
+
+def test_xgmi_timeout_is_loud():
+    (f0, r0, n0), (f1, r1, n1) = run_workers(_timeout_worker, 2)
+    assert f0 != 0 and r0 and n0             # rank 0 timed out: flag set, check raises, output poisoned
+    assert f1 == 0 and not r1 and not n1     # rank 1 found rank 0's signal and completed normally
