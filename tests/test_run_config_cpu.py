@@ -56,5 +56,5 @@ def test_resnet18_ddp_gloo_world2_via_launcher(tmp_path):
     final = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{") and '"world_size"' in ln]
     assert final and final[-1]["world_size"] == 2 and final[-1]["steps"] == 4
     assert final[-1]["loss"] == final[-1]["loss"]          # synced, finite
-    assert glob.glob(str(tmp_path / "ckpt" / "stoke-resnet18_ddp_cpu-backward-step-*.pt"))
+    assert glob.glob(str(tmp_path / "ckpt" / "stoke-resnet18_ddp_cpu-final-backward-step-*.pt"))
     assert os.path.getsize(tmp_path / "m.jsonl") > 0
