@@ -353,8 +353,8 @@ class Trainer:
     # ------------------------------------------------------------------ checkpointing
     def _model_state(self):
         eng = self._engine
-        if hasattr(eng, "sharding_strategy"):           # FSDP: full unflattened fp32 state dict
-            return eng.state_dict()
+        if hasattr(eng, "sharding_strategy"):           # FSDP: full unflattened fp32 state dict, unit by
+            return eng.state_dict(rank0_only=True, offload_to_cpu=True)   # unit to rank 0's host memory
         if hasattr(eng, "full_state_dict"):
             return eng.full_state_dict()
         return self._module.state_dict()
@@ -364,6 +364,8 @@ class Trainer:
         if hasattr(opt, "consolidate_state_dict"):
             opt.consolidate_state_dict(recipient_rank=0)
             return opt.state_dict() if self.rank_ == 0 else None
+        if hasattr(self._engine, "sharding_strategy"):
+            return self._engine.full_optim_state_dict(opt, rank0_only=True, offload_to_cpu=True)
         if hasattr(self._engine, "full_optim_state_dict"):
             return self._engine.full_optim_state_dict(opt)
         return opt.state_dict()

@@ -390,3 +390,29 @@ def test_zero2_gradient_memory():
     for held, live, total in run_workers(_w_zero2_mem, 2):
         assert held <= 0.55 * total, (held, total)
         assert live <= 0.55 * total, (live, total)
+
+
+def _w_fsdp_rank0(rank, world):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.fsdp import FullyShardedDataParallel, MixedPrecision
+    m = _model()
+    f = FullyShardedDataParallel(m, wrap_classes=(nn.Linear,), mixed_precision=MixedPrecision(torch.float32,
+                                                                                          torch.float32), device="cpu")
+    opt = FusedAdamW(f.parameters(), lr=1e-2)
+    x, y = _data(0, world)
+    nn.functional.mse_loss(f(_shard(x, rank, world)), _shard(y, rank, world)).backward()
+    opt.step()
+    full = f.state_dict()
+    r0 = f.state_dict(rank0_only=True, offload_to_cpu=True)
+    o_full = f.full_optim_state_dict(opt)
+    o_r0 = f.full_optim_state_dict(opt, rank0_only=True, offload_to_cpu=True)
+    same = (all(torch.equal(full[k], r0[k]) for k in full) and list(full) == list(r0)) if r0 else None
+    osame = all(torch.equal(o_full["state"][i]["exp_avg"], o_r0["state"][i]["exp_avg"]) for i in o_full["state"]) \
+        if o_r0 else None
+    return len(r0), same, o_r0 is None, osame
+
+
+def test_fsdp_rank0_only_offloaded_state_dicts():
+    (n0, same0, none0, os0), (n1, same1, none1, os1) = run_workers(_w_fsdp_rank0, 2)
+    assert n0 == 6 and same0 and not none0 and os0       # rank 0: the full dicts, on the host
+    assert n1 == 0 and none1                             # rank 1: nothing materialised
