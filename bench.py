@@ -40,6 +40,10 @@ def parse():
     ap.add_argument("--reshard", type=int, default=1, help="FSDP reshard after forward (FULL_SHARD)")
     ap.add_argument("--act-ckpt", type=int, default=0)
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--overlap-probe", type=int, default=1,
+                    help="world > 1: after timing, measure exposed vs communication-only time (untimed)")
+    ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"], help="swinir-stoke precision")
     return ap.parse_args()
 
 
@@ -83,10 +87,15 @@ def main():
         if world > 1:
             dist.init_process_group("gloo")
     else:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # PDT_BENCH_BACKEND=gloo + PDT_XGMI=1 rehearses the multi-rank path on a box with fewer GPUs than
+        # ranks (ranks share devices round-robin; device collectives on the xGMI kernels) -- a plumbing
+        # check, not a measurement: RCCL (the default) needs one GPU per rank.
+        backend = os.environ.get("PDT_BENCH_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank % max(1, ndev))
+        dev = torch.device("cuda", local_rank % max(1, ndev))
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         from pytorch_distributedtraining_amd.ops import _lib
         _lib.require()  # fail loudly if the HIP kernels are missing
     from pytorch_distributedtraining_amd.parallel import Comm
@@ -122,6 +131,8 @@ def timed_loop(step_fn, args, comm, dev):
     comm.barrier()
     torch_cuda.synchronize(dev)
     comm.reset_stats()
+    if dev.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step_fn()
@@ -137,7 +148,62 @@ def timed_loop(step_fn, args, comm, dev):
     comm.all_reduce(t, "max")
     timed_loop.comm = {"collectives_per_step": round(calls / args.steps, 2),
                        "comm_bytes_per_step": int(nbytes / args.steps)}
+    if dev.type == "cuda":
+        timed_loop.comm["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    if comm.world_size > 1 and dev.type == "cuda" and args.overlap_probe:
+        timed_loop.comm.update(overlap_probe(step_fn, comm, dev, float(t.item()) * 1000 / args.steps))
     return float(t.item())
+
+
+def overlap_probe(step_fn, comm, dev, step_ms):
+    """Untimed, after the measurement: (1) one more step with every collective wait bracketed by events on
+    the waiting stream -> exposed (non-overlapped) communication per step; (2) that step's collectives
+    replayed back to back with no compute -> communication-only time; overlap = 1 - exposed / comm-only."""
+    import torch
+    from pytorch_distributedtraining_amd.parallel import comm as C
+    comm.op_log = []
+    C.start_wait_timing()
+    step_fn()
+    exposed = C.stop_wait_timing()
+    ops, comm.op_log = comm.op_log, None
+    bufs = []
+    for op, n, dt, d in ops:
+        kind = op.split(":")[0]
+        if kind == "all_gather":
+            bufs.append((kind, op, torch.empty(n, dtype=dt, device=d), torch.empty(n * comm.world_size, dtype=dt, device=d)))
+        elif kind == "reduce_scatter":
+            bufs.append((kind, op, torch.empty(n // comm.world_size, dtype=dt, device=d), torch.empty(n, dtype=dt, device=d)))
+        else:
+            bufs.append((kind, op, torch.zeros(n, dtype=dt, device=d), None))
+
+    def replay():
+        for kind, op, a, b in bufs:
+            red = op.split(":")[1] if ":" in op else "sum"
+            if kind == "all_gather":
+                comm.all_gather(b, a)
+            elif kind == "reduce_scatter":
+                comm.reduce_scatter(a, b, "avg" if red == "avg" else "sum")
+            elif kind == "all_reduce":
+                comm.all_reduce(a, red)
+            elif kind == "broadcast":
+                comm.broadcast(a, 0)
+            elif kind == "reduce":
+                comm.reduce(a, 0, "sum")
+    replay()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        replay()
+    torch.cuda.synchronize(dev)
+    only = (time.perf_counter() - t0) * 1000 / 3
+    r = torch.tensor([exposed, only], dtype=torch.float64, device=dev)
+    comm.all_reduce(r, "max")
+    exposed, only = float(r[0]), float(r[1])
+    log(f"[bench] comm: exposed {exposed:.2f} ms/step, comm-only {only:.2f} ms/step, step {step_ms:.1f} ms, "
+        f"overlap {100 * max(0.0, 1 - exposed / only) if only > 0 else 0:.1f} %")
+    return {"exposed_comm_ms": round(exposed, 3), "comm_only_ms": round(only, 3),
+            "overlap_pct": round(100 * max(0.0, 1 - exposed / only), 1) if only > 0 else None}
 
 
 def comm_fields(world):
@@ -256,10 +322,15 @@ def bench_resnet(args, comm, dev, world, rank):
 
 def bench_swinir(args, comm, dev, world, rank):
     """The reference's own workload (Stoke-DDP.py:159,169-170,182-254): SwinIR-S x2 through the Stoke-style
-    Trainer with DDP + OSS (ZeRO-1) + ShardedDDP (ZeRO-2), 18 LR 128x128 -> HR 256x256 patches per device,
-    grad_accum 2, AdamW(1e-3, (0.9, 0.99), 1e-8, wd 1e-4), clip-norm 0.1, bf16 autocast; MSE loss
-    (Fairscale-DDP.py:76).  One step = one optimizer step (2 micro-batches)."""
+    Trainer, 18 LR 128x128 -> HR 256x256 patches per device, grad_accum 2, AdamW(1e-3, (0.9, 0.99), 1e-8,
+    wd 1e-4), clip-norm 0.1.  World > 1: DDP + OSS (ZeRO-1) + ShardedDDP (ZeRO-2) exactly as the reference's
+    flags; world 1: no engine is needed (the bf16 compute copy still runs through the DDP flat layout).
+    ``--loss feat`` is the reference's perceptual loss (Stoke-DDP.py:224; random-init feature net, parity
+    unpinned), ``--loss mse`` the Fairscale script's (Fairscale-DDP.py:76).  ``--precision fp32`` is the
+    reference's own precision (fp16=None, Stoke-DDP.py:247); bf16 is this framework's default.
+    One step = one optimizer step (2 micro-batches)."""
     import torch
+    from pytorch_distributedtraining_amd.models.losses import feat_loss
     from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
     from pytorch_distributedtraining_amd.trainer import ClipGradNormConfig, StokeOptimizer, Trainer
     mb = args.micro_batch or 18
@@ -267,10 +338,11 @@ def bench_swinir(args, comm, dev, world, rank):
     model = swinir_s_x2()
     opt = StokeOptimizer(optimizer=torch.optim.AdamW,
                          optimizer_kwargs={"lr": 1e-3, "betas": (0.9, 0.99), "eps": 1e-8, "weight_decay": 1e-4})
-    tr = Trainer(model, optimizer=opt, loss=torch.nn.functional.mse_loss, batch_size_per_device=mb,
+    loss_fn = feat_loss if args.loss == "feat" else torch.nn.functional.mse_loss
+    tr = Trainer(model, optimizer=opt, loss=loss_fn, batch_size_per_device=mb,
                  grad_accum_steps=accum, grad_clip=ClipGradNormConfig(max_norm=0.1, norm_type=2.0), gpu=True,
-                 fp16="bf16", distributed="ddp" if world > 1 else None, fairscale_oss=world > 1,
-                 fairscale_sddp=world > 1, verbose=False, comm=comm)
+                 fp16=None if args.precision == "fp32" else "bf16", distributed="ddp" if world > 1 else None,
+                 fairscale_oss=world > 1, fairscale_sddp=world > 1, verbose=False, comm=comm)
     g = torch.Generator(device=dev)
     g.manual_seed(2000 + rank)
     data = [(torch.rand(mb, 3, 128, 128, device=dev, generator=g), torch.rand(mb, 3, 256, 256, device=dev, generator=g))
@@ -284,13 +356,15 @@ def bench_swinir(args, comm, dev, world, rank):
 
     dt = timed_loop(step, args, comm, dev)
     sps = world * mb * accum * args.steps / dt
-    return {"metric": "samples/sec SwinIR-S x2 Stoke DDP+OSS+SDDP (whole node)", "value": round(sps, 2),
+    par = "dp{}+oss+sddp".format(world) if world > 1 else "dp1"
+    return {"metric": "samples/sec SwinIR-S x2 Stoke (whole node)", "value": round(sps, 2),
             "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-            **comm_fields(world), "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            **comm_fields(world), "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"model": "swinir-s-x2", "global_batch": world * mb * accum, "seq_len": None,
-                       "parallelism": f"dp{world}+zero2" if world > 1 else "dp1", "image": "3x128x128->3x256x256",
-                       "grad_accum": accum}}
+                       "parallelism": par, "image": "3x128x128->3x256x256", "grad_accum": accum,
+                       "loss": "feat_loss (perceptual)" if args.loss == "feat" else "mse",
+                       "compute_copy": tr.compute_dtype is not None}}
 
 
 if __name__ == "__main__":

@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--ckpt-dir", default="checkpoint/")
     p.add_argument("--metrics", default="runs/stoke_ddp_metrics.jsonl")
     p.add_argument("--wandb", action="store_true")
+    p.add_argument("--pretrained", default=None,
+                   help="SwinIR checkpoint to start from, e.g. model_zoo/002_lightweightSR_DIV2K_s64w8_SwinIR-S_x2.pth "
+                        "({'params': sd} or a raw state dict, strict key match; Stoke-DDP.py:209-213)")
     return p.parse_args()
 
 
@@ -108,6 +111,9 @@ def main():
     oss_config = FairscaleOSSConfig(broadcast_fp16=True)
 
     model = swinir_s_x2()
+    if opt.pretrained:
+        # every rank reads the file before the engines sync rank 0's weights (weights_only: no pickle exec)
+        ckpt.load_pretrained(model, opt.pretrained, key="params", strict=True)
     optimizer = StokeOptimizer(optimizer=torch.optim.AdamW,
                                optimizer_kwargs={"lr": opt.lr, "betas": (0.9, 0.99), "eps": 1e-8,
                                                  "weight_decay": opt.weight_decay})

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
+from ..ops.embedding import Embedding
 from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 
@@ -108,7 +109,7 @@ class GPT2LMHeadModel(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
         self.config = cfg
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wte = Embedding(cfg.vocab_size, cfg.n_embd)
         self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
         self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)

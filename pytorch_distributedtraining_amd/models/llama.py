@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import apply_rope, cross_entropy, flash_attn, rope_tables, swiglu
+from ..ops.embedding import Embedding
 from ..ops.linear import Linear
 from ..ops.norms import RMSNorm
 
@@ -103,7 +104,7 @@ class Llama(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.config = cfg
-        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.tok_embeddings = Embedding(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList([LlamaBlock(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.output = Linear(cfg.dim, cfg.vocab_size, bias=False)

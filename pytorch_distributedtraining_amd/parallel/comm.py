@@ -28,6 +28,27 @@ _DT_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 
             torch.uint8: 5, torch.float64: 6}
 
 
+# Exposed-communication probe (bench.py / StepTimer users): while a list is installed, every device-side
+# wait records an event pair on the WAITING stream; the GPU time between them is the time that stream
+# stalled on communication (zero when the collective already finished under earlier compute).
+_WAIT_EVENTS = None
+
+
+def start_wait_timing():
+    global _WAIT_EVENTS
+    _WAIT_EVENTS = []
+
+
+def stop_wait_timing() -> float:
+    """Stop recording; return the summed compute-stream stall (ms) of the waits seen (synchronises)."""
+    global _WAIT_EVENTS
+    evs, _WAIT_EVENTS = _WAIT_EVENTS or [], None
+    if not evs:
+        return 0.0
+    torch.cuda.synchronize()
+    return float(sum(a.elapsed_time(b) for a, b in evs))
+
+
 class Handle:
     """Async work handle; ``wait()`` orders the current stream after the collective (no host sync for
     device collectives: a c10d work's wait, or a stream wait on the xGMI comm stream's event)."""
@@ -41,10 +62,19 @@ class Handle:
     def wait(self):
         if self._done:
             return
+        timed = _WAIT_EVENTS is not None and (self._work is not None or self._event is not None) \
+            and torch.cuda.is_available()
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         if self._work is not None:
             self._work.wait()
         if self._event is not None:
             torch.cuda.current_stream().wait_event(self._event)
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _WAIT_EVENTS.append((e0, e1))
         if self._post is not None:
             self._post()
         self._done = True
@@ -79,11 +109,12 @@ class Comm:
                 os.environ.get("TORCH_DISTRIBUTED_DEBUG", "").upper() == "DETAIL"
         self.debug = debug
         self.stats = {"calls": 0, "bytes": 0}
+        self.op_log = None       # list of (op, numel, dtype, device) while recording (bench comm-only replay)
         rt = runtime()
         self.tracer = rt.CollectiveTracer(4096) if rt is not None else None
         self.xgmi = None
         if xgmi is None:
-            xgmi = os.environ.get("PDT_XGMI", "0") == "1" and self.backend == "nccl"
+            xgmi = os.environ.get("PDT_XGMI", "0") == "1"
         if xgmi and self.world_size > 1 and torch.cuda.is_available():
             from ..run_config import xgmi_kwargs
             self.enable_xgmi(**xgmi_kwargs())
@@ -111,6 +142,8 @@ class Comm:
         (``stats``: collective calls and full-payload bytes, read by bench.py per step)."""
         self.stats["calls"] += 1
         self.stats["bytes"] += t.numel() * t.element_size() if nbytes is None else nbytes
+        if self.op_log is not None:
+            self.op_log.append((op, t.numel(), t.dtype, t.device))
         if self.tracer is not None:
             self.tracer.record(op, list(t.shape), _DT_CODE.get(t.dtype, 99))
 

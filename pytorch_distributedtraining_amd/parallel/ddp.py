@@ -25,6 +25,7 @@ from contextlib import contextmanager
 import torch
 import torch.nn as nn
 
+from ..utils import profiling as prof
 from ..utils.native import require_runtime
 from .comm import Comm, default_comm
 
@@ -268,6 +269,10 @@ class DistributedDataParallel(nn.Module):
         view = g.bucket_views[vi]
         if self.comm.world_size == 1:
             return
+        with prof.range(f"ddp.all_reduce[bucket {bid}]"):
+            self._launch_bucket(view)
+
+    def _launch_bucket(self, view):
         if self.reduce_dtype is not None and self.reduce_dtype != view.dtype:
             payload = view.to(self.reduce_dtype)
             h = self.comm.all_reduce(payload, "avg", async_op=True)

@@ -32,6 +32,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 
+from ..utils import profiling as prof
 from ..utils.native import require_runtime
 from .comm import Comm, default_comm
 
@@ -138,7 +139,8 @@ class _Unit:
         if self.state != self.SHARDED:
             return
         self._alloc_full()
-        self.handle = self.comm.all_gather(self._comm_buf, self.lp_shard, async_op=True)
+        with prof.range(f"fsdp.all_gather[{self.name or 'root'}]"):
+            self.handle = self.comm.all_gather(self._comm_buf, self.lp_shard, async_op=True)
         self.state = self.GATHERING
 
     def wait(self):
@@ -179,7 +181,8 @@ class _Unit:
                 self.pending.append((None, grad))
             else:
                 out = torch.empty(self.shard_numel, dtype=self.mp.reduce_dtype, device=grad.device)
-                h = self.comm.reduce_scatter(out, grad, op="avg", async_op=True)
+                with prof.range(f"fsdp.reduce_scatter[{self.name or 'root'}]"):
+                    h = self.comm.reduce_scatter(out, grad, op="avg", async_op=True)
                 self.pending.append((h, out))
         # params are not needed again until the next forward (which re-gathers the updated shard)
         self.reshard()

@@ -40,6 +40,7 @@ import torch.nn as nn
 from torch.optim import Optimizer
 
 from ..optim.clip import clip_grad_norm_
+from ..utils import profiling as prof
 from ..utils.native import require_runtime
 from .comm import Comm, default_comm
 from .ddp import sync_buffers
@@ -186,6 +187,10 @@ class OSS(Optimizer):
 
     def _exchange(self):
         """Owners -> everyone: ONE all-gather per bank of the owners' (payload) segments."""
+        with prof.range("oss.all_gather"):
+            self._exchange_banks()
+
+    def _exchange_banks(self):
         for bank in self._banks:
             if bank.master_flat is not None and not self._fused:
                 for li, m in bank.masters.items():          # non-fused optimizer: write the compute copy here
@@ -464,6 +469,10 @@ class ShardedDataParallel(nn.Module):
         return torch.cat(pieces) if len(pieces) > 1 else pieces[0].clone()
 
     def _launch(self, b):
+        with prof.range(f"sddp.{self.reduce_mode}[bucket {b}]"):
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b):
         bank, owner, start, n, lidx = self._buckets[b]
         if self.reduce_mode == "all_reduce":
             buf = self._grad[id(bank)][start:start + n]

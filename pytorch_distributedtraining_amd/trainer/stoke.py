@@ -79,7 +79,7 @@ class Trainer:
         if self.distributed is not None:
             backend = self.ddp_config.backend if self.gpu else "gloo"
             if self.ddp_config.local_rank is not None and self.gpu:
-                torch.cuda.set_device(int(self.ddp_config.local_rank))
+                torch.cuda.set_device(int(self.ddp_config.local_rank) % torch.cuda.device_count())
             self.rank_, self.world_size_, self.device = init_distributed(backend, self.ddp_config.timeout_s)
             if not self.gpu:
                 self.device = torch.device("cpu")

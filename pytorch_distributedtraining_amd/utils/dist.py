@@ -41,6 +41,10 @@ def init_distributed(backend: str | None = None, timeout_s: float = 1800.0, rank
     rank = env_int("RANK", 0) if rank is None else rank
     lr = local_rank()
     use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if torch.cuda.is_available() and lr >= torch.cuda.device_count():
+        # more local ranks than devices: ranks share GPUs round-robin (the 1-GPU rehearsal of a multi-rank
+        # run over gloo + the xGMI kernels); RCCL itself refuses two ranks on one device, loudly
+        lr = lr % torch.cuda.device_count()
     device = torch.device("cuda", lr) if use_gpu else torch.device("cpu")
     if use_gpu and device_bind:
         torch.cuda.set_device(device)

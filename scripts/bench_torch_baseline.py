@@ -252,12 +252,18 @@ def swinir_stoke(a, dev, world, rank):
     data = [(torch.rand(mb, 3, 128, 128, device=dev, generator=g), torch.rand(mb, 3, 256, 256, device=dev, generator=g))
             for _ in range(accum)]
 
+    if a.loss == "feat":
+        from pytorch_distributedtraining_amd.models.losses import PerceptualLoss   # stock nn.Conv2d / ReLU / MaxPool
+        crit = PerceptualLoss().to(dev)
+    else:
+        crit = lambda o, t: F.mse_loss(o.float(), t)   # noqa: E731
+
     def step(i):
         for j, (x, y) in enumerate(data):
             ctx = ddp.no_sync() if j < accum - 1 else contextlib.nullcontext()
             with ctx:
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    loss = F.mse_loss(ddp(x).float(), y) / accum
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.precision == "bf16"):
+                    loss = crit(ddp(x), y) / accum
                 loss.backward()
         torch.nn.utils.clip_grad_norm_(ddp.parameters(), 0.1)
         opt.step()
@@ -271,7 +277,8 @@ def swinir_stoke(a, dev, world, rank):
         print(json.dumps({"metric": "samples/sec SwinIR-S x2 DDP (whole node) -- stock PyTorch-ROCm baseline",
                           "value": round(sps, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
                           "ms_per_step": round(1000 * dt / a.steps, 3), "micro_batch_per_gpu": mb,
-                          "stack": "torch DDP + autocast bf16 + SDPA + nn.LayerNorm + fused torch AdamW"}))
+                          "loss": a.loss, "dtype": a.precision,
+                          "stack": "torch DDP + autocast + SDPA + nn.LayerNorm + fused torch AdamW"}))
 
 
 def timed(step, a, dev):
@@ -299,6 +306,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--loss", default="feat", choices=["feat", "mse"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

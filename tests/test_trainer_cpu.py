@@ -111,3 +111,23 @@ def test_distributed_trainer_reference_combination(tmp_path):
     payload = torch.load(os.path.join(tmp_path, tag + ".pt"), weights_only=True)
     assert sorted(payload["optimizer_state_dict"]["state"]) == list(range(6))
     assert payload["stoke_status"]["oss"] and payload["stoke_status"]["effective_batch_size"] == 8
+
+
+def test_stoke_example_pretrained_flag(tmp_path):
+    """examples/stoke_ddp.py --pretrained: the reference's strict pretrained import (Stoke-DDP.py:209-213)."""
+    import subprocess
+    import sys
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    torch.manual_seed(5)
+    torch.save({"params": swinir_s_x2().state_dict()}, tmp_path / "pre.pth")
+    torch.save({"params": {"bogus.weight": torch.zeros(1)}}, tmp_path / "bad.pth")
+    base = [sys.executable, os.path.join(root, "examples", "stoke_ddp.py"), "--cpu", "--samples", "8", "--lr-size", "16",
+            "--batchSize", "2", "--nEpochs", "1", "--ckpt-dir", str(tmp_path / "ck"), "--metrics", str(tmp_path / "m.jsonl")]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    ok = subprocess.run(base + ["--pretrained", str(tmp_path / "pre.pth")], capture_output=True, text=True, env=env,
+                        timeout=300)
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    bad = subprocess.run(base + ["--pretrained", str(tmp_path / "bad.pth")], capture_output=True, text=True, env=env,
+                         timeout=300)
+    assert bad.returncode != 0 and "Missing key" in bad.stderr
