@@ -206,24 +206,30 @@ __global__ __launch_bounds__(NT) void swiglu_bwd_kernel(const T* __restrict__ dy
   }
 }
 
-// RoPE (rotate-half): x viewed as [rows = B*S*H, D] with row r at position s = (r / H) % S + pos0.
+// RoPE (rotate-half): rows = B*S*H head vectors, row r at position s = (r / H) % S + pos0.
 // out[i] = x[i] c - x[i+D/2] s_ ; out[i+D/2] = x[i+D/2] c + x[i] s_   (sign = -1 for backward).
-// cos/sin tables: [S_max, D/2] fp32.  Handles a row stride so q and k can be rotated in place
-// inside a fused qkv buffer.
+// cos/sin tables: [S_max, D/2] fp32.
+// A "row" is one head vector: row r = (position r / H, head r % H) lives at
+// (r / H) * pos_stride + (r % H) * head_stride, so the q and k heads of a packed [B, S, H + 2 Hkv, D] qkv
+// projection are rotated IN PLACE (y == x, H = Hq + Hkv) and a plain [B, S, H, D] tensor is the
+// pos_stride == H * head_stride case.  Each thread reads both halves before writing them: in-place safe.
 template <typename T>
-__global__ __launch_bounds__(NT) void rope_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
-                                                  int64_t row_stride_in, int64_t row_stride_out, int H, int S,
-                                                  int D, int pos0, const float* __restrict__ cosb,
-                                                  const float* __restrict__ sinb, float sign) {
+__global__ __launch_bounds__(NT) void rope_kernel(const T* x, T* y, int64_t rows,   // x may alias y
+                                                  int64_t head_in, int64_t pos_in, int64_t head_out,
+                                                  int64_t pos_out, int H, int S, int D, int pos0,
+                                                  const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                  float sign) {
   const int half = D / 2, h8 = half / 8;
   const int64_t n = rows * h8;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const int64_t r = i / h8;
     const int j = (int)(i % h8) * 8;
-    const int s = (int)((r / H) % S) + pos0;
+    const int64_t pr = r / H, hr = r % H;
+    const int s = (int)(pr % S) + pos0;
+    const int64_t xi = pr * pos_in + hr * head_in, yi = pr * pos_out + hr * head_out;
     float a[8], b[8], c[8], sn[8], o1[8], o2[8];
-    Vec8<T>::load(x + r * row_stride_in + j, a);
-    Vec8<T>::load(x + r * row_stride_in + half + j, b);
+    Vec8<T>::load(x + xi + j, a);
+    Vec8<T>::load(x + xi + half + j, b);
     Vec8<float>::load(cosb + (int64_t)s * half + j, c);
     Vec8<float>::load(sinb + (int64_t)s * half + j, sn);
 #pragma unroll
@@ -232,8 +238,8 @@ __global__ __launch_bounds__(NT) void rope_kernel(const T* __restrict__ x, T* __
       o1[k] = a[k] * c[k] - b[k] * ss;
       o2[k] = b[k] * c[k] + a[k] * ss;
     }
-    Vec8<T>::store(y + r * row_stride_out + j, o1);
-    Vec8<T>::store(y + r * row_stride_out + half + j, o2);
+    Vec8<T>::store(y + yi + j, o1);
+    Vec8<T>::store(y + yi + half + j, o2);
   }
 }
 
@@ -411,17 +417,18 @@ PDT_API int pdt_swiglu_bwd(const void* dy, const void* x, void* dx, int64_t rows
   return (int)hipGetLastError();
 }
 
-PDT_API int pdt_rope(const void* x, void* y, int64_t rows, int64_t stride_in, int64_t stride_out, int H, int S, int D,
-                     int pos0, const float* cosb, const float* sinb, int backward, int dt, hipStream_t st) {
-  if ((D / 2) % 8) return (int)hipErrorInvalidValue;
+PDT_API int pdt_rope(const void* x, void* y, int64_t rows, int64_t head_in, int64_t pos_in, int64_t head_out,
+                     int64_t pos_out, int H, int S, int D, int pos0, const float* cosb, const float* sinb, int backward,
+                     int dt, hipStream_t st) {
+  if ((D / 2) % 8 || H <= 0) return (int)hipErrorInvalidValue;
   const int grid = grid_for(rows * (D / 16), NT, 256 * 16);
   const float sign = backward ? -1.f : 1.f;
   if (dt == kBF16)
-    rope_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, (bf16_t*)y, rows, stride_in, stride_out, H, S, D, pos0,
-                                             cosb, sinb, sign);
+    rope_kernel<bf16_t><<<grid, NT, 0, st>>>((const bf16_t*)x, (bf16_t*)y, rows, head_in, pos_in, head_out, pos_out,
+                                             H, S, D, pos0, cosb, sinb, sign);
   else
-    rope_kernel<float><<<grid, NT, 0, st>>>((const float*)x, (float*)y, rows, stride_in, stride_out, H, S, D, pos0,
-                                            cosb, sinb, sign);
+    rope_kernel<float><<<grid, NT, 0, st>>>((const float*)x, (float*)y, rows, head_in, pos_in, head_out, pos_out,
+                                            H, S, D, pos0, cosb, sinb, sign);
   return (int)hipGetLastError();
 }
 

@@ -16,7 +16,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import apply_rope, cross_entropy, flash_attn, rope_tables, swiglu
+from ..ops import cross_entropy, rope_tables, swiglu
+from ..ops.attention import flash_attn_gqa_packed
+from ..ops.rope import apply_rope_qk_
 from ..ops.embedding import Embedding
 from ..ops.linear import Linear
 from ..ops.norms import RMSNorm
@@ -62,11 +64,12 @@ class Attention(nn.Module):
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
-        qkv = self.wqkv(x).view(B, S, self.h + 2 * self.hkv, self.d)
-        q = apply_rope(qkv[:, :, : self.h], cos, sin)
-        k = apply_rope(qkv[:, :, self.h: self.h + self.hkv], cos, sin)
-        v = qkv[:, :, self.h + self.hkv:]
-        o = flash_attn(q, k, v, causal=True)
+        qkv = apply_rope_qk_(self.wqkv(x), self.h, self.hkv, self.d, cos, sin)
+        qkv = qkv.view(B, S, self.h + 2 * self.hkv, self.d)
+        # RoPE rotates the q and k heads of the packed projection in place and the packed GQA flash attention
+        # reads q / k / v as head ranges of it (and writes ONE packed gradient): no separate rotated q / k
+        # tensors and no gradient scatter into the packed layout
+        o = flash_attn_gqa_packed(qkv, self.h, self.hkv, causal=True)
         return self.wo(o.reshape(B, S, self.h * self.d))
 
 

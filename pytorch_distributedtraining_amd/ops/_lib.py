@@ -50,8 +50,8 @@ _SIGS = {
     "pdt_bias_gelu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_swiglu_fwd": [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
-    "pdt_rope": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                 c_int, c_int, c_void_p],
+    "pdt_rope": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int,
+                 c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_fp8_quant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_fp8_dequant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p],
     "pdt_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],

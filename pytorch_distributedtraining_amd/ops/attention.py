@@ -92,6 +92,37 @@ class _FlashAttnPackedFn(torch.autograd.Function):
         return dqkv, None, None
 
 
+class _FlashAttnGQAPackedFn(torch.autograd.Function):
+    """q, k, v as head ranges of one [B, S, Hq + 2 Hkv, D] projection; backward writes the packed gradient."""
+
+    @staticmethod
+    def forward(ctx, qkv, hq, hkv, causal, scale):
+        _check(qkv, "qkv")
+        q, k, v = qkv[:, :, :hq], qkv[:, :, hq:hq + hkv], qkv[:, :, hq + hkv:]
+        o, lse = _fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.hq, ctx.hkv, ctx.causal, ctx.scale = hq, hkv, causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        hq, hkv = ctx.hq, ctx.hkv
+        d = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        _bwd(qkv[:, :, :hq], qkv[:, :, hq:hq + hkv], qkv[:, :, hq + hkv:], o, lse, do, d[:, :, :hq],
+             d[:, :, hq:hq + hkv], d[:, :, hq + hkv:], ctx.causal, ctx.scale)
+        return d, None, None, None, None
+
+
+def flash_attn_gqa_packed(qkv, n_q_heads: int, n_kv_heads: int, causal: bool = True, scale: float | None = None):
+    """qkv [B, S, Hq + 2 Hkv, D] (q heads, then k, then v) -> o [B, S, Hq, D]; GQA (Hq % Hkv == 0)."""
+    scale = 1.0 / math.sqrt(qkv.shape[-1]) if scale is None else scale
+    hq, hkv = n_q_heads, n_kv_heads
+    if not qkv.is_cuda:
+        return _reference(qkv[:, :, :hq], qkv[:, :, hq:hq + hkv], qkv[:, :, hq + hkv:], causal, scale)
+    return _FlashAttnGQAPackedFn.apply(qkv, hq, hkv, causal, scale)
+
+
 def _reference(q, k, v, causal, scale):
     # [B, S, H, D] -> [B, H, S, D]; GQA by repeating kv heads
     H, Hkv = q.shape[2], k.shape[2]

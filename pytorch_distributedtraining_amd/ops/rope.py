@@ -29,10 +29,12 @@ def _rope_ref(x, cos, sin, pos0, sign):
     return torch.cat([a * c - b * s, b * c + a * s], dim=-1).to(x.dtype)
 
 
-def _launch(x, y, cos, sin, pos0, backward):
-    B, S, H, D = x.shape
-    _lib.call("pdt_rope", x.data_ptr(), y.data_ptr(), B * S * H, x.stride(2), y.stride(2), H, S, D, int(pos0),
-              cos.data_ptr(), sin.data_ptr(), 1 if backward else 0, _lib.dtype_code(x.dtype),
+def _launch(x, y, cos, sin, pos0, backward, heads=None):
+    """Rotate heads [0, heads) of every position of x [B, S, Hx, D] into y (y may be x: in place)."""
+    B, S, Hx, D = x.shape
+    H = Hx if heads is None else heads
+    _lib.call("pdt_rope", x.data_ptr(), y.data_ptr(), B * S * H, x.stride(2), x.stride(1), y.stride(2), y.stride(1),
+              H, S, D, int(pos0), cos.data_ptr(), sin.data_ptr(), 1 if backward else 0, _lib.dtype_code(x.dtype),
               _lib.stream_handle(x.device))
 
 
@@ -75,3 +77,54 @@ def apply_rope(x, cos, sin, pos0: int = 0):
         raise ValueError(f"apply_rope: tables {tuple(cos.shape)} do not cover positions {pos0}..{pos0 + x.shape[1]}"
                          f" x head_dim/2={D // 2}")
     return _RopeFn.apply(x, cos, sin, pos0)
+
+
+def _tables_f32(cos, sin):
+    if cos.dtype != torch.float32 or not cos.is_contiguous():
+        cos = cos.float().contiguous()
+    if sin.dtype != torch.float32 or not sin.is_contiguous():
+        sin = sin.float().contiguous()
+    return cos, sin
+
+
+class _RopeQKInplaceFn(torch.autograd.Function):
+    """RoPE on the q and k heads of a packed [B, S, (Hq + 2 Hkv) * D] projection output, in place; backward
+    applies the inverse rotation in place on the packed gradient.  No separate q / k tensors exist in either
+    direction, and the packed flash attention consumes the result (and produces the packed gradient).
+    The projection output itself (not a view of it) is modified, so autograd needs no CopySlices copy."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, heads, head_dim, pos0):
+        ctx.mark_dirty(qkv)
+        B, S = qkv.shape[0], qkv.shape[1]
+        x4 = qkv.view(B, S, -1, head_dim)
+        _launch(x4, x4, cos, sin, pos0, backward=False, heads=heads)
+        ctx.save_for_backward(cos, sin)
+        ctx.heads, ctx.pos0, ctx.head_dim = heads, pos0, head_dim
+        return qkv
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        cos, sin = ctx.saved_tensors
+        dqkv = dqkv.contiguous()
+        B, S = dqkv.shape[0], dqkv.shape[1]
+        d4 = dqkv.view(B, S, -1, ctx.head_dim)
+        _launch(d4, d4, cos, sin, ctx.pos0, backward=True, heads=ctx.heads)
+        return dqkv, None, None, None, None, None
+
+
+def apply_rope_qk_(qkv, n_q_heads: int, n_kv_heads: int, head_dim: int, cos, sin, pos0: int = 0):
+    """In place: rotate the q and k heads (the first ``n_q_heads + n_kv_heads`` of ``head_dim`` each) of the
+    packed projection ``qkv`` [B, S, (Hq + 2 Hkv) * head_dim]; returns it (CPU: a rotated copy)."""
+    D = head_dim
+    heads = n_q_heads + n_kv_heads
+    if not qkv.is_cuda or (D // 2) % 8 != 0 or qkv.dtype not in (torch.float32, torch.bfloat16) or \
+            not qkv.is_contiguous():
+        B, S = qkv.shape[0], qkv.shape[1]
+        x4 = qkv.reshape(B, S, -1, D)
+        qk = _rope_ref(x4[:, :, :heads], cos, sin, pos0, 1.0)
+        return torch.cat([qk, x4[:, :, heads:]], dim=2).reshape(qkv.shape)
+    cos, sin = _tables_f32(cos, sin)
+    if cos.shape[0] < pos0 + qkv.shape[1] or cos.shape[1] != D // 2:
+        raise ValueError("apply_rope_qk_: tables do not cover the sequence / head_dim")
+    return _RopeQKInplaceFn.apply(qkv, cos, sin, heads, D, pos0)

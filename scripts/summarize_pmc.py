@@ -1,5 +1,15 @@
 #!/usr/bin/env python
-"""Per-kernel PMC summary of rocprofv3 --pmc runs (one directory per counter pass) for the hand kernels."""
+"""Per-kernel PMC summary of rocprofv3 --pmc runs (one directory per counter pass) for the hand kernels.
+
+MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 128): the MFMA counter sums busy cycles
+(32 per v_mfma_f32_32x32x16_bf16) over all 1,024 SIMDs, while rocprofv3 reports GRBM_GUI_ACTIVE summed over
+the 8 XCDs -- so GRBM/8 is the kernel's cycle count and 1,024 x GRBM/8 = 128 x GRBM the SIMD-cycles
+available (MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units" and "DVFS give-back").  A value of 1.0
+means every SIMD issued MFMAs back to back for the whole dispatch.
+
+    python scripts/summarize_pmc.py gpurun_out                # pmc_* pass directories
+    python scripts/summarize_pmc.py --from-summary old.txt    # re-derive from a summary's raw= fields
+"""
 import csv
 import glob
 import os
@@ -21,7 +31,30 @@ def load(d):
     return acc
 
 
+SIMD_CYCLES_PER_GRBM = 128     # 1,024 SIMDs / 8 XCDs (GRBM_GUI_ACTIVE is summed over the XCDs)
+
+
+def derived(c):
+    out = []
+    if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+        out.append(f"MFMA_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (SIMD_CYCLES_PER_GRBM * c['GRBM_GUI_ACTIVE']):.3f}")
+    return out
+
+
+def from_summary(path):
+    for ln in open(path):
+        if "raw=" not in ln:
+            continue
+        name = ln.split(" | ")[0]
+        raw = dict(kv.split("=") for kv in ln.split("raw=")[1].strip().split(", "))
+        c = {k: float(v) for k, v in raw.items()}
+        print(" | ".join([name] + derived(c) + [f"raw=MFMA_BUSY={c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0):.3g}, "
+                                                 f"GRBM_GUI_ACTIVE={c.get('GRBM_GUI_ACTIVE', 0):.3g}"]))
+
+
 def main():
+    if sys.argv[1] == "--from-summary":
+        return from_summary(sys.argv[2])
     out = sys.argv[1]
     merged = defaultdict(dict)
     for d in sorted(glob.glob(os.path.join(out, "pmc_*"))):
@@ -31,8 +64,7 @@ def main():
     for k in sorted(merged):
         c = merged[k]
         line = [k]
-        if c.get("SQ_BUSY_CYCLES") and c.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
-            line.append(f"MFMA_busy/SQ_busy={c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(1.0, c['SQ_BUSY_CYCLES']):.3f}")
+        line.extend(derived(c))
         if c.get("SQ_INSTS_LDS"):
             line.append(f"LDS_bank_conflict_cycles/LDS_inst={c.get('SQ_LDS_BANK_CONFLICT', 0) / c['SQ_INSTS_LDS']:.3f}")
         if c.get("SQ_WAVE_CYCLES"):

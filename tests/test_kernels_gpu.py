@@ -817,3 +817,28 @@ def test_graphed_ddp_gpt2_step_with_large_vocab():
         if se[k].dim() >= 2:
             d = (se[k].float() - sg[k].float()).abs()
             assert d.mean().item() < 5e-5, (k, d.mean().item())
+
+
+def test_llama_packed_rope_gqa_attention_matches_unfused():
+    """Llama attention: in-place RoPE on the packed qkv projection + packed GQA flash attention (one packed
+    gradient) vs the unfused path (separate rotated q / k tensors, flash_attn on views), fwd and bwd."""
+    from pytorch_distributedtraining_amd.models.llama import Attention, llama_config
+    from pytorch_distributedtraining_amd.ops import apply_rope, flash_attn, rope_tables
+    torch.manual_seed(0)
+    cfg = llama_config("llama3-tiny", dim=512, n_heads=4, n_kv_heads=2)           # head_dim 128, GQA 2:1
+    att = Attention(cfg).to(DEV).to(torch.bfloat16)
+    cos, sin = rope_tables(cfg.head_dim, 512, device=DEV)
+    x = torch.randn(2, 256, 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(2, 256, 512, device=DEV, dtype=torch.bfloat16)
+    (att(x, cos, sin) * g).sum().backward()
+    gx, gw = x.grad.clone(), att.wqkv.weight.grad.clone()
+    x.grad = None
+    att.wqkv.weight.grad = None
+    B, S, h, hkv, d = 2, 256, 4, 2, 128
+    qkv = att.wqkv(x).view(B, S, h + 2 * hkv, d)
+    q = apply_rope(qkv[:, :, :h], cos, sin)
+    k = apply_rope(qkv[:, :, h:h + hkv], cos, sin)
+    o = flash_attn(q, k, qkv[:, :, h + hkv:], causal=True)
+    (att.wo(o.reshape(B, S, h * d)) * g).sum().backward()
+    assert rel_err(gx, x.grad) < 2e-3
+    assert rel_err(gw, att.wqkv.weight.grad) < 2e-3
