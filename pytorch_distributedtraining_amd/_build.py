@@ -84,7 +84,10 @@ def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
             for f in futs:
                 f.result()
     if _newer(KERNEL_LIB, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", KERNEL_LIB], verbose)
+        # hipBLASLt (epilogue GEMMs, blaslt.hip): resolves at run time to the copy torch already mapped
+        # (same soname libhipblaslt.so.1), like libamdhip64
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", KERNEL_LIB,
+              "-L/opt/rocm/lib", "-lhipblaslt"], verbose)
         _check_no_missing_stubs(KERNEL_LIB)
     return KERNEL_LIB
 

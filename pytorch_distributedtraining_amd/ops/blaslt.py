@@ -1,0 +1,47 @@
+"""hipBLASLt GEMMs with fused epilogues, called directly (csrc/kernels/blaslt.hip): per-shape plans, the
+fastest of hipBLASLt's heuristic candidates picked by timing on a shape's first uncaptured call.
+
+Used for the Linear weight gradient with the bias gradient reduced inside the same GEMM (epilogue BGRADB):
+dW = dY^T X and db = colsum(dY) read dY once instead of twice, and the separate column-sum launches
+(2 per biased Linear per step) disappear.  The probe in scripts/probe_lt_epilogues.py
+(profiles/r2_hipblaslt_epilogue_probe.txt) shows which epilogues this hipBLASLt build has gfx950 algorithms
+for: BIAS, GELU_BIAS and BGRADB (with B transposed) yes; GELU_AUX_BIAS, DGELU and DGELU_BGRAD no -- so the
+GELU stays in the framework's own bias-GELU kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+EPI_NONE, EPI_BIAS, EPI_BGRADB = 0, 1, 6
+_UNSUPPORTED: set = set()
+TUNE = True
+
+
+def lt_matmul(epi: int, trans: int, m: int, n: int, k: int, a, b, d, bias=None) -> bool:
+    """Column-major D[m, n] = op(A) op(B) (trans bit 0: A^T, bit 1: B^T) with an epilogue; False if hipBLASLt
+    has no algorithm for the combination (cached; the caller falls back)."""
+    key = (epi, trans, m, n, k, d.dtype, None if bias is None else bias.dtype)
+    if key in _UNSUPPORTED:
+        return False
+    rc = _lib.require().pdt_lt_matmul(epi, trans, m, n, k, a.data_ptr(), b.data_ptr(), d.data_ptr(), _lib.ptr(bias),
+                                      _lib.dtype_code(bias.dtype) if bias is not None else 0, 0,
+                                      _lib.dtype_code(d.dtype), 1 if TUNE else 0, _lib.stream_handle(d.device))
+    if rc == -3:
+        _UNSUPPORTED.add(key)
+        return False
+    _lib.check(rc, "pdt_lt_matmul")
+    return True
+
+
+def wgrad_bgrad(dy2: torch.Tensor, x2: torch.Tensor):
+    """(dW [N, K], db [N]) = (dY^T X, colsum dY) for contiguous bf16 dY [M, N], X [M, K] in ONE GEMM, or None."""
+    m_rows, n = dy2.shape
+    k = x2.shape[1]
+    dw = torch.empty(n, k, dtype=dy2.dtype, device=dy2.device)
+    db = torch.empty(n, dtype=dy2.dtype, device=dy2.device)
+    # column-major: dW^T[K, N] = X^T(op N on col-major [K, M]) . dY(col-major [N, M], op T)
+    if not lt_matmul(EPI_BGRADB, 2, k, n, m_rows, x2, dy2, dw, db):
+        return None
+    return dw, db

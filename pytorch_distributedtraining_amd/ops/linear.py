@@ -15,12 +15,15 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
 from .activations import _colsum, colsum_ok
+from .blaslt import wgrad_bgrad
 
 _WGRAD_CHUNK = 4096
 
@@ -83,6 +86,17 @@ def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
             and n % 64 == 0 and k % 64 == 0 and n * k >= 4_000_000 and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
 
 
+BGRAD_IN_GEMM = os.environ.get("PDT_BGRAD_GEMM", "1") == "1"
+
+
+def _bgrad_in_gemm(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    """Plain single-GEMM weight gradients of bf16 Linears (not the split / row-split small-shape paths)."""
+    m, n = dy2.shape
+    k = w.shape[1]
+    return (BGRAD_IN_GEMM and dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and not _tall_skinny(m, n, k) and _split_k(m, n, k) == 1 and n % 8 == 0 and k % 8 == 0)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -97,7 +111,15 @@ class _LinearFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = db = None
-        if ctx.needs_input_grad[1]:
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] and want_db and _bgrad_in_gemm(dy2, w):
+            # weight AND bias gradient from one hipBLASLt GEMM (BGRADB epilogue): dY is read once
+            x2 = x.reshape(-1, x.shape[-1])
+            r = wgrad_bgrad(dy2, x2 if x2.is_contiguous() else x2.contiguous())
+            if r is not None:
+                dw, db = r
+                want_db = False
+        if ctx.needs_input_grad[1] and dw is None:
             # (a concurrent dW on a second HIP stream measured 1 % slower on the flagship shapes,
             # profiles/r1_v11_wgrad_side_stream.log, and was removed)
             x2 = x.reshape(-1, x.shape[-1])
@@ -110,7 +132,7 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dx = torch.mm(dy2, w)
             dx = dx.view(*dy.shape[:-1], w.shape[1])
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if want_db:
             db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
         return dx, dw, db
 

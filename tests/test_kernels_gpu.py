@@ -768,7 +768,13 @@ def test_embedding_backward_matches_torch(dtype):
     w = torch.randn(5000, 96, device=DEV, dtype=dtype, requires_grad=True)
     idx = torch.randint(0, 700, (8, 1024), device=DEV)
     g = torch.randn(8, 1024, 96, device=DEV, dtype=dtype)
-    (embedding(idx, w) * g).sum().backward()
+    # the HIP scatter runs when the backward is captured into a graph; force it eagerly for this check
+    from pytorch_distributedtraining_amd.ops import embedding as E
+    E.FORCE_SCATTER = True
+    try:
+        (embedding(idx, w) * g).sum().backward()
+    finally:
+        E.FORCE_SCATTER = False
     w2 = w.detach().float().clone().requires_grad_()
     (torch.nn.functional.embedding(idx, w2) * g.float()).sum().backward()
     assert w.grad.dtype == dtype
@@ -842,3 +848,21 @@ def test_llama_packed_rope_gqa_attention_matches_unfused():
     (att.wo(o.reshape(B, S, h * d)) * g).sum().backward()
     assert rel_err(gx, x.grad) < 2e-3
     assert rel_err(gw, att.wqkv.weight.grad) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(4096, 768, 768), (2048, 1024, 4096)])
+def test_linear_weight_and_bias_grad_in_one_gemm(shape):
+    """ops.linear: dW and db from one hipBLASLt GEMM (BGRADB epilogue, csrc/kernels/blaslt.hip) vs fp32 torch."""
+    from pytorch_distributedtraining_amd.ops import blaslt
+    from pytorch_distributedtraining_amd.ops.linear import linear
+    torch.manual_seed(0)
+    M, N, K = shape
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    (linear(x, w, b) * g).sum().backward()
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    (torch.nn.functional.linear(xr, wr, br) * g.float()).sum().backward()
+    assert not blaslt._UNSUPPORTED
+    assert rel_err(w.grad, wr.grad) < 1e-2 and rel_err(b.grad, br.grad) < 1e-2 and rel_err(x.grad, xr.grad) < 1e-2
