@@ -45,3 +45,34 @@ def wgrad_bgrad(dy2: torch.Tensor, x2: torch.Tensor):
     if not lt_matmul(EPI_BGRADB, 2, k, n, m_rows, x2, dy2, dw, db):
         return None
     return dw, db
+
+
+_CHOICE: dict = {}
+
+
+def prefer_bgradb(dy2: torch.Tensor, x2: torch.Tensor, separate) -> bool:
+    """Whether the one-GEMM BGRADB path beats ``separate()`` (GEMM + column-sum) for this shape -- timed once per
+    shape on its first uncaptured call.  hipBLASLt's BGRADB kernels are 1.6x faster than the pair on GPT-2 124M's
+    qkv gradient (32k x 2304 x 768) but 7-9x SLOWER on GPT-2 1.3B's qkv / fc2 (profiles/r2_bgradb_vs_separate.jsonl),
+    so the choice must be measured, not assumed."""
+    key = (dy2.shape, x2.shape[1], dy2.dtype, dy2.device)
+    c = _CHOICE.get(key)
+    if c is not None:
+        return c
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    if wgrad_bgrad(dy2, x2) is None:
+        _CHOICE[key] = False
+        return False
+
+    def t(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+    c = _CHOICE[key] = t(lambda: wgrad_bgrad(dy2, x2)) < t(separate)
+    return c

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .activations import _colsum, colsum_ok
-from .blaslt import wgrad_bgrad
+from .blaslt import prefer_bgradb, wgrad_bgrad
 
 _WGRAD_CHUNK = 4096
 
@@ -86,7 +86,7 @@ def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
             and n % 64 == 0 and k % 64 == 0 and n * k >= 4_000_000 and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
 
 
-BGRAD_IN_GEMM = os.environ.get("PDT_BGRAD_GEMM", "1") == "1"
+BGRAD_IN_GEMM = os.environ.get("PDT_BGRAD_GEMM", "0") == "1"   # opt-in: no bench workload gains (r2)
 
 
 def _bgrad_in_gemm(dy2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -94,7 +94,7 @@ def _bgrad_in_gemm(dy2: torch.Tensor, w: torch.Tensor) -> bool:
     m, n = dy2.shape
     k = w.shape[1]
     return (BGRAD_IN_GEMM and dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and not _tall_skinny(m, n, k) and _split_k(m, n, k) == 1 and n % 8 == 0 and k % 8 == 0)
+            and not _tall_skinny(m, n, k) and _split_k(m, n, k) == 1 and n % 8 == 0 and k % 8 == 0 and colsum_ok(n))
 
 
 class _LinearFn(torch.autograd.Function):
@@ -113,12 +113,15 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] and want_db and _bgrad_in_gemm(dy2, w):
-            # weight AND bias gradient from one hipBLASLt GEMM (BGRADB epilogue): dY is read once
+            # weight AND bias gradient from one hipBLASLt GEMM (BGRADB epilogue) where that is measured faster
+            # than the GEMM + column-sum pair for this shape (ops.blaslt.prefer_bgradb)
             x2 = x.reshape(-1, x.shape[-1])
-            r = wgrad_bgrad(dy2, x2 if x2.is_contiguous() else x2.contiguous())
-            if r is not None:
-                dw, db = r
-                want_db = False
+            x2 = x2 if x2.is_contiguous() else x2.contiguous()
+            if prefer_bgradb(dy2, x2, lambda: (wgrad(dy2, x2, w.dtype), _colsum(dy2, w.dtype))):
+                r = wgrad_bgrad(dy2, x2)
+                if r is not None:
+                    dw, db = r
+                    want_db = False
         if ctx.needs_input_grad[1] and dw is None:
             # (a concurrent dW on a second HIP stream measured 1 % slower on the flagship shapes,
             # profiles/r1_v11_wgrad_side_stream.log, and was removed)

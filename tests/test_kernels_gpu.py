@@ -854,7 +854,10 @@ def test_llama_packed_rope_gqa_attention_matches_unfused():
 def test_linear_weight_and_bias_grad_in_one_gemm(shape):
     """ops.linear: dW and db from one hipBLASLt GEMM (BGRADB epilogue, csrc/kernels/blaslt.hip) vs fp32 torch."""
     from pytorch_distributedtraining_amd.ops import blaslt
+    from pytorch_distributedtraining_amd.ops import linear as L
     from pytorch_distributedtraining_amd.ops.linear import linear
+    L.BGRAD_IN_GEMM = True
+    blaslt._CHOICE.clear()
     torch.manual_seed(0)
     M, N, K = shape
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -864,5 +867,9 @@ def test_linear_weight_and_bias_grad_in_one_gemm(shape):
     (linear(x, w, b) * g).sum().backward()
     xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
     (torch.nn.functional.linear(xr, wr, br) * g.float()).sum().backward()
+    L.BGRAD_IN_GEMM = False
     assert not blaslt._UNSUPPORTED
     assert rel_err(w.grad, wr.grad) < 1e-2 and rel_err(b.grad, br.grad) < 1e-2 and rel_err(x.grad, xr.grad) < 1e-2
+    # and the fused GEMM itself, whichever path the timing picked above
+    dw, db = blaslt.wgrad_bgrad(g.contiguous(), x.detach())
+    assert rel_err(dw, wr.grad) < 1e-2 and rel_err(db, br.grad) < 1e-2
