@@ -131,3 +131,37 @@ def test_stoke_example_pretrained_flag(tmp_path):
     bad = subprocess.run(base + ["--pretrained", str(tmp_path / "bad.pth")], capture_output=True, text=True, env=env,
                          timeout=300)
     assert bad.returncode != 0 and "Missing key" in bad.stderr
+
+
+def _w_trainer_equiv(rank, world):
+    """The reference's combination (ddp + OSS + ShardedDDP + SyncBN + grad_accum 2 + clip 0.1 + OneCycle) on a
+    deterministic global batch of 4: world 2 shards it 2 + 2, world 1 takes all 4."""
+    torch.manual_seed(0)
+    # no conv bias in front of the BatchNorm: that bias has an exactly-zero true gradient, so it would only carry
+    # rounding noise that Adam amplifies into +-lr steps (no equivalence signal)
+    model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1, bias=False), nn.BatchNorm2d(8), nn.ReLU(),
+                          nn.Conv2d(8, 3, 3, padding=1))
+    t = Trainer(model, _opt(), nn.MSELoss(), batch_size_per_device=4 // world, grad_accum_steps=2,
+                grad_clip=ClipGradNormConfig(0.1, 2.0), distributed="ddp" if world > 1 else None,
+                fairscale_oss=world > 1, fairscale_sddp=world > 1,
+                configs=[DDPConfig(local_rank=rank, convert_to_sync_batch_norm=True),
+                         FairscaleOSSConfig(broadcast_fp16=False)], verbose=False)
+    sched = torch.optim.lr_scheduler.OneCycleLR(t.optimizer, max_lr=0.01, pct_start=0.9, steps_per_epoch=6, epochs=1)
+    n = 4 // world
+    for s in range(6):
+        g = torch.Generator().manual_seed(s)
+        x, y = torch.randn(4, 3, 8, 8, generator=g), torch.randn(4, 3, 8, 8, generator=g)
+        t.backward(t.loss(t.model(x[rank * n:(rank + 1) * n]), y[rank * n:(rank + 1) * n]))
+        t.step()
+        sched.step()
+    sd = t._model_state()
+    return {k: v.detach().clone().float() for k, v in sd.items()}, t.optimizer_steps
+
+
+def test_distributed_trainer_reference_combination_matches_single_process():
+    (ref, steps1), = run_workers(_w_trainer_equiv, 1)
+    (sd0, steps2), (sd1, _) = run_workers(_w_trainer_equiv, 2)
+    assert steps1 == steps2 == 3
+    for k in ref:
+        assert torch.equal(sd0[k], sd1[k]), k
+        assert torch.allclose(sd0[k], ref[k], atol=2e-5, rtol=1e-4), (k, (sd0[k] - ref[k]).abs().max())
