@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--grad-clip", type=float, default=1.0)
     ap.add_argument("--reshard", type=int, default=1, help="FSDP reshard after forward (FULL_SHARD)")
     ap.add_argument("--act-ckpt", type=int, default=0)
+    ap.add_argument("--act-ckpt-layers", default="all",
+                    help="with activation checkpointing: 'all', a layer count, or 'auto' = recompute only as many "
+                         "layers as the HBM needs (sized after the first warm-up step)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--secondary", type=int, default=1,
                     help="gpt2-fsdp at one GPU: also measure BASELINE.json's ResNet-50 DDP metric (JSON 'secondary')")
@@ -267,6 +270,27 @@ def bench_gpt2(args, comm, dev, world, rank):
     vocab = 128000 if llama else 50257
     batches = [torch.randint(0, vocab, (mb, S + 1), device=dev, generator=g) for _ in range(4)]
     state = {"i": 0, "loss": None}
+    inner = model.module if hasattr(model, "module") else model
+    ckpt_on = bool(getattr(inner.config, "activation_checkpointing", False))
+    if ckpt_on and args.act_ckpt_layers not in ("all", "auto"):
+        inner.config.checkpoint_layers = int(args.act_ckpt_layers)
+
+    def size_checkpointing():
+        """After one fully checkpointed step: keep as many layers' activations as fit in 85 % of HBM
+        (per-layer bytes estimated from the saved-tensor inventory of a block, x1.2 margin)."""
+        c = inner.config
+        L = getattr(c, "n_layers", getattr(c, "n_layer", 0))
+        d = getattr(c, "dim", getattr(c, "n_embd", 0))
+        ffn = getattr(c, "ffn_dim", 4 * d)
+        qkv = (c.n_heads + 2 * c.n_kv_heads) * c.head_dim if hasattr(c, "n_kv_heads") else 3 * d
+        per_tok = 2 * (5 * d + qkv + 3 * ffn) * 1.2          # bf16 tensors a non-recomputed block keeps
+        extra = per_tok * mb * S - 2 * d * mb * S             # minus the input a checkpointed block keeps anyway
+        free = 0.85 * torch.cuda.get_device_properties(dev).total_memory - torch.cuda.max_memory_allocated(dev)
+        keep = max(0, min(L, int(free // max(extra, 1))))
+        t = torch.tensor([float(keep)], device=dev)
+        comm.all_reduce(t, "min")                             # same policy on every rank
+        c.checkpoint_layers = L - int(t.item())
+        log(f"[bench] activation checkpointing sized to HBM: {c.checkpoint_layers}/{L} layers recomputed")
 
     def step():
         b = batches[state["i"] % len(batches)]
@@ -278,6 +302,10 @@ def bench_gpt2(args, comm, dev, world, rank):
         opt.zero_grad(set_to_none=True)
         state["loss"] = loss
 
+    if ckpt_on and args.act_ckpt_layers == "auto":
+        step()
+        torch.cuda.synchronize(dev)
+        size_checkpointing()
     dt = timed_loop(step, args, comm, dev)
     tokens = world * mb * S * args.steps
     tps = tokens / dt
@@ -292,7 +320,11 @@ def bench_gpt2(args, comm, dev, world, rank):
             "scaling": "weak", **comm_fields(world), "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
                        "micro_batch_per_gpu": mb, "params": nparams, "sharding": "full_shard" if args.reshard else
-                       "shard_grad_op", "optimizer": "fused AdamW + global-norm clip"}}
+                       "shard_grad_op", "optimizer": "fused AdamW + global-norm clip",
+                       **({"act_ckpt_layers": inner.config.checkpoint_layers
+                           if inner.config.checkpoint_layers is not None else
+                           getattr(inner.config, "n_layers", getattr(inner.config, "n_layer", None))}
+                          if ckpt_on else {})}}
 
 
 def bench_resnet(args, comm, dev, world, rank):

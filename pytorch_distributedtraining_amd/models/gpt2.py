@@ -33,6 +33,10 @@ class GPT2Config:
     n_head: int = 12
     layer_norm_epsilon: float = 1e-5
     activation_checkpointing: bool = False
+    # selective checkpointing: how many of the layers (the first ones) recompute their forward in backward;
+    # None = all of them when activation_checkpointing is on.  With 288 GB of HBM most of the recompute can be
+    # bought back (bench.py --act-ckpt-layers auto sizes it to the memory)
+    checkpoint_layers: int | None = None
 
     @property
     def head_dim(self):
@@ -147,8 +151,9 @@ class GPT2LMHeadModel(nn.Module):
         pos = torch.arange(S, device=input_ids.device)
         x = self.wte(input_ids)
         pending = self.wpe(pos).unsqueeze(0).expand(B, S, -1)
-        for blk in self.h:
-            if self.config.activation_checkpointing and self.training:
+        n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.h)
+        for i, blk in enumerate(self.h):
+            if self.config.activation_checkpointing and self.training and i < n_ckpt:
                 x, pending = torch.utils.checkpoint.checkpoint(blk, x, pending, use_reentrant=False)
             else:
                 x, pending = blk(x, pending)

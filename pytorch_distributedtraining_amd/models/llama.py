@@ -36,6 +36,10 @@ class LlamaConfig:
     rope_theta: float = 500000.0
     max_seq_len: int = 8192
     activation_checkpointing: bool = False
+    # selective checkpointing: how many of the layers (the first ones) recompute their forward in backward;
+    # None = all of them when activation_checkpointing is on.  With 288 GB of HBM most of the recompute can be
+    # bought back (bench.py --act-ckpt-layers auto sizes it to the memory)
+    checkpoint_layers: int | None = None
 
     @property
     def head_dim(self):
@@ -138,8 +142,9 @@ class Llama(nn.Module):
         x = self.tok_embeddings(tokens)
         cos, sin = self.rope_cos[:S], self.rope_sin[:S]
         pending = None
-        for layer in self.layers:
-            if self.config.activation_checkpointing and self.training:
+        n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.layers)
+        for i, layer in enumerate(self.layers):
+            if self.config.activation_checkpointing and self.training and i < n_ckpt:
                 x, pending = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, pending, use_reentrant=False)
             else:
                 x, pending = layer(x, cos, sin, pending)
