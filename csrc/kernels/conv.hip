@@ -172,3 +172,86 @@ PDT_API int pdt_window_perm(const void* src, const void* res, void* dst, int64_t
   }
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// SwinIR 'pixelshuffledirect' tail: PixelShuffle(r) of the upsample convolution's output
+// fused with the model's de-normalisation ``x / img_range + mean[c]`` -- one pass instead of a
+// pixel_shuffle copy plus two elementwise passes (and their three backward passes).  The conv output
+// arrives as its channels_last view (any strides), the image leaves NCHW-contiguous:
+//   out[n, c, h*r + i, w*r + j] = y[n, c*r*r + i*r + j, h, w] * a + b[c]
+// Backward writes dy NHWC-contiguous ([N*H*W, C*r*r] rows), the layout the conv's backward GEMMs read
+// without a copy:  dy[n, c*r*r + i*r + j, h, w] = dout[n, c, h*r + i, w*r + j] * a
+// ------------------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void pixel_shuffle_affine_fwd(const T* __restrict__ y, int64_t sn, int64_t sc,
+                                                                int64_t sh, int64_t sw, int C, int H, int W, int r,
+                                                                float a, const float* __restrict__ b,
+                                                                T* __restrict__ out, int64_t total) {
+  const int Ho = H * r, Wo = W * r;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int wo = (int)(e % Wo);
+    int64_t t = e / Wo;
+    const int ho = (int)(t % Ho);
+    t /= Ho;
+    const int c = (int)(t % C);
+    const int64_t n = t / C;
+    const int h = ho / r, i = ho - h * r, w = wo / r, j = wo - w * r;
+    const float v = to_f(y[n * sn + (int64_t)(c * r * r + i * r + j) * sc + h * sh + w * sw]);
+    out[e] = from_f<T>(fmaf(v, a, b ? b[c] : 0.f));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pixel_shuffle_affine_bwd(const T* __restrict__ dout, int64_t dn, int64_t dc,
+                                                                int64_t dh, int64_t dw, int C, int H, int W, int r,
+                                                                float a, T* __restrict__ dy, int64_t total) {
+  const int crr = C * r * r;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(e % crr);
+    int64_t p = e / crr;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int64_t n = p / H;
+    const int c = ch / (r * r), i = (ch / r) % r, j = ch % r;
+    dy[e] = from_f<T>(to_f(dout[n * dn + c * dc + (int64_t)(h * r + i) * dh + (int64_t)(w * r + j) * dw]) * a);
+  }
+}
+}  // namespace
+
+// y: logical [N, C*r*r, H, W] with element strides (sn, sc, sh, sw); out: [N, C, H*r, W*r] contiguous.
+// b: optional fp32 [C] (nullptr = 0).  dtype: kF32 / kBF16.
+PDT_API int pdt_pixel_shuffle_affine_fwd(const void* y, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int N, int C,
+                                         int H, int W, int r, float a, const float* b, void* out, int dt,
+                                         hipStream_t st) {
+  if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || r <= 0) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * C * H * r * W * r;
+  const int grid = grid_for(total, 256, 256 * 16);
+  if (dt == kBF16)
+    pixel_shuffle_affine_fwd<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)y, sn, sc, sh, sw, C, H, W, r, a, b,
+                                                           (bf16_t*)out, total);
+  else if (dt == kF32)
+    pixel_shuffle_affine_fwd<float><<<grid, 256, 0, st>>>((const float*)y, sn, sc, sh, sw, C, H, W, r, a, b,
+                                                          (float*)out, total);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// dout: logical [N, C, H*r, W*r] with element strides (dn, dc, dh, dw); dy: [N*H*W, C*r*r] contiguous.
+PDT_API int pdt_pixel_shuffle_affine_bwd(const void* dout, int64_t dn, int64_t dc, int64_t dh, int64_t dw, int N,
+                                         int C, int H, int W, int r, float a, void* dy, int dt, hipStream_t st) {
+  if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || r <= 0) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * C * r * r;
+  const int grid = grid_for(total, 256, 256 * 16);
+  if (dt == kBF16)
+    pixel_shuffle_affine_bwd<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)dout, dn, dc, dh, dw, C, H, W, r, a,
+                                                           (bf16_t*)dy, total);
+  else if (dt == kF32)
+    pixel_shuffle_affine_bwd<float><<<grid, 256, 0, st>>>((const float*)dout, dn, dc, dh, dw, C, H, W, r, a,
+                                                          (float*)dy, total);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}

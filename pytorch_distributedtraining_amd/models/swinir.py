@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.activations import bias_gelu
-from ..ops.conv import Conv2d3x3
+from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
 from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
@@ -265,8 +265,15 @@ class SwinIR(nn.Module):
         x = (x - mean) * self.img_range
         x = self.conv_first(x)
         x = self.conv_after_body(self.forward_features(x)) + x
-        x = self.upsample(x)
-        x = x / self.img_range + mean
+        if x.is_cuda and isinstance(self.upsample[0], Conv2d3x3):
+            # conv -> PixelShuffle -> x / img_range + mean as conv + ONE fused HIP pass
+            y = self.upsample[0](x)
+            x = pixel_shuffle_affine(y, self.upscale, 1.0 / self.img_range, mean)
+            dt = torch.promote_types(y.dtype, mean.dtype)    # the unfused tail's type promotion
+            x = x if x.dtype == dt else x.to(dt)
+        else:
+            x = self.upsample(x)
+            x = x / self.img_range + mean
         return x[:, :, : H * self.upscale, : W * self.upscale]
 
 

@@ -104,6 +104,10 @@ _SIGS = {
     "pdt_window_perm": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,
                       c_int, c_void_p],
+    "pdt_pixel_shuffle_affine_fwd": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int,
+                                     c_float, c_void_p, c_void_p, c_int, c_void_p],
+    "pdt_pixel_shuffle_affine_bwd": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int,
+                                     c_float, c_void_p, c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int,

@@ -128,3 +128,37 @@ class Conv2d3x3(nn.Conv2d):
 
     def forward(self, x):
         return conv3x3(x, self.weight, self.bias)
+
+
+class _PixelShuffleAffineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, r, a, b):
+        N, Crr, H, W = y.shape
+        C = Crr // (r * r)
+        out = torch.empty((N, C, H * r, W * r), dtype=y.dtype, device=y.device)
+        bb = None if b is None else b.detach().reshape(-1).float().contiguous()
+        _lib.call("pdt_pixel_shuffle_affine_fwd", y.data_ptr(), *y.stride(), N, C, H, W, r, float(a), _lib.ptr(bb),
+                  out.data_ptr(), _lib.dtype_code(y.dtype), _lib.stream_handle(y.device))
+        ctx.r, ctx.a, ctx.shape = r, float(a), (N, C, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        N, C, H, W = ctx.shape
+        r = ctx.r
+        dy = torch.empty((N, H, W, C * r * r), dtype=dout.dtype, device=dout.device)
+        _lib.call("pdt_pixel_shuffle_affine_bwd", dout.data_ptr(), *dout.stride(), N, C, H, W, r, ctx.a,
+                  dy.data_ptr(), _lib.dtype_code(dout.dtype), _lib.stream_handle(dout.device))
+        return dy.permute(0, 3, 1, 2), None, None, None
+
+
+def pixel_shuffle_affine(y: torch.Tensor, r: int, a: float = 1.0, b: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.pixel_shuffle(y, r) * a + b[c]`` in one HIP pass (SwinIR's 'pixelshuffledirect'
+    upsampler followed by the ``x / img_range + mean`` de-normalisation, Stoke-DDP.py:206-208).  ``y`` may be
+    any-strided (the channels_last output of ``conv3x3``); the gradient is returned channels_last, the layout
+    the convolution's backward GEMMs consume without a copy.  ``b`` is a constant (no gradient)."""
+    if not y.is_cuda or y.dtype not in (torch.float32, torch.bfloat16):
+        out = F.pixel_shuffle(y, r) * a
+        return out if b is None else out + b.reshape(1, -1, 1, 1).to(out.dtype)
+    _lib.require()
+    return _PixelShuffleAffineFn.apply(y, r, a, b)

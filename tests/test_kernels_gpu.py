@@ -461,6 +461,29 @@ def test_conv3x3_im2col_gemm(cin, cout, dt, layout):
     assert rel_err(b.grad, br.grad) < tol * 2
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("r,C", [(2, 3), (3, 1), (4, 3)])
+def test_pixel_shuffle_affine(dt, r, C):
+    """Fused PixelShuffle + x / img_range + mean (SwinIR 'pixelshuffledirect' tail) vs torch in fp32, on the
+    channels_last conv-output layout; the gradient must come back channels_last with the same values."""
+    from pytorch_distributedtraining_amd.ops.conv import pixel_shuffle_affine
+    torch.manual_seed(0)
+    N, H, W = 2, 13, 17
+    y = torch.randn(N, H, W, C * r * r, device=DEV).permute(0, 3, 1, 2).to(dt).requires_grad_()
+    mean = torch.rand(C, device=DEV)
+    out = pixel_shuffle_affine(y, r, 0.5, mean)
+    yr = y.detach().float().requires_grad_()
+    ref = F.pixel_shuffle(yr, r) * 0.5 + mean.view(1, C, 1, 1)
+    assert out.shape == ref.shape and out.dtype == dt
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-6
+    assert rel_err(out, ref) < tol
+    g = torch.randn_like(ref)
+    out.backward(g.to(dt))
+    ref.backward(g)
+    assert y.grad.permute(0, 2, 3, 1).is_contiguous()
+    assert rel_err(y.grad, yr.grad) < tol
+
+
 @pytest.mark.parametrize("H,W,ws,shift,C", [(16, 24, 8, 4, 60), (14, 21, 7, 0, 12), (16, 16, 8, 3, 96)])
 def test_window_perm_fused(H, W, ws, shift, C):
     """Fused shifted-window partition / reverse(+residual) vs torch.roll + view/permute, values and grads."""
