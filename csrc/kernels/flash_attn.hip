@@ -30,6 +30,7 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 constexpr int NT = 256;
 constexpr int TILE = 64;          // rows per staged LDS tile
@@ -291,6 +292,16 @@ __device__ __forceinline__ int swz_f(int r) {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Barrier that retires this wave's LDS-DMA before other waves read what it wrote.  hipcc treats
+// buffer/global_load ... lds as plain VMEM loads: a workgroup-scope fence does not wait for loads, so
+// __syncthreads() alone emits NO s_waitcnt vmcnt(0) where the waitcnt pass sees no register dependency
+// (the first barrier of a 2x-unrolled ring loop had none: under load, waves read a tile before its DMA
+// landed -- wrong rows of O at B*H >= 512 on the GPT-2 1.3B shape).  The explicit wait is mandatory.
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 template <int D>
 __device__ __forceinline__ void dma_tile(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
                                          int w, int lane) {
@@ -381,7 +392,7 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
   float m = -INFINITY, l = 0.f;
 
   for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();   // vmcnt(0): tile t resident; every wave is done with the buffer refilled below
+    dma_barrier();   // vmcnt(0): tile t resident; every wave is done with the buffer refilled below
     if (t + 1 < ntiles) {
       bf16_t* nb = smem + ((t + 1) & 1) * 2 * TE;
       dma_tile<D>(Kp, p.k_ss, (t + 1) * TILE, p.Sk, nb, w, lane);
@@ -626,7 +637,7 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u) {
       const int tt = t + u;
       if (tt < ntiles) {
-        __syncthreads();
+        dma_barrier();
         if (tt + 1 < ntiles) {
           bf16_t* nb = smem + (1 - u) * 2 * TE;
           lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
@@ -655,6 +666,219 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
       }
     if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Row-per-lane epilogue with 16-byte stores (cdna_hip_programming.md T21): a lane holds 4 consecutive
+// columns per (dt, g) of its row and its xor-32 partner the next 4, so a v_permlane32_swap per dword
+// pair hands each lane 8 consecutive columns -- D/16 dwordx4 stores per lane instead of D/8 dwordx2
+// (the store-issue-bound tail of MI355X_MICROARCH.md 'attention epilogue store tail').  Every lane must
+// run it (EXEC all ones for the swap); `ok` only gates the stores (both partner lanes share one row).
+// ------------------------------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ void store_row16(bf16_t* row, const f32x16 (&acc)[DT], float scale, int h, bool ok) {
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      unsigned a[2], c[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int g0 = 2 * pr, g1 = 2 * pr + 1;
+        a[k] = (unsigned)f2bf(acc[dt][4 * g0 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g0 + 2 * k + 1] * scale) << 16);
+        c[k] = (unsigned)f2bf(acc[dt][4 * g1 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g1 + 2 * k + 1] * scale) << 16);
+        const auto r = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+        a[k] = r[0];
+        c[k] = r[1];
+      }
+      if (ok) {
+        u32x4 v;
+        v[0] = a[0]; v[1] = a[1]; v[2] = c[0]; v[3] = c[1];
+        *reinterpret_cast<u32x4*>(row + dt * 32 + 16 * pr + 8 * h) = v;
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward v5 = v4 + (1) deferred rescale (T13): the running max m used in exp2 moves only when some
+// row's tile max exceeds it by more than RESCALE_THR (log2 units), so the 64-register O rescale runs on a
+// handful of tiles instead of most of them (probabilities stay <= 2^THR, exact in fp32 / bf16 range);
+// (2) the K row fragments stream two MFMA steps ahead of their use and the V transposed fragments one
+// step ahead, each step its own scheduling region, so an LDS read's latency hides behind the MFMAs
+// instead of stalling every pair; (3) the 16-byte permlane epilogue.
+// ------------------------------------------------------------------------------------------------
+constexpr float RESCALE_THR = 8.0f;
+
+template <int D, bool CAUSAL>
+struct FwdV5 {
+  static constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+
+  __device__ __forceinline__ static u16x8 kfr(const bf16_t* lds, const int (&koff)[KS], int i) {
+    // step i: k-step i / 2, key subtile i % 2
+    return *reinterpret_cast<const u16x8*>(lds + koff[i >> 1] + (i & 1) * 32 * D);
+  }
+  __device__ __forceinline__ static u16x8 vfr(const bf16_t* vs, const int (&voff)[DT][2], int j) {
+    // step j: dt = j / 4, key block kb = 16 * (j % 4)
+    const int dt = j >> 2, kb = 16 * (j & 3);
+    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][0] + kb * D));
+    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][1] + kb * D));
+    return __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+
+  __device__ __forceinline__ static void tile(const bf16_t* __restrict__ lds, const int (&koff)[KS],
+                                              const int (&voff)[DT][2], const u16x8 (&qf)[KS], f32x16 (&o)[DT],
+                                              float& m, float& l, float sl2, int k0, bool diag, int lim) {
+    constexpr int NS = 2 * KS;   // QK^T steps (one MFMA each)
+    f32x16 s[2];
+    u16x8 kb0 = kfr(lds, koff, 0), kb1 = kfr(lds, koff, 1);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      u16x8 kn;
+      if (i + 2 < NS) kn = kfr(lds, koff, i + 2);
+      __builtin_amdgcn_sched_barrier(0);   // the read issues BEFORE this step's MFMA (two steps of cover)
+      const int ks = i >> 1, st = i & 1;
+      s[st] = mfma32(kb0, qf[ks], ks == 0 ? zero16() : s[st]);
+      kb0 = kb1;
+      kb1 = kn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bf16_t* vs = lds + TE;
+    u16x8 vb0 = vfr(vs, voff, 0), vb1 = vfr(vs, voff, 1);   // first V fragments in flight under the softmax
+    if (diag) {   // keys k0 + kt*32 + acc_row(r, h) > lim are masked (future / past Sk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        s[0][r] = (k0 + rr > lim) ? -INFINITY : s[0][r];
+        s[1][r] = (k0 + 32 + rr > lim) ? -INFINITY : s[1][r];
+      }
+    }
+    float mx = fmaxf(s[0][0], s[1][0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+    if (!__all(mx <= m + RESCALE_THR)) {   // some row's max ran past the deferred reference: move it
+      const float mn = fmaxf(m, mx);
+      const float alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mn);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      l *= alpha;
+      m = mn;
+    }
+    const float msub = (m == -INFINITY) ? 0.f : m;
+    float ls = 0.f;
+    u16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[t][r] = fast_exp2(fmaf(s[t][r], sl2, -msub));
+        ls += s[t][r];
+      }
+      pf[t][0] = pack8(s[t], 0);
+      pf[t][1] = pack8(s[t], 1);
+    }
+    l += ls;
+    constexpr int NV = 4 * DT;   // PV steps: (dt, kt, ss)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      u16x8 vn;
+      if (j + 2 < NV) vn = vfr(vs, voff, j + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      const int dt = j >> 2, kt = (j >> 1) & 1, ss = j & 1;
+      o[dt] = mfma32(vb0, pf[kt][ss], o[dt]);
+      vb0 = vb1;
+      vb1 = vn;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
+  using K = FwdV5<D, CAUSAL>;
+  constexpr int KS = K::KS, DT = K::DT, TE = K::TE;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const BlockCoord bc = heavy_first(true);
+  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
+  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  DmaLane<D> lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
+  if (ntiles > 0) {
+    lk.issue(Kp, p.k_ss, 0, p.Sk, smem, w);
+    lv.issue(Vp, p.v_ss, 0, p.Sk, smem + TE, w);
+  }
+
+  int koff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int voff[DT][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int r1 = 4 * (g >> 1) + q;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
+      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
+    }
+  }
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+    }
+  }
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  for (int t = 0; t < ntiles; t += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tt = t + u;
+      if (tt < ntiles) {
+        dma_barrier();
+        if (tt + 1 < ntiles) {
+          bf16_t* nb = smem + (1 - u) * 2 * TE;
+          lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
+          lv.issue(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w);
+        }
+        const int k0 = tt * TILE;
+        if (!(CAUSAL && k0 > qw + 31 + off)) {
+          const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+          K::tile(smem + u * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
+        }
+      }
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  store_row16<DT>(p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss, o, inv, h, qrow < p.Sq);
+  if (qrow < p.Sq && h == 0)
+    p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -993,7 +1217,7 @@ __global__ __launch_bounds__(NT) void fa_bwd_dkdv_v2_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u) {
       const int cur = it + u;
       if (cur >= total) break;
-      __syncthreads();
+      dma_barrier();
       if (cur + 1 < total) issue(cur + 1, 1 - u);
       const int q0 = qstart + (cur % qtiles) * TILE;
       const bf16_t* Qs = smem + u * 2 * TE;
@@ -1115,7 +1339,7 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_v2_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u) {
       const int tt = t + u;
       if (tt >= ntiles) break;
-      __syncthreads();
+      dma_barrier();
       if (tt + 1 < ntiles) {
         bf16_t* nb = smem + (1 - u) * 2 * TE;
         dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
@@ -1359,7 +1583,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u) {
       const int cur = it + u;
       if (cur >= total) break;
-      __syncthreads();
+      dma_barrier();
       if (cur + 1 < total) issue(cur + 1, 1 - u);
       const int q0 = qstart + (cur % qtiles) * TILE;
       if (CAUSAL && q0 + TILE - 1 + off < kw) continue;         // every query of the tile precedes these keys
@@ -1372,20 +1596,8 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
     }
   }
   acc_fence();
-  if (key < p.Sk) {
-    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
-    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 a, c;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
-        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
-        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
-      }
-  }
+  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
+  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
 }
 
 template <int D, bool CAUSAL>
@@ -1512,7 +1724,7 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u) {
       const int tt = t + u;
       if (tt >= ntiles) break;
-      __syncthreads();
+      dma_barrier();
       if (tt + 1 < ntiles) {
         bf16_t* nb = smem + (1 - u) * 2 * TE;
         lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
@@ -1524,24 +1736,13 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
       BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
   }
-  if (qrow < p.Sq) {
-    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
-        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
-      }
-  }
+  store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
 }
 
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
 int g_fwd_variant = -1, g_bwd_variant = -1;
 int fwd_variant() {
-  if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 4; }
+  if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 5; }
   return g_fwd_variant;
 }
 int bwd_variant() {
@@ -1558,6 +1759,9 @@ int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   } else if (variant == 4) {
     if (causal) fa_fwd_v4_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v4_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else if (variant == 5) {
+    if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
+    else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
   } else {
     if (causal) fa_fwd_v3_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v3_kernel<D, false><<<grid, NT, 0, st>>>(p);

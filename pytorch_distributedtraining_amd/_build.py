@@ -36,7 +36,8 @@ HIPCC_FLAGS = [
 # MFMA kernels whose accumulators are post-processed by VALU (softmax / gradient tiles): keep the MFMA
 # results in arch VGPRs (no v_accvgpr_read/write shuttling through AGPRs).
 PER_FILE_FLAGS = {
-    "flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    # no-NaN float mode: fmaxf on MFMA outputs compiles to bare v_max3 (no canonicalising v_max x,x first)
+    "flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-mno-amdgpu-ieee"],
 }
 
 

@@ -156,7 +156,7 @@ def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None):
 
 def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:
     """Select the flash-attention kernel generation (0 keeps the current one).  fwd: 2 register-staged,
-    3 LDS-DMA ring, 4 (default) VALU-lean LDS-DMA.  bwd: 1 baseline, 2 LDS-DMA, 3 (default) hand-pipelined
+    3 LDS-DMA ring, 4 VALU-lean LDS-DMA, 5 (default) v4 + deferred rescale + read prefetch + 16-B epilogue.  bwd: 1 baseline, 2 LDS-DMA, 3 (default) hand-pipelined
     dK/dV (v3).  Returns the (fwd, bwd) pair now in effect."""
     r = _lib.require().pdt_flash_attn_set_variant(int(fwd), int(bwd))
     return r // 16, r % 16

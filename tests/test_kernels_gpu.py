@@ -138,7 +138,7 @@ def _attn_ref(q, k, v, causal, scale):
     return (s.softmax(-1) @ vt).transpose(1, 2)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [(4, 2), (4, 3), (5, 3)])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,S,H,Hkv", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 1024, 2, 1), (1, 77, 2, 2)])
@@ -146,7 +146,7 @@ def test_flash_attn(D, causal, B, S, H, Hkv, variant):
     from pytorch_distributedtraining_amd.ops import flash_attn
     from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
     prev = set_kernel_variant()
-    set_kernel_variant(bwd=variant)
+    set_kernel_variant(*variant)
     try:
         _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv)
     finally:
@@ -167,6 +167,73 @@ def _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv):
     assert rel_err(q.grad, qr.grad) < 2e-2
     assert rel_err(k.grad, kr.grad) < 2e-2
     assert rel_err(v.grad, vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("fwd", [4, 5])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attn_forced_rescale(fwd, causal):
+    """Forward v5 defers the online-softmax rescale until a row's max runs RESCALE_THR past the reference
+    (cdna_hip_programming.md §5.4 rule 26): spike a few keys against chosen query rows so the running max
+    jumps ~9.5 (log2 units, past the 8 threshold) at a late tile, and check O and the LSE-dependent gradients against fp32."""
+    from pytorch_distributedtraining_amd.ops import flash_attn
+    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    prev = set_kernel_variant()
+    set_kernel_variant(fwd=fwd)
+    try:
+        torch.manual_seed(0)
+        B, S, H, D = 1, 512, 2, 128
+        q = 0.3 * torch.randn(B, S, H, D, device=DEV)
+        k = 0.3 * torch.randn(B, S, H, D, device=DEV)
+        v = torch.randn(B, S, H, D, device=DEV)
+        for qi, ki in ((400, 330), (401, 200), (100, 90), (511, 460)):   # spike keys in later tiles
+            k[0, ki] = 2.0 * q[0, qi] / q[0, qi].norm(dim=-1, keepdim=True) * math.sqrt(D)
+        q, k, v = (t.to(torch.bfloat16).requires_grad_() for t in (q, k, v))
+        _check_flash_attn_tensors(flash_attn, q, k, v, causal)
+    finally:
+        set_kernel_variant(*prev)
+
+
+def _check_flash_attn_tensors(flash_attn, q, k, v, causal):
+    o = flash_attn(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, causal, 1 / math.sqrt(q.shape[-1]))
+    orf.backward(do.float())
+    assert rel_err(o, orf) < 1e-2
+    assert rel_err(q.grad, qr.grad) < 2e-2
+    assert rel_err(k.grad, kr.grad) < 2e-2
+    assert rel_err(v.grad, vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("fwd", [4, 5])
+def test_flash_attn_full_grid_rows(fwd):
+    """The flagship shape (GPT-2 1.3B: B32 S1024 H16 D128 causal) keeps thousands of workgroups in flight,
+    the load under which an LDS-DMA tile read before its DMA landed (a missing vmcnt wait before the ring
+    barrier) corrupted the last query block's rows while every small-grid test passed.  Check every row of
+    the first and last batch element, forward and all three gradients, against fp32."""
+    from pytorch_distributedtraining_amd.ops import flash_attn
+    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    prev = set_kernel_variant()
+    set_kernel_variant(fwd=fwd)
+    try:
+        B, S, H, D = 32, 1024, 16, 128
+        q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+        o = flash_attn(q, k, v, causal=True)
+        do = torch.randn_like(o)
+        o.backward(do)
+        for b in (0, B - 1):
+            qr, kr, vr = (t[b:b + 1].detach().float().requires_grad_() for t in (q, k, v))
+            orf = _attn_ref(qr, kr, vr, True, 1 / math.sqrt(D))
+            orf.backward(do[b:b + 1].float())
+            for got, ref, tol in ((o[b:b + 1], orf, 2e-2), (q.grad[b:b + 1], qr.grad, 4e-2),
+                                  (k.grad[b:b + 1], kr.grad, 4e-2), (v.grad[b:b + 1], vr.grad, 4e-2)):
+                # per-row error against the typical row norm (a query-0 dq row is ~0 in exact math)
+                rn = ref.norm(dim=-1)
+                row_err = (got.float() - ref).norm(dim=-1) / torch.maximum(rn, rn.mean())   # [1, S, H]
+                assert float(row_err.max()) < tol, (b, float(row_err.max()), int(row_err.argmax()))
+    finally:
+        set_kernel_variant(*prev)
 
 
 def test_flash_attn_qkvpacked_matches_unpacked():
