@@ -16,8 +16,9 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
-                         "libpdt_kernels.so")
+# PDT_KERNEL_LIB points at another build of the library (A/B of two kernel builds on one box)
+_LIB_PATH = os.environ.get("PDT_KERNEL_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libpdt_kernels.so")
 _lock = threading.Lock()
 _lib = None
 _load_error: Exception | None = None
