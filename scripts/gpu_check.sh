@@ -22,7 +22,7 @@ fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 900 python bench.py $BENCH_ARGS || exit $?
 if [ "${PROFILE:-1}" == "1" ]; then
-  step rocprof 900 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o bench --output-format csv -- python bench.py --steps 3 --warmup 1 || exit $?
+  step rocprof 900 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o bench --output-format csv -- python bench.py --steps 3 --warmup 1 --secondary 0 || exit $?
   find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv
   python - <<'PY'
 import csv, os
