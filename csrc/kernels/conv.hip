@@ -177,7 +177,8 @@ PDT_API int pdt_window_perm(const void* src, const void* res, void* dst, int64_t
 // SwinIR 'pixelshuffledirect' tail: PixelShuffle(r) of the upsample convolution's output
 // fused with the model's de-normalisation ``x / img_range + mean[c]`` -- one pass instead of a
 // pixel_shuffle copy plus two elementwise passes (and their three backward passes).  The conv output
-// arrives as its channels_last view (any strides), the image leaves NCHW-contiguous:
+// arrives as its channels_last view (any strides), the image leaves channels_last (NHWC buffer), the
+// layout torch's pixel_shuffle keeps for a channels_last input and the loss network's convolutions take:
 //   out[n, c, h*r + i, w*r + j] = y[n, c*r*r + i*r + j, h, w] * a + b[c]
 // Backward writes dy NHWC-contiguous ([N*H*W, C*r*r] rows), the layout the conv's backward GEMMs read
 // without a copy:  dy[n, c*r*r + i*r + j, h, w] = dout[n, c, h*r + i, w*r + j] * a
@@ -190,12 +191,12 @@ __global__ __launch_bounds__(256) void pixel_shuffle_affine_fwd(const T* __restr
                                                                 T* __restrict__ out, int64_t total) {
   const int Ho = H * r, Wo = W * r;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int wo = (int)(e % Wo);
-    int64_t t = e / Wo;
+    const int c = (int)(e % C);              // NHWC order: the channels of one output pixel are adjacent
+    int64_t t = e / C;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
     const int ho = (int)(t % Ho);
-    t /= Ho;
-    const int c = (int)(t % C);
-    const int64_t n = t / C;
+    const int64_t n = t / Ho;
     const int h = ho / r, i = ho - h * r, w = wo / r, j = wo - w * r;
     const float v = to_f(y[n * sn + (int64_t)(c * r * r + i * r + j) * sc + h * sh + w * sw]);
     out[e] = from_f<T>(fmaf(v, a, b ? b[c] : 0.f));
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256) void pixel_shuffle_affine_bwd(const T* __restr
 }
 }  // namespace
 
-// y: logical [N, C*r*r, H, W] with element strides (sn, sc, sh, sw); out: [N, C, H*r, W*r] contiguous.
+// y: logical [N, C*r*r, H, W] with element strides (sn, sc, sh, sw); out: NHWC buffer [N, H*r, W*r, C].
 // b: optional fp32 [C] (nullptr = 0).  dtype: kF32 / kBF16.
 PDT_API int pdt_pixel_shuffle_affine_fwd(const void* y, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int N, int C,
                                          int H, int W, int r, float a, const float* b, void* out, int dt,

@@ -17,6 +17,7 @@ every one of them back to the stock torch module (the baseline of scripts/bench_
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -28,6 +29,9 @@ from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
                                     window_reverse_shifted_add)
+
+# PDT_SWINIR_FUSED_TAIL=0: stock PixelShuffle + de-normalisation (A/B of the fused HIP tail)
+_FUSED_TAIL = os.environ.get("PDT_SWINIR_FUSED_TAIL", "1") == "1"
 
 
 def window_partition(x, ws):
@@ -265,7 +269,7 @@ class SwinIR(nn.Module):
         x = (x - mean) * self.img_range
         x = self.conv_first(x)
         x = self.conv_after_body(self.forward_features(x)) + x
-        if x.is_cuda and isinstance(self.upsample[0], Conv2d3x3):
+        if x.is_cuda and _FUSED_TAIL and isinstance(self.upsample[0], Conv2d3x3):
             # conv -> PixelShuffle -> x / img_range + mean as conv + ONE fused HIP pass
             y = self.upsample[0](x)
             x = pixel_shuffle_affine(y, self.upscale, 1.0 / self.img_range, mean)

@@ -135,12 +135,12 @@ class _PixelShuffleAffineFn(torch.autograd.Function):
     def forward(ctx, y, r, a, b):
         N, Crr, H, W = y.shape
         C = Crr // (r * r)
-        out = torch.empty((N, C, H * r, W * r), dtype=y.dtype, device=y.device)
+        out = torch.empty((N, H * r, W * r, C), dtype=y.dtype, device=y.device)   # channels_last
         bb = None if b is None else b.detach().reshape(-1).float().contiguous()
         _lib.call("pdt_pixel_shuffle_affine_fwd", y.data_ptr(), *y.stride(), N, C, H, W, r, float(a), _lib.ptr(bb),
                   out.data_ptr(), _lib.dtype_code(y.dtype), _lib.stream_handle(y.device))
         ctx.r, ctx.a, ctx.shape = r, float(a), (N, C, H, W)
-        return out
+        return out.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dout):
@@ -155,8 +155,9 @@ class _PixelShuffleAffineFn(torch.autograd.Function):
 def pixel_shuffle_affine(y: torch.Tensor, r: int, a: float = 1.0, b: torch.Tensor | None = None) -> torch.Tensor:
     """``F.pixel_shuffle(y, r) * a + b[c]`` in one HIP pass (SwinIR's 'pixelshuffledirect'
     upsampler followed by the ``x / img_range + mean`` de-normalisation, Stoke-DDP.py:206-208).  ``y`` may be
-    any-strided (the channels_last output of ``conv3x3``); the gradient is returned channels_last, the layout
-    the convolution's backward GEMMs consume without a copy.  ``b`` is a constant (no gradient)."""
+    any-strided (the channels_last output of ``conv3x3``); the result is channels_last like torch's
+    pixel_shuffle of a channels_last input, and the gradient is returned channels_last, the layout the
+    convolution's backward GEMMs consume without a copy.  ``b`` is a constant (no gradient)."""
     if not y.is_cuda or y.dtype not in (torch.float32, torch.bfloat16):
         out = F.pixel_shuffle(y, r) * a
         return out if b is None else out + b.reshape(1, -1, 1, 1).to(out.dtype)

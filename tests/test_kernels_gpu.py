@@ -542,6 +542,7 @@ def test_pixel_shuffle_affine(dt, r, C):
     yr = y.detach().float().requires_grad_()
     ref = F.pixel_shuffle(yr, r) * 0.5 + mean.view(1, C, 1, 1)
     assert out.shape == ref.shape and out.dtype == dt
+    assert out.is_contiguous(memory_format=torch.channels_last)
     tol = 1e-2 if dt == torch.bfloat16 else 1e-6
     assert rel_err(out, ref) < tol
     g = torch.randn_like(ref)
