@@ -9,10 +9,13 @@ Requirements on ``step_fn`` (the usual graph-capture rules): static input buffer
 (``FusedAdamW(capturable=True)``: device step counter, device clip coefficient), and gradients zeroed in
 place (``zero_grad(set_to_none=False)``) so they keep their addresses.
 
-Status: tested on a plain bf16-autocast GPT-2 (tests/test_kernels_gpu.py::test_graphed_training_step_matches_eager,
-losses and weights match the eager run).  Replaying a DistributedDataParallel-wrapped GPT-2 124M step
-(vocab 50,257) faulted with an illegal address in a rocprim partition kernel, so bench.py does not use
-graphs and engine-wrapped models are not supported yet.
+Status: a plain bf16-autocast GPT-2 step (tests/test_kernels_gpu.py::test_graphed_training_step_matches_eager)
+and a DistributedDataParallel-wrapped GPT-2 step with a 50,257-row vocabulary
+(test_graphed_ddp_gpt2_step_with_large_vocab) replay with losses and weights equal to eager.  The round-1
+replay fault (illegal address in a rocprim partition kernel) was torch's embedding dense backward, whose
+sort / unique sizes are data-dependent; under capture ``ops.embedding`` uses a fixed-shape HIP scatter-add
+instead.  The benchmarked steps are GPU-bound (kernel time ~= step time in the rocprofv3 tables), so
+bench.py runs them eagerly.
 
     step = GraphedStep(train_step, x_static, y_static, warmup=3)
     for x, y in loader:
