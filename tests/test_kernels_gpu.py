@@ -602,6 +602,22 @@ def test_swinir_conv_path_matches_stock_model():
         assert rel_err(p.grad, q.grad) < 6e-2, n
 
 
+@pytest.mark.parametrize("splits", [1, 2, 4])
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 256), (4096, 768, 1024), (16384, 256, 512)])
+def test_hip_wgrad_gemm(M, N, K, splits):
+    """Hand MFMA weight-gradient GEMM (gemm_wgrad.hip: both operands token-major, transposed LDS reads,
+    split-K fp32 slabs) vs the fp32 product dY^T X."""
+    from pytorch_distributedtraining_amd.ops.linear import hip_wgrad
+    torch.manual_seed(0)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    got = hip_wgrad(dy, x, splits=splits)
+    ref = dy.float().t() @ x.float()
+    assert got.shape == (N, K) and got.dtype == torch.bfloat16
+    assert rel_err(got, ref) < 4e-3
+    assert float((got.float() - ref).abs().max()) < 0.05 * float(ref.abs().max())
+
+
 @pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60), (16384, 768, 768), (16384, 768, 3072),
                                    (8192 + 512, 3072, 768)])
 def test_linear_tall_skinny_wgrad(M, K, N):
