@@ -19,6 +19,7 @@
 // 32-lane group land on 4 distinct 64-B bank groups).  Split-K over the tokens (fp32 partial slabs + a
 // reduce pass) keeps >= 256 workgroups for small outputs (GPT-2 1.3B attention projection: 64 tiles).
 #include "common.h"
+#include <stdlib.h>
 
 using namespace pdt;
 
@@ -30,9 +31,8 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BR = 256, BC = 256, BK = 64, NTH = 512;
-constexpr int TILE_ELEMS = BK * 256;          // one operand stage: 64 token rows x 256 columns
-constexpr int STAGE = 2 * TILE_ELEMS;         // A + B
+constexpr int BR = 256, BC = 256, NTH = 512;
+constexpr int BK = 64;                        // token granularity every split / M must respect
 
 __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -49,12 +49,14 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r & 3) << 2); }
 // element (T8): per K-step only the SGPR descriptor moves, the per-lane byte offsets are computed once.
 // (global_load_lds through a plain pointer made hipcc wait vmcnt(0) before the first LDS read after it --
 // it cannot tell the DMA target stage from the stage being read -- which serialised every prefetch.)
+template <int BKT>
 struct DmaOp {
-  uint32_t off[4];
+  static constexpr int NP = BKT / 16;   // 16-B chunks per thread per operand tile (BKT rows x 512 B / 512 thr)
+  uint32_t off[NP];
   __device__ __forceinline__ void init(int64_t ld, int tid) {
     const int w = tid >> 6, lane = tid & 63;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NP; ++i) {
       const int ci = i * NTH + w * 64 + lane;
       const int r = ci >> 5, c = ci & 31;
       off[i] = (uint32_t)((r * ld + swz(r, c) * 8) * 2);
@@ -62,15 +64,14 @@ struct DmaOp {
   }
   // Issued from inline asm: for a builtin LDS-DMA, hipcc's waitcnt pass cannot tell the target stage from the
   // stage being read and drains the whole prefetch (vmcnt(0)) before the next ds_read -- which serialised
-  // every K-step.  Hidden from it, the DMA is ordered only by dma_barrier()'s explicit vmcnt(0) + barrier
-  // (the stage a wave reads was DMA'd one K-step earlier and retired by that barrier).
+  // every K-step.  Hidden from it, the DMA is ordered only by the K-loop's explicit counted vmcnt + barrier.
   __device__ __forceinline__ void piece(const bf16_t* tile0, int64_t ld, bf16_t* lds, int tid, int i) const {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const uint64_t addr = (uint64_t)(uintptr_t)tile0;
     v4i rsrc;
     rsrc[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)addr);
     rsrc[1] = __builtin_amdgcn_readfirstlane((int)((addr >> 32) & 0xffff));
-    rsrc[2] = __builtin_amdgcn_readfirstlane((int)((BK - 1) * ld * 2 + 512));   // num_records (bytes)
+    rsrc[2] = __builtin_amdgcn_readfirstlane((int)((BKT - 1) * ld * 2 + 512));   // num_records (bytes)
     rsrc[3] = 0x00020000;
     const int w = tid >> 6;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(
@@ -79,6 +80,13 @@ struct DmaOp {
                  :: "s"(m0), "v"(off[i]), "s"(rsrc) : "memory");   // m0: reserved, never allocated
   }
 };
+
+// s_waitcnt vmcnt(n) for the few counts the ring uses (the count must be an immediate)
+__device__ __forceinline__ void wait_vm(int n) {
+  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 __device__ __forceinline__ void dma_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -105,21 +113,43 @@ __device__ __forceinline__ u16x8 frag(const bf16_t* lds, const FragAddr& a) {
   return __builtin_bit_cast(u16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// grid.x = row tiles * col tiles (row-tile-major after an XCD-aware remap), grid.y = split-K slices.
-template <bool PARTIAL>
+// grid.x = row tiles * col tiles (XCD-aware order), grid.y = split-K slices.
+// BKT tokens per K-step, NST ring stages: the DMA of stage t + NST - 1 is issued in K-step t, so a stage has
+// NST - 1 K-steps to land; the barrier of K-step t waits only for stage t (counted vmcnt: the younger
+// stages' pieces may stay in flight across it).
+// OPT bit 0: s_setprio 1 around each step's MFMAs; bit 1: plain (non-XCD-aware) tile order.
+template <bool PARTIAL, int BKT, int NST, int OPT>
 __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                       void* __restrict__ C, int M, int Nr, int Nc, int m_per_split) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];   // 2 stages x (A | B), 128 KiB
+                                                       void* __restrict__ C, int M, int Nr, int Nc, int m_per_split,
+                                                       int xpr) {
+  constexpr int TILE_ELEMS = BKT * 256, STAGE = 2 * TILE_ELEMS, KS = BKT / 16;
+  constexpr int P = 2 * DmaOp<BKT>::NP;                              // DMA instructions per stage per thread
+  static_assert(NST * STAGE * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5;
   const int wr = w >> 2, wc = w & 3;                               // wave: rows 128*wr.., cols 64*wc..
-  // XCD-aware tile order: workgroups b and b + 8 share an XCD (round-robin dispatch), so give each XCD a
-  // contiguous run of tiles (neighbours share A row blocks / B column blocks in that XCD's L2).
-  const int ntiles = gridDim.x, xcd = blockIdx.x & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-  const int ctiles = Nc / BC;
-  const int n0 = (tile / ctiles) * BR, c0 = (tile % ctiles) * BC;
+  // XCD-aware tile order (speed only): workgroups b and b + 8 share an XCD under round-robin dispatch.
+  // xpr > 0: the R x C tile grid is cut into xpr x (8 / xpr) blocks, one per XCD, the cut chosen on the
+  // host to minimise the A row tiles + B column tiles an XCD's L2 must hold per K-step (GPT-2 1.3B fc1
+  // 32 x 8 tiles -> 4 x 2 blocks of 8 x 4; fc2 8 x 32 -> 1 x 8 blocks of 8 x 4).  xpr == 0: each XCD takes
+  // a contiguous run of tiles (grids the cut does not divide).
+  const int ctiles = Nc / BC, rtiles = Nr / BR;
+  const int ntiles = gridDim.x, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  int tr, tc;
+  if (OPT & 2) {
+    tr = blockIdx.x / ctiles; tc = blockIdx.x % ctiles;
+  } else if (xpr > 0) {
+    const int xpc = 8 / xpr, rb = rtiles / xpr, cb = ctiles / xpc;
+    tr = (xcd / xpc) * rb + loc / cb;
+    tc = (xcd % xpc) * cb + loc % cb;
+  } else {
+    const int q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    tr = tile / ctiles; tc = tile % ctiles;
+  }
+  const int n0 = tr * BR, c0 = tc * BC;
   const int mbeg = blockIdx.y * m_per_split, mend = min(M, mbeg + m_per_split);
-  const int T = (mend - mbeg) / BK;
+  const int T = (mend - mbeg) / BKT;
 
   // per-lane fragment offsets of token step 0: 4 A blocks (rows), 2 B blocks (cols).  Step s adds exactly
   // 16 * s rows (the swizzle depends on row & 3 only), a compile-time immediate on the ds_read.
@@ -136,25 +166,28 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  DmaOp da, db;
+  DmaOp<BKT> da, db;
   da.init(Nr, tid);
   db.init(Nc, tid);
   const bf16_t* Ab = A + n0;   // column offset of this tile; rows advance per K-step
   const bf16_t* Bb = B + c0;
-  if (T > 0) {
+  auto issue = [&](int stage_t, bf16_t* buf, int i) {   // piece i of both operands of stage stage_t
+    const int m = mbeg + stage_t * BKT;
+    da.piece(Ab + (int64_t)m * Nr, Nr, buf, tid, i);
+    db.piece(Bb + (int64_t)m * Nc, Nc, buf + TILE_ELEMS, tid, i);
+  };
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      da.piece(Ab + (int64_t)mbeg * Nr, Nr, smem, tid, i);
-      db.piece(Bb + (int64_t)mbeg * Nc, Nc, smem + TILE_ELEMS, tid, i);
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < T) {
+#pragma unroll
+      for (int i = 0; i < P / 2; ++i) issue(st, smem + st * STAGE, i);
     }
-  }
-  // K-loop unrolled by the 2-stage ring so every LDS address (read stage and DMA target stage) is a
-  // compile-time offset: hipcc then proves the DMA target disjoint from the stage being read and does not
-  // drain the prefetch (vmcnt(0)) before the fragment reads.
+
+  // K-loop unrolled by the ring so every LDS address (read stage and DMA target stage) is compile-time
   auto kstep = [&](const int t, const bf16_t* as, bf16_t* nb) {
-    dma_barrier();   // stage t resident; every wave is done with the other stage (read at step t-1)
-    const bool more = t + 1 < T;
-    const int mn = mbeg + (t + 1) * BK;
+    wait_vm(min(NST - 2, T - 1 - t) * P);   // stage t landed (this wave's pieces) ...
+    __syncthreads();                         // ... for every wave; all done reading stage t-1's buffer (= nb)
+    const bool more = t + NST - 1 < T;
     const bf16_t* bs = as + TILE_ELEMS;
     u16x8 a[4], b[2];
 #pragma unroll
@@ -162,29 +195,30 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < 2; ++j) b[j] = frag(bs, fb[j]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < KS; ++s) {
       u16x8 an[4], bn[2];
-      // the next stage's 8 DMA pieces ride in the first two steps' MFMA shadow (an LDS-DMA issue costs ~60
-      // cycles beside bare MFMAs; issued back to back after the barrier they were ~500 exposed cycles)
-      if (more && s < 2) {
-        da.piece(Ab + (int64_t)mn * Nr, Nr, nb, tid, 2 * s);
-        da.piece(Ab + (int64_t)mn * Nr, Nr, nb, tid, 2 * s + 1);
-        db.piece(Bb + (int64_t)mn * Nc, Nc, nb + TILE_ELEMS, tid, 2 * s);
-        db.piece(Bb + (int64_t)mn * Nc, Nc, nb + TILE_ELEMS, tid, 2 * s + 1);
+      // the new stage's DMA pieces ride in the first steps' MFMA shadow (an LDS-DMA issue costs ~60 cycles
+      // beside bare MFMAs; issued back to back after the barrier they were ~500 exposed cycles)
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < P / 2; ++i)
+          if (i * KS / (P / 2) == s || (KS < P / 2 && s == 0 && i >= KS)) issue(t + NST - 1, nb, i);
       }
-      if (s + 1 < 4) {   // next step's fragments issue ahead of this step's MFMAs, in their own region
+      if (s + 1 < KS) {   // next step's fragments issue ahead of this step's MFMAs, in their own region
 #pragma unroll
         for (int i = 0; i < 4; ++i) an[i] = frag(as + (s + 1) * 16 * 256, fa[i]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) bn[j] = frag(bs + (s + 1) * 16 * 256, fb[j]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 4) {
+      if (s + 1 < KS) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i] = an[i];
 #pragma unroll
@@ -192,9 +226,10 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
       }
     }
   };
-  for (int t = 0; t < T; t += 2) {
-    kstep(t, smem, smem + STAGE);
-    if (t + 1 < T) kstep(t + 1, smem + STAGE, smem);
+  for (int t = 0; t < T; t += NST) {
+#pragma unroll
+    for (int u = 0; u < NST; ++u)
+      if (t + u < T) kstep(t + u, smem + u * STAGE, smem + ((u + NST - 1) % NST) * STAGE);
   }
   // epilogue: acc[i][j] register r, lane l -> C[n0 + 128wr + 32i + acc_row(r, h)][c0 + 64wc + 32j + (l & 31)]
   const int col = c0 + 64 * wc + (lane & 31);
@@ -230,6 +265,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+
 }  // namespace
 
 // Shapes the kernel takes: Nr % 256 == 0, Nc % 256 == 0, M % (64 * splits) == 0, 16-B aligned rows.
@@ -239,21 +275,57 @@ PDT_API int pdt_wgrad_ok(int64_t M, int64_t Nr, int64_t Nc, int splits) {
 }
 
 // C[Nr, Nc] (bf16) = A[M, Nr]^T B[M, Nc]; splits > 1 needs an fp32 workspace of splits * Nr * Nc floats.
+namespace {
+
+// kernel variant: 1 = BK 64 x 2 stages (default), 2 = BK 32 x 4 stages (measured 1-6 % slower), 3 = 1 + s_setprio
+// around the MFMAs, 4 = 1 in plain row-major tile order (no XCD blocking); PDT_WGRAD_VARIANT or pdt_wgrad_set_variant
+int g_wgrad_variant = -1;
+int wgrad_variant() {
+  if (g_wgrad_variant < 0) { const char* e = getenv("PDT_WGRAD_VARIANT"); g_wgrad_variant = e ? atoi(e) : 1; }
+  return g_wgrad_variant;
+}
+
+template <int BKT, int NST, int OPT>
+void launch_wgrad(const void* A, const void* B, void* C, int64_t M, int64_t Nr, int64_t Nc, int splits, float* ws,
+                  hipStream_t st) {
+  const int R = (int)(Nr / BR), Cc = (int)(Nc / BC), tiles = R * Cc;
+  const int mps = (int)(M / splits);
+  dim3 grid(tiles, splits);
+  int xpr = 0, best = 1 << 30;   // XCD block cut: xpr row parts x (8 / xpr) column parts
+  for (int pr = 1; pr <= 8; pr *= 2) {
+    const int pc = 8 / pr;
+    if (R % pr || Cc % pc) continue;
+    const int cost = R / pr + Cc / pc;
+    if (cost < best) { best = cost; xpr = pr; }
+  }
+  if (splits == 1) {
+    wgrad_kernel<false, BKT, NST, OPT><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (int)M, (int)Nr,
+                                                        (int)Nc, mps, xpr);
+  } else {
+    wgrad_kernel<true, BKT, NST, OPT><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, ws, (int)M, (int)Nr,
+                                                       (int)Nc, mps, xpr);
+    const int64_t n4 = Nr * Nc / 4;
+    splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, st>>>(ws, (bf16_t*)C, n4, splits, Nr * Nc);
+  }
+}
+
+}  // namespace
+
+PDT_API int pdt_wgrad_set_variant(int v) {
+  if (v > 0) g_wgrad_variant = v;
+  return wgrad_variant();
+}
+
+// C[Nr, Nc] (bf16) = A[M, Nr]^T B[M, Nc]; splits > 1 needs an fp32 workspace of splits * Nr * Nc floats.
 PDT_API int pdt_wgrad_bf16(const void* A, const void* B, void* C, int64_t M, int64_t Nr, int64_t Nc, int splits,
                            float* ws, hipStream_t st) {
   if (!pdt_wgrad_ok(M, Nr, Nc, splits)) return (int)hipErrorInvalidValue;
-  const int tiles = (int)((Nr / BR) * (Nc / BC));
-  const int mps = (int)(M / splits);
-  dim3 grid(tiles, splits);
-  if (splits == 1) {
-    wgrad_kernel<false><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (int)M, (int)Nr, (int)Nc,
-                                                      mps);
-  } else {
-    if (!ws) return (int)hipErrorInvalidValue;
-    wgrad_kernel<true><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, ws, (int)M, (int)Nr, (int)Nc,
-                                                     mps);
-    const int64_t n4 = Nr * Nc / 4;
-    splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, st>>>(ws, (bf16_t*)C, n4, splits, Nr * Nc);
+  if (splits > 1 && !ws) return (int)hipErrorInvalidValue;
+  switch (wgrad_variant()) {
+    case 2: launch_wgrad<32, 4, 0>(A, B, C, M, Nr, Nc, splits, ws, st); break;
+    case 3: launch_wgrad<64, 2, 1>(A, B, C, M, Nr, Nc, splits, ws, st); break;
+    case 4: launch_wgrad<64, 2, 2>(A, B, C, M, Nr, Nc, splits, ws, st); break;
+    default: launch_wgrad<64, 2, 0>(A, B, C, M, Nr, Nc, splits, ws, st); break;
   }
   return (int)hipGetLastError();
 }

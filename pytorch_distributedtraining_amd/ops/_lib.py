@@ -110,6 +110,7 @@ _SIGS = {
     "pdt_pixel_shuffle_affine_bwd": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int,
                                      c_float, c_void_p, c_int, c_void_p],
     "pdt_wgrad_ok": [c_int64, c_int64, c_int64, c_int],
+    "pdt_wgrad_set_variant": [c_int],
     "pdt_wgrad_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -1,9 +1,9 @@
 """Linear layer with an MI355X-shaped backward:
 
 * large bf16 weight gradients dW = dY^T X run on the hand MFMA kernel ``csrc/kernels/gemm_wgrad.hip``
-  (both operands token-major, read transposed from LDS; 6-21 % faster than hipBLASLt's kernels for this
-  layout on the GPT-2 1.3B / Llama-3 8B shapes, profiles/r2_wgrad_hip_vs_hipblaslt.jsonl);
-  ``PDT_WGRAD_HIP=0`` returns them to hipBLASLt;
+  (both operands token-major, read transposed from LDS) where it is measured faster than hipBLASLt for the
+  shape (timed once per shape; profiles/r2_wgrad_hip_vs_hipblaslt.jsonl); ``PDT_WGRAD_HIP=0/1`` forces
+  hipBLASLt / the hand kernel;
 
 * the bias gradient is reduced with the framework's column-sum kernel (2x the bandwidth of the generic
   reduction torch uses for ``grad_output.sum(0)``);
@@ -51,7 +51,36 @@ def _split_k(m: int, n: int, k: int) -> int:
     return s
 
 
-HIP_WGRAD = os.environ.get("PDT_WGRAD_HIP", "1") == "1"
+# PDT_WGRAD_HIP: "auto" (default: per shape, the faster of the hand kernel and hipBLASLt, timed once on the
+# shape's first uncaptured call), "1" (always the hand kernel where it applies), "0" (never)
+HIP_WGRAD = os.environ.get("PDT_WGRAD_HIP", "auto")
+_WGRAD_CHOICE: dict = {}
+
+
+def _timed_ms(fn, iters: int = 3) -> float:
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Hand kernel vs hipBLASLt for this weight-gradient shape.  Measured, not assumed: the two trade places
+    by shape and by box (GPT-2 1.3B attention projection +12 %, fc1 +3 %, Llama-3 8B qkv -14 % on one box;
+    the flagship gained 3 % on another, profiles/r2_wgrad_hip_vs_hipblaslt.jsonl)."""
+    if HIP_WGRAD != "auto":
+        return HIP_WGRAD == "1"
+    key = (dy2.shape, x2.shape[1], dy2.device)
+    c = _WGRAD_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip_wgrad(dy2, x2)) < _timed_ms(lambda: torch.mm(dy2.t(), x2))
+    return c
 
 
 def hip_wgrad_splits(m: int, n: int, k: int, cus: int = 256) -> int:
@@ -76,7 +105,7 @@ def hip_wgrad_splits(m: int, n: int, k: int, cus: int = 256) -> int:
 def hip_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> bool:
     m, n = dy2.shape
     k = x2.shape[1]
-    return (HIP_WGRAD and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+    return (HIP_WGRAD != "0" and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
             and out_dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0 and m >= 4096 and n % 256 == 0
             and k % 256 == 0 and bool(_lib.require().pdt_wgrad_ok(m, n, k, hip_wgrad_splits(m, n, k))))
@@ -101,7 +130,7 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.
     k = x2.shape[1]
     if not dy2.is_cuda:
         return torch.mm(dy2.t(), x2).to(out_dtype)
-    if hip_wgrad_ok(dy2, x2, out_dtype):
+    if hip_wgrad_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2):
         return hip_wgrad(dy2, x2)
     if not _tall_skinny(m, n, k):
         sk = _split_k(m, n, k)
