@@ -31,13 +31,21 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BR = 256, BC = 256, NTH = 512;
+constexpr int BR = 256, BC = 256;
 constexpr int BK = 64;                        // token granularity every split / M must respect
 
 __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                  0, 0, 0);
 }
+
+// Accumulate into an AGPR-resident tile (the 4-wave variant's 256 accumulators do not fit beside the
+// fragments in the 256 arch VGPRs).  acc_fence() before any VALU read: the hazard recognizer does not
+// see through inline asm.
+__device__ __forceinline__ void mfma32_acc(f32x16& acc, const u16x8& a, const u16x8& b) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"); }
 
 // 16-B chunk swizzle of a 512-B LDS row (32 chunks)
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r & 3) << 2); }
@@ -49,9 +57,9 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r & 3) << 2); }
 // element (T8): per K-step only the SGPR descriptor moves, the per-lane byte offsets are computed once.
 // (global_load_lds through a plain pointer made hipcc wait vmcnt(0) before the first LDS read after it --
 // it cannot tell the DMA target stage from the stage being read -- which serialised every prefetch.)
-template <int BKT>
+template <int BKT, int NTH>
 struct DmaOp {
-  static constexpr int NP = BKT / 16;   // 16-B chunks per thread per operand tile (BKT rows x 512 B / 512 thr)
+  static constexpr int NP = BKT * 32 / NTH;   // 16-B chunks per thread per operand tile (BKT rows x 512 B)
   uint32_t off[NP];
   __device__ __forceinline__ void init(int64_t ld, int tid) {
     const int w = tid >> 6, lane = tid & 63;
@@ -118,16 +126,19 @@ __device__ __forceinline__ u16x8 frag(const bf16_t* lds, const FragAddr& a) {
 // NST - 1 K-steps to land; the barrier of K-step t waits only for stage t (counted vmcnt: the younger
 // stages' pieces may stay in flight across it).
 // OPT bit 0: s_setprio 1 around each step's MFMAs; bit 1: plain (non-XCD-aware) tile order.
-template <bool PARTIAL, int BKT, int NST, int OPT>
+// NTH = 512: 8 waves as 2 x 4, each a 128 x 64 block (4 x 2 MFMA tiles, 2 waves per SIMD);
+// NTH = 256: 4 waves as 2 x 2, each a 128 x 128 block (4 x 4 MFMA tiles, 256 accumulators, 1 wave per SIMD).
+template <bool PARTIAL, int BKT, int NST, int OPT, int NTH>
 __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                        void* __restrict__ C, int M, int Nr, int Nc, int m_per_split,
                                                        int xpr) {
   constexpr int TILE_ELEMS = BKT * 256, STAGE = 2 * TILE_ELEMS, KS = BKT / 16;
-  constexpr int P = 2 * DmaOp<BKT>::NP;                              // DMA instructions per stage per thread
+  constexpr int P = 2 * DmaOp<BKT, NTH>::NP;                         // DMA instructions per stage per thread
+  constexpr int WN = NTH == 512 ? 4 : 2, JB = NTH == 512 ? 2 : 4;    // wave columns, 32-col blocks per wave
   static_assert(NST * STAGE * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5;
-  const int wr = w >> 2, wc = w & 3;                               // wave: rows 128*wr.., cols 64*wc..
+  const int wr = w / WN, wc = w % WN;                              // wave: rows 128*wr.., cols 32*JB*wc..
   // XCD-aware tile order (speed only): workgroups b and b + 8 share an XCD under round-robin dispatch.
   // xpr > 0: the R x C tile grid is cut into xpr x (8 / xpr) blocks, one per XCD, the cut chosen on the
   // host to minimise the A row tiles + B column tiles an XCD's L2 must hold per K-step (GPT-2 1.3B fc1
@@ -153,20 +164,20 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
 
   // per-lane fragment offsets of token step 0: 4 A blocks (rows), 2 B blocks (cols).  Step s adds exactly
   // 16 * s rows (the swizzle depends on row & 3 only), a compile-time immediate on the ds_read.
-  FragAddr fa[4], fb[2];
+  FragAddr fa[4], fb[JB];
 #pragma unroll
   for (int i = 0; i < 4; ++i) fa[i] = frag_addr(lane, 128 * wr + 32 * i, 0);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) fb[j] = frag_addr(lane, 64 * wc + 32 * j, 0);
-  f32x16 acc[4][2];
+  for (int j = 0; j < JB; ++j) fb[j] = frag_addr(lane, 32 * JB * wc + 32 * j, 0);
+  f32x16 acc[4][JB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JB; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  DmaOp<BKT> da, db;
+  DmaOp<BKT, NTH> da, db;
   da.init(Nr, tid);
   db.init(Nc, tid);
   const bf16_t* Ab = A + n0;   // column offset of this tile; rows advance per K-step
@@ -189,40 +200,43 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
     __syncthreads();                         // ... for every wave; all done reading stage t-1's buffer (= nb)
     const bool more = t + NST - 1 < T;
     const bf16_t* bs = as + TILE_ELEMS;
-    u16x8 a[4], b[2];
+    u16x8 a[4], b[JB];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = frag(as, fa[i]);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = frag(bs, fb[j]);
+    for (int j = 0; j < JB; ++j) b[j] = frag(bs, fb[j]);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      u16x8 an[4], bn[2];
+      u16x8 an[4], bn[JB];
       // the new stage's DMA pieces ride in the first steps' MFMA shadow (an LDS-DMA issue costs ~60 cycles
       // beside bare MFMAs; issued back to back after the barrier they were ~500 exposed cycles)
       if (more) {
 #pragma unroll
         for (int i = 0; i < P / 2; ++i)
-          if (i * KS / (P / 2) == s || (KS < P / 2 && s == 0 && i >= KS)) issue(t + NST - 1, nb, i);
+          if (i * (KS > 1 ? KS / 2 : 1) / (P / 2) == s) issue(t + NST - 1, nb, i);   // first half of the K-step
       }
       if (s + 1 < KS) {   // next step's fragments issue ahead of this step's MFMAs, in their own region
 #pragma unroll
         for (int i = 0; i < 4; ++i) an[i] = frag(as + (s + 1) * 16 * 256, fa[i]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bn[j] = frag(bs + (s + 1) * 16 * 256, fb[j]);
+        for (int j = 0; j < JB; ++j) bn[j] = frag(bs + (s + 1) * 16 * 256, fb[j]);
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < JB; ++j) {
+          if constexpr (NTH == 256) mfma32_acc(acc[i][j], a[i], b[j]);
+          else acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+        }
       if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < KS) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i] = an[i];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = bn[j];
+        for (int j = 0; j < JB; ++j) b[j] = bn[j];
       }
     }
   };
@@ -231,15 +245,16 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const bf16_t* __restrict_
     for (int u = 0; u < NST; ++u)
       if (t + u < T) kstep(t + u, smem + u * STAGE, smem + ((u + NST - 1) % NST) * STAGE);
   }
-  // epilogue: acc[i][j] register r, lane l -> C[n0 + 128wr + 32i + acc_row(r, h)][c0 + 64wc + 32j + (l & 31)]
-  const int col = c0 + 64 * wc + (lane & 31);
+  if constexpr (NTH == 256) acc_fence();
+  // epilogue: acc[i][j] register r, lane l -> C[n0 + 128wr + 32i + acc_row(r, h)][c0 + 32JB wc + 32j + (l & 31)]
+  const int col = c0 + 32 * JB * wc + (lane & 31);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = n0 + 128 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < JB; ++j) {
         if constexpr (PARTIAL) {
           float* Cp = reinterpret_cast<float*>(C) + (int64_t)blockIdx.y * Nr * Nc;
           Cp[(int64_t)row * Nc + col + 32 * j] = acc[i][j][r];
@@ -278,14 +293,16 @@ PDT_API int pdt_wgrad_ok(int64_t M, int64_t Nr, int64_t Nc, int splits) {
 namespace {
 
 // kernel variant: 1 = BK 64 x 2 stages (default), 2 = BK 32 x 4 stages (measured 1-6 % slower), 3 = 1 + s_setprio
-// around the MFMAs, 4 = 1 in plain row-major tile order (no XCD blocking); PDT_WGRAD_VARIANT or pdt_wgrad_set_variant
+// around the MFMAs, 4 = 1 in plain row-major tile order (no XCD blocking).  (A 4-wave variant with 128 x 128
+// blocks per wave, NTH = 256, needs 256 AGPR accumulators + ~300 VGPRs and hipcc spills 234 of them: not
+// launched); PDT_WGRAD_VARIANT or pdt_wgrad_set_variant
 int g_wgrad_variant = -1;
 int wgrad_variant() {
   if (g_wgrad_variant < 0) { const char* e = getenv("PDT_WGRAD_VARIANT"); g_wgrad_variant = e ? atoi(e) : 1; }
   return g_wgrad_variant;
 }
 
-template <int BKT, int NST, int OPT>
+template <int BKT, int NST, int OPT, int NTH = 512>
 void launch_wgrad(const void* A, const void* B, void* C, int64_t M, int64_t Nr, int64_t Nc, int splits, float* ws,
                   hipStream_t st) {
   const int R = (int)(Nr / BR), Cc = (int)(Nc / BC), tiles = R * Cc;
@@ -299,10 +316,10 @@ void launch_wgrad(const void* A, const void* B, void* C, int64_t M, int64_t Nr, 
     if (cost < best) { best = cost; xpr = pr; }
   }
   if (splits == 1) {
-    wgrad_kernel<false, BKT, NST, OPT><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (int)M, (int)Nr,
+    wgrad_kernel<false, BKT, NST, OPT, NTH><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (int)M, (int)Nr,
                                                         (int)Nc, mps, xpr);
   } else {
-    wgrad_kernel<true, BKT, NST, OPT><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, ws, (int)M, (int)Nr,
+    wgrad_kernel<true, BKT, NST, OPT, NTH><<<grid, NTH, 0, st>>>((const bf16_t*)A, (const bf16_t*)B, ws, (int)M, (int)Nr,
                                                        (int)Nc, mps, xpr);
     const int64_t n4 = Nr * Nc / 4;
     splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, st>>>(ws, (bf16_t*)C, n4, splits, Nr * Nc);
