@@ -326,7 +326,43 @@ __device__ __forceinline__ void dma_tile(const bf16_t* base, int64_t row_stride,
 // descriptor (base = first row of the window, num_records = bytes of the rows that exist) is rebuilt
 // in SGPRs, so `buffer_load_dwordx4 ... offen lds` issues with no VALU address math, and rows past the
 // end of the tensor come back as zeros from the range check (callers mask them) -- no clamping path.
-template <int D>
+// LDS-DMA issued from inline asm, hidden from hipcc's waitcnt pass.  For the builtin forms the pass cannot
+// tell the ring stage being filled from the stage being read, and in the backward kernels it drained the
+// freshly issued prefetch (s_waitcnt vmcnt(0)) before the tile's first ds_read -- the next tile's DMA
+// latency exposed on every tile.  Ordering is then entirely the rings' dma_barrier() (explicit vmcnt(0) +
+// barrier before a stage is read); hipcc's own counted waits for its loads only over-wait beside these.
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i make_rsrc(const void* base, int num_bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  v4i r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = __builtin_amdgcn_readfirstlane(num_bytes);   // range check: lanes past it read zeros
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t voff, const void* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(m0), "v"(voff), "s"(rsrc) : "memory");   // m0: reserved, never allocated by hipcc
+}
+__device__ __forceinline__ void dma4_asm(const v4i& rsrc, uint32_t voff, const void* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "s"(m0), "v"(voff), "s"(rsrc) : "memory");
+}
+
+// Consume registers loaded by plain global loads in a kernel prologue, so hipcc's wait for them lands
+// HERE, before the tile loop.  Otherwise its first use sits inside the loop, the waitcnt pass (merging the
+// loop entry with the back edge) re-emits the wait every tile, and -- blind to the inline-asm DMA queued
+// behind those loads -- as vmcnt(0), which drains the tile prefetch.
+template <int N>
+__device__ __forceinline__ void retire(const u16x8 (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" :: "v"(x[i]));
+}
+
+template <int D, bool ASM = true>
 struct DmaLane {
   static constexpr int RPI = 1024 / (D * 2), NI = 16 / RPI, LPR = 64 / RPI;
   uint32_t off[NI];
@@ -340,15 +376,22 @@ struct DmaLane {
   }
   __device__ __forceinline__ void issue(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
                                         int w) const {
-#if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
     const int rows_left = nrows - row0;
     const int bytes = rows_left > 0 ? (int)((int64_t)(rows_left - 1) * row_stride * 2 + D * 2) : 0;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * row_stride), 0, bytes, 0x00020000);
+    if constexpr (ASM) {
+      const v4i rsrc = make_rsrc(base + (int64_t)row0 * row_stride, bytes);
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off[i], 0, 0, 0);
+      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off[i], lds + (16 * w + RPI * i) * D);
+    } else {
+#if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * row_stride), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off[i], 0, 0,
+                                                 0);
 #endif
+    }
   }
 };
 
@@ -854,6 +897,7 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
       for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
     }
   }
+  retire(qf);
   f32x16 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
@@ -1136,10 +1180,11 @@ __global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
 // rows travel by LDS-DMA too (4-byte pieces), so no ordinary global load sits in the loop to force
 // a vmcnt(0) drain of the prefetch.
 // ------------------------------------------------------------------------------------------------
+// one wave: 64 fp32 rows [row0, row0 + 64) of a row vector into LDS (rows past nrows read as 0: they pair with
+// the zero Q / dO rows of the ragged tile and contribute nothing)
 __device__ __forceinline__ void dma_f32_row(const float* src, int row0, int nrows, float* lds, int lane) {
-  int g = row0 + lane;
-  g = g < nrows ? g : nrows - 1;
-  __builtin_amdgcn_global_load_lds((const void*)(src + g), (lds_void*)lds, 4, 0, 0);
+  const int left = nrows - row0;
+  dma4_asm(make_rsrc(src + row0, left > 0 ? left * 4 : 0), (uint32_t)lane * 4, lds);
 }
 
 // transposed-fragment offsets for a [TILE][D] swizzled image (rows kb + 4(g>>1) + q (+8), column
@@ -1554,6 +1599,8 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
       for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
     }
   }
+  retire(kf);
+  retire(vf);
   f32x16 dk[DT], dv[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
@@ -1693,7 +1740,8 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int kend = p.Sk;
   if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
   const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  DmaLane<D> lk, lv;
+  // builtin DMA here: the inline-asm form's SGPR-quad operands cost this 256-VGPR kernel 25 more spills
+  DmaLane<D, false> lk, lv;
   lk.init(p.k_ss, w, lane);
   lv.init(p.v_ss, w, lane);
   if (ntiles > 0) {
@@ -1713,6 +1761,9 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
   }
   const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
   const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  retire(qf);
+  retire(gf);
+  asm volatile("" :: "v"(nlse2), "v"(dl));
   f32x16 dq[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
