@@ -1719,8 +1719,8 @@ struct BwdQTile {
   }
 };
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
+template <int D, bool CAUSAL, int OCC = 2>
+__global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
 
@@ -1740,8 +1740,8 @@ __global__ __launch_bounds__(NT, 2) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int kend = p.Sk;
   if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
   const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  // builtin DMA here: the inline-asm form's SGPR-quad operands cost this 256-VGPR kernel 25 more spills
-  DmaLane<D, false> lk, lv;
+  // OCC 2 (256 VGPRs): builtin DMA -- the inline-asm form's SGPR-quad operands cost 25 more spills there
+  DmaLane<D, OCC == 1> lk, lv;
   lk.init(p.k_ss, w, lane);
   lv.init(p.v_ss, w, lane);
   if (ntiles > 0) {
@@ -1859,6 +1859,15 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
       else fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
       if (variant == 5) fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
       else fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+    }
+  } else if (variant == 7) {   // v3 with the dQ kernel at one wave per SIMD (inline-asm DMA, no spills):
+                               // 4-8 % slower than variant 3's two waves per SIMD (profiles/r2_attn_experiments.txt)
+    if (causal) {
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
+      fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(p);
     }
   } else if (variant == 3) {   // v3, one wave per SIMD for dK/dV (no spills)
     if (causal) {
