@@ -343,13 +343,15 @@ __device__ __forceinline__ v4i make_rsrc(const void* base, int num_bytes) {
 }
 __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t voff, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_dst);
+  // no "memory" clobber: the ring barriers (asm memory clobber + __syncthreads) already order every LDS access
+  // of the target stage around the DMA, and leaving the compiler free to move other accesses lowers pressure
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :: "s"(m0), "v"(voff), "s"(rsrc) : "memory");   // m0: reserved, never allocated by hipcc
+               :: "s"(m0), "v"(voff), "s"(rsrc));   // m0: reserved, never allocated by hipcc
 }
 __device__ __forceinline__ void dma4_asm(const v4i& rsrc, uint32_t voff, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_dst);
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
-               :: "s"(m0), "v"(voff), "s"(rsrc) : "memory");
+               :: "s"(m0), "v"(voff), "s"(rsrc));
 }
 
 // Consume registers loaded by plain global loads in a kernel prologue, so hipcc's wait for them lands
@@ -365,15 +367,16 @@ __device__ __forceinline__ void retire(const u16x8 (&x)[N]) {
 template <int D, bool ASM = true>
 struct DmaLane {
   static constexpr int RPI = 1024 / (D * 2), NI = 16 / RPI, LPR = 64 / RPI;
-  uint32_t off[NI];
+  uint32_t off_[NI];
   __device__ __forceinline__ void init(int64_t row_stride, int w, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int row = 16 * w + RPI * i + lane / LPR;
       const int c = (lane % LPR) ^ swz_f<D>(row);
-      off[i] = (uint32_t)((row * row_stride + c * 8) * 2);
+      off_[i] = (uint32_t)((row * row_stride + c * 8) * 2);
     }
   }
+  __device__ __forceinline__ uint32_t off(int i, int) const { return off_[i]; }
   __device__ __forceinline__ void issue(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
                                         int w) const {
     const int rows_left = nrows - row0;
@@ -381,15 +384,15 @@ struct DmaLane {
     if constexpr (ASM) {
       const v4i rsrc = make_rsrc(base + (int64_t)row0 * row_stride, bytes);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off[i], lds + (16 * w + RPI * i) * D);
+      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off(i, w), lds + (16 * w + RPI * i) * D);
     } else {
 #if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
       const __amdgpu_buffer_rsrc_t rsrc =
           __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * row_stride), 0, bytes, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off[i], 0, 0,
-                                                 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off(i, w), 0,
+                                                 0, 0);
 #endif
     }
   }
@@ -1740,7 +1743,8 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int kend = p.Sk;
   if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
   const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  // OCC 2 (256 VGPRs): builtin DMA -- the inline-asm form's SGPR-quad operands cost 25 more spills there
+  // OCC 2 (256 VGPRs): the builtin DMA -- the inline-asm form spills 21-27 VGPRs here (scratch reloads with
+  // vmcnt(0) before every DMA), even with the per-lane offsets recomputed at each issue
   DmaLane<D, OCC == 1> lk, lv;
   lk.init(p.k_ss, w, lane);
   lv.init(p.v_ss, w, lane);
