@@ -51,6 +51,12 @@ def parse():
                     help="world > 1: after timing, measure exposed vs communication-only time (untimed)")
     ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"], help="swinir-stoke precision")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="gpt2-ddp at one rank: capture the whole training step (fwd, bwd, clip, fused AdamW) in a "
+                         "HIP graph and replay it (utils.graphs.GraphedStep)")
+    ap.add_argument("--fp8", type=int, default=0,
+                    help="gpt2/llama: run the transformer linears' GEMMs in fp8 (ops.fp8.fp8_autocast, delayed "
+                         "scaling); reported with dtype 'fp8-linears' -- never the bf16 headline")
     return ap.parse_args()
 
 
@@ -266,7 +272,8 @@ def bench_gpt2(args, comm, dev, world, rank):
         params = model.optimizer_parameters()
         sharded = False
         par = f"dp{world}"
-    opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    graph = bool(args.graph) and not fsdp and world == 1 and dev.type == "cuda"
+    opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, capturable=graph)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     vocab = 128000 if llama else 50257
@@ -294,16 +301,36 @@ def bench_gpt2(args, comm, dev, world, rank):
         c.checkpoint_layers = L - int(t.item())
         log(f"[bench] activation checkpointing sized to HBM: {c.checkpoint_layers}/{L} layers recomputed")
 
+    from pytorch_distributedtraining_amd.ops.fp8 import fp8_autocast
+
     def step():
         b = batches[state["i"] % len(batches)]
         state["i"] += 1
-        loss = model(b[:, :-1], labels=b[:, 1:])
+        with fp8_autocast(enabled=bool(args.fp8)):
+            loss = model(b[:, :-1], labels=b[:, 1:])
         loss.backward()
         _, coef, found = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=sharded, apply=False)
         opt.step(grad_scale=coef)
         opt.zero_grad(set_to_none=True)
         state["loss"] = loss
 
+    if graph:
+        from pytorch_distributedtraining_amd.utils.graphs import GraphedStep
+        static = batches[0].clone()
+
+        def graph_body(b):
+            opt.zero_grad(set_to_none=False)          # gradients keep their addresses across replays
+            loss = model(b[:, :-1], labels=b[:, 1:])
+            loss.backward()
+            _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
+            opt.step(grad_scale=coef)
+            return loss.detach()
+        graphed = GraphedStep(graph_body, static, warmup=2)
+
+        def step():                                   # noqa: F811 - the graphed replacement
+            b = batches[state["i"] % len(batches)]
+            state["i"] += 1
+            state["loss"] = graphed(b)
     if ckpt_on and args.act_ckpt_layers == "auto":
         step()
         torch.cuda.synchronize(dev)
@@ -319,9 +346,10 @@ def bench_gpt2(args, comm, dev, world, rank):
         metric = f"tokens/sec {name} FSDP + act-ckpt (whole node)"
     return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", **comm_fields(world), "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": "weak", **comm_fields(world), "vs_baseline": None,
+            "dtype": "fp8-linears" if args.fp8 else "bf16", "data": "synthetic",
             "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
-                       "micro_batch_per_gpu": mb, "params": nparams, "sharding": "full_shard" if args.reshard else
+                       "micro_batch_per_gpu": mb, "params": nparams, "hip_graph": graph, "sharding": "full_shard" if args.reshard else
                        "shard_grad_op", "optimizer": "fused AdamW + global-norm clip",
                        **({"act_ckpt_layers": inner.config.checkpoint_layers
                            if inner.config.checkpoint_layers is not None else

@@ -1,0 +1,141 @@
+// fp8 training support for gfx950 (OCP e4m3fn / e5m2 -- MI355X's encodings, not MI300's fnuz):
+//
+//  * fp8_cast_transpose: one HBM pass over a bf16/fp32 activation, weight or gradient [R, C] that writes
+//    the scaled fp8 copy in row layout [R, C] AND its transpose [C, R] (either optional) and max-reduces
+//    |x| into the tensor's delayed-scaling amax slot.  The three GEMMs of an fp8 linear need each operand
+//    in two layouts (forward x W^T, data-gradient dY W, weight-gradient dY^T X: hipBLASLt takes A
+//    row-major and B column-major), so producing both from one read halves the cast traffic against a
+//    cast followed by a transpose.  64 x 64 tiles staged through LDS; each block walks several tiles so
+//    the amax atomic is issued once per block, not once per tile.
+//  * fp8_update_scales: the delayed-scaling bookkeeping (TransformerEngine's "max" recipe) for a range of
+//    a module's tensor slots in ONE launch: push the last iteration's amax into the history, clear it,
+//    scale = fmax / max(history) / 2^margin, scale_inv = 1 / scale.  Keeps the whole recipe on the device
+//    (no host sync per layer).
+#include "common.h"
+
+#include <hip/hip_fp8.h>
+
+namespace pdt {
+namespace {
+
+constexpr int CT_TS = 64;       // tile edge
+constexpr int CT_LD = 68;       // LDS row stride in bytes (17 words: column gathers spread over banks)
+
+template <int FMT>
+__device__ __forceinline__ uint8_t to_fp8(float v) {
+  return __hip_cvt_float_to_fp8(v, __HIP_SATFINITE, FMT == 0 ? __HIP_E4M3 : __HIP_E5M2);
+}
+
+// x [R, C] (T = bf16 or fp32), R % 64 == 0, C % 64 == 0.  q [R, C] and qt [C, R] may each be null;
+// with both null the kernel only measures amax (first-iteration "current scaling").
+template <typename T, int FMT>
+__global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
+                                                                 uint8_t* __restrict__ qt, int R, int C,
+                                                                 const float* __restrict__ scale,
+                                                                 unsigned int* __restrict__ amax_bits) {
+  __shared__ uint32_t tile[CT_TS * CT_LD / 4];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const int lc = (tid & 7) * 8, lr = tid >> 3;   // 8 threads x 8 columns per row, 32 rows per pass
+  const float sc = scale ? *scale : 1.f;
+  const int tiles_c = C / CT_TS;
+  const int ntiles = tiles_c * (R / CT_TS);
+  float amax = 0.f;
+  uint8_t* t8 = reinterpret_cast<uint8_t*>(tile);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int r0 = (t / tiles_c) * CT_TS, c0 = (t % tiles_c) * CT_TS;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int r = lr + 32 * p;
+      float v[8];
+      Vec8<T>::load(x + (int64_t)(r0 + r) * C + c0 + lc, v);
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        amax = fmaxf(amax, fmaxf(fabsf(v[k]), fabsf(v[k + 4])));
+        lo |= (uint32_t)to_fp8<FMT>(v[k] * sc) << (8 * k);
+        hi |= (uint32_t)to_fp8<FMT>(v[k + 4] * sc) << (8 * k);
+      }
+      if (q) *reinterpret_cast<uint2*>(q + (int64_t)(r0 + r) * C + c0 + lc) = make_uint2(lo, hi);
+      if (qt) {
+        uint32_t* dst = tile + (r * CT_LD + lc) / 4;
+        dst[0] = lo;
+        dst[1] = hi;
+      }
+    }
+    if (qt) {
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int c = lr + 32 * p;              // output row (= input column)
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          lo |= (uint32_t)t8[(lc + k) * CT_LD + c] << (8 * k);
+          hi |= (uint32_t)t8[(lc + 4 + k) * CT_LD + c] << (8 * k);
+        }
+        *reinterpret_cast<uint2*>(qt + (int64_t)(c0 + c) * R + r0 + lc) = make_uint2(lo, hi);
+      }
+      __syncthreads();                          // tile reused by the next iteration
+    }
+  }
+  if (amax_bits) {
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) red[tid >> 6] = amax;
+    __syncthreads();
+    if (tid == 0) atomicMax(amax_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  }
+}
+
+// Slots [s0, s1) of a module's fp8 meta: hist [n_slots, H], cur [n_slots] (amax bits), scale / scale_inv
+// [n_slots].  One thread per slot (a module has 3).
+__global__ void fp8_update_scales_kernel(float* __restrict__ hist, unsigned int* __restrict__ cur,
+                                         float* __restrict__ scale, float* __restrict__ scale_inv, int H, int s0,
+                                         int s1, float fmax, float margin_mul) {
+  const int s = s0 + threadIdx.x;
+  if (s >= s1) return;
+  float* h = hist + (int64_t)s * H;
+  const float a = __uint_as_float(cur[s]);
+  float m = a;
+  for (int i = H - 1; i > 0; --i) {
+    const float v = h[i - 1];
+    h[i] = v;
+    m = fmaxf(m, v);
+  }
+  h[0] = a;
+  cur[s] = 0u;
+  if (m > 0.f && isfinite(m)) {
+    const float sc = fmax / m * margin_mul;
+    scale[s] = sc;
+    scale_inv[s] = 1.f / sc;
+  }
+}
+
+}  // namespace
+}  // namespace pdt
+
+using namespace pdt;
+
+// fmt: 0 = e4m3fn, 1 = e5m2; dt: kF32 / kBF16.  Returns hipErrorInvalidValue for unsupported shapes
+// (the Python side then takes its torch path).
+PDT_API int pdt_fp8_cast_transpose(const void* x, void* q, void* qt, int R, int C, int dt, int fmt,
+                                   const float* scale, unsigned int* amax_bits, hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS) return (int)hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(x) & 15) return (int)hipErrorInvalidValue;
+  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
+  const int grid = (int)(tiles < 2048 ? tiles : 2048);   // 8 blocks per CU, <= 2048 amax atomics
+#define PDT_L(T, F) \
+  fp8_cast_transpose_kernel<T, F><<<grid, 256, 0, st>>>((const T*)x, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits)
+  if (dt == kBF16) { if (fmt == 0) PDT_L(bf16_t, 0); else PDT_L(bf16_t, 1); }
+  else if (dt == kF32) { if (fmt == 0) PDT_L(float, 0); else PDT_L(float, 1); }
+  else return (int)hipErrorInvalidValue;
+#undef PDT_L
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_fp8_update_scales(float* hist, unsigned int* cur, float* scale, float* scale_inv, int H, int s0, int s1,
+                                  float fmax, float margin_mul, hipStream_t st) {
+  if (H <= 0 || s1 <= s0 || s1 - s0 > 64) return (int)hipErrorInvalidValue;
+  fp8_update_scales_kernel<<<1, 64, 0, st>>>(hist, cur, scale, scale_inv, H, s0, s1, fmax, margin_mul);
+  return (int)hipGetLastError();
+}

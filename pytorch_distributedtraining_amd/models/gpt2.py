@@ -81,7 +81,7 @@ class MLP(nn.Module):
         self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        h = linear(x, self.c_fc.weight)              # hipBLASLt GEMM, bias folded into the GELU kernel
+        h = self.c_fc.matmul(x)                      # GEMM without bias: the bias is folded into the GELU kernel
         h = bias_gelu(h, self.c_fc.bias, approximate="tanh")
         return self.c_proj(h)
 

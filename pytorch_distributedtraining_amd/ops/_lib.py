@@ -58,6 +58,10 @@ _SIGS = {
                  c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_fp8_quant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_fp8_dequant": [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p],
+    "pdt_fp8_cast_transpose": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               c_void_p],
+    "pdt_fp8_update_scales": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
+                              c_void_p],
     "pdt_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "pdt_transpose16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_ce_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_int, c_void_p],

@@ -29,6 +29,7 @@ import torch.nn.functional as F
 from . import _lib
 from .activations import _colsum, colsum_ok
 from .blaslt import prefer_bgradb, wgrad_bgrad
+from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 
 _WGRAD_CHUNK = 4096
 
@@ -232,5 +233,29 @@ def linear(x, weight, bias=None):
 
 
 class Linear(nn.Linear):
+    """nn.Linear on the framework GEMM paths; inside ``ops.fp8.fp8_autocast()`` its three GEMMs run in fp8
+    with this module's delayed-scaling state (created on first fp8 use, not part of the state_dict)."""
+
+    def _fp8_meta(self, x):
+        if not (fp8_enabled() and x.dtype in (torch.bfloat16, torch.float16) and self.in_features % 16 == 0
+                and self.out_features % 16 == 0):
+            return None
+        meta = self.__dict__.get("_fp8")
+        if meta is None:
+            meta = self.__dict__["_fp8"] = Fp8Meta(x.device)
+        return meta
+
     def forward(self, x):
-        return linear(x, self.weight, self.bias)
+        return self.matmul(x, self.bias)
+
+    def matmul(self, x, bias=None):
+        """x W^T (+ bias): ``matmul(x)`` is the bias-free product for callers that fuse the bias into the
+        following kernel (GPT-2's bias-GELU)."""
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            x = x.to(torch.get_autocast_dtype("cuda"))
+        meta = self._fp8_meta(x)
+        if meta is not None and x.shape[:-1].numel() % 16 == 0:
+            w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
+            b = None if bias is None else bias.to(x.dtype)
+            return fp8_linear(x, w, b, meta)
+        return linear(x, self.weight, bias)

@@ -78,7 +78,8 @@ def loss_fn(cfg: RunConfig, kind: str):
 
 def run(cfg: RunConfig) -> dict:
     from .trainer import ClipGradNormConfig, DDPConfig, FairscaleFSDPConfig, StokeOptimizer, Trainer
-    from .utils.logging import MetricsSink
+    from .utils.logging import MetricsSink, ThroughputMeter
+    from .utils.profiling import StepTimer
 
     gpu = cfg.gpu and torch.cuda.is_available()
     torch.manual_seed(cfg.seed)
@@ -139,20 +140,33 @@ def run(cfg: RunConfig) -> dict:
     if gpu:
         torch.cuda.synchronize(dev)
     tr.barrier()
-    t0 = time.perf_counter()
+    if gpu:
+        torch.cuda.reset_peak_memory_stats(dev)
+    inner = getattr(tr.model, "module", tr.model)
+    flops = inner.flops_per_token(cfg.seq_len) * cfg.seq_len if kind == "lm" and hasattr(inner, "flops_per_token") \
+        else None
+    meter = ThroughputMeter(tr.world_size, flops_per_sample=flops)   # whole-job samples/s (+ TFLOP/s for LMs)
+    timer = StepTimer(enabled=gpu and cfg.log_every > 0)              # per-step GPU time from HIP events
+    meter.start()
+    t0 = meter.t0
     last, loss = None, None
     first = max(start, cfg.warmup)
     for step in range(first, total):
-        loss = opt_step()
+        with timer.phase("optimizer_step"):
+            loss = opt_step()
+        meter.add(cfg.batch_size_per_device * cfg.grad_accum_steps)
         i = step - cfg.warmup
         maybe_save(step + 1)
         if (i + 1) % cfg.log_every == 0 or step + 1 == total:
             last = tr.detach_and_sync_loss(loss)       # one host sync per log line only
-            el = time.perf_counter() - t0
-            samples = (step + 1 - first) * cfg.batch_size_per_device * cfg.grad_accum_steps * tr.world_size
-            rec = {"step": step + 1, "loss": last, "samples_per_s": samples / el}
+            rate = meter.rate()
+            rec = {"step": step + 1, "loss": last, "samples_per_s": rate["samples_per_s"]}
             if kind == "lm":
-                rec["tokens_per_s"] = samples * cfg.seq_len / el
+                rec["tokens_per_s"] = rate["samples_per_s"] * cfg.seq_len
+                if "tflops_per_s" in rate:
+                    rec["tflops_per_s_per_rank"] = rate["tflops_per_s"] / tr.world_size
+            if gpu:
+                rec["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
             tr.print(json.dumps(rec))
             if sink:
                 sink.log(rec, step=step + 1)
@@ -166,6 +180,11 @@ def run(cfg: RunConfig) -> dict:
               "resumed_from": start, "ms_per_step": 1000 * dt / n, "samples_per_s": samples / dt, "loss": last}
     if kind == "lm":
         result["tokens_per_s"] = samples * cfg.seq_len / dt
+    st = timer.summary().get("optimizer_step")
+    if st:
+        result["gpu_ms_per_step"] = round(st["mean_ms"], 3)
+    if gpu:
+        result["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     if cfg.checkpoint_dir:
         result["checkpoint"] = tr.save(cfg.checkpoint_dir, name=f"{cfg.name}-final", extras={"step": total})
     if sink:

@@ -14,8 +14,9 @@ and a DistributedDataParallel-wrapped GPT-2 step with a 50,257-row vocabulary
 (test_graphed_ddp_gpt2_step_with_large_vocab) replay with losses and weights equal to eager.  The round-1
 replay fault (illegal address in a rocprim partition kernel) was torch's embedding dense backward, whose
 sort / unique sizes are data-dependent; under capture ``ops.embedding`` uses a fixed-shape HIP scatter-add
-instead.  The benchmarked steps are GPU-bound (kernel time ~= step time in the rocprofv3 tables), so
-bench.py runs them eagerly.
+instead.  The benchmarked steps are GPU-bound (kernel time ~= step time in the rocprofv3 tables):
+``bench.py --workload gpt2-ddp --graph 1`` replays the whole GPT-2 124M step as one graph at 23.26 ms/step vs
+23.39 eager (+0.6 %, profiles/r2_gpt2_124m_ddp_graph_ab.log), so the bench default stays eager.
 
     step = GraphedStep(train_step, x_static, y_static, warmup=3)
     for x, y in loader:

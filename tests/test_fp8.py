@@ -1,0 +1,131 @@
+"""fp8 training linears (ops/fp8.py + csrc/kernels/fp8.hip): delayed-scaling bookkeeping, the fused
+cast+transpose kernel against torch's own fp8 conversion, and fp8 GEMMs (hipBLASLt via torch._scaled_mm)
+against an fp32 reference of the same linear."""
+import pytest
+import torch
+
+from pytorch_distributedtraining_amd.ops import fp8 as F8
+from pytorch_distributedtraining_amd.ops.linear import Linear
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _check_linear(dev, M=256, K=128, N=192, bias=True, tol=0.08):
+    torch.manual_seed(0)
+    lin = Linear(K, N, bias=bias).to(dev).to(torch.bfloat16)
+    ref = torch.nn.Linear(K, N, bias=bias).to(dev)
+    with torch.no_grad():
+        ref.weight.copy_(lin.weight.float())
+        if bias:
+            ref.bias.copy_(lin.bias.float())
+    x = torch.randn(4, M // 4, K, device=dev)
+    dy = torch.randn(4, M // 4, N, device=dev)
+    for it in range(3):                               # iteration 0 (current scaling) and delayed-scaling steps
+        xb = x.bfloat16().requires_grad_()
+        lin.zero_grad()
+        with F8.fp8_autocast():
+            y = lin(xb)
+        y.backward(dy.bfloat16())
+        xr = x.clone().requires_grad_()
+        ref.zero_grad()
+        yr = ref(xr)
+        yr.backward(dy)
+        assert y.dtype == torch.bfloat16
+        assert rel_err(y, yr) < tol, it
+        assert rel_err(xb.grad, xr.grad) < tol, it
+        assert rel_err(lin.weight.grad, ref.weight.grad) < tol, it
+        if bias:
+            assert rel_err(lin.bias.grad, ref.bias.grad) < 0.02
+    meta = lin.__dict__["_fp8"]
+    assert not any(meta.fresh)
+    # history holds the measured amax of x / w / dy; scales follow fmax / amax
+    amax_x = float(x.abs().max())
+    assert abs(float(meta.hist[0].max()) - amax_x) / amax_x < 0.01
+    assert abs(float(meta.scale[0]) - F8.E4M3_MAX / float(meta.hist[0].max())) < 1e-3 * float(meta.scale[0])
+    assert abs(float(meta.scale[2]) - F8.E5M2_MAX / float(meta.hist[2].max())) < 1e-3 * float(meta.scale[2])
+
+
+def test_fp8_linear_cpu():
+    _check_linear("cpu")
+
+
+def test_fp8_update_scales_history_cpu():
+    m = F8.Fp8Meta("cpu", history=4)
+    for a in (2.0, 8.0, 1.0, 1.0, 1.0, 1.0):
+        m.cur[0] = a
+        m.update(0, 1, 0)
+    # 8.0 left the 4-deep window after 4 more pushes
+    assert float(m.hist[0].max()) == 1.0
+    assert abs(float(m.scale[0]) - F8.E4M3_MAX) < 1e-3
+    assert float(m.cur[0]) == 0.0
+
+
+def test_fp8_off_outside_autocast_cpu():
+    lin = Linear(64, 64).bfloat16()
+    lin(torch.randn(16, 64).bfloat16())
+    assert "_fp8" not in lin.__dict__
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,C", [(128, 64), (4096, 2048), (640, 192)])
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fp8_cast_transpose_gpu(R, C, fmt, dt):
+    torch.manual_seed(0)
+    x = (torch.randn(R, C, device="cuda") * 3).to(dt)
+    x[0, 0] = 1e4                                     # saturates after scaling (SATFINITE, not NaN)
+    meta = F8.Fp8Meta("cuda")
+    meta.scale[0] = 0.37
+    q, qt = F8.cast_transpose(x, meta, 0, fmt)
+    fmax = F8._FMT_MAX[fmt]
+    ref = (x.float() * 0.37).clamp(-fmax, fmax).to(F8._FMT_DTYPE[fmt])
+    assert torch.equal(q.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), ref.t().contiguous().view(torch.uint8))
+    assert float(meta.cur[0]) == float(x.float().abs().max())
+    # amax-only pass
+    meta.cur.zero_()
+    a, b = F8.cast_transpose(x, meta, 0, fmt, want_q=False, want_t=False)
+    assert a is None and b is None and float(meta.cur[0]) == float(x.float().abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bias", [True, False])
+def test_fp8_linear_gpu(bias):
+    _check_linear("cuda", M=4096, K=1024, N=2048, bias=bias)
+
+
+@pytest.mark.gpu
+def test_fp8_gpt2_trains_like_bf16():
+    """A small GPT-2 under fp8_autocast follows the bf16 loss curve (same init, same batches)."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+
+    def run(fp8):
+        torch.manual_seed(0)
+        with torch.device("cuda"):
+            m = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2).bfloat16()
+        opt = torch.optim.AdamW(m.parameters(), lr=3e-3)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(1)
+        # learnable streams (next token = previous + stride mod 512, random start / stride per sequence)
+        start = torch.randint(0, 512, (8, 8, 1), device="cuda", generator=g)
+        stride = torch.randint(1, 4, (8, 8, 1), device="cuda", generator=g)
+        data = (start + stride * torch.arange(257, device="cuda")) % 512
+        losses = []
+        for i in range(30):
+            b = data[i % 8]
+            with F8.fp8_autocast(enabled=fp8):
+                loss = m(b[:, :-1], labels=b[:, 1:])
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            losses.append(float(loss))
+        return losses, m
+
+    l8, m8 = run(True)
+    lb, _ = run(False)
+    assert "_fp8" in m8.h[0].mlp.c_fc.__dict__
+    assert l8[-1] < 0.5 * l8[0], l8
+    assert abs(l8[-1] - lb[-1]) < 0.15 * lb[-1], (l8[-1], lb[-1])
