@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
 from ..ops.linear import Linear, linear
+from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
 from ..ops.norms import LayerNorm
 from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
                                     window_reverse_shifted_add)
@@ -115,6 +116,9 @@ class Mlp(nn.Module):
 
     def forward(self, x):
         if x.is_cuda and self.native:
+            if fused_mlp_ok(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias):
+                # C = 60 -> 120 -> 60: whole MLP in one MFMA kernel per direction (hidden kept on chip)
+                return fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
             # GEMM without bias -> fused bias + erf-GELU kernel (backward also reduces the bias gradient)
             h = linear(x, self.fc1.weight)
             return self.fc2(bias_gelu(h, self.fc1.bias, approximate="none"))

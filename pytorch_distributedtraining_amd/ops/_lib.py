@@ -113,6 +113,12 @@ _SIGS = {
                                      c_float, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_pixel_shuffle_affine_bwd": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int,
                                      c_float, c_void_p, c_int, c_void_p],
+    "pdt_swin_mlp_ok": [c_int, c_int],
+    "pdt_swin_mlp_ws_floats": [c_int],
+    "pdt_swin_mlp_bwd_blocks": [c_int64],
+    "pdt_swin_mlp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_swin_mlp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p],
     "pdt_wgrad_ok": [c_int64, c_int64, c_int64, c_int],
     "pdt_wgrad_set_variant": [c_int],
     "pdt_wgrad_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p],
@@ -125,6 +131,8 @@ _SIGS = {
     "pdt_syncbn_bwd_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_int64, c_int, c_int64, c_int, c_int, c_void_p],
 }
+
+_RET64 = {"pdt_swin_mlp_ws_floats"}
 
 F32, BF16, F16 = 0, 1, 2
 
@@ -162,7 +170,7 @@ def load():
             if fn is None:
                 continue
             fn.argtypes = args
-            fn.restype = c_int
+            fn.restype = ctypes.c_int64 if name in _RET64 else c_int
         _lib = lib
         return _lib
 

@@ -980,3 +980,26 @@ def test_linear_weight_and_bias_grad_in_one_gemm(shape):
     # and the fused GEMM itself, whichever path the timing picked above
     dw, db = blaslt.wgrad_bgrad(g.contiguous(), x.detach())
     assert rel_err(dw, wr.grad) < 1e-2 and rel_err(db, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T", [4999, 64 * 300, 294912])
+def test_swin_fused_mlp_matches_fp32(T):
+    """SwinIR-S MLP (60 -> 120 -> 60, exact GELU) on the fused MFMA kernels vs fp32 torch: y, dx, dW1, db1, dW2, db2."""
+    from pytorch_distributedtraining_amd.ops.swin_mlp import fused_mlp, fused_mlp_ok
+    C, H = 60, 120
+    x = torch.randn(T, C, device=DEV).bfloat16().requires_grad_()
+    w1 = (0.1 * torch.randn(H, C, device=DEV)).bfloat16().requires_grad_()
+    b1 = (0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_()
+    w2 = (0.1 * torch.randn(C, H, device=DEV)).bfloat16().requires_grad_()
+    b2 = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    assert fused_mlp_ok(x, w1, b1, w2, b2)
+    y = fused_mlp(x, w1, b1, w2, b2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = [t.detach().float().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    yr = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2])), ref[3], ref[4])
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    for got, want in zip((x.grad, w1.grad, b1.grad, w2.grad, b2.grad), ref):
+        assert got.dtype == torch.bfloat16
+        assert rel_err(got, want.grad) < 1.5e-2, (T, rel_err(got, want.grad))
