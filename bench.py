@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"], help="swinir-stoke precision")
     ap.add_argument("--graph", type=int, default=0,
-                    help="gpt2-ddp at one rank: capture the whole training step (fwd, bwd, clip, fused AdamW) in a "
-                         "HIP graph and replay it (utils.graphs.GraphedStep)")
+                    help="gpt2-ddp / swinir-stoke at one rank: capture the whole training step (fwd, bwd, clip, fused "
+                         "AdamW) in a HIP graph and replay it (utils.graphs.GraphedStep / Trainer.graph)")
     ap.add_argument("--fp8", type=int, default=0,
                     help="gpt2/llama: run the transformer linears' GEMMs in fp8 (ops.fp8.fp8_autocast, delayed "
                          "scaling); reported with dtype 'fp8-linears' -- never the bf16 headline")
@@ -434,6 +434,11 @@ def bench_swinir(args, comm, dev, world, rank):
             tr.backward(loss)
             tr.step()
 
+    graph = bool(args.graph) and world == 1 and args.precision == "bf16"
+    if graph:
+        # the whole optimizer step (2 micro-batches + fused AdamW) replayed as one HIP graph (Trainer.graph)
+        eager_step = step
+        step = tr.graph(eager_step)                    # noqa: F811
     dt = timed_loop(step, args, comm, dev)
     sps = world * mb * accum * args.steps / dt
     par = "dp{}+oss+sddp".format(world) if world > 1 else "dp1"
@@ -444,7 +449,7 @@ def bench_swinir(args, comm, dev, world, rank):
             "config": {"model": "swinir-s-x2", "global_batch": world * mb * accum, "seq_len": None,
                        "parallelism": par, "image": "3x128x128->3x256x256", "grad_accum": accum,
                        "loss": "feat_loss (perceptual)" if args.loss == "feat" else "mse",
-                       "compute_copy": tr.compute_dtype is not None}}
+                       "compute_copy": tr.compute_dtype is not None, "hip_graph": graph}}
 
 
 if __name__ == "__main__":

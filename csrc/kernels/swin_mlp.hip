@@ -119,7 +119,8 @@ __device__ __forceinline__ void frag_cols(u16x8 (&f)[RB][KS], const bf16_t* __re
 // ------------------------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void swin_mlp_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                            const bf16_t* __restrict__ b1, const bf16_t* __restrict__ w2,
-                                                           const bf16_t* __restrict__ b2, bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ b2,
+                                                           const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                                                            int64_t T, int C, int H) {
   __shared__ float b1s[HPAD], b2s[CPAD];
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
@@ -169,7 +170,12 @@ __global__ __launch_bounds__(256) void swin_mlp_fwd_kernel(const bf16_t* __restr
       for (int ob = 0; ob < 4; ++ob) {
         const int o = 16 * ob + 4 * g;
         if (o < C) {
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(b2s + o);
+          f32x4 bb = *reinterpret_cast<const f32x4*>(b2s + o);
+          if (res) {                                      // fused residual add: y = res + MLP(x)
+            const uint2 rv = *reinterpret_cast<const uint2*>(res + t * C + o);
+            bb[0] += bf2f((bf16_t)(rv.x & 0xffff)); bb[1] += bf2f((bf16_t)(rv.x >> 16));
+            bb[2] += bf2f((bf16_t)(rv.y & 0xffff)); bb[3] += bf2f((bf16_t)(rv.y >> 16));
+          }
           const uint32_t lo = (uint32_t)f2bf(acc2[ob][0] + bb[0]) | ((uint32_t)f2bf(acc2[ob][1] + bb[1]) << 16);
           const uint32_t hi = (uint32_t)f2bf(acc2[ob][2] + bb[2]) | ((uint32_t)f2bf(acc2[ob][3] + bb[3]) << 16);
           *reinterpret_cast<uint2*>(y + t * C + o) = make_uint2(lo, hi);
@@ -208,15 +214,22 @@ __global__ __launch_bounds__(256) void swin_mlp_bwd_kernel(const bf16_t* __restr
   __syncthreads();
   const int64_t nchunks = (T + 63) / 64;
   const int tl = 16 * w + r;                        // this lane's token within the 64-token chunk
+  uint2 xn[4], dyn[4];                              // next chunk's x / dy rows, loaded one chunk ahead
+  auto load_rows = [&](int64_t chunk) {
+    const int64_t tt = chunk * 64 + tl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c0 = 32 * (q >> 1) + 8 * g + 4 * (q & 1);
+      xn[q] = ld4(x, tt, T, c0, C, C);
+      dyn[q] = ld4(dy, tt, T, c0, C, C);
+    }
+  };
+  if ((int64_t)blockIdx.x < nchunks) load_rows(blockIdx.x);
   for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const int64_t t = ch * 64 + tl;
-    u16x8 Bx[2], Bdy[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c0 = 32 * ks + 8 * g;
-      Bx[ks] = pack2(ld4(x, t, T, c0, C, C), ld4(x, t, T, c0 + 4, C, C));
-      Bdy[ks] = pack2(ld4(dy, t, T, c0, C, C), ld4(dy, t, T, c0 + 4, C, C));
-    }
+    const u16x8 Bx[2] = {pack2(xn[0], xn[1]), pack2(xn[2], xn[3])};
+    const u16x8 Bdy[2] = {pack2(dyn[0], dyn[1]), pack2(dyn[2], dyn[3])};
+    if (ch + gridDim.x < nchunks) load_rows(ch + gridDim.x);
     // stage [x | 1]^T and dy^T (feature-major) for the weight gradients
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -308,7 +321,20 @@ __global__ __launch_bounds__(256) void swin_mlp_bwd_kernel(const bf16_t* __restr
       }
 }
 
-// sum the per-workgroup partials into dW1 [H, C], db1 [H], dW2 [C, H], db2 [C] (T_OUT = bf16 or fp32)
+// stage 1 of the partial reduction: ws2[slice][e] = sum of partials 8 * slice .. 8 * slice + 7 (float4 per thread,
+// 16 x ceil(nb / 8) workgroups: a single-stage column sum over 256 partials ran one wave per CU, latency-bound)
+constexpr int RED_SLICE = 8;
+__global__ __launch_bounds__(256) void swin_mlp_partial_sum(const float* __restrict__ ws, int nb, float* __restrict__ ws2) {
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int b0 = blockIdx.y * RED_SLICE;
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int b = 0; b < RED_SLICE; ++b)
+    if (b0 + b < nb) acc += *reinterpret_cast<const f32x4*>(ws + (int64_t)(b0 + b) * (2 * HPAD * CPAD) + e);
+  *reinterpret_cast<f32x4*>(ws2 + (int64_t)blockIdx.y * (2 * HPAD * CPAD) + e) = acc;
+}
+
+// sum the (stage-1) partials into dW1 [H, C], db1 [H], dW2 [C, H], db2 [C] (T_OUT = bf16 or fp32)
 template <typename TO>
 __global__ __launch_bounds__(256) void swin_mlp_wgrad_reduce(const float* __restrict__ ws, int nb, int C, int H,
                                                              TO* __restrict__ dw1, TO* __restrict__ db1,
@@ -341,20 +367,24 @@ static bool swin_mlp_shape_ok(int C, int H, const void* a, const void* b) {
 PDT_API int pdt_swin_mlp_ok(int C, int H) { return swin_mlp_shape_ok(C, H, nullptr, nullptr) ? 1 : 0; }
 
 // fp32 floats of backward workspace for `nb` workgroups
-PDT_API int64_t pdt_swin_mlp_ws_floats(int nb) { return (int64_t)nb * 2 * HPAD * CPAD; }
+PDT_API int64_t pdt_swin_mlp_ws_floats(int nb) {
+  return ((int64_t)nb + (nb + RED_SLICE - 1) / RED_SLICE) * 2 * HPAD * CPAD;
+}
 PDT_API int pdt_swin_mlp_bwd_blocks(int64_t T) {
   const int64_t ch = (T + 63) / 64;
   return (int)(ch < 256 ? ch : 256);   // one workgroup per CU: fp32 partials stay 16 MB
 }
 
-PDT_API int pdt_swin_mlp_fwd(const void* x, const void* w1, const void* b1, const void* w2, const void* b2, void* y,
-                             int64_t T, int C, int H, hipStream_t st) {
-  if (T <= 0 || !swin_mlp_shape_ok(C, H, x, y)) return (int)hipErrorInvalidValue;
+// y = MLP(x) (+ res when non-null, same [T, C] layout as y)
+PDT_API int pdt_swin_mlp_fwd(const void* x, const void* w1, const void* b1, const void* w2, const void* b2,
+                             const void* res, void* y, int64_t T, int C, int H, hipStream_t st) {
+  if (T <= 0 || !swin_mlp_shape_ok(C, H, x, y) || !swin_mlp_shape_ok(C, H, res, res)) return (int)hipErrorInvalidValue;
   const int64_t tiles = (T + 15) / 16;
   int64_t grid = (tiles + 3) / 4;
   if (grid > 1024) grid = 1024;
   swin_mlp_fwd_kernel<<<(int)grid, 256, 0, st>>>((const bf16_t*)x, (const bf16_t*)w1, (const bf16_t*)b1,
-                                                 (const bf16_t*)w2, (const bf16_t*)b2, (bf16_t*)y, T, C, H);
+                                                 (const bf16_t*)w2, (const bf16_t*)b2, (const bf16_t*)res, (bf16_t*)y,
+                                                 T, C, H);
   return (int)hipGetLastError();
 }
 
@@ -373,12 +403,15 @@ PDT_API int pdt_swin_mlp_bwd(const void* x, const void* dy, const void* w1, cons
   }
   swin_mlp_bwd_kernel<<<nb, 256, sizeof(BwdLds), st>>>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)w1,
                                                        (const bf16_t*)b1, (const bf16_t*)w2, (bf16_t*)dx, ws, T, C, H);
+  const int slices = (nb + RED_SLICE - 1) / RED_SLICE;
+  float* ws2 = ws + (int64_t)nb * 2 * HPAD * CPAD;
+  swin_mlp_partial_sum<<<dim3(2 * HPAD * CPAD / 1024, slices), 256, 0, st>>>(ws, nb, ws2);
   const int rgrid = (2 * HPAD * CPAD + 255) / 256;
   if (out_dt == kBF16)
-    swin_mlp_wgrad_reduce<bf16_t><<<rgrid, 256, 0, st>>>(ws, nb, C, H, (bf16_t*)dw1, (bf16_t*)db1, (bf16_t*)dw2,
+    swin_mlp_wgrad_reduce<bf16_t><<<rgrid, 256, 0, st>>>(ws2, slices, C, H, (bf16_t*)dw1, (bf16_t*)db1, (bf16_t*)dw2,
                                                          (bf16_t*)db2);
   else
-    swin_mlp_wgrad_reduce<float><<<rgrid, 256, 0, st>>>(ws, nb, C, H, (float*)dw1, (float*)db1, (float*)dw2,
+    swin_mlp_wgrad_reduce<float><<<rgrid, 256, 0, st>>>(ws2, slices, C, H, (float*)dw1, (float*)db1, (float*)dw2,
                                                         (float*)db2);
   return (int)hipGetLastError();
 }

@@ -114,15 +114,19 @@ class Mlp(nn.Module):
         self.fc2 = Linear(hidden, dim)
         self.native = True
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
+        """MLP(x), plus ``residual`` when given (fused into the kernel's epilogue on the fused path)."""
         if x.is_cuda and self.native:
-            if fused_mlp_ok(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias):
+            if fused_mlp_ok(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias) and (
+                    residual is None or (residual.dtype == torch.bfloat16 and residual.shape == x.shape)):
                 # C = 60 -> 120 -> 60: whole MLP in one MFMA kernel per direction (hidden kept on chip)
-                return fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+                return fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual)
             # GEMM without bias -> fused bias + erf-GELU kernel (backward also reduces the bias gradient)
             h = linear(x, self.fc1.weight)
-            return self.fc2(bias_gelu(h, self.fc1.bias, approximate="none"))
-        return self.fc2(self.act(self.fc1(x)))
+            y = self.fc2(bias_gelu(h, self.fc1.bias, approximate="none"))
+        else:
+            y = self.fc2(self.act(self.fc1(x)))
+        return y if residual is None else residual + y
 
 
 class SwinTransformerBlock(nn.Module):
@@ -152,26 +156,37 @@ class SwinTransformerBlock(nn.Module):
         m = mw.unsqueeze(1) - mw.unsqueeze(2)
         return m.masked_fill(m != 0, -100.0).masked_fill(m == 0, 0.0)
 
+    def _mask_for(self, H, W, device):
+        """Shifted-window mask for an H x W input, built once per resolution / device and kept (no host-built
+        mask + H2D copy per forward; required for HIP-graph capture of the step)."""
+        if (H, W) == tuple(self.input_resolution) and self.attn_mask.device == device:
+            return self.attn_mask
+        cache = self.__dict__.setdefault("_mask_cache", {})
+        m = cache.get((H, W, device))
+        if m is None:
+            m = cache[(H, W, device)] = self._mask((H, W)).to(device)
+        return m
+
     def forward(self, x, x_size):
         H, W = x_size
         B, L, C = x.shape
         if self.attn.native and fused_window_ok(x, H, W, self.window_size, self.shift_size):
             # roll + partition and reverse + roll + residual add as one permutation pass each
             if self.shift_size > 0:
-                mask = self.attn_mask if (H, W) == tuple(self.input_resolution) else self._mask((H, W)).to(x.device)
+                mask = self._mask_for(H, W, x.device)
             else:
                 mask = None
             h = self.norm1(x).to(torch.bfloat16)
             win = window_partition_shifted(h, H, W, self.window_size, self.shift_size)
             a = self.attn(win, mask=mask).to(torch.bfloat16)
             x = window_reverse_shifted_add(a, x, H, W, self.window_size, self.shift_size)
-            return x + self.mlp(self.norm2(x))
+            return self.mlp(self.norm2(x), residual=x)
         sc = x
         x = self.norm1(x).view(B, H, W, C)
         if self.shift_size > 0:
             x = torch.roll(x, shifts=(-self.shift_size, -self.shift_size), dims=(1, 2))
         if self.shift_size > 0:
-            mask = self.attn_mask if (H, W) == tuple(self.input_resolution) else self._mask((H, W)).to(x.device)
+            mask = self._mask_for(H, W, x.device)
         else:
             mask = None
         a = self.attn(window_partition(x, self.window_size), mask=mask)

@@ -116,7 +116,8 @@ _SIGS = {
     "pdt_swin_mlp_ok": [c_int, c_int],
     "pdt_swin_mlp_ws_floats": [c_int],
     "pdt_swin_mlp_bwd_blocks": [c_int64],
-    "pdt_swin_mlp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_swin_mlp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                         c_void_p],
     "pdt_swin_mlp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p],
     "pdt_wgrad_ok": [c_int64, c_int64, c_int64, c_int],

@@ -29,17 +29,23 @@ def fused_mlp_ok(x: torch.Tensor, w1: torch.Tensor, b1, w2: torch.Tensor, b2) ->
 
 class _FusedMlpFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, res):
         H, C = w1.shape
         x2 = x.reshape(-1, C)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         T = x2.shape[0]
         y = torch.empty(T, C, dtype=x.dtype, device=x.device)
+        r2 = None
+        if res is not None:
+            r2 = res.reshape(-1, C)
+            if not r2.is_contiguous():
+                r2 = r2.contiguous()
         _lib.call("pdt_swin_mlp_fwd", x2.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-                  y.data_ptr(), T, C, H, _lib.stream_handle(x.device))
+                  _lib.ptr(r2), y.data_ptr(), T, C, H, _lib.stream_handle(x.device))
         ctx.save_for_backward(x2, w1, b1, w2)
         ctx.xshape = x.shape
+        ctx.has_res = res is not None
         return y.view(x.shape)
 
     @staticmethod
@@ -59,9 +65,10 @@ class _FusedMlpFn(torch.autograd.Function):
         _lib.call("pdt_swin_mlp_bwd", x2.data_ptr(), dy2.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
                   dx.data_ptr(), dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
                   _lib.dtype_code(w1.dtype), ws.data_ptr(), nb, T, C, H, _lib.stream_handle(dy.device))
-        return dx.view(ctx.xshape), dw1, db1, dw2, db2
+        return dx.view(ctx.xshape), dw1, db1, dw2, db2, (dy if ctx.has_res else None)
 
 
-def fused_mlp(x, w1, b1, w2, b2):
-    """GELU(x W1^T + b1) W2^T + b2 (exact erf GELU) on the fused HIP kernel; callers check fused_mlp_ok."""
-    return _FusedMlpFn.apply(x, w1, b1, w2, b2)
+def fused_mlp(x, w1, b1, w2, b2, residual=None):
+    """[residual +] GELU(x W1^T + b1) W2^T + b2 (exact erf GELU) on the fused HIP kernel; callers check
+    fused_mlp_ok (and that ``residual`` is a bf16 tensor of x's shape)."""
+    return _FusedMlpFn.apply(x, w1, b1, w2, b2, residual)

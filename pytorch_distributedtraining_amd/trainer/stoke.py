@@ -249,7 +249,10 @@ class Trainer:
         if isinstance(out, (list, tuple)):
             out = sum(out)
         d = out.detach().float()
-        self._ema = d.clone() if self._ema is None else self._ema * (1 - self._ema_weight) + d * self._ema_weight
+        if self._ema is None:
+            self._ema = d.clone()
+        else:      # in place: a captured step (Trainer.graph) keeps chaining the same device scalar on replay
+            self._ema.mul_(1 - self._ema_weight).add_(d, alpha=self._ema_weight)
         self._last_loss = d
         if self._module.training and self.grad_accum > 1:
             out = out / self.grad_accum
@@ -308,6 +311,39 @@ class Trainer:
         if self.scaler is not None:
             self.scaler.update()
         self.zero_grads()
+
+    def graph(self, step_fn, *static_inputs: torch.Tensor, warmup: int = 2):
+        """Capture ``step_fn(*static_inputs)`` -- one or more WHOLE optimizer steps written against this Trainer
+        (``model`` / ``loss`` / ``backward`` / ``step`` calls over the accumulation micro-batches) -- into a HIP
+        graph (utils.graphs.GraphedStep) and return a callable that copies its arguments into the static
+        buffers and replays the graph, advancing the Trainer's step counters exactly as the eager call does.
+        Removes the per-launch host cost of many-small-kernel steps (SwinIR: ~3,500 launches per step).
+
+        Needs one rank (collectives are not captured), the fused optimizer (switched to its capturable device
+        step count here) and no fp16 GradScaler (its scale update is host logic)."""
+        from ..utils.graphs import GraphedStep
+        fused = isinstance(self._optimizer, FusedAdamW)
+        if not (self.gpu and self.world_size_ == 1 and fused and self.scaler is None):
+            raise RuntimeError("Trainer.graph needs one GPU rank, FusedAdamW and no fp16 GradScaler")
+        for g in self._optimizer.param_groups:
+            g["capturable"] = True
+        gs = GraphedStep(step_fn, *static_inputs, warmup=warmup)
+        tr = self
+        state = {"delta": None}
+
+        def run(*inputs):
+            before = (tr._backward_steps, tr._optimizer_steps)
+            first = gs.graph is None
+            out = gs(*inputs)
+            if first:      # python ran warmup + 1 times (warm-up + capture); the device ran warmup + 1 (+ replay)
+                n = gs.warmup + 1
+                state["delta"] = ((tr._backward_steps - before[0]) // n, (tr._optimizer_steps - before[1]) // n)
+            else:
+                tr._backward_steps += state["delta"][0]
+                tr._optimizer_steps += state["delta"][1]
+            return out
+        run.graphed = gs
+        return run
 
     def zero_grads(self):
         if hasattr(self._engine, "zero_grad") and self._engine is not self._module:

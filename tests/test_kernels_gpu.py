@@ -982,8 +982,8 @@ def test_linear_weight_and_bias_grad_in_one_gemm(shape):
     assert rel_err(dw, wr.grad) < 1e-2 and rel_err(db, br.grad) < 1e-2
 
 
-@pytest.mark.parametrize("T", [4999, 64 * 300, 294912])
-def test_swin_fused_mlp_matches_fp32(T):
+@pytest.mark.parametrize("T,with_res", [(4999, False), (4999, True), (64 * 300, False), (294912, True)])
+def test_swin_fused_mlp_matches_fp32(T, with_res):
     """SwinIR-S MLP (60 -> 120 -> 60, exact GELU) on the fused MFMA kernels vs fp32 torch: y, dx, dW1, db1, dW2, db2."""
     from pytorch_distributedtraining_amd.ops.swin_mlp import fused_mlp, fused_mlp_ok
     C, H = 60, 120
@@ -992,14 +992,67 @@ def test_swin_fused_mlp_matches_fp32(T):
     b1 = (0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_()
     w2 = (0.1 * torch.randn(C, H, device=DEV)).bfloat16().requires_grad_()
     b2 = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    res = torch.randn(T, C, device=DEV).bfloat16().requires_grad_() if with_res else None
     assert fused_mlp_ok(x, w1, b1, w2, b2)
-    y = fused_mlp(x, w1, b1, w2, b2)
+    y = fused_mlp(x, w1, b1, w2, b2, res)
     dy = torch.randn_like(y)
     y.backward(dy)
     ref = [t.detach().float().requires_grad_() for t in (x, w1, b1, w2, b2)]
     yr = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2])), ref[3], ref[4])
+    if with_res:
+        yr = yr + res.detach().float()
+        assert torch.equal(res.grad, dy)
     yr.backward(dy.float())
     assert rel_err(y, yr) < 1e-2
     for got, want in zip((x.grad, w1.grad, b1.grad, w2.grad, b2.grad), ref):
         assert got.dtype == torch.bfloat16
         assert rel_err(got, want.grad) < 1.5e-2, (T, rel_err(got, want.grad))
+
+
+def test_trainer_graph_matches_eager_swinir():
+    """Trainer.graph: a SwinIR-S Stoke step (2 accumulation micro-batches, bf16 compute copy, clip, fused AdamW)
+    captured once and replayed gives the eager losses / weights and advances the Trainer's counters."""
+    import copy
+    from pytorch_distributedtraining_amd.models.swinir import swinir_s_x2
+    from pytorch_distributedtraining_amd.trainer import ClipGradNormConfig, StokeOptimizer, Trainer
+    torch.manual_seed(0)
+    base = swinir_s_x2()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    data = [(torch.rand(2, 3, 32, 32, device=DEV, generator=g), torch.rand(2, 3, 64, 64, device=DEV, generator=g))
+            for _ in range(2)]
+
+    def make():
+        opt = StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs={"lr": 1e-3, "betas": (0.9, 0.99),
+                                                                             "eps": 1e-8, "weight_decay": 1e-4})
+        tr = Trainer(copy.deepcopy(base), optimizer=opt, loss=F.mse_loss, batch_size_per_device=2,
+                     grad_accum_steps=2, grad_clip=ClipGradNormConfig(max_norm=0.1, norm_type=2.0), gpu=True,
+                     fp16="bf16", distributed=None, verbose=False)
+        losses = []
+
+        def step():
+            for x, y in data:
+                loss = tr.loss(tr.model(x), y)
+                tr.backward(loss)
+                tr.step()
+            losses.append(tr._last_loss)
+        return tr, step, losses
+
+    tr_e, step_e, _ = make()
+    ema_e = []
+    for _ in range(6):
+        step_e()
+        ema_e.append(float(tr_e._ema))
+    tr_g, step_g, _ = make()
+    run = tr_g.graph(step_g, warmup=2)
+    ema_g = []
+    for _ in range(4):              # first call = 2 warm-up steps + capture + replay (3 steps), then 3 replays
+        run()
+        ema_g.append(float(tr_g._ema))
+    assert tr_g.optimizer_steps == tr_e.optimizer_steps == 6
+    assert tr_g.backward_steps == 12
+    assert abs(ema_g[-1] - ema_e[-1]) < 2e-3 * max(1.0, abs(ema_e[-1])), (ema_e, ema_g)
+    se, sg = tr_e.model_access.state_dict(), tr_g.model_access.state_dict()
+    for k in se:
+        if se[k].is_floating_point() and se[k].dim() >= 2:
+            d = (se[k].float() - sg[k].float()).abs().mean().item()
+            assert d < 1e-4, (k, d)
