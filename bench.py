@@ -249,7 +249,9 @@ def bench_gpt2(args, comm, dev, world, rank):
     fsdp = args.workload in ("gpt2-fsdp", "llama3-fsdp")
     llama = args.workload.startswith("llama")
     name = args.model or ("llama3-8b" if llama else "gpt2-1.3b" if fsdp else "gpt2-124m")
-    mb = args.micro_batch or (8 if llama else 64 if fsdp else 16)
+    # per-GPU micro-batch sized for 288 GB HBM: GPT-2 124M DDP 16 -> 64 sequences 700k -> 886k tokens/s
+    # (profiles/r2_gpt2_124m_ddp_microbatch.log), GPT-2 1.3B FSDP 32 -> 64 +2.8 % (module docstring)
+    mb = args.micro_batch or (8 if llama else 64)
     S = args.seq
     with torch.device(dev):
         if llama:
