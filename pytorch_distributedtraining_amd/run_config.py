@@ -26,7 +26,7 @@ class RunConfig:
     distributed: Optional[str] = "ddp"      # None | "ddp" | "fsdp"
     fairscale_oss: bool = False             # ZeRO-1 (Fairscale OSS)
     fairscale_sddp: bool = False            # ZeRO-2 (Fairscale ShardedDDP)
-    precision: str = "bf16"                 # bf16 | amp (fp16 + loss scaling) | fp32
+    precision: str = "bf16"                 # bf16 | fp8 (bf16 + fp8 linear GEMMs) | amp (fp16 + loss scaling) | fp32
     gpu: bool = True
     backend: str = "nccl"                   # RCCL on ROCm; gloo for CPU runs
     batch_size_per_device: int = 32

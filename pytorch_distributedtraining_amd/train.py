@@ -95,14 +95,15 @@ def run(cfg: RunConfig) -> dict:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     distributed = cfg.distributed if (world > 1 or cfg.distributed == "fsdp") else None
     opt = StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs=dict(cfg.optimizer))
-    precision = None if cfg.precision == "fp32" else cfg.precision
+    precision = None if cfg.precision == "fp32" else "bf16" if cfg.precision == "fp8" else cfg.precision
     tr = Trainer(model, optimizer=opt, loss=loss_fn(cfg, kind), batch_size_per_device=cfg.batch_size_per_device,
                  grad_accum_steps=cfg.grad_accum_steps,
                  grad_clip=ClipGradNormConfig(max_norm=cfg.grad_clip) if cfg.grad_clip else None, gpu=gpu,
                  fp16=precision if gpu else None, distributed=distributed,
                  fairscale_oss=cfg.fairscale_oss and distributed is not None,
                  fairscale_sddp=cfg.fairscale_sddp and distributed is not None,
-                 fairscale_fsdp=distributed == "fsdp", configs=configs, verbose=False)
+                 fairscale_fsdp=distributed == "fsdp", configs=configs, verbose=False,
+                 fp8=cfg.precision == "fp8" and gpu)
     dev = tr.device
     gen = torch.Generator(device=dev)
     gen.manual_seed(cfg.seed + 1000 * tr.rank)

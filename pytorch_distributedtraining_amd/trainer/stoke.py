@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from ..data.loader import DeviceDataLoader
+from ..ops.fp8 import fp8_autocast
 from ..optim import FusedAdamW, GradScaler, clip_grad_norm_
 from ..parallel.comm import Comm
 from ..utils import checkpoint as ckpt
@@ -45,7 +46,10 @@ class Trainer:
     def __init__(self, model: nn.Module, optimizer, loss, batch_size_per_device: int, grad_accum_steps: int = 1,
                  grad_clip=None, gpu: bool = False, fp16=None, distributed=None, fairscale_oss: bool = False,
                  fairscale_sddp: bool = False, fairscale_fsdp: bool = False, configs=None, info_rank=0,
-                 verbose: bool = True, ema_weight: float = 0.1, comm: Comm | None = None):
+                 verbose: bool = True, ema_weight: float = 0.1, comm: Comm | None = None, fp8: bool = False):
+        """``fp8=True`` (with bf16 precision on GPU): every framework ``Linear`` of the model runs its forward,
+        data- and weight-gradient GEMMs in fp8 with delayed scaling (``ops.fp8.fp8_autocast``); norms,
+        attention, the loss and the optimizer stay bf16 / fp32."""
         self.verbose = verbose
         self.logger = RankLogger(info_rank, verbose)
         self._loss_fn = loss
@@ -66,6 +70,9 @@ class Trainer:
         if distributed == "fsdp":
             fairscale_fsdp = True
         self.fp16 = {"apex_O1": "amp", "apex_O2": "bf16", "deepspeed": "bf16"}.get(fp16, fp16)
+        if fp8 and not (self.gpu and self.fp16 == "bf16"):
+            raise ValueError("Trainer(fp8=True) needs gpu=True and fp16='bf16' (fp8 GEMMs under a bf16 compute dtype)")
+        self.fp8 = bool(fp8)
         self.ddp_config = find_config(configs, DDPConfig) or DDPConfig()
         self.amp_config = find_config(configs, AMPConfig) or AMPConfig()
         self.oss_config = find_config(configs, FairscaleOSSConfig) or FairscaleOSSConfig()
@@ -238,7 +245,7 @@ class Trainer:
         return torch.autocast(self.device.type, dtype=self.autocast_dtype)
 
     def model(self, *args, **kwargs):
-        with prof.range("pdt.forward"), self._autocast():
+        with prof.range("pdt.forward"), self._autocast(), fp8_autocast(enabled=self.fp8):
             return self._engine(*args, **kwargs)
 
     __call__ = model

@@ -129,3 +129,31 @@ def test_fp8_gpt2_trains_like_bf16():
     assert "_fp8" in m8.h[0].mlp.c_fc.__dict__
     assert l8[-1] < 0.5 * l8[0], l8
     assert abs(l8[-1] - lb[-1]) < 0.15 * lb[-1], (l8[-1], lb[-1])
+
+
+def test_trainer_fp8_requires_bf16_gpu_cpu():
+    from pytorch_distributedtraining_amd.trainer import StokeOptimizer, Trainer
+    with pytest.raises(ValueError):
+        Trainer(torch.nn.Linear(16, 16), optimizer=StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs={}),
+                loss=torch.nn.functional.mse_loss, batch_size_per_device=2, gpu=False, fp16=None, fp8=True,
+                verbose=False)
+
+
+@pytest.mark.gpu
+def test_trainer_fp8_gpt2_step():
+    """Trainer(fp8=True): the model's Linears take the fp8 path inside Trainer.model and training steps run."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.trainer import StokeOptimizer, Trainer
+    torch.manual_seed(0)
+    m = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2)
+    tr = Trainer(m, optimizer=StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs={"lr": 1e-3}),
+                 loss=lambda out, y: out, batch_size_per_device=4, gpu=True, fp16="bf16", fp8=True, verbose=False)
+    x = torch.randint(0, 512, (4, 129), device="cuda")
+    losses = []
+    for _ in range(3):
+        loss = tr.loss(tr.model(x[:, :-1], labels=x[:, 1:]), None)
+        tr.backward(loss)
+        tr.step()
+        losses.append(float(loss.detach()))
+    assert "_fp8" in m.h[0].attn.c_attn.__dict__
+    assert all(l == l for l in losses) and losses[-1] < losses[0]
