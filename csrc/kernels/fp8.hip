@@ -12,6 +12,7 @@
 //    scale = fmax / max(history) / 2^margin, scale_inv = 1 / scale.  Keeps the whole recipe on the device
 //    (no host sync per layer).
 #include "common.h"
+#include "reduce.h"
 
 #include <hip/hip_fp8.h>
 
@@ -21,6 +22,18 @@ namespace {
 constexpr int CT_TS = 64;       // tile edge
 constexpr int CT_LD = 68;       // LDS row stride in bytes (17 words: column gathers spread over banks)
 
+// prologue applied to each element before the cast (GPT-2 MLP, tanh-form GELU via the sigmoid identity)
+enum CtOp : int { kPlain = 0, kBiasGelu = 1, kBiasGeluBwd = 2 };
+__device__ __forceinline__ float sig2z(float u) {
+  const float z = 0.7978845608028654f * (u + 0.044715f * u * u * u);
+  return __builtin_amdgcn_rcpf(1.f + __expf(-2.f * z));
+}
+__device__ __forceinline__ float gelu_tanh(float u) { return u * sig2z(u); }
+__device__ __forceinline__ float gelu_tanh_grad(float u) {
+  const float s = sig2z(u);
+  return s + 2.f * u * s * (1.f - s) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * u * u);
+}
+
 template <int FMT>
 __device__ __forceinline__ uint8_t to_fp8(float v) {
   return __hip_cvt_float_to_fp8(v, __HIP_SATFINITE, FMT == 0 ? __HIP_E4M3 : __HIP_E5M2);
@@ -28,13 +41,20 @@ __device__ __forceinline__ uint8_t to_fp8(float v) {
 
 // x [R, C] (T = bf16 or fp32), R % 64 == 0, C % 64 == 0.  q [R, C] and qt [C, R] may each be null;
 // with both null the kernel only measures amax (first-iteration "current scaling").
-template <typename T, int FMT>
+// OP == kBiasGelu:    v = gelu(x + bias)            (GPT-2 MLP forward: the hidden goes straight to fp8)
+// OP == kBiasGeluBwd: v = x * gelu'(aux + bias)     (x = dH, aux = the pre-activation; column sums of v per
+//                                                    64-row tile -> dbias_part[R / 64, C], reduced afterwards)
+template <typename T, int FMT, int OP = kPlain>
 __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
                                                                  uint8_t* __restrict__ qt, int R, int C,
                                                                  const float* __restrict__ scale,
-                                                                 unsigned int* __restrict__ amax_bits) {
+                                                                 unsigned int* __restrict__ amax_bits,
+                                                                 const T* __restrict__ aux = nullptr,
+                                                                 const T* __restrict__ bias = nullptr,
+                                                                 float* __restrict__ dbias_part = nullptr) {
   __shared__ uint32_t tile[CT_TS * CT_LD / 4];
   __shared__ float red[4];
+  __shared__ float colp[OP == kBiasGeluBwd ? 32 : 1][OP == kBiasGeluBwd ? CT_TS : 1];
   const int tid = threadIdx.x;
   const int lc = (tid & 7) * 8, lr = tid >> 3;   // 8 threads x 8 columns per row, 32 rows per pass
   const float sc = scale ? *scale : 1.f;
@@ -44,11 +64,32 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
   uint8_t* t8 = reinterpret_cast<uint8_t*>(tile);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r0 = (t / tiles_c) * CT_TS, c0 = (t % tiles_c) * CT_TS;
+    float cs[8];
+    if (OP == kBiasGeluBwd) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cs[k] = 0.f;
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int r = lr + 32 * p;
       float v[8];
       Vec8<T>::load(x + (int64_t)(r0 + r) * C + c0 + lc, v);
+      if (OP != kPlain) {
+        float b[8];
+        Vec8<T>::load(bias + c0 + lc, b);
+        if (OP == kBiasGelu) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = gelu_tanh(v[k] + b[k]);
+        } else {
+          float a[8];
+          Vec8<T>::load(aux + (int64_t)(r0 + r) * C + c0 + lc, a);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            v[k] *= gelu_tanh_grad(a[k] + b[k]);
+            cs[k] += v[k];
+          }
+        }
+      }
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -62,6 +103,18 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
         dst[0] = lo;
         dst[1] = hi;
       }
+    }
+    if (OP == kBiasGeluBwd) {                   // this tile's column sums of dA (deterministic, no atomics)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) colp[lr][lc + k] = cs[k];
+      __syncthreads();
+      if (tid < CT_TS) {
+        float sum = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) sum += colp[i][tid];
+        dbias_part[(int64_t)(r0 / CT_TS) * C + c0 + tid] = sum;
+      }
+      if (!qt) __syncthreads();                 // colp reused by the next tile
     }
     if (qt) {
       __syncthreads();
@@ -130,6 +183,44 @@ PDT_API int pdt_fp8_cast_transpose(const void* x, void* q, void* qt, int R, int 
   else if (dt == kF32) { if (fmt == 0) PDT_L(float, 0); else PDT_L(float, 1); }
   else return (int)hipErrorInvalidValue;
 #undef PDT_L
+  return (int)hipGetLastError();
+}
+
+// GPT-2 MLP in fp8 (kernels above with the GELU prologues), bf16 tensors, bias [C] bf16:
+//   fwd: q / qt = fp8(gelu(a + bias) * scale)            amax of the GELU output
+//   bwd: q / qt = fp8(dh * gelu'(a + bias) * scale)     amax of dA, dbias[C] (bf16) = column sums of dA
+// ws: pdt_fp8_gelu_bwd_ws_floats(R, C) floats.
+PDT_API long long pdt_fp8_gelu_bwd_ws_floats(int R, int C) { return (long long)(R / CT_TS) * C + red::col_ws_floats(R / CT_TS, C); }
+
+PDT_API int pdt_fp8_bias_gelu_ct(const void* a, const void* bias, void* q, void* qt, int R, int C, int fmt,
+                                 const float* scale, unsigned int* amax_bits, hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias) return (int)hipErrorInvalidValue;
+  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
+  const int grid = (int)(tiles < 2048 ? tiles : 2048);
+  if (fmt == 0)
+    fp8_cast_transpose_kernel<bf16_t, 0, kBiasGelu><<<grid, 256, 0, st>>>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R,
+                                                                          C, scale, amax_bits, nullptr,
+                                                                          (const bf16_t*)bias, nullptr);
+  else
+    fp8_cast_transpose_kernel<bf16_t, 1, kBiasGelu><<<grid, 256, 0, st>>>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R,
+                                                                          C, scale, amax_bits, nullptr,
+                                                                          (const bf16_t*)bias, nullptr);
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_fp8_bias_gelu_bwd_ct(const void* dh, const void* a, const void* bias, void* q, void* qt, void* dbias,
+                                     float* ws, int R, int C, int fmt, const float* scale, unsigned int* amax_bits,
+                                     hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias || !ws) return (int)hipErrorInvalidValue;
+  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
+  const int grid = (int)(tiles < 2048 ? tiles : 2048);
+  if (fmt == 0)
+    fp8_cast_transpose_kernel<bf16_t, 0, kBiasGeluBwd><<<grid, 256, 0, st>>>(
+        (const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, (const bf16_t*)a, (const bf16_t*)bias, ws);
+  else
+    fp8_cast_transpose_kernel<bf16_t, 1, kBiasGeluBwd><<<grid, 256, 0, st>>>(
+        (const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, (const bf16_t*)a, (const bf16_t*)bias, ws);
+  if (dbias) red::col_reduce<bf16_t>(ws, R / CT_TS, C, (bf16_t*)dbias, ws + (long long)(R / CT_TS) * C, 0, st);
   return (int)hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
 from ..ops.embedding import Embedding
+from ..ops.fp8 import fp8_enabled, fp8_gelu_mlp, fp8_gelu_mlp_ok
 from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 
@@ -81,6 +82,12 @@ class MLP(nn.Module):
         self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
+        if fp8_enabled():
+            m1, m2 = self.c_fc._fp8_meta(x), self.c_proj._fp8_meta(x)
+            if m1 is not None and m2 is not None and fp8_gelu_mlp_ok(x, self.c_fc.weight, self.c_fc.bias,
+                                                                    self.c_proj.weight, self.c_proj.bias):
+                # fp8 GEMMs with bias + GELU fused into the casts (the bf16 hidden never reaches HBM)
+                return fp8_gelu_mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, m1, m2)
         h = self.c_fc.matmul(x)                      # GEMM without bias: the bias is folded into the GELU kernel
         h = bias_gelu(h, self.c_fc.bias, approximate="tanh")
         return self.c_proj(h)

@@ -62,6 +62,10 @@ _SIGS = {
                                c_void_p],
     "pdt_fp8_update_scales": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
                               c_void_p],
+    "pdt_fp8_gelu_bwd_ws_floats": [c_int, c_int],
+    "pdt_fp8_bias_gelu_ct": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "pdt_fp8_bias_gelu_bwd_ct": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                 c_int, c_void_p, c_void_p, c_void_p],
     "pdt_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "pdt_transpose16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_ce_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_int, c_void_p],
@@ -133,7 +137,7 @@ _SIGS = {
                              c_int64, c_int, c_int64, c_int, c_int, c_void_p],
 }
 
-_RET64 = {"pdt_swin_mlp_ws_floats"}
+_RET64 = {"pdt_swin_mlp_ws_floats", "pdt_fp8_gelu_bwd_ws_floats"}
 
 F32, BF16, F16 = 0, 1, 2
 

@@ -121,11 +121,15 @@ class Fp8Meta:
 
     def prepare(self, slot_tensors, fmt: int):
         """Before casting the slots' tensors: refresh their scales.  A slot's first use measures the tensor's
-        own amax first (one read-only pass) so iteration 0 is not cast with scale 1."""
+        own amax first (one read-only pass) so iteration 0 is not cast with scale 1.  An entry may give a
+        callable instead of a tensor: it runs that amax-only pass itself (fused GELU casts)."""
         s0, s1 = slot_tensors[0][0], slot_tensors[-1][0] + 1
         for slot, t in slot_tensors:
             if self.fresh[slot]:
-                cast_transpose(t, self, slot, fmt, want_q=False, want_t=False)
+                if callable(t):
+                    t()
+                else:
+                    cast_transpose(t, self, slot, fmt, want_q=False, want_t=False)
                 self.fresh[slot] = False
         self.update(s0, s1, fmt)
 
@@ -211,3 +215,118 @@ class _Fp8LinearFn(torch.autograd.Function):
 
 def fp8_linear(x: torch.Tensor, weight: torch.Tensor, bias, meta: Fp8Meta) -> torch.Tensor:
     return _Fp8LinearFn.apply(x, weight, bias, meta)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# GPT-2 MLP in fp8 with the GELU fused into the casts: c_fc's output goes bias + GELU -> fp8 (row + transposed)
+# in one pass (the bf16 hidden is never written), and backward's dH -> dA = dH * GELU'(A) -> e5m2 (row +
+# transposed) + the c_fc bias gradient in one pass.  Against the per-Linear fp8 path this drops a write and a
+# read of the [tokens, 4 d] hidden in each direction.
+# ---------------------------------------------------------------------------------------------------------------
+
+def _gelu_tanh(u):
+    return 0.5 * u * (1.0 + torch.tanh(0.7978845608028654 * (u + 0.044715 * u * u * u)))
+
+
+def _gelu_tanh_grad(u):
+    t = torch.tanh(0.7978845608028654 * (u + 0.044715 * u * u * u))
+    return 0.5 * (1 + t) + 0.5 * u * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * u * u)
+
+
+def bias_gelu_cast_transpose(a, bias, meta: Fp8Meta, slot: int, fmt: int, want_q=True, want_t=True):
+    """fp8(gelu_tanh(a + bias) * scale) as [R, C] / [C, R]; amax of the GELU output into meta.cur[slot]."""
+    R, C = a.shape
+    if _ct_ok(a) and a.dtype == torch.bfloat16 and bias.dtype == torch.bfloat16:
+        dt = _FMT_DTYPE[fmt]
+        q = torch.empty(R, C, dtype=dt, device=a.device) if want_q else None
+        qt = torch.empty(C, R, dtype=dt, device=a.device) if want_t else None
+        _lib.call("pdt_fp8_bias_gelu_ct", a.data_ptr(), bias.data_ptr(), _lib.ptr(q), _lib.ptr(qt), R, C, fmt,
+                  meta.scale[slot:slot + 1].data_ptr(), meta.cur[slot:slot + 1].data_ptr(), _lib.stream_handle(a.device))
+        return q, qt
+    return cast_transpose(_gelu_tanh(a.float() + bias.float()), meta, slot, fmt, want_q, want_t)
+
+
+def bias_gelu_bwd_cast_transpose(dh, a, bias, meta: Fp8Meta, slot: int, fmt: int, want_q=True, want_t=True,
+                                 want_db=True):
+    """dA = dh * gelu_tanh'(a + bias) cast to fp8 as [R, C] / [C, R] (amax into meta.cur[slot]) and, with
+    ``want_db``, dbias = column sums of dA (bias dtype).  Returns (q, qt, dbias)."""
+    R, C = a.shape
+    if _ct_ok(a) and _ct_ok(dh) and a.dtype == torch.bfloat16 and dh.dtype == torch.bfloat16 \
+            and bias.dtype == torch.bfloat16:
+        dt = _FMT_DTYPE[fmt]
+        q = torch.empty(R, C, dtype=dt, device=a.device) if want_q else None
+        qt = torch.empty(C, R, dtype=dt, device=a.device) if want_t else None
+        db = torch.empty(C, dtype=bias.dtype, device=a.device) if want_db else None
+        ws = torch.empty(int(_lib.require().pdt_fp8_gelu_bwd_ws_floats(R, C)), dtype=torch.float32, device=a.device)
+        _lib.call("pdt_fp8_bias_gelu_bwd_ct", dh.data_ptr(), a.data_ptr(), bias.data_ptr(), _lib.ptr(q), _lib.ptr(qt),
+                  _lib.ptr(db), ws.data_ptr(), R, C, fmt, meta.scale[slot:slot + 1].data_ptr(),
+                  meta.cur[slot:slot + 1].data_ptr(), _lib.stream_handle(a.device))
+        return q, qt, db
+    da = dh.float() * _gelu_tanh_grad(a.float() + bias.float())
+    q, qt = cast_transpose(da, meta, slot, fmt, want_q, want_t)
+    return q, qt, (da.sum(0).to(bias.dtype) if want_db else None)
+
+
+def fp8_gelu_mlp_ok(x, w1, b1, w2, b2) -> bool:
+    ts = (x, w1, b1, w2, b2)
+    if any(t is None or t.dtype != torch.bfloat16 for t in ts):
+        return False
+    M = x.shape[:-1].numel()
+    return all(d % 64 == 0 for d in (M, w1.shape[0], w1.shape[1], w2.shape[0])) and w1.is_contiguous() \
+        and w2.is_contiguous()
+
+
+class _Fp8GeluMlpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, m1: Fp8Meta, m2: Fp8Meta):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        need_dx = x.requires_grad
+        m1.prepare([(SLOT_X, x2), (SLOT_W, w1)], 0)
+        xq, xt = cast_transpose(x2, m1, SLOT_X, 0, want_q=True, want_t=w1.requires_grad)
+        wq1, wt1 = cast_transpose(w1, m1, SLOT_W, 0, want_q=True, want_t=need_dx)
+        s1 = m1.scale_inv.clone()
+        a = fp8_mm(xq, wq1.t(), s1[0:1], s1[1:2], out_dtype=x.dtype)
+        m2.prepare([(SLOT_X, lambda: bias_gelu_cast_transpose(a, b1, m2, SLOT_X, 0, False, False)),
+                    (SLOT_W, w2)], 0)
+        hq, ht = bias_gelu_cast_transpose(a, b1, m2, SLOT_X, 0, want_q=True, want_t=w2.requires_grad)
+        wq2, wt2 = cast_transpose(w2, m2, SLOT_W, 0, want_q=True, want_t=True)
+        s2 = m2.scale_inv.clone()
+        y = fp8_mm(hq, wq2.t(), s2[0:1], s2[1:2], b2, out_dtype=x.dtype)
+        ctx.save_for_backward(xt, wt1, a, b1, ht, wt2, s1, s2)
+        ctx.m1, ctx.m2, ctx.xshape = m1, m2, x.shape
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xt, wt1, a, b1, ht, wt2, s1, s2 = ctx.saved_tensors
+        m1, m2 = ctx.m1, ctx.m2
+        N2 = dy.shape[-1]
+        dy2 = dy.reshape(-1, N2)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        m2.prepare([(SLOT_DY, dy2)], 1)
+        dyq, dyt = cast_transpose(dy2, m2, SLOT_DY, 1, want_q=True, want_t=ctx.needs_input_grad[3])
+        sdy = m2.scale_inv[SLOT_DY:SLOT_DY + 1]
+        dh = fp8_mm(dyq, wt2.t(), sdy, s2[1:2], out_dtype=dy.dtype)
+        dw2 = fp8_mm(dyt, ht.t(), sdy, s2[0:1], out_dtype=torch.bfloat16) if ctx.needs_input_grad[3] else None
+        db2 = None
+        if ctx.needs_input_grad[4]:
+            from .activations import _colsum, colsum_ok
+            db2 = _colsum(dy2, torch.bfloat16) if dy2.is_cuda and colsum_ok(N2) else dy2.sum(0).to(torch.bfloat16)
+        need_dx, need_dw1 = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        m1.prepare([(SLOT_DY, lambda: bias_gelu_bwd_cast_transpose(dh, a, b1, m1, SLOT_DY, 1, False, False, False))],
+                   1)
+        daq, dat, db1 = bias_gelu_bwd_cast_transpose(dh, a, b1, m1, SLOT_DY, 1, want_q=need_dx, want_t=need_dw1,
+                                                     want_db=ctx.needs_input_grad[2])
+        sda = m1.scale_inv[SLOT_DY:SLOT_DY + 1]
+        dx = fp8_mm(daq, wt1.t(), sda, s1[1:2], out_dtype=dy.dtype).view(ctx.xshape) if need_dx else None
+        dw1 = fp8_mm(dat, xt.t(), sda, s1[0:1], out_dtype=torch.bfloat16) if need_dw1 else None
+        return dx, dw1, db1, dw2, db2, None, None
+
+
+def fp8_gelu_mlp(x, w1, b1, w2, b2, m1: Fp8Meta, m2: Fp8Meta):
+    """GPT-2 MLP  gelu_tanh(x W1^T + b1) W2^T + b2  with fp8 GEMMs and the GELU fused into the casts."""
+    return _Fp8GeluMlpFn.apply(x, w1, b1, w2, b2, m1, m2)

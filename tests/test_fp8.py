@@ -157,3 +157,43 @@ def test_trainer_fp8_gpt2_step():
         losses.append(float(loss.detach()))
     assert "_fp8" in m.h[0].attn.c_attn.__dict__
     assert all(l == l for l in losses) and losses[-1] < losses[0]
+
+
+def _check_gelu_mlp(dev, M=256, d=128, tol=0.12):   # two e5m2-quantised gradient stages
+    from pytorch_distributedtraining_amd.models.gpt2 import MLP, gpt2_config
+    torch.manual_seed(0)
+    cfg = gpt2_config("gpt2-tiny", n_embd=d, n_head=2)
+    mlp = MLP(cfg).to(dev).bfloat16()
+    with torch.no_grad():
+        mlp.c_fc.bias.normal_(0, 0.5)
+        mlp.c_proj.bias.normal_(0, 0.5)
+    ref = [p.detach().float().clone().requires_grad_() for p in (mlp.c_fc.weight, mlp.c_fc.bias, mlp.c_proj.weight,
+                                                                 mlp.c_proj.bias)]
+    x = torch.randn(2, M // 2, d, device=dev)
+    dy = torch.randn(2, M // 2, d, device=dev)
+    for it in range(3):
+        xb = x.bfloat16().requires_grad_()
+        mlp.zero_grad()
+        with F8.fp8_autocast():
+            y = mlp(xb)
+        y.backward(dy.bfloat16())
+        xr = x.clone().requires_grad_()
+        for r in ref:
+            r.grad = None
+        h = F8._gelu_tanh(torch.nn.functional.linear(xr, ref[0], ref[1]))
+        yr = torch.nn.functional.linear(h, ref[2], ref[3])
+        yr.backward(dy)
+        assert rel_err(y, yr) < tol, it
+        assert rel_err(xb.grad, xr.grad) < tol, it
+        for got, want in zip((mlp.c_fc.weight, mlp.c_fc.bias, mlp.c_proj.weight, mlp.c_proj.bias), ref):
+            assert rel_err(got.grad, want.grad) < tol, (it, got.shape)
+    assert "_fp8" in mlp.c_fc.__dict__ and "_fp8" in mlp.c_proj.__dict__
+
+
+def test_fp8_gelu_mlp_cpu():
+    _check_gelu_mlp("cpu")
+
+
+@pytest.mark.gpu
+def test_fp8_gelu_mlp_gpu():
+    _check_gelu_mlp("cuda", M=4096, d=1024)
