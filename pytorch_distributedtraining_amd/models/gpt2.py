@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
 from ..ops.embedding import Embedding
-from ..ops.fp8 import fp8_enabled, fp8_gelu_mlp, fp8_gelu_mlp_ok
+from ..ops.fp8 import fp8_enabled, fp8_gelu_mlp, fp8_gelu_mlp_ok, fp8_recompute_safe
 from ..ops.linear import Linear, linear
 from ..ops.norms import LayerNorm
 
@@ -161,7 +161,7 @@ class GPT2LMHeadModel(nn.Module):
         n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.h)
         for i, blk in enumerate(self.h):
             if self.config.activation_checkpointing and self.training and i < n_ckpt:
-                x, pending = torch.utils.checkpoint.checkpoint(blk, x, pending, use_reentrant=False)
+                x, pending = torch.utils.checkpoint.checkpoint(fp8_recompute_safe(blk), x, pending, use_reentrant=False)
             else:
                 x, pending = blk(x, pending)
         x, _ = self.ln_f.forward_add(x, pending)

@@ -20,6 +20,7 @@ from ..ops import cross_entropy, rope_tables, swiglu
 from ..ops.attention import flash_attn_gqa_packed
 from ..ops.rope import apply_rope_qk_
 from ..ops.embedding import Embedding
+from ..ops.fp8 import fp8_recompute_safe
 from ..ops.linear import Linear
 from ..ops.norms import RMSNorm
 
@@ -145,7 +146,8 @@ class Llama(nn.Module):
         n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.layers)
         for i, layer in enumerate(self.layers):
             if self.config.activation_checkpointing and self.training and i < n_ckpt:
-                x, pending = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, pending, use_reentrant=False)
+                x, pending = torch.utils.checkpoint.checkpoint(fp8_recompute_safe(layer), x, cos, sin, pending,
+                                                               use_reentrant=False)
             else:
                 x, pending = layer(x, cos, sin, pending)
         h = self.norm(x) if pending is None else self.norm.forward_add(x, pending)[0]

@@ -89,6 +89,18 @@ def fp8_enabled() -> bool:
     return _Fp8State.enabled
 
 
+def fp8_recompute_safe(fn):
+    """Wrap an activation-checkpointed function so its backward-time recomputation runs under the fp8 setting
+    of the original forward (the recompute happens outside ``fp8_autocast``; without this it would take the
+    bf16 path and save different tensors)."""
+    state = (_Fp8State.enabled, _Fp8State.margin, _Fp8State.history)
+
+    def run(*args, **kwargs):
+        with fp8_autocast(state[0], state[1], state[2]):
+            return fn(*args, **kwargs)
+    return run
+
+
 class Fp8Meta:
     """Delayed-scaling state of one linear: slots x / w / dy, amax history [3, H], the amax being
     accumulated this iteration (fp32 bits, max-reduced by the cast kernels), scale and 1 / scale."""
@@ -188,7 +200,7 @@ class _Fp8LinearFn(torch.autograd.Function):
         y = fp8_mm(xq, wq.t(), sinv[0:1], sinv[1:2], bias, out_dtype=x.dtype)
         ctx.save_for_backward(xt, wt, sinv)
         ctx.meta, ctx.has_bias, ctx.xshape, ctx.wdtype = meta, bias is not None, x.shape, weight.dtype
-        return y.view(*x.shape[:-1], weight.shape[0])
+        return y            # 2-D: callers reshape OUTSIDE the Function (in-place RoPE on a view of it is legal)
 
     @staticmethod
     def backward(ctx, dy):
@@ -214,7 +226,8 @@ class _Fp8LinearFn(torch.autograd.Function):
 
 
 def fp8_linear(x: torch.Tensor, weight: torch.Tensor, bias, meta: Fp8Meta) -> torch.Tensor:
-    return _Fp8LinearFn.apply(x, weight, bias, meta)
+    y = _Fp8LinearFn.apply(x.reshape(-1, x.shape[-1]), weight, bias, meta)
+    return y.view(*x.shape[:-1], weight.shape[0])
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -297,7 +310,7 @@ class _Fp8GeluMlpFn(torch.autograd.Function):
         y = fp8_mm(hq, wq2.t(), s2[0:1], s2[1:2], b2, out_dtype=x.dtype)
         ctx.save_for_backward(xt, wt1, a, b1, ht, wt2, s1, s2)
         ctx.m1, ctx.m2, ctx.xshape = m1, m2, x.shape
-        return y.view(*x.shape[:-1], w2.shape[0])
+        return y
 
     @staticmethod
     def backward(ctx, dy):
@@ -329,4 +342,5 @@ class _Fp8GeluMlpFn(torch.autograd.Function):
 
 def fp8_gelu_mlp(x, w1, b1, w2, b2, m1: Fp8Meta, m2: Fp8Meta):
     """GPT-2 MLP  gelu_tanh(x W1^T + b1) W2^T + b2  with fp8 GEMMs and the GELU fused into the casts."""
-    return _Fp8GeluMlpFn.apply(x, w1, b1, w2, b2, m1, m2)
+    y = _Fp8GeluMlpFn.apply(x.reshape(-1, x.shape[-1]), w1, b1, w2, b2, m1, m2)
+    return y.view(*x.shape[:-1], w2.shape[0])

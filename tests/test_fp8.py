@@ -197,3 +197,30 @@ def test_fp8_gelu_mlp_cpu():
 @pytest.mark.gpu
 def test_fp8_gelu_mlp_gpu():
     _check_gelu_mlp("cuda", M=4096, d=1024)
+
+
+def test_fp8_linear_output_allows_inplace_cpu():
+    """Llama rotates q / k in place inside the qkv projection output: the fp8 linear's output must allow it."""
+    lin = Linear(64, 192, bias=False).bfloat16()
+    x = torch.randn(2, 16, 64).bfloat16().requires_grad_()
+    with F8.fp8_autocast():
+        y = lin(x)
+    y.view(2, 16, 3, 64)[:, :, 0].mul_(2.0)
+    y.float().sum().backward()
+    assert x.grad is not None and lin.weight.grad is not None
+
+
+def test_fp8_with_activation_checkpointing_cpu():
+    """Checkpointed blocks recompute under the forward's fp8 setting (same saved tensors, same gradients)."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+
+    def grads(ckpt):
+        torch.manual_seed(0)
+        m = build_gpt2("gpt2-tiny", n_embd=128, n_head=2, n_layer=2, activation_checkpointing=ckpt).bfloat16()
+        x = torch.randint(0, 512, (2, 65))
+        with F8.fp8_autocast():
+            loss = m(x[:, :-1], labels=x[:, 1:])
+        loss.backward()
+        return m.h[0].mlp.c_fc.weight.grad.float()
+    g0, g1 = grads(False), grads(True)
+    assert rel_err(g1, g0) < 1e-2
