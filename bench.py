@@ -1,10 +1,10 @@
 #!/usr/bin/env python
 """Flagship benchmark: GPT-2 1.3B, FSDP full-shard, bf16, fused AdamW + global grad-norm clipping,
-synthetic tokens (random-init weights), seq 1024, 64 sequences per GPU (weak scaling; the MI355X's
+synthetic tokens (random-init weights), seq 1024, 96 sequences per GPU (weak scaling; the MI355X's
 288 GB let the per-GPU batch grow -- larger GEMMs, the optimizer step and every FSDP all-gather /
 reduce-scatter amortised over more tokens: 16 -> 32 sequences +4 % (r1_v5 logs), 32 -> 64 +2.8 % at a
 132 GB peak, 126.3k -> 129.8k tokens/s; stock torch FSDP gains 3.9 % from the same change,
-profiles/r2_flagship_microbatch.log).
+profiles/r2_flagship_microbatch.log; 64 -> 96 +1.3 % at 188 GB, profiles/r2_flagship_microbatch_64_96_128.log).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gpt2-fsdp|gpt2-ddp|resnet50-ddp]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -250,8 +250,10 @@ def bench_gpt2(args, comm, dev, world, rank):
     llama = args.workload.startswith("llama")
     name = args.model or ("llama3-8b" if llama else "gpt2-1.3b" if fsdp else "gpt2-124m")
     # per-GPU micro-batch sized for 288 GB HBM: GPT-2 124M DDP 16 -> 64 sequences 700k -> 886k tokens/s
-    # (profiles/r2_gpt2_124m_ddp_microbatch.log), GPT-2 1.3B FSDP 32 -> 64 +2.8 % (module docstring)
-    mb = args.micro_batch or (8 if llama else 64)
+    # (profiles/r2_gpt2_124m_ddp_microbatch.log); GPT-2 1.3B FSDP 32 -> 64 +2.8 % (module docstring), 64 -> 96
+    # +1.3 % at 188 GB peak (128: +2.0 % at 243 GB -- not taken, leaves < 50 GB headroom;
+    # profiles/r2_flagship_microbatch_64_96_128.log)
+    mb = args.micro_batch or (8 if llama else 96 if fsdp else 64)
     S = args.seq
     with torch.device(dev):
         if llama:
