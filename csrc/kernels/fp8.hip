@@ -62,8 +62,31 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
   const int ntiles = tiles_c * (R / CT_TS);
   float amax = 0.f;
   uint8_t* t8 = reinterpret_cast<uint8_t*>(tile);
+  // software pipeline: the next tile's rows are loaded into registers before this tile's convert / LDS /
+  // barrier phases, so every wave keeps a tile of reads in flight through the barriers
+  typename Vec8<T>::raw_t xr[2], ar[2];
+  auto load_tile = [&](int tt) {
+    const int rr0 = (tt / tiles_c) * CT_TS, cc0 = (tt % tiles_c) * CT_TS;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      xr[p] = Vec8<T>::load_raw(x + (int64_t)(rr0 + lr + 32 * p) * C + cc0 + lc);
+      if (OP == kBiasGeluBwd) ar[p] = Vec8<T>::load_raw(aux + (int64_t)(rr0 + lr + 32 * p) * C + cc0 + lc);
+    }
+  };
+  if ((int)blockIdx.x < ntiles) load_tile(blockIdx.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r0 = (t / tiles_c) * CT_TS, c0 = (t % tiles_c) * CT_TS;
+    float vin[2][8], ain[2][8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      Vec8<T>::unpack(xr[p], vin[p]);
+      if (OP == kBiasGeluBwd) Vec8<T>::unpack(ar[p], ain[p]);
+    }
+    float b[8];                                 // bias before the prefetch: in-order vmcnt would otherwise
+    if (OP != kPlain) Vec8<T>::load(bias + c0 + lc, b);   // make the bias wait drain the next tile's loads too
+    // unconditional (clamped) prefetch: a branch around it would make hipcc's waitcnt pass drain it at the
+    // merge (vmcnt(0) before the bias / first use), serialising the pipeline again
+    load_tile(min(t + (int)gridDim.x, ntiles - 1));
     float cs[8];
     if (OP == kBiasGeluBwd) {
 #pragma unroll
@@ -72,17 +95,13 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int r = lr + 32 * p;
-      float v[8];
-      Vec8<T>::load(x + (int64_t)(r0 + r) * C + c0 + lc, v);
+      float* v = vin[p];
       if (OP != kPlain) {
-        float b[8];
-        Vec8<T>::load(bias + c0 + lc, b);
         if (OP == kBiasGelu) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = gelu_tanh(v[k] + b[k]);
         } else {
-          float a[8];
-          Vec8<T>::load(aux + (int64_t)(r0 + r) * C + c0 + lc, a);
+          const float* a = ain[p];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             v[k] *= gelu_tanh_grad(a[k] + b[k]);
