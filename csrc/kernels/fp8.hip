@@ -15,6 +15,7 @@
 #include "reduce.h"
 
 #include <hip/hip_fp8.h>
+#include <stdlib.h>
 
 namespace pdt {
 namespace {
@@ -159,6 +160,115 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
   }
 }
 
+// 128 x 128-tile variant for R % 128 == 0 and C % 128 == 0 (every GPT-2 / Llama shape): each lane converts 16
+// consecutive elements, so a wave's row store is 8 rows x 128 contiguous bytes (16 B per lane) and its transposed
+// store 8 output rows x 128 B -- the 64 x 64 tiles' 8-byte-per-lane / 64-byte-segment stores capped the casts at
+// ~3.5-3.75 TB/s (scripts/bench_fp8_cast.py).  LDS rows are 132 B (33 words): the transposed byte gathers of a
+// wave touch 16 banks twice (2-way), the 16-byte row writes go as four ds_write_b32.
+constexpr int CT2 = 128, CT2_LD = 132;
+template <typename T, int FMT, int OP = kPlain>
+__global__ __launch_bounds__(256) void fp8_ct128_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
+                                                        uint8_t* __restrict__ qt, int R, int C,
+                                                        const float* __restrict__ scale,
+                                                        unsigned int* __restrict__ amax_bits,
+                                                        const T* __restrict__ aux, const T* __restrict__ bias,
+                                                        float* __restrict__ dbias_part) {
+  __shared__ uint32_t tile[CT2 * CT2_LD / 4];
+  __shared__ float red[4];
+  __shared__ float colp[OP == kBiasGeluBwd ? 32 : 1][OP == kBiasGeluBwd ? CT2 : 1];
+  const int tid = threadIdx.x;
+  const int lc = (tid & 7) * 16, lr = tid >> 3;  // 8 lanes x 16 columns per row, 32 rows per pass, 4 passes
+  const float sc = scale ? *scale : 1.f;
+  const int tiles_c = C / CT2;
+  const int ntiles = tiles_c * (R / CT2);
+  float amax = 0.f;
+  const uint8_t* t8 = reinterpret_cast<const uint8_t*>(tile);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int r0 = (t / tiles_c) * CT2, c0 = (t % tiles_c) * CT2;
+    float b[16], cs[16];
+    if (OP != kPlain) {
+      Vec8<T>::load(bias + c0 + lc, b);
+      Vec8<T>::load(bias + c0 + lc + 8, b + 8);
+    }
+    if (OP == kBiasGeluBwd) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) cs[k] = 0.f;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = lr + 32 * p;
+      const int64_t off = (int64_t)(r0 + r) * C + c0 + lc;
+      float v[16];
+      Vec8<T>::load(x + off, v);
+      Vec8<T>::load(x + off + 8, v + 8);
+      if (OP == kBiasGelu) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = gelu_tanh(v[k] + b[k]);
+      } else if (OP == kBiasGeluBwd) {
+        float a[16];
+        Vec8<T>::load(aux + off, a);
+        Vec8<T>::load(aux + off + 8, a + 8);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          v[k] *= gelu_tanh_grad(a[k] + b[k]);
+          cs[k] += v[k];
+        }
+      }
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w[j] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float e = v[4 * j + k];
+          amax = fmaxf(amax, fabsf(e));
+          w[j] |= (uint32_t)to_fp8<FMT>(e * sc) << (8 * k);
+        }
+      }
+      if (q) *reinterpret_cast<uint4*>(q + off) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (qt) {
+        uint32_t* dst = tile + (r * CT2_LD + lc) / 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = w[j];
+      }
+    }
+    if (OP == kBiasGeluBwd) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) colp[lr][lc + k] = cs[k];
+      __syncthreads();
+      if (tid < CT2) {
+        float sum = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) sum += colp[i][tid];
+        dbias_part[(int64_t)(r0 / CT2) * C + c0 + tid] = sum;
+      }
+      if (!qt) __syncthreads();
+    }
+    if (qt) {
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int c = lr + 32 * p;               // output row (= input column); 16 input rows lc..lc+15
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          w[j] = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) w[j] |= (uint32_t)t8[(lc + 4 * j + k) * CT2_LD + c] << (8 * k);
+        }
+        *reinterpret_cast<uint4*>(qt + (int64_t)(c0 + c) * R + r0 + lc) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      __syncthreads();
+    }
+  }
+  if (amax_bits) {
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) red[tid >> 6] = amax;
+    __syncthreads();
+    if (tid == 0) atomicMax(amax_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  }
+}
+
 // Slots [s0, s1) of a module's fp8 meta: hist [n_slots, H], cur [n_slots] (amax bits), scale / scale_inv
 // [n_slots].  One thread per slot (a module has 3).
 __global__ void fp8_update_scales_kernel(float* __restrict__ hist, unsigned int* __restrict__ cur,
@@ -188,16 +298,31 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ hist, unsigned int*
 
 using namespace pdt;
 
+// 128-tile kernel when the shape allows (16-byte stores), else the 64-tile one; tile-row count of the dbias
+// partials follows the tile (ct_tile_rows)
+static bool ct_wide(int R, int C) { return R % CT2 == 0 && C % CT2 == 0 && getenv("PDT_FP8_CT64") == nullptr; }
+static int ct_tile_rows(int R, int C) { return ct_wide(R, C) ? CT2 : CT_TS; }
+template <typename T, int FMT, int OP>
+static void ct_launch(const T* x, uint8_t* q, uint8_t* qt, int R, int C, const float* scale, unsigned int* amax,
+                      const T* aux, const T* bias, float* dbp, hipStream_t st) {
+  const int ts = ct_tile_rows(R, C);
+  const long long tiles = (long long)(R / ts) * (C / ts);
+  const int grid = (int)(tiles < 2048 ? tiles : 2048);
+  if (ts == CT2)
+    fp8_ct128_kernel<T, FMT, OP><<<grid, 256, 0, st>>>(x, q, qt, R, C, scale, amax, aux, bias, dbp);
+  else
+    fp8_cast_transpose_kernel<T, FMT, OP><<<grid, 256, 0, st>>>(x, q, qt, R, C, scale, amax, aux, bias, dbp);
+}
+
 // fmt: 0 = e4m3fn, 1 = e5m2; dt: kF32 / kBF16.  Returns hipErrorInvalidValue for unsupported shapes
 // (the Python side then takes its torch path).
 PDT_API int pdt_fp8_cast_transpose(const void* x, void* q, void* qt, int R, int C, int dt, int fmt,
                                    const float* scale, unsigned int* amax_bits, hipStream_t st) {
   if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS) return (int)hipErrorInvalidValue;
-  if (reinterpret_cast<uintptr_t>(x) & 15) return (int)hipErrorInvalidValue;
-  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
-  const int grid = (int)(tiles < 2048 ? tiles : 2048);   // 8 blocks per CU, <= 2048 amax atomics
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(qt)) & 15)
+    return (int)hipErrorInvalidValue;
 #define PDT_L(T, F) \
-  fp8_cast_transpose_kernel<T, F><<<grid, 256, 0, st>>>((const T*)x, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits)
+  ct_launch<T, F, kPlain>((const T*)x, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, nullptr, nullptr, nullptr, st)
   if (dt == kBF16) { if (fmt == 0) PDT_L(bf16_t, 0); else PDT_L(bf16_t, 1); }
   else if (dt == kF32) { if (fmt == 0) PDT_L(float, 0); else PDT_L(float, 1); }
   else return (int)hipErrorInvalidValue;
@@ -209,21 +334,19 @@ PDT_API int pdt_fp8_cast_transpose(const void* x, void* q, void* qt, int R, int 
 //   fwd: q / qt = fp8(gelu(a + bias) * scale)            amax of the GELU output
 //   bwd: q / qt = fp8(dh * gelu'(a + bias) * scale)     amax of dA, dbias[C] (bf16) = column sums of dA
 // ws: pdt_fp8_gelu_bwd_ws_floats(R, C) floats.
-PDT_API long long pdt_fp8_gelu_bwd_ws_floats(int R, int C) { return (long long)(R / CT_TS) * C + red::col_ws_floats(R / CT_TS, C); }
+PDT_API long long pdt_fp8_gelu_bwd_ws_floats(int R, int C) {
+  return (long long)(R / CT_TS) * C + red::col_ws_floats(R / CT_TS, C);   // sized for the 64-row tiles (the larger)
+}
 
 PDT_API int pdt_fp8_bias_gelu_ct(const void* a, const void* bias, void* q, void* qt, int R, int C, int fmt,
                                  const float* scale, unsigned int* amax_bits, hipStream_t st) {
   if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias) return (int)hipErrorInvalidValue;
-  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
-  const int grid = (int)(tiles < 2048 ? tiles : 2048);
   if (fmt == 0)
-    fp8_cast_transpose_kernel<bf16_t, 0, kBiasGelu><<<grid, 256, 0, st>>>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R,
-                                                                          C, scale, amax_bits, nullptr,
-                                                                          (const bf16_t*)bias, nullptr);
+    ct_launch<bf16_t, 0, kBiasGelu>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, nullptr,
+                                    (const bf16_t*)bias, nullptr, st);
   else
-    fp8_cast_transpose_kernel<bf16_t, 1, kBiasGelu><<<grid, 256, 0, st>>>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R,
-                                                                          C, scale, amax_bits, nullptr,
-                                                                          (const bf16_t*)bias, nullptr);
+    ct_launch<bf16_t, 1, kBiasGelu>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, nullptr,
+                                    (const bf16_t*)bias, nullptr, st);
   return (int)hipGetLastError();
 }
 
@@ -231,15 +354,14 @@ PDT_API int pdt_fp8_bias_gelu_bwd_ct(const void* dh, const void* a, const void* 
                                      float* ws, int R, int C, int fmt, const float* scale, unsigned int* amax_bits,
                                      hipStream_t st) {
   if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias || !ws) return (int)hipErrorInvalidValue;
-  const long long tiles = (long long)(R / CT_TS) * (C / CT_TS);
-  const int grid = (int)(tiles < 2048 ? tiles : 2048);
   if (fmt == 0)
-    fp8_cast_transpose_kernel<bf16_t, 0, kBiasGeluBwd><<<grid, 256, 0, st>>>(
-        (const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, (const bf16_t*)a, (const bf16_t*)bias, ws);
+    ct_launch<bf16_t, 0, kBiasGeluBwd>((const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits,
+                                       (const bf16_t*)a, (const bf16_t*)bias, ws, st);
   else
-    fp8_cast_transpose_kernel<bf16_t, 1, kBiasGeluBwd><<<grid, 256, 0, st>>>(
-        (const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, (const bf16_t*)a, (const bf16_t*)bias, ws);
-  if (dbias) red::col_reduce<bf16_t>(ws, R / CT_TS, C, (bf16_t*)dbias, ws + (long long)(R / CT_TS) * C, 0, st);
+    ct_launch<bf16_t, 1, kBiasGeluBwd>((const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits,
+                                       (const bf16_t*)a, (const bf16_t*)bias, ws, st);
+  const int pr = R / ct_tile_rows(R, C);   // dbias partial rows
+  if (dbias) red::col_reduce<bf16_t>(ws, pr, C, (bf16_t*)dbias, ws + (long long)pr * C, 0, st);
   return (int)hipGetLastError();
 }
 

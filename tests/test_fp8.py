@@ -70,7 +70,7 @@ def test_fp8_off_outside_autocast_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R,C", [(128, 64), (4096, 2048), (640, 192)])
+@pytest.mark.parametrize("R,C", [(128, 64), (4096, 2048), (640, 192), (384, 256)])
 @pytest.mark.parametrize("fmt", [0, 1])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_fp8_cast_transpose_gpu(R, C, fmt, dt):
