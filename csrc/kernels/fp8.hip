@@ -166,6 +166,9 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const T* __rest
 // ~3.5-3.75 TB/s (scripts/bench_fp8_cast.py).  LDS rows are 132 B (33 words): the transposed byte gathers of a
 // wave touch 16 banks twice (2-way), the 16-byte row writes go as four ds_write_b32.
 constexpr int CT2 = 128, CT2_LD = 132;
+// LDS word of (tile row, 4-column word w): 33-word rows, words of rows >= 64 rotated by 8 so the transposed
+// gathers (16-row stride per lane group) spread over all 64 banks
+__device__ __forceinline__ int ct2_word(int row, int w) { return row * (CT2_LD / 4) + ((w + ((row >> 6) << 3)) & 31); }
 template <typename T, int FMT, int OP = kPlain>
 __global__ __launch_bounds__(256) void fp8_ct128_kernel(const T* __restrict__ x, uint8_t* __restrict__ q,
                                                         uint8_t* __restrict__ qt, int R, int C,
@@ -182,7 +185,6 @@ __global__ __launch_bounds__(256) void fp8_ct128_kernel(const T* __restrict__ x,
   const int tiles_c = C / CT2;
   const int ntiles = tiles_c * (R / CT2);
   float amax = 0.f;
-  const uint8_t* t8 = reinterpret_cast<const uint8_t*>(tile);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r0 = (t / tiles_c) * CT2, c0 = (t % tiles_c) * CT2;
     float b[16], cs[16];
@@ -227,9 +229,8 @@ __global__ __launch_bounds__(256) void fp8_ct128_kernel(const T* __restrict__ x,
       }
       if (q) *reinterpret_cast<uint4*>(q + off) = make_uint4(w[0], w[1], w[2], w[3]);
       if (qt) {
-        uint32_t* dst = tile + (r * CT2_LD + lc) / 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = w[j];
+        for (int j = 0; j < 4; ++j) tile[ct2_word(r, lc / 4 + j)] = w[j];
       }
     }
     if (OP == kBiasGeluBwd) {
@@ -246,18 +247,26 @@ __global__ __launch_bounds__(256) void fp8_ct128_kernel(const T* __restrict__ x,
     }
     if (qt) {
       __syncthreads();
+      // lane: 4 output rows (input columns 4g..4g+3) x 16 input rows (16j..16j+15): 16 word reads, 4x4 byte
+      // transposes in registers (v_perm_b32), 4 x 16-byte stores -- 8 lanes cover an output row's 128 bytes
+      const int j = tid & 7, g = tid >> 3;
+      uint32_t o[4][4];                          // o[i][m]: output row 4g + i, input rows 16j + 4m .. + 3
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int c = lr + 32 * p;               // output row (= input column); 16 input rows lc..lc+15
+      for (int m = 0; m < 4; ++m) {
         uint32_t w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          w[j] = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) w[j] |= (uint32_t)t8[(lc + 4 * j + k) * CT2_LD + c] << (8 * k);
-        }
-        *reinterpret_cast<uint4*>(qt + (int64_t)(c0 + c) * R + r0 + lc) = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int k = 0; k < 4; ++k) w[k] = tile[ct2_word(16 * j + 4 * m + k, g)];
+        const uint32_t t0 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u), t1 = __builtin_amdgcn_perm(w[3], w[2], 0x05010400u);
+        const uint32_t t2 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u), t3 = __builtin_amdgcn_perm(w[3], w[2], 0x07030602u);
+        o[0][m] = __builtin_amdgcn_perm(t1, t0, 0x05040100u);
+        o[1][m] = __builtin_amdgcn_perm(t1, t0, 0x07060302u);
+        o[2][m] = __builtin_amdgcn_perm(t3, t2, 0x05040100u);
+        o[3][m] = __builtin_amdgcn_perm(t3, t2, 0x07060302u);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(qt + (int64_t)(c0 + 4 * g + i) * R + r0 + 16 * j) =
+            make_uint4(o[i][0], o[i][1], o[i][2], o[i][3]);
       __syncthreads();
     }
   }
