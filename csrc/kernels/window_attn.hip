@@ -263,8 +263,19 @@ constexpr int BP = 68;       // padded bias row (bf16): conflict-free 8-byte rea
 constexpr int TP = 68;       // transposed-tile row pitch (tokens)
 constexpr int TT = 17 * TP;  // transposed tile: rows 0..15 = head dims, row 16 = zeros for lanes dd >= 16
 constexpr int WA_NT = 256;   // 4 waves per workgroup
-constexpr int FWD_WAVE = 2 * 1024 + TT + 4;                   // QR, KR, VT (u16, padded to 16 B)
-constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4;         // QR KR VR GR, SL SD (fp32), 2 transposed
+constexpr int FWD_WAVE = 2 * 1024 + TT + 4 + 32;              // QR, KR, VT (u16, padded to 16 B), 64 B labels
+constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4 + 32;    // QR KR VR GR, SL SD (fp32), 2 transposed, labels
+// Shift-mask modes (template MK): 0 none, 1 dense fp32 mask [nw, N, N] read from L2, 2 region labels
+// [nw, N] uint8 -- Swin's mask is -100 exactly where the query's and key's image regions differ, so the
+// kernel rebuilds it from 64 label bytes per window staged in LDS (one 4-byte read per 4 keys) instead of
+// reading 16 KB of fp32 mask per window and head.
+__device__ __forceinline__ f32x4 label_mask(const uint8_t* lab, int base, uint32_t mine) {
+  const uint32_t four = *reinterpret_cast<const uint32_t*>(lab + base);
+  f32x4 m;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[j] = ((four >> (8 * j)) & 0xffu) != mine ? -100.f : 0.f;
+  return m;
+}
 
 __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -356,10 +367,11 @@ __device__ __forceinline__ void stage_bias(const float* g, u16* s, int N) {
   }
 }
 
-template <int D, bool HAS_MASK, bool FULL>
+template <int D, int MK, bool FULL>
 __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __restrict__ qkv,
                                                                const float* __restrict__ bias,
-                                                               const float* __restrict__ mask, int nw,
+                                                               const float* __restrict__ mask,
+                                                               const uint8_t* __restrict__ labels, int nw,
                                                                bf16_t* __restrict__ o, float* __restrict__ lse, int Bw,
                                                                int N, int H, float scale, int P) {
   extern __shared__ __attribute__((aligned(16))) u16 smf[];
@@ -370,6 +382,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
   u16* QR = smf + 64 * BP + wv * FWD_WAVE;          // this wave's tiles
   u16* KR = QR + 1024;
   u16* VT = KR + 1024;
+  uint8_t* LAB = reinterpret_cast<uint8_t*>(VT + TT + 4);
   stage_bias<false>(bias + (int64_t)h * N * N, BR, N);
   for (int e = lane; e < TT; e += 64) VT[e] = 0;
   __syncthreads();
@@ -384,9 +397,10 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
         q.zero(); k.zero(); v.zero();
       }
       q.put_row(QR, lane); k.put_row(KR, lane); v.put_col(VT, lane);
+      if (MK == 2) LAB[lane] = lane < N ? labels[(int64_t)(bw % nw) * N + lane] : (uint8_t)255;
     }
     wave_sync();
-    const float* mw = HAS_MASK ? mask + (int64_t)(bw % nw) * N * N : nullptr;
+    const float* mw = MK == 1 ? mask + (int64_t)(bw % nw) * N * N : nullptr;
     u16x8 kf[2], qf[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -399,6 +413,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
     for (int qt = 0; qt < 2; ++qt) {
       const int q = 32 * qt + l32;
       const int qc = FULL ? q : min(q, N - 1);
+      const uint32_t qlab = MK == 2 ? LAB[q] : 0u;
       float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -408,7 +423,9 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
           const int base = 32 * kt + 8 * i + 4 * hh;
           const u16x4 bv = ld4(BR + q * BP + base);
           f32x4 mv = {0.f, 0.f, 0.f, 0.f};
-          if (HAS_MASK) {
+          if (MK == 2) {
+            mv = label_mask(LAB, base, qlab);
+          } else if (MK == 1) {
             if (FULL) {
               mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
             } else {
@@ -462,9 +479,10 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
 // Backward pass PASS (1: dQ + relative-bias gradient, lane = query; 2: dK, dV, lane = key).  Two launches
 // rather than one so neither holds the other's registers (the 64-register bias-gradient accumulator of
 // pass 1 next to pass 2's P / dS tiles spilled).  Both recompute delta = rowsum(dO o O) while staging.
-template <int D, bool HAS_MASK, bool FULL, int PASS>
+template <int D, int MK, bool FULL, int PASS>
 __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
-    const bf16_t* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask, int nw,
+    const bf16_t* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask,
+    const uint8_t* __restrict__ labels, int nw,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P) {
   extern __shared__ __attribute__((aligned(16))) u16 smb[];
@@ -480,6 +498,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
   float* SD = SL + 64;                               // [64] delta
   u16* T0 = GR + 1024 + 256;                         // pass 1: K^T; pass 2: Q^T
   u16* T1 = T0 + TT;                                 // pass 2: dO^T
+  uint8_t* LAB = reinterpret_cast<uint8_t*>(T1 + TT + 4);
   stage_bias<PASS == 2>(bias + (int64_t)h * N * N, BB, N);
   for (int e = lane; e < 2 * TT; e += 64) T0[e] = 0;
   __syncthreads();
@@ -516,9 +535,10 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
       }
       SL[lane] = L;
       SD[lane] = dl;
+      if (MK == 2) LAB[lane] = lane < N ? labels[(int64_t)(bw % nw) * N + lane] : (uint8_t)255;
     }
     wave_sync();
-    const float* mw = HAS_MASK ? mask + (int64_t)(bw % nw) * N * N : nullptr;
+    const float* mw = MK == 1 ? mask + (int64_t)(bw % nw) * N * N : nullptr;
     if (PASS == 1) {
       // lane = query (S^T layout): dS^T, dQ = dS K * scale, dS summed for the bias gradient
       u16x8 ktf[4];
@@ -529,6 +549,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
         const int q = 32 * qt + l32;
         const int qc = FULL ? q : min(q, N - 1);
         const float Lq = SL[q], Dq = SD[q];
+        const uint32_t qlab = MK == 2 ? LAB[q] : 0u;
         const u16x8 qf = rfrag(QR, q, hh), gf = rfrag(GR, q, hh);
         u16x8 dsk[4];
 #pragma unroll
@@ -541,7 +562,9 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
             const int base = 32 * kt + 8 * i + 4 * hh;
             const u16x4 bv = ld4(BB + q * BP + base);
             f32x4 mv = {0.f, 0.f, 0.f, 0.f};
-            if (HAS_MASK) {
+            if (MK == 2) {
+              mv = label_mask(LAB, base, qlab);
+            } else if (MK == 1) {
               if (FULL) {
                 mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
               } else {
@@ -574,6 +597,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
         const int key = 32 * kt + l32;
         const int kc = FULL ? key : min(key, N - 1);
         const u16x8 kf = rfrag(KR, key, hh), vf = rfrag(VR, key, hh);
+        const uint32_t klab = MK == 2 ? LAB[key] : 0u;
         f32x16 av = zero16(), ak = zero16();
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
@@ -586,8 +610,10 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
             const u16x4 bv = ld4(BB + key * BP + base);
             const f32x4 L4 = *reinterpret_cast<const f32x4*>(SL + base);
             const f32x4 D4 = *reinterpret_cast<const f32x4*>(SD + base);
-            float mv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (HAS_MASK) {
+            f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+            if (MK == 2) {
+              mv = label_mask(LAB, base, klab);        // the 4 queries' labels vs this lane's key
+            } else if (MK == 1) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) mv[j] = (FULL || base + j < N) ? mw[(base + j) * N + kc] : 0.f;
             }
@@ -671,67 +697,78 @@ PDT_API int pdt_win_attn_mfma_grid(int Bw, int H) { return mfma_blocks_per_head(
 
 namespace {
 template <int D>
-int wa_fwd_launch(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse, int Bw, int N,
-                  int H, float scale, hipStream_t st) {
+int wa_fwd_launch(const void* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, void* o,
+                  float* lse, int Bw, int N, int H, float scale, hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 4);
   const size_t lds = fwd_mfma_lds();
   const bool full = N == 64;
-#define PDT_WF(M, F)                                                                                            \
-  win_attn_fwd_mfma<D, M, F><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (bf16_t*)o, lse, Bw, N, \
-                                                        H, scale, P)
-  if (mask) { if (full) PDT_WF(true, true); else PDT_WF(true, false); }
-  else { if (full) PDT_WF(false, true); else PDT_WF(false, false); }
+#define PDT_WF(M, F)                                                                                          \
+  win_attn_fwd_mfma<D, M, F><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, labels, nw, (bf16_t*)o, \
+                                                        lse, Bw, N, H, scale, P)
+  if (labels) { if (full) PDT_WF(2, true); else PDT_WF(2, false); }
+  else if (mask) { if (full) PDT_WF(1, true); else PDT_WF(1, false); }
+  else { if (full) PDT_WF(0, true); else PDT_WF(0, false); }
 #undef PDT_WF
   return (int)hipGetLastError();
 }
 template <int D>
-int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, int nw, const void* o, const void* dout,
-                  const float* lse, void* dqkv, float* dbias_part, int Bw, int N, int H, float scale, hipStream_t st) {
+int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, const void* o,
+                  const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N, int H, float scale,
+                  hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 2);
   const size_t lds = bwd_mfma_lds();
   static bool attr = [] {
     bool ok = true;
-    const void* fns[8] = {
-        (const void*)win_attn_bwd_mfma<D, true, true, 1>,   (const void*)win_attn_bwd_mfma<D, true, false, 1>,
-        (const void*)win_attn_bwd_mfma<D, false, true, 1>,  (const void*)win_attn_bwd_mfma<D, false, false, 1>,
-        (const void*)win_attn_bwd_mfma<D, true, true, 2>,   (const void*)win_attn_bwd_mfma<D, true, false, 2>,
-        (const void*)win_attn_bwd_mfma<D, false, true, 2>,  (const void*)win_attn_bwd_mfma<D, false, false, 2>};
+    const void* fns[12] = {
+        (const void*)win_attn_bwd_mfma<D, 1, true, 1>,  (const void*)win_attn_bwd_mfma<D, 1, false, 1>,
+        (const void*)win_attn_bwd_mfma<D, 0, true, 1>,  (const void*)win_attn_bwd_mfma<D, 0, false, 1>,
+        (const void*)win_attn_bwd_mfma<D, 1, true, 2>,  (const void*)win_attn_bwd_mfma<D, 1, false, 2>,
+        (const void*)win_attn_bwd_mfma<D, 0, true, 2>,  (const void*)win_attn_bwd_mfma<D, 0, false, 2>,
+        (const void*)win_attn_bwd_mfma<D, 2, true, 1>,  (const void*)win_attn_bwd_mfma<D, 2, false, 1>,
+        (const void*)win_attn_bwd_mfma<D, 2, true, 2>,  (const void*)win_attn_bwd_mfma<D, 2, false, 2>};
     for (const void* f : fns)
       ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_mfma_lds()) == hipSuccess;
     return ok;
   }();
   if (!attr) return (int)hipErrorInvalidValue;
   const bool full = N == 64;
-#define PDT_WB(M, F, PS)                                                                                       \
-  win_attn_bwd_mfma<D, M, F, PS><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, nw, (const bf16_t*)o, \
-                                                            (const bf16_t*)dout, lse, (bf16_t*)dqkv, dbias_part, Bw, N, \
-                                                            H, scale, P)
-  if (mask) {
-    if (full) { PDT_WB(true, true, 1); PDT_WB(true, true, 2); }
-    else { PDT_WB(true, false, 1); PDT_WB(true, false, 2); }
+#define PDT_WB(M, F, PS)                                                                                           \
+  win_attn_bwd_mfma<D, M, F, PS><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, labels, nw,              \
+                                                            (const bf16_t*)o, (const bf16_t*)dout, lse, (bf16_t*)dqkv, \
+                                                            dbias_part, Bw, N, H, scale, P)
+  if (labels) {
+    if (full) { PDT_WB(2, true, 1); PDT_WB(2, true, 2); }
+    else { PDT_WB(2, false, 1); PDT_WB(2, false, 2); }
+  } else if (mask) {
+    if (full) { PDT_WB(1, true, 1); PDT_WB(1, true, 2); }
+    else { PDT_WB(1, false, 1); PDT_WB(1, false, 2); }
   } else {
-    if (full) { PDT_WB(false, true, 1); PDT_WB(false, true, 2); }
-    else { PDT_WB(false, false, 1); PDT_WB(false, false, 2); }
+    if (full) { PDT_WB(0, true, 1); PDT_WB(0, true, 2); }
+    else { PDT_WB(0, false, 1); PDT_WB(0, false, 2); }
   }
 #undef PDT_WB
   return (int)hipGetLastError();
 }
 }  // namespace
 
-PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, int nw, void* o, float* lse,
-                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || (mask && nw <= 0)) return (int)hipErrorInvalidValue;
-#define PDT_C(D) return wa_fwd_launch<D>(qkv, bias, mask, nw, o, lse, Bw, N, H, scale, st)
+// mask [nw, N, N] fp32 or null; labels [nw, N] uint8 region labels or null (takes precedence over mask:
+// mask value = -100 where the query's and key's labels differ, 0 elsewhere)
+PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
+                                  void* o, float* lse, int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D) return wa_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }
 
 // dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw, H), H, N, N] fp32 fully written
-PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, int nw, const void* o,
-                                  const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N,
-                                  int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || (mask && nw <= 0)) return (int)hipErrorInvalidValue;
-#define PDT_C(D) return wa_bwd_launch<D>(qkv, bias, mask, nw, o, dout, lse, dqkv, dbias_part, Bw, N, H, scale, st)
+PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
+                                  const void* o, const void* dout, const float* lse, void* dqkv, float* dbias_part,
+                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D)                                                                                                   \
+  return wa_bwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, dout, lse, dqkv, dbias_part, Bw, N, H, \
+                          scale, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }

@@ -80,10 +80,10 @@ _SIGS = {
     "pdt_win_attn_grid": [c_int],
     "pdt_win_attn_mfma_ok": [c_int, c_int, c_int, c_int],
     "pdt_win_attn_mfma_grid": [c_int, c_int],
-    "pdt_win_attn_mfma_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                              c_float, c_void_p],
-    "pdt_win_attn_mfma_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "pdt_win_attn_mfma_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                              c_int, c_float, c_void_p],
+    "pdt_win_attn_mfma_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
     "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                          c_int, c_void_p],
     "pdt_win_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

@@ -9,12 +9,15 @@ formula (also the numerics reference in the GPU tests).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _lib
 
 _MASK_T_CACHE: dict = {}
+USE_LABELS = os.environ.get("PDT_WIN_MASK_LABELS", "1") == "1"   # A/B switch: 0 = dense fp32 mask reads
 
 
 def _mask_t(mask):
@@ -28,6 +31,27 @@ def _mask_t(mask):
         hit = (m, m.transpose(1, 2).contiguous())
         _MASK_T_CACHE[key] = hit
     return hit
+
+
+_LABEL_CACHE: dict = {}
+
+
+def _mask_labels(mask):
+    """Swin shift masks are -100 exactly where a query's and a key's image regions differ: return per-window
+    region labels [nw, N] uint8 (label = first key of the token's region) when ``mask`` has that form, else None.
+    The MFMA kernels then rebuild the mask from 64 label bytes per window instead of reading the fp32 mask.
+    Derived once per mask buffer (one host check, in the first -- eager -- call)."""
+    key = (mask.data_ptr(), mask._version, tuple(mask.shape), mask.device)
+    if key in _LABEL_CACHE:
+        return _LABEL_CACHE[key]
+    if len(_LABEL_CACHE) > 64:
+        _LABEL_CACHE.clear()
+    m = mask.float()
+    lab = (m == 0).float().argmax(-1)                                      # [nw, N]
+    rebuilt = torch.where(lab[:, :, None] != lab[:, None, :], -100.0, 0.0)
+    out = lab.to(torch.uint8).contiguous() if (mask.shape[-1] <= 64 and torch.equal(rebuilt, m)) else None
+    _LABEL_CACHE[key] = out
+    return out
 
 
 def reference(qkv, rel_bias, mask, num_heads, scale):
@@ -59,10 +83,11 @@ class _WindowAttnFn(torch.autograd.Function):
         if ctx.mfma:
             # MFMA kernels: dense bias [h, N(q), N(key)] and mask [nw, N, N], no transposed copies
             m = mask.float().contiguous() if mask is not None else None
-            _lib.call("pdt_win_attn_mfma_fwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
-                      lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.stream_handle(qkv.device))
+            lab = _mask_labels(mask) if (mask is not None and USE_LABELS) else None
+            _lib.call("pdt_win_attn_mfma_fwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
+                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.stream_handle(qkv.device))
             ctx.save_for_backward(qkv, bias, o, lse)
-            ctx.mask = (m, None, nw)
+            ctx.mask = (m, lab, nw)
             ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
             return o
         bias_t = bias.transpose(1, 2).contiguous()
@@ -79,14 +104,15 @@ class _WindowAttnFn(torch.autograd.Function):
     def backward(ctx, do):
         if ctx.mfma:
             qkv, bias, o, lse = ctx.saved_tensors
-            m, _, nw = ctx.mask
+            m, lab, nw = ctx.mask
             Bw, N, C3 = qkv.shape
             d = C3 // 3 // ctx.h
             G = _lib.require().pdt_win_attn_mfma_grid(Bw, ctx.h)
             dqkv = torch.empty_like(qkv)
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
             do = do.contiguous().to(qkv.dtype)
-            _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), nw, o.data_ptr(),
+            _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
+                      o.data_ptr(),
                       do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
                       ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
             return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None

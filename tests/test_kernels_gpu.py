@@ -1056,3 +1056,34 @@ def test_trainer_graph_matches_eager_swinir():
         if se[k].is_floating_point() and se[k].dim() >= 2:
             d = (se[k].float() - sg[k].float()).abs().mean().item()
             assert d < 1e-4, (k, d)
+
+
+@pytest.mark.parametrize("res", [(64, 64), (40, 24)])
+def test_window_attention_label_mask_matches_dense(res):
+    """Swin shift masks rebuilt in-kernel from per-window region labels == the dense fp32 mask path (fwd, dq/dk/dv,
+    relative-bias grad), and the label derivation recognises the mask SwinIR builds."""
+    from pytorch_distributedtraining_amd.models.swinir import SwinTransformerBlock
+    from pytorch_distributedtraining_amd.ops import window_attention as WA
+    blk = SwinTransformerBlock(60, res, 6, window_size=8, shift_size=4)
+    mask = blk._mask(res).to(DEV)
+    lab = WA._mask_labels(mask)
+    assert lab is not None and lab.shape == mask.shape[:2]
+    nw = mask.shape[0]
+    Bw, N, h, d = 2 * nw, 64, 6, 10
+    qkv = torch.randn(Bw, N, 3 * h * d, device=DEV).bfloat16().requires_grad_()
+    rb = (0.5 * torch.randn(h, N, N, device=DEV)).requires_grad_()
+    g = torch.randn(Bw, N, h * d, device=DEV).bfloat16()
+    outs = []
+    for use in (True, False):
+        WA.USE_LABELS = use
+        try:
+            qkv.grad = rb.grad = None
+            o = WA.window_attention(qkv, rb, mask, h, d ** -0.5)
+            (o.float() * g.float()).sum().backward()
+            outs.append((o.detach().float(), qkv.grad.float(), rb.grad.float()))
+        finally:
+            WA.USE_LABELS = True
+    for a, b in zip(*outs):
+        assert rel_err(a, b) < 1e-3
+    ref = WA.reference(qkv.detach(), rb.detach(), mask, h, d ** -0.5)
+    assert rel_err(outs[0][0], ref) < 1e-2
