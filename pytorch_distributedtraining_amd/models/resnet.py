@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import Conv2d1x1
 
 
 def _bn(c, act, fused):
@@ -25,7 +26,11 @@ def conv3x3(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
-def conv1x1(cin, cout, stride=1):
+def conv1x1(cin, cout, stride=1, fused=False):
+    """Stride-1 1x1 convs of the fused model go through ops.conv.Conv2d1x1 (MIOpen or GEMM per shape and
+    direction, measured); same parameters / state_dict as nn.Conv2d."""
+    if fused and stride == 1:
+        return Conv2d1x1(cin, cout)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
@@ -57,11 +62,11 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, planes, stride=1, downsample=None, fused=True):
         super().__init__()
         self.fused = fused
-        self.conv1 = conv1x1(cin, planes)
+        self.conv1 = conv1x1(cin, planes, fused=fused)
         self.bn1 = _bn(planes, "relu", fused)
         self.conv2 = conv3x3(planes, planes, stride)
         self.bn2 = _bn(planes, "relu", fused)
-        self.conv3 = conv1x1(planes, planes * 4)
+        self.conv3 = conv1x1(planes, planes * 4, fused=fused)
         self.bn3 = _bn(planes * 4, "relu", fused)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
@@ -108,7 +113,7 @@ class ResNet(nn.Module):
     def _make(self, block, planes, n, stride=1):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
-            down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
+            down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride, fused=self.fused),
                                  _bn(planes * block.expansion, None, self.fused))
         layers = [block(self.inplanes, planes, stride, down, fused=self.fused)]
         self.inplanes = planes * block.expansion

@@ -163,3 +163,106 @@ def pixel_shuffle_affine(y: torch.Tensor, r: int, a: float = 1.0, b: torch.Tenso
         return out if b is None else out + b.reshape(1, -1, 1, 1).to(out.dtype)
     _lib.require()
     return _PixelShuffleAffineFn.apply(y, r, a, b)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# 1x1 / stride-1 convolutions (ResNet bottlenecks) on channels_last storage ARE GEMMs: y[NHW, Co] = x[NHW, Ci] W^T,
+# dX = dY W, dW = dY^T X.  MIOpen's 1x1 kernels win some forward shapes (56x56, C <= 256), hipBLASLt + the
+# framework weight-gradient path win most backward ones (ResNet-50 at batch 256: up to 0.41 -> 0.32 ms per
+# backward, profiles/r2_resnet50_conv1x1_miopen_vs_gemm.jsonl) -- so each direction of each shape is timed once
+# (first uncaptured call) and the faster implementation kept.  PDT_CONV1X1=miopen / gemm forces one side.
+# ------------------------------------------------------------------------------------------------------------------
+import os as _os
+
+_C1_MODE = _os.environ.get("PDT_CONV1X1", "auto")
+_C1_CHOICE: dict = {}
+
+
+def _c1_rows(t):
+    N, C, H, W = t.shape
+    return t.permute(0, 2, 3, 1).reshape(N * H * W, C)
+
+
+def _c1_from_rows(y2, N, H, W):
+    return y2.view(N, H, W, y2.shape[1]).permute(0, 3, 1, 2)
+
+
+def _c1_fwd_gemm(x, w):
+    N, _, H, W = x.shape
+    return _c1_from_rows(_c1_rows(x) @ w.view(w.shape[0], -1).t(), N, H, W)
+
+
+def _c1_bwd_gemm(dy, x, w):
+    N, _, H, W = x.shape
+    dy2, x2 = _c1_rows(dy), _c1_rows(x)
+    dx = _c1_from_rows(dy2 @ w.view(w.shape[0], -1), N, H, W)
+    dw = wgrad(dy2, x2, w.dtype).view_as(w)
+    return dx, dw
+
+
+def _c1_bwd_miopen(dy, x, w):
+    dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
+                                                     (True, True, False))
+    return dx, dw
+
+
+def _c1_pick(key, gemm_fn, miopen_fn):
+    if _C1_MODE != "auto":
+        return _C1_MODE == "gemm"
+    c = _C1_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        from .linear import _timed_ms
+        c = _C1_CHOICE[key] = _timed_ms(gemm_fn) < _timed_ms(miopen_fn)
+    return c
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        key = ("f", tuple(x.shape), w.shape[0], x.device)
+        if _c1_pick(key, lambda: _c1_fwd_gemm(x, w), lambda: F.conv2d(x, w)):
+            y = _c1_fwd_gemm(x, w)
+        else:
+            y = F.conv2d(x, w)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        key = ("b", tuple(x.shape), w.shape[0], x.device)
+        if _c1_pick(key, lambda: _c1_bwd_gemm(dy, x, w), lambda: _c1_bwd_miopen(dy, x, w)):
+            dx, dw = _c1_bwd_gemm(dy, x, w)
+        else:
+            dx, dw = _c1_bwd_miopen(dy, x, w)
+        return dx, dw
+
+
+def conv1x1_ok(x, w) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[0] * x.shape[2] * x.shape[3] >= 4096)
+
+
+class Conv2d1x1(nn.Conv2d):
+    """1x1 / stride-1 / bias-free nn.Conv2d (same parameters and state_dict) whose passes run on MIOpen or as
+    GEMMs on the channels_last storage, whichever is measured faster per shape and direction."""
+
+    def __init__(self, in_channels, out_channels, device=None, dtype=None):
+        super().__init__(in_channels, out_channels, 1, stride=1, padding=0, bias=False, device=device, dtype=dtype)
+
+    def forward(self, x):
+        w = self.weight
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            x, w = x.to(dt), w.to(dt)
+            if conv1x1_ok(x, w):
+                with torch.autocast("cuda", enabled=False):
+                    return _Conv1x1Fn.apply(x, w)
+            return F.conv2d(x, w)
+        if conv1x1_ok(x, w):
+            return _Conv1x1Fn.apply(x, w)
+        return F.conv2d(x, w)

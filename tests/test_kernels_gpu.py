@@ -1087,3 +1087,24 @@ def test_window_attention_label_mask_matches_dense(res):
         assert rel_err(a, b) < 1e-3
     ref = WA.reference(qkv.detach(), rb.detach(), mask, h, d ** -0.5)
     assert rel_err(outs[0][0], ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["gemm", "miopen", "auto"])
+def test_conv1x1_gemm_matches_fp32(mode, monkeypatch):
+    """ResNet 1x1 convs through ops.conv.Conv2d1x1 (channels_last GEMMs or MIOpen, per-shape choice) vs fp32."""
+    from pytorch_distributedtraining_amd.ops import conv as CV
+    monkeypatch.setattr(CV, "_C1_MODE", mode)
+    m = CV.Conv2d1x1(256, 128).to(DEV)
+    x = torch.randn(16, 256, 28, 28, device=DEV).to(memory_format=torch.channels_last).requires_grad_()
+    g = torch.randn(16, 128, 28, 28, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    (y.float() * g).sum().backward()
+    xr = x.detach().clone().requires_grad_()
+    wr = m.weight.detach().clone().requires_grad_()
+    yr = F.conv2d(xr, wr)
+    (yr * g).sum().backward()
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(m.weight.grad, wr.grad) < 1e-2
