@@ -80,7 +80,9 @@ def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     if c is None:
         if torch.cuda.is_current_stream_capturing():
             return True
-        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip_wgrad(dy2, x2)) < _timed_ms(lambda: torch.mm(dy2.t(), x2))
+        # against the path wgrad() would otherwise take (split-K batched GEMM for small outputs, else one GEMM)
+        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip_wgrad(dy2, x2)) < \
+            _timed_ms(lambda: _library_wgrad(dy2, x2, torch.bfloat16))
     return c
 
 
@@ -93,7 +95,8 @@ def hip_wgrad_splits(m: int, n: int, k: int, cus: int = 256) -> int:
     if tiles == 0 or tiles >= cus:          # a full wave already: a split only adds the fp32 slab pass (Llama-3 8B: -4..-11 %)
         return 1
     best, best_eff = 1, 0.0
-    for s in (1, 2, 4):
+    # 8 / 16 slices for the few-tile outputs of small models (GPT-2 124M at 64 x 1024 tokens: 9-36 tiles)
+    for s in (1, 2, 4, 8, 16):
         if s > 1 and (m % (64 * s) or m // s < 4096):
             break
         wgs = tiles * s
@@ -133,6 +136,13 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.
         return torch.mm(dy2.t(), x2).to(out_dtype)
     if hip_wgrad_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2):
         return hip_wgrad(dy2, x2)
+    return _library_wgrad(dy2, x2, out_dtype)
+
+
+def _library_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """dW on hipBLASLt: one GEMM, a token-split batched GEMM (small outputs) or the row-split tall-skinny form."""
+    m, n = dy2.shape
+    k = x2.shape[1]
     if not _tall_skinny(m, n, k):
         sk = _split_k(m, n, k)
         if sk == 1:
