@@ -172,9 +172,13 @@ def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
     """dX = dY W ([M, N] x [N, K]) as F.linear(dY, W^T): hipBLASLt's NN-layout kernels for this product ran
     10-25 % below the forward's x W^T layout on the flagship shapes (qkv 0.79 -> 0.59 ms, fc2 0.89 -> 0.75 ms,
     tied LM head 4.97 -> 4.36 ms at 32 x 1024 tokens, profiles/r1_v11_gemm_dgrad_layout.jsonl); the weight
-    transpose costs ~1 % of the GEMM.  Small weights (GPT-2 124M, SwinIR) keep the single mm."""
+    transpose costs ~1 % of the GEMM.  GPT-2 124M's 0.6-2.4M-element weights gain too (901k -> 930-936k tokens/s,
+    profiles/r2_gpt2_124m_dgrad_nt_threshold.log); SwinIR's (< 11k elements) keep the single mm."""
     return (w.dtype in (torch.bfloat16, torch.float16) and w.is_contiguous() and m >= 4096
-            and n % 64 == 0 and k % 64 == 0 and n * k >= 4_000_000 and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
+            and n % 64 == 0 and k % 64 == 0 and n * k >= _DGRAD_T_MIN and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
+
+
+_DGRAD_T_MIN = int(os.environ.get("PDT_DGRAD_T_MIN", "500000"))    # smallest weight (elements) for the NT dgrad
 
 
 BGRAD_IN_GEMM = os.environ.get("PDT_BGRAD_GEMM", "0") == "1"   # opt-in: no bench workload gains (r2)
