@@ -309,7 +309,13 @@ using namespace pdt;
 
 // 128-tile kernel when the shape allows (16-byte stores), else the 64-tile one; tile-row count of the dbias
 // partials follows the tile (ct_tile_rows)
-static bool ct_wide(int R, int C) { return R % CT2 == 0 && C % CT2 == 0 && getenv("PDT_FP8_CT64") == nullptr; }
+static bool ct_wide(int R, int C) {
+  static const bool force64 = getenv("PDT_FP8_CT64") != nullptr;
+  return R % CT2 == 0 && C % CT2 == 0 && !force64;
+}
+static bool aligned16(const void* a, const void* b, const void* c) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+}
 static int ct_tile_rows(int R, int C) { return ct_wide(R, C) ? CT2 : CT_TS; }
 template <typename T, int FMT, int OP>
 static void ct_launch(const T* x, uint8_t* q, uint8_t* qt, int R, int C, const float* scale, unsigned int* amax,
@@ -349,7 +355,7 @@ PDT_API long long pdt_fp8_gelu_bwd_ws_floats(int R, int C) {
 
 PDT_API int pdt_fp8_bias_gelu_ct(const void* a, const void* bias, void* q, void* qt, int R, int C, int fmt,
                                  const float* scale, unsigned int* amax_bits, hipStream_t st) {
-  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias) return (int)hipErrorInvalidValue;
+  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias || !aligned16(a, q, qt)) return (int)hipErrorInvalidValue;
   if (fmt == 0)
     ct_launch<bf16_t, 0, kBiasGelu>((const bf16_t*)a, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits, nullptr,
                                     (const bf16_t*)bias, nullptr, st);
@@ -362,7 +368,8 @@ PDT_API int pdt_fp8_bias_gelu_ct(const void* a, const void* bias, void* q, void*
 PDT_API int pdt_fp8_bias_gelu_bwd_ct(const void* dh, const void* a, const void* bias, void* q, void* qt, void* dbias,
                                      float* ws, int R, int C, int fmt, const float* scale, unsigned int* amax_bits,
                                      hipStream_t st) {
-  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias || !ws) return (int)hipErrorInvalidValue;
+  if (R <= 0 || C <= 0 || R % CT_TS || C % CT_TS || !bias || !ws || !aligned16(dh, q, qt) || !aligned16(a, a, a))
+    return (int)hipErrorInvalidValue;
   if (fmt == 0)
     ct_launch<bf16_t, 0, kBiasGeluBwd>((const bf16_t*)dh, (uint8_t*)q, (uint8_t*)qt, R, C, scale, amax_bits,
                                        (const bf16_t*)a, (const bf16_t*)bias, ws, st);
