@@ -66,10 +66,11 @@ def test_rms_norm(N):
 
 @pytest.mark.parametrize("approx", ["tanh", "none"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-def test_bias_gelu(approx, dt):
+@pytest.mark.parametrize("rows,N", [(300, 1024), (301, 4096)])
+def test_bias_gelu(approx, dt, rows, N):
     from pytorch_distributedtraining_amd.ops import bias_gelu
-    h = torch.randn(300, 1024, device=DEV).to(dt).requires_grad_()
-    b = (0.5 * torch.randn(1024, device=DEV)).to(dt).requires_grad_()
+    h = torch.randn(rows, N, device=DEV).to(dt).requires_grad_()
+    b = (0.5 * torch.randn(N, device=DEV)).to(dt).requires_grad_()
     y = bias_gelu(h, b, approximate=approx)
     dy = torch.randn_like(y)
     y.backward(dy)
