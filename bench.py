@@ -46,7 +46,12 @@ def parse():
                          "layers as the HBM needs (sized after the first warm-up step)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--secondary", type=int, default=1,
-                    help="gpt2-fsdp at one GPU: also measure BASELINE.json's ResNet-50 DDP metric (JSON 'secondary')")
+                    help="gpt2-fsdp: also measure BASELINE.json's ResNet-50 DDP metric at the same world size "
+                         "(JSON 'secondary')")
+    ap.add_argument("--secondary-micro-batch", type=int, default=None,
+                    help="images per GPU of the secondary ResNet measurement (default 256)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: plumbing rehearsal of any workload on gloo (tiny --model / --micro-batch)")
     ap.add_argument("--overlap-probe", type=int, default=1,
                     help="world > 1: after timing, measure exposed vs communication-only time (untimed)")
     ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
@@ -95,10 +100,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.workload == "resnet18-cpu":      # BASELINE.json config 1: CPU / gloo plumbing run
+    if args.workload == "resnet18-cpu" or args.device == "cpu":   # config 1 / CPU plumbing rehearsal
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
+        if args.device == "cpu":
+            torch.set_num_threads(max(1, int(os.environ.get("OMP_NUM_THREADS", "2"))))
     else:
         # PDT_BENCH_BACKEND=gloo + PDT_XGMI=1 rehearses the multi-rank path on a box with fewer GPUs than
         # ranks (ranks share devices round-robin; device collectives on the xGMI kernels) -- a plumbing
@@ -121,20 +128,25 @@ def main():
         result = bench_swinir(args, comm, dev, world, rank)
     else:
         result = bench_resnet(args, comm, dev, world, rank)
-    if args.secondary and args.workload == "gpt2-fsdp" and world == 1 and dev.type == "cuda":
-        # BASELINE.json names TWO headline metrics (GPT-2-1.3B FSDP tokens/s and ResNet-50 DDP samples/s): at one
-        # GPU the same run also measures the second one, so the driver's own invocation records both.  Untimed
-        # for the primary value; a failure here is reported and never loses the primary line.
+    result["topology"] = topology(comm, dev)
+    if args.secondary and args.workload == "gpt2-fsdp":
+        # BASELINE.json names TWO headline metrics (GPT-2-1.3B FSDP tokens/s and ResNet-50 DDP samples/s, both
+        # "at 1/2/4/8"): every run also measures the second one at the SAME world size, so each point of the
+        # driver's scaling curve records both.  Outside the primary's timed region; a failure here is reported
+        # and never loses the primary line.
         import copy
         import gc
         gc.collect()
         torch.cuda.empty_cache()
         try:
             a2 = copy.copy(args)
-            a2.workload, a2.micro_batch, a2.steps, a2.warmup = "resnet50-ddp", None, 10, 3
+            a2.workload, a2.micro_batch, a2.steps, a2.warmup = "resnet50-ddp", args.secondary_micro_batch, 10, 3
+            if dev.type == "cpu":
+                a2.steps, a2.warmup = 1, 1
             sec = bench_resnet(a2, comm, dev, world, rank)
-            result["secondary"] = {k: sec[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
-                                                       "dtype", "config")}
+            result["secondary"] = {k: sec[k] for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "steps",
+                                                       "warmup", "dtype", "config", "collectives_per_step",
+                                                       "comm_bytes_per_step") if k in sec}
         except Exception as e:   # pragma: no cover - reported, primary result kept
             log(f"[bench] secondary ResNet-50 measurement failed: {e!r}")
     if rank == 0:
@@ -142,6 +154,25 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def topology(comm, dev):
+    """Proof of what ran: the c10d world size read back from the process group, and every rank's device
+    (ordinal, PCI domain:bus:device, gfx arch) gathered to rank 0 -- N distinct bus ids = N distinct GPUs."""
+    import torch
+    import torch.distributed as dist
+    me = {"rank": comm.rank, "host": os.uname().nodename}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        me.update(device=torch.cuda.current_device(),
+                  pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", arch=p.gcnArchName)
+    else:
+        me.update(device="cpu")
+    ranks = comm.all_gather_object(me) if comm.world_size > 1 else [me]
+    pcis = {r.get("pci") for r in ranks if r.get("pci")}
+    return {"c10d_world": dist.get_world_size() if dist.is_initialized() else 1,
+            "c10d_backend": dist.get_backend() if dist.is_initialized() else None,
+            "distinct_devices": len(pcis) if pcis else 0, "devices": ranks}
 
 
 def timed_loop(step_fn, args, comm, dev):
@@ -280,7 +311,7 @@ def bench_gpt2(args, comm, dev, world, rank):
     opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, capturable=graph)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
-    vocab = 128000 if llama else 50257
+    vocab = (model.module if hasattr(model, "module") else model).config.vocab_size
     batches = [torch.randint(0, vocab, (mb, S + 1), device=dev, generator=g) for _ in range(4)]
     state = {"i": 0, "loss": None}
     inner = model.module if hasattr(model, "module") else model
@@ -348,7 +379,8 @@ def bench_gpt2(args, comm, dev, world, rank):
         f"tokens/sec {name} {'FSDP' if fsdp else 'DDP'} (whole node)"
     if llama:
         metric = f"tokens/sec {name} FSDP + act-ckpt (whole node)"
-    return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+    return {"metric": metric, "value": round(tps, 2), "unit": "tokens/s",
+            "n_gpus": world if dev.type == "cuda" else 0, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", **comm_fields(world), "vs_baseline": None,
             "dtype": "fp8-linears" if args.fp8 else "bf16", "data": "synthetic",

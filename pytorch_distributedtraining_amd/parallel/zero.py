@@ -87,6 +87,11 @@ class OSS(Optimizer):
         self.optim_cls = optim or FusedAdamW
         self.broadcast_fp16 = broadcast_fp16
         self.compute_dtype = compute_dtype
+        if compute_dtype is not None and not issubclass(self.optim_cls, FusedAdamW):
+            # the fp32 masters read their gradient through _pdt_grad_src, which only FusedAdamW follows: a
+            # torch optimizer would see master.grad None and silently never update anything
+            raise ValueError("OSS(compute_dtype=...) needs optim=FusedAdamW (the fp32 masters' gradients are "
+                             f"the compute-dtype module gradients), got {self.optim_cls.__name__}")
         super().__init__(params, defaults)
         world, rank = self.comm.world_size, self.comm.rank
         self._all_params = [p for g in self.param_groups for p in g["params"]]
@@ -143,6 +148,11 @@ class OSS(Optimizer):
                 for li, p in enumerate(ps):
                     if bank.owners[li] == rank:
                         p._pdt_lp_shard = bank.view(bank.lp, li)   # AdamW epilogue writes the payload
+                # The epilogue only rewrites what it steps: a frozen / gradient-less parameter or a skipped
+                # (found_inf) step leaves the owner's slice as is, so it must hold the current values from
+                # the start -- never zeros that the all-gather would spread to every peer.
+                with torch.no_grad():
+                    bank.own(bank.lp).copy_(bank.own(bank.flat))
             for li, i in enumerate(idxs):
                 self._bank_of[i] = (bank, li)
             self._banks.append(bank)
@@ -250,6 +260,8 @@ class OSS(Optimizer):
                     continue
                 v = values[p].to(device=bank.device)
                 bank.view(bank.flat, li).copy_(v)
+                if bank.lp is not None:               # keep the all-gather payload in step with the values
+                    bank.view(bank.lp, li).copy_(v)
                 if li in bank.masters:
                     bank.masters[li].copy_(v)
                     bank.masters[li]._pdt_lp_version = bank.masters[li]._version

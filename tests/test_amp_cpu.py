@@ -2,6 +2,7 @@
 torch.amp.GradScaler skips optimizer.step() (torch/amp/grad_scaler.py:360), and with sharded gradients
 the overflow seen by ONE rank skips the step on EVERY rank (sharded_grad_scaler.py:262-283).
 Reference configuration: AMPConfig(init_scale=2**14), FP16Options.amp (Stoke-DDP.py:182-184,247)."""
+import pytest
 import torch
 
 from dist_utils import run_workers
@@ -59,9 +60,11 @@ def _sharded_overflow(rank, world):
     return out
 
 
-def test_sharded_overflow_on_one_rank_skips_every_rank():
-    r0, r1 = run_workers(_sharded_overflow, 2)
-    assert r0 == r1
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_overflow_on_one_rank_skips_every_rank(world):
+    outs = run_workers(_sharded_overflow, world)
+    r0 = outs[0]
+    assert all(r == r0 for r in outs)
     (f0, c0, s0, n0), (f1, c1, s1, n1), (f2, c2, s2, n2) = r0
     assert (f0, c0, n0) == (0, True, 1.0)
     assert (f1, c1, n1) == (1, False, 1.0)     # skipped everywhere, Adam step count unchanged

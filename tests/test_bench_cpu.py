@@ -31,6 +31,26 @@ def test_bench_self_launches_two_gloo_ranks():
     assert res["comm_bytes_per_step"] >= 4 * 11_000_000
 
 
+def test_bench_world2_reports_topology_and_secondary_headline():
+    """Both BASELINE headlines at every N (the ResNet DDP one as 'secondary'), with the c10d world size read
+    back from the process group and every rank's device in 'topology'."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--workload", "gpt2-fsdp",
+                        "--model", "gpt2-tiny", "--micro-batch", "2", "--seq", "64", "--steps", "2", "--warmup", "1",
+                        "--secondary-micro-batch", "2"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["config"]["parallelism"] == "fsdp2" and res["collectives_per_step"] > 0
+    topo = res["topology"]
+    assert topo["c10d_world"] == 2 and topo["c10d_backend"] == "gloo"
+    assert [d["rank"] for d in topo["devices"]] == [0, 1]
+    sec = res["secondary"]
+    assert sec["config"]["parallelism"] == "dp2" and sec["value"] > 0
+    assert sec["collectives_per_step"] >= 2
+
+
 def test_bench_refuses_mismatched_world_size():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--workload", "resnet18-cpu"], cwd=ROOT,
                        env=_env(WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)

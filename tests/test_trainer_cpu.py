@@ -102,15 +102,18 @@ def _w_trainer(rank, world, tmp):
     return sd, t.optimizer_steps, type(t.model_access[1]).__name__, tag, total
 
 
-def test_distributed_trainer_reference_combination(tmp_path):
-    outs = run_workers(_w_trainer, 2, str(tmp_path))
-    (sd0, steps, bn_type, tag, _), (sd1, _, _, _, _) = outs
-    assert steps == 2 and bn_type == "SyncBatchNorm"
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), k
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_trainer_reference_combination(tmp_path, world):
+    """world 4 = the reference's own launch (Stoke-DDP.py:2 --nproc_per_node=4)."""
+    outs = run_workers(_w_trainer, world, str(tmp_path))
+    sd0, steps, bn_type, tag, _ = outs[0]
+    assert steps == 8 // (2 * world) and bn_type == "SyncBatchNorm"
+    for o in outs[1:]:
+        for k in sd0:
+            assert torch.equal(sd0[k], o[0][k]), k
     payload = torch.load(os.path.join(tmp_path, tag + ".pt"), weights_only=True)
     assert sorted(payload["optimizer_state_dict"]["state"]) == list(range(6))
-    assert payload["stoke_status"]["oss"] and payload["stoke_status"]["effective_batch_size"] == 8
+    assert payload["stoke_status"]["oss"] and payload["stoke_status"]["effective_batch_size"] == 4 * world
 
 
 def test_stoke_example_pretrained_flag(tmp_path):
@@ -158,10 +161,13 @@ def _w_trainer_equiv(rank, world):
     return {k: v.detach().clone().float() for k, v in sd.items()}, t.optimizer_steps
 
 
-def test_distributed_trainer_reference_combination_matches_single_process():
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_trainer_reference_combination_matches_single_process(world):
     (ref, steps1), = run_workers(_w_trainer_equiv, 1)
-    (sd0, steps2), (sd1, _) = run_workers(_w_trainer_equiv, 2)
+    outs = run_workers(_w_trainer_equiv, world)
+    sd0, steps2 = outs[0]
     assert steps1 == steps2 == 3
     for k in ref:
-        assert torch.equal(sd0[k], sd1[k]), k
+        for o in outs[1:]:
+            assert torch.equal(sd0[k], o[0][k]), k
         assert torch.allclose(sd0[k], ref[k], atol=2e-5, rtol=1e-4), (k, (sd0[k] - ref[k]).abs().max())
