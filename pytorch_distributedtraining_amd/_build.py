@@ -110,12 +110,17 @@ def runtime_ext_path() -> str:
     return os.path.join(PKG, "_pdt_runtime" + suffix)
 
 
-def build_runtime(verbose: bool = False) -> str:
+def build_runtime(verbose: bool = False, out_dir: str | None = None, sanitize: bool | None = None) -> str:
+    """``out_dir``: build the module there instead of in-tree (the sanitizer test's private copy, loaded
+    through ``PDT_RUNTIME_DIR``); ``sanitize``: ASan + UBSan instrumented host code (default: env
+    ``PDT_SANITIZE``)."""
     import pybind11
 
     srcs = sorted(glob.glob(os.path.join(RUNTIME_DIR, "*.cpp")))
     headers = sorted(glob.glob(os.path.join(RUNTIME_DIR, "*.h")))
-    out = runtime_ext_path()
+    out = runtime_ext_path() if out_dir is None else os.path.join(out_dir, os.path.basename(runtime_ext_path()))
+    if sanitize is None:
+        sanitize = bool(os.environ.get("PDT_SANITIZE"))
     if not srcs:
         return out
     if _newer(out, srcs + headers + [__file__]):
@@ -126,8 +131,9 @@ def build_runtime(verbose: bool = False) -> str:
         for i in inc:
             cmd += ["-I", i]
         cmd += ["-I", RUNTIME_DIR, *srcs, "-o", out]
-        if os.environ.get("PDT_SANITIZE"):
-            cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        if sanitize:
+            cmd[1:1] = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                        "-fno-omit-frame-pointer", "-g"]
         _run(cmd, verbose)
     return out
 

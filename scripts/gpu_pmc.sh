@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC counter passes over the hand-written kernels (kernel-trace only, no sys/runtime traces).
 set -u
-PROBE=${PROBE:-scripts/kernel_probe.py}
+PROBE=${PROBE:-scripts/pmc_kernels.py}
 export PYTHONPATH=.
 OUT=gpurun_out
 mkdir -p $OUT

@@ -171,3 +171,32 @@ def test_distributed_trainer_reference_combination_matches_single_process(world)
         for o in outs[1:]:
             assert torch.equal(sd0[k], o[0][k]), k
         assert torch.allclose(sd0[k], ref[k], atol=2e-5, rtol=1e-4), (k, (sd0[k] - ref[k]).abs().max())
+
+
+def _w_trainer_debug(rank, world, diverge_at):
+    """PDT_COMM_DEBUG=1 PDT_VERIFY_EVERY=1: the Trainer checks the cross-rank collective sequence after every
+    optimizer step.  At ``diverge_at`` the ranks issue mismatched collectives (rank 1 reduces with MAX where
+    rank 0 uses SUM -- gloo runs it without complaint, the result is silently wrong)."""
+    os.environ["PDT_COMM_DEBUG"] = "1"
+    os.environ["PDT_VERIFY_EVERY"] = "1"
+    from pytorch_distributedtraining_amd.parallel.comm import Comm
+    comm = Comm()
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, grad_accum_steps=1,
+                grad_clip=ClipGradNormConfig(0.1, 2.0), distributed="ddp", fairscale_oss=True, fairscale_sddp=True,
+                configs=[DDPConfig(local_rank=rank)], verbose=False, comm=comm)
+    g = torch.Generator().manual_seed(rank)
+    for s in range(4):
+        if s == diverge_at:
+            x = torch.ones(1)
+            t.comm.all_reduce(x, "max" if rank == 1 else "sum")
+        t.backward(t.loss(t.model(torch.randn(2, 3, 8, 8, generator=g)), torch.randn(2, 3, 8, 8, generator=g)))
+        try:
+            t.step()
+        except RuntimeError as e:
+            return ("mismatch", s) if "collective mismatch" in str(e) else ("error", repr(e))
+    return ("ok", None)
+
+
+def test_trainer_debug_mode_catches_divergent_collective():
+    assert run_workers(_w_trainer_debug, 2, -1) == [("ok", None)] * 2            # consistent run: no false alarm
+    assert run_workers(_w_trainer_debug, 2, 2) == [("mismatch", 2)] * 2          # caught at that very step
