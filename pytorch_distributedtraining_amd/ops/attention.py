@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import math
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -92,6 +94,23 @@ class _FlashAttnPackedFn(torch.autograd.Function):
         return dqkv, None, None
 
 
+_FRESH_GRADS = weakref.WeakValueDictionary()
+
+
+def mark_fresh_grad(t):
+    """Record that ``t`` is a gradient buffer this backward just allocated and hands to exactly one consumer,
+    so that consumer may rewrite it in place (ops.rope's inverse rotation)."""
+    _FRESH_GRADS[t.untyped_storage().data_ptr()] = t
+
+
+def take_fresh_grad(t) -> bool:
+    """True (once) if ``t`` views a buffer marked by ``mark_fresh_grad`` that is still alive.  A gradient that
+    autograd accumulated from several consumers is a new buffer and reads False."""
+    ptr = t.untyped_storage().data_ptr()
+    src = _FRESH_GRADS.pop(ptr, None)
+    return src is not None and src.untyped_storage().data_ptr() == ptr
+
+
 class _FlashAttnGQAPackedFn(torch.autograd.Function):
     """q, k, v as head ranges of one [B, S, Hq + 2 Hkv, D] projection; backward writes the packed gradient."""
 
@@ -111,6 +130,7 @@ class _FlashAttnGQAPackedFn(torch.autograd.Function):
         d = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         _bwd(qkv[:, :, :hq], qkv[:, :, hq:hq + hkv], qkv[:, :, hq + hkv:], o, lse, do, d[:, :, :hq],
              d[:, :, hq:hq + hkv], d[:, :, hq + hkv:], ctx.causal, ctx.scale)
+        mark_fresh_grad(d)
         return d, None, None, None, None
 
 

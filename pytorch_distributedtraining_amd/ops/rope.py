@@ -105,8 +105,12 @@ class _RopeQKInplaceFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dqkv):
+        from .attention import take_fresh_grad
         cos, sin = ctx.saved_tensors
-        dqkv = dqkv.contiguous()
+        # In place only on a buffer the packed attention backward allocated for this node alone; any other
+        # gradient (accumulated from several consumers, or a buffer shared with another node) gets a copy.
+        if not (dqkv.is_contiguous() and take_fresh_grad(dqkv)):
+            dqkv = dqkv.clone(memory_format=torch.contiguous_format)
         B, S = dqkv.shape[0], dqkv.shape[1]
         d4 = dqkv.view(B, S, -1, ctx.head_dim)
         _launch(d4, d4, cos, sin, ctx.pos0, backward=True, heads=ctx.heads)

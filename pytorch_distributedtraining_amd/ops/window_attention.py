@@ -10,6 +10,7 @@ formula (also the numerics reference in the GPU tests).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -23,14 +24,14 @@ USE_LABELS = os.environ.get("PDT_WIN_MASK_LABELS", "1") == "1"   # A/B switch: 0
 def _mask_t(mask):
     """[nw, N(i), N(j)] -> [nw, N(j), N(i)] fp32, cached per (storage, version) -- masks are buffers."""
     key = (mask.data_ptr(), mask._version, tuple(mask.shape), mask.device)
-    hit = _MASK_T_CACHE.get(key)
-    if hit is None:
+    ent = _MASK_T_CACHE.get(key)
+    if ent is None or ent[0]() is not mask:
         if len(_MASK_T_CACHE) > 64:
             _MASK_T_CACHE.clear()
         m = mask.float().contiguous()
-        hit = (m, m.transpose(1, 2).contiguous())
-        _MASK_T_CACHE[key] = hit
-    return hit
+        ent = (weakref.ref(mask), (m, m.transpose(1, 2).contiguous()))
+        _MASK_T_CACHE[key] = ent
+    return ent[1]
 
 
 _LABEL_CACHE: dict = {}
@@ -41,16 +42,19 @@ def _mask_labels(mask):
     region labels [nw, N] uint8 (label = first key of the token's region) when ``mask`` has that form, else None.
     The MFMA kernels then rebuild the mask from 64 label bytes per window instead of reading the fp32 mask.
     Derived once per mask buffer (one host check, in the first -- eager -- call)."""
+    # keyed by address + version, and the entry holds a weak reference to the mask it was derived from: a new
+    # mask allocated at a freed mask's address (same shape, version 0) is a miss, not stale labels
     key = (mask.data_ptr(), mask._version, tuple(mask.shape), mask.device)
-    if key in _LABEL_CACHE:
-        return _LABEL_CACHE[key]
+    ent = _LABEL_CACHE.get(key)
+    if ent is not None and ent[0]() is mask:
+        return ent[1]
     if len(_LABEL_CACHE) > 64:
         _LABEL_CACHE.clear()
     m = mask.float()
     lab = (m == 0).float().argmax(-1)                                      # [nw, N]
     rebuilt = torch.where(lab[:, :, None] != lab[:, None, :], -100.0, 0.0)
     out = lab.to(torch.uint8).contiguous() if (mask.shape[-1] <= 64 and torch.equal(rebuilt, m)) else None
-    _LABEL_CACHE[key] = out
+    _LABEL_CACHE[key] = (weakref.ref(mask), out)
     return out
 
 

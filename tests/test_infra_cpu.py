@@ -151,3 +151,25 @@ def test_device_loader_cpu_passthrough():
     x, y = next(iter(dl))
     assert x.shape == (4, 16) and torch.equal(x[:, 1:], y[:, :-1])
     assert len(dl) == 3
+
+
+def test_window_mask_label_cache_is_identity_checked():
+    """ops.window_attention caches the region labels derived from a mask buffer.  A fresh mask of the same shape
+    allocated at a freed mask's address (version 0 again) must not be served the old mask's labels."""
+    from pytorch_distributedtraining_amd.ops.window_attention import _mask_labels
+
+    def swin_mask(split):
+        lab = torch.zeros(2, 64, dtype=torch.long)
+        lab[:, split:] = split
+        return torch.where(lab[:, :, None] != lab[:, None, :], -100.0, 0.0)
+
+    for _ in range(20):                    # the allocator hands the freed block back for the next same-size mask
+        a = swin_mask(10)
+        la = _mask_labels(a)
+        assert la is not None and int(la[0, 63]) == 10
+        ptr = a.data_ptr()
+        del a
+        b = swin_mask(40)
+        lb = _mask_labels(b)
+        assert int(lb[0, 63]) == 40 and int(lb[0, 39]) == 0, (ptr == b.data_ptr())
+        del b

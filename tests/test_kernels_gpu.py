@@ -958,6 +958,40 @@ def test_llama_packed_rope_gqa_attention_matches_unfused():
     assert rel_err(gw, att.wqkv.weight.grad) < 2e-3
 
 
+def test_packed_rope_backward_with_second_consumer():
+    """The in-place inverse rotation of apply_rope_qk_'s backward may only rewrite the packed attention's own
+    fresh gradient: when the rotated projection also feeds another op, autograd accumulates a new gradient
+    buffer and the rotation must act on that -- checked against fp32 torch (RoPE reference + SDPA)."""
+    from pytorch_distributedtraining_amd.ops import rope_tables
+    from pytorch_distributedtraining_amd.ops.attention import flash_attn_gqa_packed
+    from pytorch_distributedtraining_amd.ops.rope import _rope_ref, apply_rope_qk_
+    torch.manual_seed(1)
+    B, S, h, hkv, d = 2, 128, 4, 2, 128
+    cos, sin = rope_tables(d, 256, device=DEV)
+    base = torch.randn(B, S, (h + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(B, S, h, d, device=DEV, dtype=torch.bfloat16)
+    g2 = torch.randn(B, S, (h + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    for second in (False, True):
+        x = base.clone().requires_grad_()
+        qkv = apply_rope_qk_(x * 1.0, h, hkv, d, cos, sin)
+        o = flash_attn_gqa_packed(qkv.view(B, S, h + 2 * hkv, d), h, hkv, causal=True)
+        loss = (o * g).sum() + ((qkv * g2).sum() if second else 0.0)
+        loss.backward()
+        xr = base.float().requires_grad_()
+        x4 = xr.view(B, S, h + 2 * hkv, d)
+        q = _rope_ref(x4[:, :, :h], cos, sin, 0, 1.0)
+        k = _rope_ref(x4[:, :, h:h + hkv], cos, sin, 0, 1.0)
+        v = x4[:, :, h + hkv:]
+        rot = torch.cat([q, k, v], dim=2).reshape(B, S, -1)
+        kk = k.repeat_interleave(h // hkv, dim=2)
+        vv = v.repeat_interleave(h // hkv, dim=2)
+        oref = torch.nn.functional.scaled_dot_product_attention(
+            q.transpose(1, 2), kk.transpose(1, 2), vv.transpose(1, 2), is_causal=True).transpose(1, 2)
+        lref = (oref * g.float()).sum() + ((rot * g2.float()).sum() if second else 0.0)
+        lref.backward()
+        assert rel_err(x.grad, xr.grad) < 2e-2, (second, rel_err(x.grad, xr.grad))
+
+
 @pytest.mark.parametrize("shape", [(4096, 768, 768), (2048, 1024, 4096)])
 def test_linear_weight_and_bias_grad_in_one_gemm(shape):
     """ops.linear: dW and db from one hipBLASLt GEMM (BGRADB epilogue, csrc/kernels/blaslt.hip) vs fp32 torch."""
