@@ -456,7 +456,7 @@ def bench_swinir(args, comm, dev, world, rank):
                          optimizer_kwargs={"lr": 1e-3, "betas": (0.9, 0.99), "eps": 1e-8, "weight_decay": 1e-4})
     loss_fn = feat_loss if args.loss == "feat" else torch.nn.functional.mse_loss
     tr = Trainer(model, optimizer=opt, loss=loss_fn, batch_size_per_device=mb,
-                 grad_accum_steps=accum, grad_clip=ClipGradNormConfig(max_norm=0.1, norm_type=2.0), gpu=True,
+                 grad_accum_steps=accum, grad_clip=ClipGradNormConfig(max_norm=0.1, norm_type=2.0), gpu=dev.type == "cuda",
                  fp16=None if args.precision == "fp32" else "bf16", distributed="ddp" if world > 1 else None,
                  fairscale_oss=world > 1, fairscale_sddp=world > 1, verbose=False, comm=comm)
     g = torch.Generator(device=dev)
@@ -479,7 +479,8 @@ def bench_swinir(args, comm, dev, world, rank):
     sps = world * mb * accum * args.steps / dt
     par = "dp{}+oss+sddp".format(world) if world > 1 else "dp1"
     return {"metric": "samples/sec SwinIR-S x2 Stoke (whole node)", "value": round(sps, 2),
-            "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "unit": "samples/s", "n_gpus": world if dev.type == "cuda" else 0, "steps": args.steps,
+            "warmup": args.warmup,
             "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             **comm_fields(world), "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"model": "swinir-s-x2", "global_batch": world * mb * accum, "seq_len": None,

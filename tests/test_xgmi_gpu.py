@@ -1,4 +1,4 @@
-"""Peer-mapped xGMI collectives (parallel/xgmi.py, csrc/kernels/xgmi_comm.hip) on ONE MI355X: two ranks
+"""Peer-mapped xGMI collectives (parallel/xgmi.py, csrc/kernels/xgmi_comm.hip) on ONE MI355X: 2, 4 or 8 ranks
 share cuda:0 and map each other's symmetric buffers through hipIpcOpenMemHandle (the same IPC + kernel
 path the 8-GPU node uses, with the peer reached over the local fabric instead of an xGMI link).
 Results are checked against the exact sums computed from the ranks' deterministic inputs."""
@@ -46,8 +46,9 @@ def _xgmi_worker(rank, world):
     return out
 
 
-def test_xgmi_collectives_two_ranks_on_one_gpu():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_collectives_several_ranks_on_one_gpu(world):
+    """World 2 / 4 / 8 (the node size: MAXW-peer loops, two-shot chunks of 16 * world bytes, 8-way pitches)."""
     res = run_workers(_xgmi_worker, world)
     cases = [("one_f32", 4096, torch.float32, 1), ("one_bf16", 8192, torch.bfloat16, 2),
              ("two_f32", 1 << 20, torch.float32, 3), ("two_bf16", 3 << 19, torch.bfloat16, 4)]
@@ -96,8 +97,8 @@ def _chunked_worker(rank, world):
     return out
 
 
-def test_xgmi_chunked_collectives_and_reduce():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_chunked_collectives_and_reduce(world):
     res = run_workers(_chunked_worker, world)
     ar = sum(_data(r, 3 * (1 << 18) + 40, torch.float32, 11) for r in range(world))
     ag = torch.cat([_data(r, 5 * (1 << 18) // 2, torch.bfloat16, 12).float() for r in range(world)])
@@ -108,8 +109,10 @@ def test_xgmi_chunked_collectives_and_reduce():
         assert torch.allclose(res[r]["ar"], ar, atol=1e-5)
         assert torch.equal(res[r]["ag"], ag)
         assert torch.allclose(res[r]["rs"], sum(t[r * n:(r + 1) * n] for t in rs_in) / world, atol=1e-6)
-    assert torch.allclose(res[1]["red"], red, atol=3e-2, rtol=1e-2)       # the root holds the sum ...
-    assert torch.equal(res[0]["red"], res[0]["red_keep"])                 # ... the others keep their input
+    assert torch.allclose(res[1]["red"], red, atol=3e-2 * world / 2, rtol=1e-2)   # the root holds the sum ...
+    for r in range(world):
+        if r != 1:
+            assert torch.equal(res[r]["red"], res[r]["red_keep"])          # ... the others keep their input
 
 
 def _timeout_worker(rank, world):
