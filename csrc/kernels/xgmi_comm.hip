@@ -53,7 +53,7 @@ struct XArgs {
   unsigned* host_err;                 // host-mapped error word (may be null)
   int rank, world;
   unsigned epoch;
-  unsigned spin_limit;
+  unsigned timeout_us;                // wall-clock budget of one mesh wait
   int64_t slot_bytes;
 };
 
@@ -79,9 +79,15 @@ __device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
     gu32* remote = (gu32*)(a.buf[t]) + b * MAXW + a.rank;
     __hip_atomic_store(remote, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     gu32* mine = (gu32*)(a.buf[a.rank]) + b * MAXW + t;
+    // wall-clock budget (s_memrealtime: 100 MHz): ranks that share a GPU time-slice its queues, and a rank
+    // whose host is still in a first-call library load can arrive a second late -- an iteration count
+    // mis-measures both
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t budget = (uint64_t)a.timeout_us * 100;
     unsigned spins = 0;
     while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
-      if (++spins > a.spin_limit) {   // give up: record the failure, never hang the queue
+      if ((++spins & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > budget) {
+        // give up: record the failure, never hang the queue
         __hip_atomic_fetch_or((gu32*)(a.buf[a.rank] + ERR_OFF), 1u << b, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_SYSTEM);
         if (a.host_err != nullptr)   // plain system-scope store (no PCIe atomics needed): any bit = failure
@@ -282,7 +288,7 @@ PDT_API int pdt_xgmi_host_flag_free(void* host_ptr) { return (int)hipHostFree(ho
 //   scale multiplies reduced values (1/world = AVG).
 PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t bytes, int64_t pitch_bytes, int dtype,
                                 float scale, const void* const* bufs, int rank, int world, unsigned epoch,
-                                int64_t slot_bytes, unsigned spin_limit, unsigned* host_err, hipStream_t s) {
+                                int64_t slot_bytes, unsigned timeout_us, unsigned* host_err, hipStream_t s) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || epoch == 0) return (int)hipErrorInvalidValue;
   if (bytes % 16 != 0 || pitch_bytes % 16 != 0 || (dtype != kF32 && dtype != kBF16)) return (int)hipErrorInvalidValue;
   if (slot_bytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;   // 32-bit buffer offsets
@@ -294,7 +300,7 @@ PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t byt
   a.rank = rank;
   a.world = world;
   a.epoch = epoch;
-  a.spin_limit = spin_limit;
+  a.timeout_us = timeout_us;
   a.slot_bytes = slot_bytes;
   if (kind == 4) {
     hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, s, a);

@@ -138,12 +138,45 @@ def build_runtime(verbose: bool = False, out_dir: str | None = None, sanitize: b
     return out
 
 
+HOOKS_DIR = os.path.join(ROOT, "csrc", "hooks")
+
+
+def hooks_ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG, "_pdt_hooks" + suffix)
+
+
+def build_hooks(verbose: bool = False) -> str:
+    """``_pdt_hooks``: C++ AccumulateGrad post hooks for the reducers, compiled by g++ against the installed
+    torch's headers and libraries (host code only; no HIP)."""
+    import torch
+
+    srcs = sorted(glob.glob(os.path.join(HOOKS_DIR, "*.cpp")))
+    out = hooks_ext_path()
+    if not srcs or not _newer(out, srcs + [__file__]):
+        return out
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+           sysconfig.get_paths()["include"]]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-w",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_pdt_hooks", "-DTORCH_API_INCLUDE_EXTENSION_H"]
+    for i in inc:
+        cmd += ["-isystem", i]
+    cmd += [*srcs, "-o", out, "-L", os.path.join(tdir, "lib"), "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+    _run(cmd, verbose)
+    return out
+
+
 def build_all(verbose: bool = False) -> None:
-    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+    with cf.ThreadPoolExecutor(max_workers=3) as ex:
         a = ex.submit(build_runtime, verbose)
         b = ex.submit(build_kernels, verbose)
+        c = ex.submit(build_hooks, verbose)
         a.result()
         b.result()
+        c.result()
 
 
 if __name__ == "__main__":

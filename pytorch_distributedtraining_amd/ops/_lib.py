@@ -124,6 +124,9 @@ _SIGS = {
                          c_void_p],
     "pdt_swin_mlp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p],
+    "pdt_gemm_ok": [c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int],
+    "pdt_gemm_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                      c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_wgrad_ok": [c_int64, c_int64, c_int64, c_int],
     "pdt_wgrad_set_variant": [c_int],
     "pdt_wgrad_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p],

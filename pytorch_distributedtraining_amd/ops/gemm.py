@@ -1,0 +1,107 @@
+"""Hand MFMA GEMMs with fused epilogues (``csrc/kernels/gemm.hip``).
+
+* ``gemm_nt(a, b)``            a [M, K] @ b [N, K]^T  (Linear forward; dgrad against a transposed weight)
+* ``gemm_nt(..., bias=)``      + bias
+* ``gemm_nt_gelu(a, b, bias)`` -> (gelu_tanh(a b^T + bias), pre-activation): GPT-2's c_fc in ONE pass
+* ``gemm_nt_dgelu(a, b, pre)`` -> (g = (a b^T) * gelu_tanh'(pre), colsum(g)): c_proj's dgrad, the GELU
+  backward and c_fc's bias gradient in ONE pass
+* ``gemm_tt(a, b)``            a [K, M]^T @ b [K, N]  (weight gradient dY^T X), optional token split
+
+hipBLASLt has no gfx950 kernel for the GELU_AUX_BIAS / DGELU_BGRAD epilogues
+(profiles/r2_hipblaslt_epilogue_probe.txt), so without these the bias + GELU work is two extra HBM passes
+over the [tokens, 4d] hidden per layer ("fuse into a GEMM epilogue").
+Shapes: M, N multiples of 256, K a multiple of 32 (``gemm_ok``); callers fall back to library GEMMs
+otherwise.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+L_NT, L_TT = 0, 1
+E_PLAIN, E_BIAS, E_GELU, E_DGELU = 0, 1, 2, 3
+
+
+def gemm_ok(layout: int, m: int, n: int, k: int, lda: int, ldb: int, splits: int = 1) -> bool:
+    return bool(_lib.require().pdt_gemm_ok(layout, m, n, k, lda, ldb, splits))
+
+
+def _bf16_2d(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1 and t.data_ptr() % 16 == 0
+
+
+def nt_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (_bf16_2d(a) and _bf16_2d(b) and a.shape[1] == b.shape[1]
+            and gemm_ok(L_NT, a.shape[0], b.shape[0], a.shape[1], a.stride(0), b.stride(0)))
+
+
+def tt_ok(a: torch.Tensor, b: torch.Tensor, splits: int = 1) -> bool:
+    return (_bf16_2d(a) and _bf16_2d(b) and a.shape[0] == b.shape[0]
+            and gemm_ok(L_TT, a.shape[1], b.shape[1], a.shape[0], a.stride(0), b.stride(0), splits))
+
+
+def _launch(layout, epi, a, b, c, m, n, k, bias=None, aux=None, aux_out=None, dbias=None, ws=None, splits=1):
+    _lib.call("pdt_gemm_bf16", layout, epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
+              b.stride(0), c.stride(0), _lib.ptr(bias), _lib.ptr(aux), _lib.ptr(aux_out), _lib.ptr(dbias),
+              _lib.ptr(ws), splits, _lib.stream_handle(a.device))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N]."""
+    m, k = a.shape
+    n = b.shape[0]
+    c = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
+    _launch(L_NT, E_BIAS if bias is not None else E_PLAIN, a, b, c, m, n, k, bias=bias)
+    return c
+
+
+def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor):
+    """(gelu_tanh(a b^T + bias), a b^T + bias) -- both bf16 [M, N]; the GELU reads the stored (rounded)
+    pre-activation, which is what the backward differentiates."""
+    m, k = a.shape
+    n = b.shape[0]
+    y = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
+    pre = torch.empty_like(y)
+    _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
+    return y, pre
+
+
+def gemm_nt_dgelu(a: torch.Tensor, b: torch.Tensor, pre: torch.Tensor, bias_dtype=torch.bfloat16):
+    """(g, db): g = (a b^T) * gelu_tanh'(pre) bf16 [M, N], db = g.sum(0) (fp32 partial per 256-row tile,
+    reduced in a fixed order)."""
+    m, k = a.shape
+    n = b.shape[0]
+    g = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
+    db = torch.empty(n, dtype=torch.bfloat16, device=a.device)
+    ws = torch.empty((m // 256) * n, dtype=torch.float32, device=a.device)
+    _launch(L_NT, E_DGELU, a, b, g, m, n, k, aux=pre, dbias=db, ws=ws)
+    return g, db.to(bias_dtype)
+
+
+def tt_splits(m: int, n: int, k: int, cus: int = 256) -> int:
+    """Token split (1, 2, 4, 8, 16) whose tiles x slices fill whole waves of the CUs best (>= 4096 tokens
+    per slice); outputs of at least one wave of tiles are not split (the fp32 slab pass costs more)."""
+    tiles = (m // 256) * (n // 256)
+    if tiles == 0 or tiles >= cus:
+        return 1
+    best, best_eff = 1, 0.0
+    for s in (1, 2, 4, 8, 16):
+        if s > 1 and (k % (32 * s) or k // s < 4096):
+            break
+        wgs = tiles * s
+        eff = wgs / (-(-wgs // cus) * cus)
+        if eff > best_eff + 1e-9:
+            best, best_eff = s, eff
+    return best
+
+
+def gemm_tt(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """a[K, M]^T @ b[K, N] -> bf16 [M, N] (dW = dY^T X with a = dY, b = X)."""
+    k, m = a.shape
+    n = b.shape[1]
+    s = splits or tt_splits(m, n, k)
+    c = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
+    ws = torch.empty(s * m * n, dtype=torch.float32, device=a.device) if s > 1 else None
+    _launch(L_TT, E_PLAIN, a, b, c, m, n, k, ws=ws, splits=s)
+    return c

@@ -20,6 +20,7 @@ MI355X-first design:
 from __future__ import annotations
 
 import warnings
+import weakref
 from contextlib import contextmanager
 
 import torch
@@ -27,6 +28,7 @@ import torch.nn as nn
 
 from ..utils import profiling as prof
 from ..utils.native import require_runtime
+from ._readiness import Readiness
 from .comm import Comm, default_comm
 
 _DT_ID = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
@@ -163,7 +165,7 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._observed = []
         self._warned_unused = False
-        self._hook_handles = []
+        self._ready = None
 
         module.to(self.device)
         if compute_dtype is not None:
@@ -205,11 +207,20 @@ class DistributedDataParallel(nn.Module):
             self.groups.append(g)
         for g in self.groups:
             g.attach_grads()
-        self.tracker = rt.ReadyTracker([list(b.params) for b in plan], len(self.params))
-        for h in self._hook_handles:
-            h.remove()
-        self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
-                              for i, p in enumerate(self.params)]
+        self._arm_readiness()
+
+    def _arm_readiness(self):
+        """Bucket readiness for the current plan: C++ AccumulateGrad post hooks (one Python call per ready
+        bucket) once the plan is final; per-parameter Python hooks while the first iteration records the
+        gradient order for the rebuild.  Callbacks hold the engine weakly (the C++ side is invisible to GC)."""
+        if self._ready is not None:
+            self._ready.remove()
+        ref = weakref.ref(self)
+        self._ready = Readiness(
+            self.params, [list(b.params) for b in self.plan],
+            on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b),
+            observe=(lambda i: ref()._observed.append(i)) if self._rebuild_pending else None)
+        self._ready.set_enabled(not self._no_sync)
 
     def _rebuild(self):
         """Re-plan buckets in the observed gradient-ready order (first iteration), keeping values."""
@@ -252,18 +263,7 @@ class DistributedDataParallel(nn.Module):
                 om._pdt_lp_version = om._version
                 g.master = om
 
-    # ------------------------------------------------------------------ hooks
-    def _make_hook(self, idx):
-        def hook(_p):
-            if self._no_sync:
-                return
-            if self._rebuild_pending:
-                self._observed.append(idx)
-            self._queue_finalize()
-            for bid in self.tracker.mark_ready(idx):
-                self._launch(bid)
-        return hook
-
+    # ------------------------------------------------------------------ hooks (parallel/_readiness.py)
     def _launch(self, bid):
         g, vi = self.bucket_loc[bid]
         view = g.bucket_views[vi]
@@ -290,22 +290,25 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         self._callback_queued = False
         self.comm.check_errors()
-        if not self.tracker.all_launched():
+        if not self._ready.all_released():
             if not self.find_unused_parameters and not self._warned_unused:
                 warnings.warn("DDP: some parameters received no gradient this iteration; their buckets were "
                               "reduced as zeros (pass find_unused_parameters=True to silence)")
                 self._warned_unused = True
-            for bid in self.tracker.flush():
+            for bid in self._ready.flush():
                 self._launch(bid)
         for h, view, payload in self._handles:
             h.wait()
             if view is not None:
                 view.copy_(payload)
         self._handles.clear()
-        self.tracker.reset()
+        self._ready.reset()
         if self._rebuild_pending:
             self._rebuild_pending = False
             self._rebuild()
+            self._observed = []
+            if self._ready.observing:
+                self._arm_readiness()      # order recorded (the plan kept): stop recording, native hooks now
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
@@ -325,10 +328,12 @@ class DistributedDataParallel(nn.Module):
     def no_sync(self):
         old = self._no_sync
         self._no_sync = True
+        self._ready.set_enabled(False)
         try:
             yield
         finally:
             self._no_sync = old
+            self._ready.set_enabled(not old)
 
     # ------------------------------------------------------------------ optimizer / checkpoint helpers
     def optimizer_parameters(self):

@@ -19,8 +19,8 @@ of the compute stream.  Payloads larger than a staging slot are chunked (one epo
 kernels address reduce-scatter inputs and all-gather outputs with a per-peer pitch, so a chunk is a
 strided window of the caller's tensor (no extra copy).
 
-Failure is loud: a mesh wait that exceeds ``spin_limit`` makes the kernel poison its output with NaN and
-set a host-mapped error word; ``raise_if_failed()`` (called by every engine at its end-of-backward and
+Failure is loud: a mesh wait longer than ``timeout_us`` (wall clock, s_memrealtime; default 60 s) makes the
+kernel poison its output with NaN and set a host-mapped error word; ``raise_if_failed()`` (called by every engine at its end-of-backward and
 optimizer sync points through ``Comm.check_errors``) reads that word without synchronising and raises.
 
 ``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes eligible CUDA collectives here (fp32/bf16, sizes a multiple
@@ -44,7 +44,7 @@ class XGMIComm:
     """Peer-mapped collectives for ``comm``'s ranks (one process per GPU of one node)."""
 
     def __init__(self, comm, slot_bytes: int = 256 << 20, oneshot_max_bytes: int = 256 << 10,
-                 spin_limit: int = 1 << 24, uncached: bool = True):
+                 timeout_us: int = 60_000_000, uncached: bool = True):
         if comm.world_size > MAX_WORLD:
             raise ValueError(f"XGMIComm spans one node (<= {MAX_WORLD} GPUs), got world_size={comm.world_size}")
         self.comm = comm
@@ -54,7 +54,7 @@ class XGMIComm:
             # the kernels address a slot with 32-bit buffer-resource offsets
             raise ValueError(f"xGMI slot_bytes must be a positive multiple of 4 KiB below 2 GiB, got {slot_bytes}")
         self.oneshot_max_bytes = int(oneshot_max_bytes)
-        self.spin_limit = int(spin_limit)
+        self.timeout_us = max(1, min(int(timeout_us), (1 << 32) - 1))
         self.device = torch.device("cuda", torch.cuda.current_device())
         lib = _lib.require()   # ctypes signatures: ops/_lib.py _SIGS (checked against the C sources)
         self._lib = lib
@@ -98,7 +98,7 @@ class XGMIComm:
         code = _lib.dtype_code(dtype) if dtype is not None else 0
         err = self._lib.pdt_xgmi_collective(_KIND[kind], inp, out, int(nbytes), int(pitch), code, float(scale),
                                             self._bufs, self.rank, self.world, self.epoch, self.slot_bytes,
-                                            self.spin_limit, self._dev_flag, self.stream.cuda_stream)
+                                            self.timeout_us, self._dev_flag, self.stream.cuda_stream)
         _lib.check(err, f"pdt_xgmi_collective[{kind}]")
 
     def _issue(self, tensors, launch, async_op: bool = False) -> torch.cuda.Event:

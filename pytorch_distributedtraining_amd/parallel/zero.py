@@ -33,6 +33,7 @@ MI355X-first design (not Fairscale's per-rank broadcasts and per-parameter reduc
 """
 from __future__ import annotations
 
+import weakref
 from contextlib import contextmanager
 
 import torch
@@ -42,6 +43,7 @@ from torch.optim import Optimizer
 from ..optim.clip import clip_grad_norm_
 from ..utils import profiling as prof
 from ..utils.native import require_runtime
+from ._readiness import Readiness
 from .comm import Comm, default_comm
 from .ddp import sync_buffers
 
@@ -411,14 +413,16 @@ class ShardedDataParallel(nn.Module):
         for bi, (bank, _o, _s, _n, lidx) in enumerate(self._buckets):
             for li in lidx:
                 gidx.setdefault(bi, []).append(bank.idxs[li])
-        self.tracker = require_runtime().ReadyTracker([gidx[b] for b in range(len(self._buckets))], len(self.params))
         self._bank_li = {}
         for bank in sharded_optimizer.banks():
             for li, gi in enumerate(bank.idxs):
                 self._bank_li[gi] = (bank, li)
-        for i, p in enumerate(self.params):
-            if p.requires_grad:       # frozen parameters: their buckets are released at the end of backward
-                p.register_post_accumulate_grad_hook(self._make_hook(i))
+        # bucket readiness on C++ AccumulateGrad post hooks (parallel/_readiness.py): Python runs once per ready
+        # bucket; frozen parameters get no hook and their buckets are released at the end of backward
+        ref = weakref.ref(self)
+        self._ready = Readiness(self.params, [gidx[b] for b in range(len(self._buckets))],
+                                on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b))
+        self._ready.set_enabled(self.comm.world_size > 1)
 
     # ------------------------------------------------------------------ gradient storage
     def _grad_view(self, bank, li):
@@ -449,15 +453,6 @@ class ShardedDataParallel(nn.Module):
         return n
 
     # ------------------------------------------------------------------ hooks / reduction
-    def _make_hook(self, idx):
-        def hook(_p):
-            if self._no_sync or self.comm.world_size == 1:
-                return
-            self._queue_finalize()
-            for b in self.tracker.mark_ready(idx):
-                self._launch(b)
-        return hook
-
     def _zeros(self, n, dtype, device):
         z = self._pad.get((n, dtype, device))
         if z is None:
@@ -513,14 +508,14 @@ class ShardedDataParallel(nn.Module):
     def _finalize(self):
         self._callback_queued = False
         self.comm.check_errors()
-        for b in self.tracker.flush():      # buckets with parameters that got no gradient
+        for b in self._ready.flush():       # buckets with parameters that got no gradient
             self._launch(b)
         for h, dst, payload in self._handles:
             h.wait()
             if dst is not None:
                 dst.copy_(payload)
         self._handles.clear()
-        self.tracker.reset()
+        self._ready.reset()
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
@@ -541,10 +536,12 @@ class ShardedDataParallel(nn.Module):
     def no_sync(self):
         old = self._no_sync
         self._no_sync = True
+        self._ready.set_enabled(False)
         try:
             yield
         finally:
             self._no_sync = old
+            self._ready.set_enabled(not old and self.comm.world_size > 1)
 
     # ------------------------------------------------------------------ checkpoint helpers
     def full_state_dict(self):

@@ -92,11 +92,13 @@ def apply_env_overrides(cfg: RunConfig, env=None) -> RunConfig:
 
 
 def xgmi_kwargs(env=None) -> Dict[str, Any]:
-    """XGMIComm tuning from the environment (PDT_XGMI_ONESHOT_KB, PDT_XGMI_SLOT_MB)."""
+    """XGMIComm tuning from the environment (PDT_XGMI_ONESHOT_KB, PDT_XGMI_SLOT_MB, PDT_XGMI_TIMEOUT_S)."""
     env = os.environ if env is None else env
     kw = {}
     if env.get("PDT_XGMI_ONESHOT_KB"):
         kw["oneshot_max_bytes"] = int(float(env["PDT_XGMI_ONESHOT_KB"]) * 1024)
     if env.get("PDT_XGMI_SLOT_MB"):
         kw["slot_bytes"] = int(float(env["PDT_XGMI_SLOT_MB"]) * (1 << 20))
+    if env.get("PDT_XGMI_TIMEOUT_S"):
+        kw["timeout_us"] = int(float(env["PDT_XGMI_TIMEOUT_S"]) * 1e6)
     return kw

@@ -66,7 +66,7 @@ def test_xgmi_collectives_several_ranks_on_one_gpu(world):
         assert torch.equal(res[r]["ag"], ag_ref)
         rs_ref = sum(t[r * 4096:(r + 1) * 4096] for t in rs_in) / world
         assert torch.allclose(res[r]["rs"], rs_ref, atol=1e-6)
-        assert torch.equal(res[r]["comm_sum"], torch.full((4,), 3.0))
+        assert torch.equal(res[r]["comm_sum"], torch.full((4,), float(world * (world + 1) // 2)))
 
 
 def _chunked_worker(rank, world):
@@ -120,7 +120,7 @@ def _timeout_worker(rank, world):
     from pytorch_distributedtraining_amd.parallel import Comm
     torch.cuda.set_device(0)
     comm = Comm(xgmi=False)
-    x = comm.enable_xgmi(slot_bytes=1 << 20, spin_limit=2000)
+    x = comm.enable_xgmi(slot_bytes=1 << 20, timeout_us=20_000)
     if rank == 1:
         time.sleep(3.0)                      # rank 1 is late: rank 0's mesh wait runs out of budget
     t = torch.ones(4096, device="cuda")
