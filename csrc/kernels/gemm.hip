@@ -45,10 +45,10 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((address_space(3))) u16x8 lds_u16x8;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int TM = 256, TN = 256, KB = 64, NTH = 512;
+constexpr int TM = 256, TN = 256, KB = 64, NTH = 256;
 constexpr int OPB = TM * KB * 2;           // bytes of one operand tile of one K-step (32 KiB)
 constexpr int STB = 2 * OPB;               // one ring slot: A tile then B tile (2 slots = 128 KiB)
-constexpr int PIECES = OPB / (NTH * 16);   // LDS-DMA instructions per thread per operand per K-step (4)
+constexpr int PIECES = OPB / (NTH * 16);   // LDS-DMA instructions per thread per operand per K-step (8)
 
 enum { L_NT = 0, L_TT = 1 };
 enum { E_PLAIN = 0, E_BIAS = 1, E_GELU = 2, E_DGELU = 3, E_F32 = 4 };
@@ -61,27 +61,49 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
 // TT image swizzle: 16-B chunk c of k-row r is stored at chunk c ^ tt_f(r)
 __device__ __forceinline__ int tt_f(int r) { return 2 * ((r & 3) | ((r >> 1) & 4)); }
 
-// One operand's LDS-DMA: per-lane source byte offsets (relative to the K-step's tile origin) of this
-// thread's PIECES wave-instructions (1 KiB each, lane-linear LDS destination, swizzle on the source).
+// One operand's LDS-DMA for one K-step: PIECES wave-instructions of 1 KiB (lane-linear LDS destination,
+// swizzle on the per-lane SOURCE offset).  Piece i of wave w is 1-KiB block q = 4 i + w of the tile; its
+// per-lane byte offset is a lane term (the same for every piece, or one per piece parity for TT) plus a
+// wave-uniform row term passed as the buffer instruction's scalar offset.
 template <int LAYOUT>
 struct Dma {
-  uint32_t off[PIECES];
+  uint32_t off0, off1;   // lane terms (NT: off1 unused)
+  uint32_t rowstep;      // bytes between consecutive pieces' first rows x 2 (scalar offsets are i * rowstep / 2)
   __device__ __forceinline__ void init(int64_t ld, int w, int lane) {
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const int q = i * 8 + w;   // 1-KiB piece index within the operand tile (0..31)
-      int row, c;
-      if (LAYOUT == L_NT) {      // 8 rows x 128 B per piece; chunk ^= (row >> 1) & 7
-        row = 8 * q + (lane >> 3);
-        c = (lane & 7) ^ ((row >> 1) & 7);
-      } else {                   // 2 k-rows x 512 B per piece
-        row = 2 * q + (lane >> 5);
-        c = (lane & 31) ^ tt_f(row);
-      }
-      off[i] = (uint32_t)(row * ld * 2 + c * 16);
+    if (LAYOUT == L_NT) {        // 8 rows x 128 B per piece: rows 8 q + (lane >> 3); piece i: +32 i rows
+      const int row = 8 * w + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);      // (row >> 1) & 7 does not depend on i (32 i rows)
+      off0 = off1 = (uint32_t)(row * ld * 2 + c * 16);
+      rowstep = (uint32_t)(32 * ld * 2);
+    } else {                     // 2 k-rows x 512 B per piece: rows 8 i + 2 w + (lane >> 5)
+      const int r0 = 2 * w + (lane >> 5);
+      off0 = (uint32_t)(r0 * ld * 2 + ((lane & 31) ^ tt_f(r0)) * 16);        // even i (row bit 3 clear)
+      off1 = (uint32_t)(r0 * ld * 2 + ((lane & 31) ^ tt_f(r0 + 8)) * 16);    // odd i
+      rowstep = (uint32_t)(8 * ld * 2);
     }
   }
-  // pieces [i0, i1) of the tile at byte address `tile` (wave-uniform) into the LDS tile `lds_op`
+  // wave-uniform state of one tile's DMA (descriptor, LDS base, row step), then single pieces
+  struct Tile {
+    v4i rsrc;
+    uint32_t lds0, rs;
+  };
+  __device__ __forceinline__ Tile tile(const char* t, uint32_t nbytes, const char* lds_op, int w) const {
+    const uint64_t addr = (uint64_t)(uintptr_t)t;
+    Tile d;
+    d.rsrc[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)addr);
+    d.rsrc[1] = __builtin_amdgcn_readfirstlane((int)((addr >> 32) & 0xffff));
+    d.rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
+    d.rsrc[3] = 0x00020000;
+    d.lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_op + w * 1024);
+    d.rs = __builtin_amdgcn_readfirstlane(rowstep);
+    return d;
+  }
+  template <int I>
+  __device__ __forceinline__ void piece(const Tile& d) const {
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(d.lds0 + I * 4096), "v"((I & 1) ? off1 : off0), "s"(d.rsrc), "s"(I * d.rs) : "memory");
+  }
+  // pieces [I0, I1) of the tile at byte address `tile` (wave-uniform) into the LDS tile `lds_op`
   template <int I0, int I1>
   __device__ __forceinline__ void issue(const char* tile, uint32_t nbytes, const char* lds_op, int w) const {
     const uint64_t addr = (uint64_t)(uintptr_t)tile;
@@ -90,21 +112,22 @@ struct Dma {
     rsrc[1] = __builtin_amdgcn_readfirstlane((int)((addr >> 32) & 0xffff));
     rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
     rsrc[3] = 0x00020000;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_op + w * 1024);
+    const uint32_t rs = __builtin_amdgcn_readfirstlane(rowstep);
 #pragma unroll
     for (int i = I0; i < I1; ++i) {
-      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(lds_void*)(lds_op + (i * 8 + w) * 1024));
-      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                   :: "s"(m0), "v"(off[i]), "s"(rsrc) : "memory");
+      const uint32_t m0 = lds0 + i * 4096;
+      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(m0), "v"((i & 1) ? off1 : off0), "s"(rsrc), "s"(i * rs) : "memory");
     }
   }
 };
 
-// Fragment of 16 rows (NT: rows of the operand tile; TT: columns) x 32 k (k-substep s of the 64-deep
-// K-step) for the 16x16x32 MFMA: lane l gets row/col (l & 15), k = 32 s + 8 (l >> 4) + e, e = 0..7.
+// Fragment of 16 rows (NT: rows of the operand tile; TT: columns) x 32 k (k-substep S of the 64-deep
+// K-step) for the 16x16x32 MFMA: lane l gets row/col (l & 15), k = 32 S + 8 (l >> 4) + e, e = 0..7.
 template <int LAYOUT>
 struct Frag {
-  uint32_t o0, o1;   // NT: byte offsets of block 0 for s = 0 / 1;  TT: row offset, swizzle term
+  uint32_t o0, o1;   // NT: byte offsets of block 0 for S = 0 / 1;  TT: row offset, swizzle term
   __device__ __forceinline__ void init(int lane) {
     const int x = lane & 15, g = lane >> 4;
     if (LAYOUT == L_NT) {
@@ -162,29 +185,23 @@ __device__ __forceinline__ void tile_of(const GemmArgs& p, int& tm, int& tn) {
   }
 }
 
-__device__ __forceinline__ void bar() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// Main-loop schedule (per K-step of 64, 2-slot LDS ring, 8 waves as two groups of four: g = wave >> 2,
-// one wave of each group per SIMD).  A wave's 128 x 64 output is cut into four quadrants of 64 x 32
-// (16 MFMAs each: 4 m-blocks x 2 n-blocks x 2 k-substeps); every quadrant is one PHASE = {R: its
-// fragment reads (+ DMA pieces of the next K-step), barrier, M: its 16 MFMAs, barrier}.  Group 1 runs
-// one barrier behind group 0, so in every barrier interval one wave of each SIMD is in M while its
-// partner is in R: the matrix pipe never waits for the fragment reads (cdna_hip_programming.md §5,
-// the 8-phase template's stagger).  Quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) re-reads only one
-// operand per phase.
-//   DMA of K-step t+1 into the other slot: phases 1 and 2 of step t (a slot is free once both groups'
-//   phase-3 reads of step t-1 have been waited for, which every wave does before the first barrier of
-//   step t's phase 1); each wave drains its own pieces (vmcnt(0)) before the barrier that precedes the
-//   first read of step t+1 -- group 0 after M of phase 3, group 1 after R of phase 3.
+// Main loop: 4 waves (one per SIMD: the accumulators of a 128 x 128 wave tile -- 8 x 8 MFMA tiles, 256
+// registers -- plus two fragment sets fill its register file), K-step 64 = two 32-deep substeps, 2-slot
+// LDS ring (2 x 64 KiB) filled by LDS-DMA.  Software pipeline per K-step t (one barrier):
+//   A : 64 MFMAs of substep 0 (fragments F0)  ||  ds_reads of substep 1 of tile t -> F1
+//   B1: 32 MFMAs of substep 1 (rows 0-63)
+//       s_waitcnt vmcnt(0) (tile t+1 landed) + lgkmcnt(0) + barrier: tile t+1 visible to all waves, and every
+//       wave is done reading tile t's slot
+//   B2: 32 MFMAs of substep 1 (rows 64-127)  ||  ds_reads of substep 0 of tile t+1 -> F0  ||  LDS-DMA of
+//       tile t+2 into tile t's slot (half of its pieces; the other half rides in the next step's A)
+// A tile's DMA therefore has ~1.5 K-steps of MFMAs to land, no ds_read ever waits at a step boundary, and
+// the matrix pipe of a SIMD sees 128 MFMAs per barrier (cf. the 2-wave-per-SIMD staggered variant: 56 %
+// MFMA busy against hipBLASLt's 85 % at 8192^3, profiles/r3_pmc_gemm_v2_vs_hipblaslt.txt).
 template <int LAYOUT, int EPI>
 __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STB];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int wr = w >> 2, wc = w & 3;
+  const int wr = w >> 1, wc = w & 1;
   int tm, tn;
   tile_of(p, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
@@ -209,111 +226,132 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     astep = KB * p.lda * 2; bstep = KB * p.ldb * 2;
     abytes = (uint32_t)((KB - 1) * p.lda * 2 + TM * 2); bbytes = (uint32_t)((KB - 1) * p.ldb * 2 + TN * 2);
   }
-  // pieces [I0, I1) of both operands of K-step t into slot t & 1
-  auto issue_a = [&](auto i0, auto i1, int t) {
-    da.template issue<decltype(i0)::value, decltype(i1)::value>(Ab + a0 + t * astep, abytes, smem + (t & 1) * STB, w);
+  // pieces [I0, I1) of BOTH operands of K-step t into slot t & 1
+  auto issue = [&](auto i0, auto i1, int t) {
+    constexpr int J0 = decltype(i0)::value, J1 = decltype(i1)::value;
+    da.template issue<J0, J1>(Ab + a0 + t * astep, abytes, smem + (t & 1) * STB, w);
+    db.template issue<J0, J1>(Bb + b0 + t * bstep, bbytes, smem + (t & 1) * STB + OPB, w);
   };
-  auto issue_b = [&](auto i0, auto i1, int t) {
-    db.template issue<decltype(i0)::value, decltype(i1)::value>(Bb + b0 + t * bstep, bbytes,
-                                                                smem + (t & 1) * STB + OPB, w);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I2 = std::integral_constant<int, 2>;
-  using I4 = std::integral_constant<int, 4>;
+  using P0 = std::integral_constant<int, 0>;
+  using PH = std::integral_constant<int, PIECES / 2>;
+  using PE = std::integral_constant<int, PIECES>;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16x8 fa[4][2], fb[2][2];   // the current phase's fragments: 4 m-blocks / 2 n-blocks x 2 k-substeps
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 fa0[8], fb0[8], fa1[8], fb1[8];   // F0 / F1: 8 A blocks (rows 128 wr..) + 8 B blocks (128 wc..)
 
-  // prologue: K-step 0 in flight, landed and visible; group 1 falls one barrier behind
-  issue_a(I0{}, I4{}, 0);
-  issue_b(I0{}, I4{}, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar();
-  if (__builtin_amdgcn_readfirstlane(wr) == 1) bar();
+  // prologue: tiles 0 and 1 in flight, tile 0 landed + visible, its substep-0 fragments in F0
+  issue(P0{}, PE{}, 0);
+  if (T > 1) issue(P0{}, PE{}, 1);
+  if (T > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PIECES) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = fr.template read<0>(smem, 8 * wr + i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(smem + OPB, 8 * wc + j);
 
-  // phase body: R (reads of this quadrant + DMA), barrier, M (16 MFMAs), barrier
-  for (int t = 0; t < T; ++t) {
+  // one K-step; G (guarded) only for the last two steps, so the steady state is branch-free and its
+  // instruction interleave can be pinned with sched_group_barrier (hipcc otherwise issues a stage's reads
+  // just in time and waits on them between MFMAs).  Measured: this form (DMA pieces issued as one group
+  // ahead of each MFMA stretch, reads interleaved 1 : 4 / 1 : 2 with the MFMAs) beat spreading the DMA
+  // pieces between 8-MFMA groups by 8 % on the weight-gradient (TT) shapes (profiles/r3_gemm_variants.txt).
+  auto kstep = [&](auto guarded, const int t) {
+    constexpr bool G = decltype(guarded)::value;
     const char* sa = smem + (t & 1) * STB;
-    const char* sb = sa + OPB;
-    const bool more = t + 1 < T;
+    const char* na = smem + ((t + 1) & 1) * STB;
+    // ---- A: substep 0 MFMAs || substep 1 reads (tile t) || second half of tile t+1's DMA
+    if (t >= 1 && (!G || t + 1 < T)) issue(PH{}, PE{}, t + 1);
+    // read order = order of first use: every B block (all of B1's MFMAs need them), then A blocks 0..7
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int mh = (q == 0 || q == 1) ? 0 : 1;
-      const int nh = (q == 0 || q == 3) ? 0 : 1;
-      // ---- R
-      if (q == 0 || q == 2) {
+    for (int j = 0; j < 8; ++j) fb1[j] = fr.template read<1>(sa + OPB, 8 * wc + j);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          fa[i][0] = fr.template read<0>(sa, 8 * wr + 4 * mh + i);
-          fa[i][1] = fr.template read<1>(sa, 8 * wr + 4 * mh + i);
-        }
+    for (int i = 0; i < 8; ++i) fa1[i] = fr.template read<1>(sa, 8 * wr + i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb0[j], fa0[i], acc[i][j]);
+    if (!G) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 LDS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // 4 MFMAs
       }
-      if (q != 2) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          fb[j][0] = fr.template read<0>(sb, 4 * wc + 2 * nh + j);
-          fb[j][1] = fr.template read<1>(sb, 4 * wc + 2 * nh + j);
-        }
-      }
-      if (more) {
-        if (q == 1) { issue_a(I0{}, I4{}, t + 1); }
-        if (q == 2) { issue_b(I0{}, I4{}, t + 1); }
-      }
-      if (q == 3 && __builtin_amdgcn_readfirstlane(wr) == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      // ---- M
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            acc[4 * mh + i][2 * nh + j] = mfma16(fb[j][s], fa[i][s], acc[4 * mh + i][2 * nh + j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (q == 3 && __builtin_amdgcn_readfirstlane(wr) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
     }
-  }
-  if (__builtin_amdgcn_readfirstlane(wr) == 0) bar();   // group 0 catches up: equal barrier counts
+    // ---- B1: substep 1, rows 0-63
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    // ---- B2: substep 1, rows 64-127 || tile t+1 substep-0 reads || first half of tile t+2's DMA
+    if (!G || t + 2 < T) issue(P0{}, PH{}, t + 2);
+    const bool more = !G || t + 1 < T;
+    if (more) {   // the next step's A needs every B block first, then A blocks in order
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(na + OPB, 8 * wc + j);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa0[i] = fr.template read<0>(na, 8 * wr + i);
+    }
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
+    if (!G) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);   // 1 LDS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);   // 2 MFMAs
+      }
+    }
+  };
+  using Steady = std::integral_constant<bool, false>;
+  using Guarded = std::integral_constant<bool, true>;
+  int t = 0;
+  for (; t + 2 < T; ++t) kstep(Steady{}, t);
+  for (; t < T; ++t) kstep(Guarded{}, t);
 
   // ---------------------------------------------------------------- epilogue
-  // acc[i][j][r] = C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 64 wc + 16 j + 4 (lane >> 4) + r]
+  // acc[i][j][r] = C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
   const int mrow = m0 + 128 * wr + (lane & 15);
-  const int ncol = n0 + 64 * wc + 4 * (lane >> 4);
+  const int ncol = n0 + 128 * wc + 4 * (lane >> 4);
   if constexpr (EPI == E_F32) {
     float* C = p.ws + (int64_t)blockIdx.y * p.M * p.N;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 8; ++j)
         *reinterpret_cast<f32x4*>(C + (int64_t)(mrow + 16 * i) * p.N + ncol + 16 * j) = acc[i][j];
     return;
   } else {
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-    float bj[4][4];
+    float bj[8][4];
     if constexpr (EPI == E_BIAS || EPI == E_GELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 8; ++j) {
         const u16x4 b = *reinterpret_cast<const u16x4*>(p.bias + ncol + 16 * j);
 #pragma unroll
         for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(b[r]);
       }
     }
-    float cs[4][4];   // E_DGELU: this lane's column sums over its 8 rows
+    float cs[8][4];   // E_DGELU: this lane's column sums over its 8 rows
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int64_t rowoff = (int64_t)(mrow + 16 * i) * p.ldc;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 8; ++j) {
         const int64_t e = rowoff + ncol + 16 * j;
         u16x4 o;
         if constexpr (EPI == E_PLAIN) {
@@ -348,7 +386,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
       // sum over the 16 lanes that share (lane >> 4) (rows), then over the two wave rows through LDS;
       // one fp32 partial per column per 256-row tile (deterministic; reduced by colpart_reduce_kernel)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = cs[j][r];
@@ -362,12 +400,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
       float* red = reinterpret_cast<float*>(smem);       // [2 wave rows][256 columns]
       if ((lane & 15) == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[wr * 256 + 64 * wc + 16 * j + 4 * (lane >> 4) + r] = cs[j][r];
+          for (int r = 0; r < 4; ++r) red[wr * 256 + 128 * wc + 16 * j + 4 * (lane >> 4) + r] = cs[j][r];
       }
       __syncthreads();
-      if (tid < 256) p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
+      p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
     }
   }
 }

@@ -53,7 +53,7 @@ struct XArgs {
   unsigned* host_err;                 // host-mapped error word (may be null)
   int rank, world;
   unsigned epoch;
-  unsigned timeout_us;                // wall-clock budget of one mesh wait
+  uint64_t timeout_ticks;             // wall-clock budget of one mesh wait, in s_memrealtime ticks
   int64_t slot_bytes;
 };
 
@@ -83,7 +83,7 @@ __device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
     // whose host is still in a first-call library load can arrive a second late -- an iteration count
     // mis-measures both
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t budget = (uint64_t)a.timeout_us * 100;
+    const uint64_t budget = a.timeout_ticks;
     unsigned spins = 0;
     while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
       if ((++spins & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > budget) {
@@ -218,6 +218,20 @@ __global__ void xgmi_barrier_kernel(XArgs a) { (void)mesh_barrier(a, 3); }
 // Communication kernels share the GPU with the compute stream: a modest grid (<= 128 blocks of 256
 // lanes, half a block per CU) keeps enough 16-B loads in flight to saturate the links while leaving most
 // of every CU to the GEMMs it overlaps with.
+// s_memrealtime rate of the current device (hipDeviceAttributeWallClockRate, kHz; 100 MHz on gfx950)
+int wallclock_khz() {
+  static int khz = 0;
+  if (khz <= 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) == hipSuccess &&
+        v > 0)
+      khz = v;
+    else
+      khz = 100000;
+  }
+  return khz;
+}
+
 int grid_of(int64_t nvec) {
   int64_t g = (nvec + NT - 1) / NT;
   if (g < 1) g = 1;
@@ -279,6 +293,9 @@ PDT_API int pdt_xgmi_host_flag_alloc(void** host_ptr, void** dev_ptr) {
 
 PDT_API int pdt_xgmi_host_flag_free(void* host_ptr) { return (int)hipHostFree(host_ptr); }
 
+// the device's s_memrealtime rate in kHz (the mesh-wait budget's unit conversion)
+PDT_API int pdt_xgmi_wallclock_khz() { return wallclock_khz(); }
+
 // kind: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter, 4 barrier,
 //       5 reduce to root (root rank passed as pitch_bytes / 16).
 //   bytes: all-reduce: the whole payload (two-shot: multiple of 16 * world); all-gather / reduce-scatter:
@@ -300,7 +317,7 @@ PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t byt
   a.rank = rank;
   a.world = world;
   a.epoch = epoch;
-  a.timeout_us = timeout_us;
+  a.timeout_ticks = (uint64_t)timeout_us * (uint64_t)wallclock_khz() / 1000;
   a.slot_bytes = slot_bytes;
   if (kind == 4) {
     hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, s, a);

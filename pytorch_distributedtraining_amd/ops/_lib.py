@@ -99,6 +99,7 @@ _SIGS = {
                             ctypes.c_uint, c_int64, ctypes.c_uint, c_void_p, c_void_p],
     "pdt_xgmi_host_flag_alloc": [c_void_p, c_void_p],
     "pdt_xgmi_host_flag_free": [c_void_p],
+    "pdt_xgmi_wallclock_khz": [],
     "pdt_bn_ws_floats": [c_int],
     "pdt_bn_ok": [c_int],
     "pdt_bn_stats": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
@@ -127,9 +128,6 @@ _SIGS = {
     "pdt_gemm_ok": [c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int],
     "pdt_gemm_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                       c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
-    "pdt_wgrad_ok": [c_int64, c_int64, c_int64, c_int],
-    "pdt_wgrad_set_variant": [c_int],
-    "pdt_wgrad_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_syncbn_elemt": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int,

@@ -1,9 +1,9 @@
 """Linear layer with an MI355X-shaped backward:
 
-* large bf16 weight gradients dW = dY^T X run on the hand MFMA kernel ``csrc/kernels/gemm_wgrad.hip``
-  (both operands token-major, read transposed from LDS) where it is measured faster than hipBLASLt for the
-  shape (timed once per shape; profiles/r2_wgrad_hip_vs_hipblaslt.jsonl); ``PDT_WGRAD_HIP=0/1`` forces
-  hipBLASLt / the hand kernel;
+* large bf16 weight gradients dW = dY^T X run on the hand MFMA GEMM ``csrc/kernels/gemm.hip`` (TT layout:
+  both operands token-major, read transposed from LDS; 1.26-1.36 PFLOP/s on the GPT-2 1.3B shapes against
+  hipBLASLt's 1.0-1.22, profiles/r3_gemm_variants.txt) where it is measured faster than hipBLASLt for the
+  shape (timed once per shape); ``PDT_WGRAD_HIP=0/1`` forces hipBLASLt / the hand kernel;
 
 * the bias gradient is reduced with the framework's column-sum kernel (2x the bandwidth of the generic
   reduction torch uses for ``grad_output.sum(0)``);
@@ -30,6 +30,7 @@ from . import _lib
 from .activations import _colsum, colsum_ok
 from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
+from .gemm import gemm_tt, tt_ok, tt_splits
 
 _WGRAD_CHUNK = 4096
 
@@ -87,44 +88,25 @@ def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 
 
 def hip_wgrad_splits(m: int, n: int, k: int, cus: int = 256) -> int:
-    """Token-dimension split of the HIP weight-gradient GEMM: the slice count (1, 2, 4) whose
-    256x256-tile x slice workgroups fill whole waves of the 256 CUs best, >= 4096 tokens per slice
-    (scripts/bench_wgrad_hip.py: GPT-2 1.3B qkv 192 tiles -> 4 slices 1.14 vs 1.03 PFLOP/s, attention
-    projection 64 tiles -> 4 slices 1.10 vs 0.39); grids of >= one wave of tiles are not split."""
-    tiles = (n // 256) * (k // 256)
-    if tiles == 0 or tiles >= cus:          # a full wave already: a split only adds the fp32 slab pass (Llama-3 8B: -4..-11 %)
-        return 1
-    best, best_eff = 1, 0.0
-    # 8 / 16 slices for the few-tile outputs of small models (GPT-2 124M at 64 x 1024 tokens: 9-36 tiles)
-    for s in (1, 2, 4, 8, 16):
-        if s > 1 and (m % (64 * s) or m // s < 4096):
-            break
-        wgs = tiles * s
-        eff = wgs / (-(-wgs // cus) * cus)
-        if eff > best_eff + 1e-9:
-            best, best_eff = s, eff
-    return best
+    """Token-dimension split of the HIP weight-gradient GEMM (``ops.gemm.tt_splits``): the slice count whose
+    256x256-tile x slice workgroups fill whole waves of the 256 CUs best, >= 4096 tokens per slice; outputs
+    of >= one wave of tiles are not split (the fp32 slab pass would cost more)."""
+    return tt_splits(n, k, m, cus)
 
 
 def hip_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> bool:
     m, n = dy2.shape
     k = x2.shape[1]
-    return (HIP_WGRAD != "0" and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
-            and out_dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
-            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0 and m >= 4096 and n % 256 == 0
-            and k % 256 == 0 and bool(_lib.require().pdt_wgrad_ok(m, n, k, hip_wgrad_splits(m, n, k))))
+    return (HIP_WGRAD != "0" and dy2.is_cuda and out_dtype == torch.bfloat16 and m >= 4096
+            and tt_ok(dy2, x2, hip_wgrad_splits(m, n, k)))
 
 
 def hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int | None = None) -> torch.Tensor:
-    """dW [N, K] = dy2^T x2 on the hand MFMA kernel (csrc/kernels/gemm_wgrad.hip), bf16 out."""
+    """dW [N, K] = dy2^T x2 on the hand MFMA GEMM (csrc/kernels/gemm.hip, TT layout: both operands token-major,
+    fragments read transposed from LDS), bf16 out."""
     m, n = dy2.shape
     k = x2.shape[1]
-    s = splits or hip_wgrad_splits(m, n, k)
-    out = torch.empty(n, k, dtype=torch.bfloat16, device=dy2.device)
-    ws = torch.empty(s * n * k, dtype=torch.float32, device=dy2.device) if s > 1 else None
-    _lib.call("pdt_wgrad_bf16", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), m, n, k, s, _lib.ptr(ws),
-              _lib.stream_handle(dy2.device))
-    return out
+    return gemm_tt(dy2, x2, splits or hip_wgrad_splits(m, n, k))
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:

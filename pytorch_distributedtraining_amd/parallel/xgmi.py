@@ -55,6 +55,7 @@ class XGMIComm:
             raise ValueError(f"xGMI slot_bytes must be a positive multiple of 4 KiB below 2 GiB, got {slot_bytes}")
         self.oneshot_max_bytes = int(oneshot_max_bytes)
         self.timeout_us = max(1, min(int(timeout_us), (1 << 32) - 1))
+        self.wallclock_khz = int(_lib.require().pdt_xgmi_wallclock_khz())   # s_memrealtime rate (budget unit)
         self.device = torch.device("cuda", torch.cuda.current_device())
         lib = _lib.require()   # ctypes signatures: ops/_lib.py _SIGS (checked against the C sources)
         self._lib = lib

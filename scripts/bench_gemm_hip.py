@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Hand MFMA GEMM (csrc/kernels/gemm.hip) vs hipBLASLt (torch) and the round-2 weight-gradient kernel:
+"""Hand MFMA GEMM (csrc/kernels/gemm.hip) vs hipBLASLt (torch):
 correctness against fp32 torch, then interleaved timing rounds in one process (cdna_hip_programming.md §5.4
 rule 24) at the GPT-2 1.3B flagship shapes (96 x 1024 tokens) on random data.  One JSON line per case."""
 import json
@@ -12,7 +12,6 @@ import torch  # noqa: E402
 
 from pytorch_distributedtraining_amd.ops import gemm as G  # noqa: E402
 from pytorch_distributedtraining_amd.ops.activations import bias_gelu  # noqa: E402
-from pytorch_distributedtraining_amd.ops.linear import hip_wgrad  # noqa: E402
 
 dev = torch.device("cuda")
 TOK = int(os.environ.get("TOK", str(96 * 1024)))
@@ -98,10 +97,9 @@ def bench():
         dy = torch.randn(TOK, No, device=dev).bfloat16()
         x = torch.randn(TOK, Ki, device=dev).bfloat16()
         fl = 2.0 * TOK * No * Ki
-        res = {"hip": [], "r2_wgrad": [], "lt": []}
+        res = {"hip": [], "lt": []}
         for _ in range(ROUNDS):
             res["hip"].append(timeit(lambda: G.gemm_tt(dy, x)))
-            res["r2_wgrad"].append(timeit(lambda: hip_wgrad(dy, x)))
             res["lt"].append(timeit(lambda: torch.mm(dy.t(), x)))
         r = {k: min(v) for k, v in res.items()}
         out(case=f"tt_{name}", M=No, N=Ki, K=TOK, splits=G.tt_splits(No, Ki, TOK), ms=r,

@@ -92,6 +92,22 @@ def test_fp8_cast_transpose_gpu(R, C, fmt, dt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R,C", [(96 * 1024, 8192), (96 * 1024 + 64, 8192 + 64)])
+def test_fp8_cast_transpose_full_grid_production_shape(R, C):
+    """The flagship MLP hidden (96 x 1024 tokens x 8192) through the 128 x 128-tile kernel, and the 64 x 64-tile
+    kernel at the same scale (dimensions not multiples of 128): every byte of both outputs and the amax."""
+    torch.manual_seed(1)
+    x = (torch.randn(R, C, device="cuda") * 3).to(torch.bfloat16)
+    meta = F8.Fp8Meta("cuda")
+    meta.scale[0] = 0.37
+    q, qt = F8.cast_transpose(x, meta, 0, 0)
+    ref = (x.float() * 0.37).clamp(-F8._FMT_MAX[0], F8._FMT_MAX[0]).to(F8._FMT_DTYPE[0])
+    assert torch.equal(q.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), ref.t().contiguous().view(torch.uint8))
+    assert float(meta.cur[0]) == float(x.float().abs().max())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bias", [True, False])
 def test_fp8_linear_gpu(bias):
     _check_linear("cuda", M=4096, K=1024, N=2048, bias=bias)

@@ -606,7 +606,7 @@ def test_swinir_conv_path_matches_stock_model():
 @pytest.mark.parametrize("splits", [1, 2, 4])
 @pytest.mark.parametrize("M,N,K", [(8192, 512, 256), (4096, 768, 1024), (16384, 256, 512)])
 def test_hip_wgrad_gemm(M, N, K, splits):
-    """Hand MFMA weight-gradient GEMM (gemm_wgrad.hip: both operands token-major, transposed LDS reads,
+    """Hand MFMA weight-gradient GEMM (gemm.hip TT layout: both operands token-major, transposed LDS reads,
     split-K fp32 slabs) vs the fp32 product dY^T X."""
     from pytorch_distributedtraining_amd.ops.linear import hip_wgrad
     torch.manual_seed(0)
@@ -617,6 +617,25 @@ def test_hip_wgrad_gemm(M, N, K, splits):
     assert got.shape == (N, K) and got.dtype == torch.bfloat16
     assert rel_err(got, ref) < 4e-3
     assert float((got.float() - ref).abs().max()) < 0.05 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("splits", [1, 2, 4])
+@pytest.mark.parametrize("N,K", [(8192, 2048), (2048, 8192), (6144, 2048), (2048, 2048)])
+def test_hip_wgrad_full_grid_production_shapes(N, K, splits):
+    """The flagship's weight gradients (GPT-2 1.3B at 96 x 1024 tokens: c_fc, c_proj, qkv, attention projection)
+    on the FULL grid of 256 x 256 tiles, every split the autotuner can pick, EVERY element against fp32 torch:
+    the LDS-DMA ring must hold under full-chip load (a round-2 attention DMA race passed every small test)."""
+    from pytorch_distributedtraining_amd.ops.linear import hip_wgrad
+    M = 96 * 1024
+    torch.manual_seed(N + K + splits)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    got = hip_wgrad(dy, x, splits=splits).float()
+    ref = dy.float().t() @ x.float()
+    rms = float(ref.square().mean().sqrt())
+    err = (got - ref).abs()
+    bad = err > 0.008 * ref.abs() + 0.01 * rms       # bf16 output rounding + fp32 accumulation order
+    assert int(bad.sum()) == 0, (int(bad.sum()), float(err.max()), rms)
 
 
 @pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60), (16384, 768, 768), (16384, 768, 3072),
