@@ -150,6 +150,7 @@ struct AttnParams {
   int64_t dv_sb, dv_ss, dv_sh;
   int B, H, Hkv, Sq, Sk;
   float scale;   // softmax scale (natural domain)
+  int order;     // workgroup -> block order: 0 heavy-first, 1 XCD-grouped (block_order)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -364,14 +365,16 @@ __device__ __forceinline__ void retire(const u16x8 (&x)[N]) {
   for (int i = 0; i < N; ++i) asm volatile("" :: "v"(x[i]));
 }
 
-template <int D, bool ASM = true>
+template <int D, bool ASM = true, int NW = 4>
 struct DmaLane {
-  static constexpr int RPI = 1024 / (D * 2), NI = 16 / RPI, LPR = 64 / RPI;
+  // NW waves fill a TILE-row window, RW rows each, RPI rows per 1-KiB wave-instruction
+  static constexpr int RW = TILE / NW, RPI = 1024 / (D * 2), NI = RW / RPI, LPR = 64 / RPI;
+  static_assert(NI >= 1 && RW % RPI == 0, "tile rows per wave must be whole DMA instructions");
   uint32_t off_[NI];
   __device__ __forceinline__ void init(int64_t row_stride, int w, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int row = 16 * w + RPI * i + lane / LPR;
+      const int row = RW * w + RPI * i + lane / LPR;
       const int c = (lane % LPR) ^ swz_f<D>(row);
       off_[i] = (uint32_t)((row * row_stride + c * 8) * 2);
     }
@@ -384,14 +387,14 @@ struct DmaLane {
     if constexpr (ASM) {
       const v4i rsrc = make_rsrc(base + (int64_t)row0 * row_stride, bytes);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off(i, w), lds + (16 * w + RPI * i) * D);
+      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off(i, w), lds + (RW * w + RPI * i) * D);
     } else {
 #if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
       const __amdgpu_buffer_rsrc_t rsrc =
           __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * row_stride), 0, bytes, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (16 * w + RPI * i) * D), 16, off(i, w), 0,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (RW * w + RPI * i) * D), 16, off(i, w), 0,
                                                  0, 0);
 #endif
     }
@@ -543,6 +546,24 @@ __device__ __forceinline__ BlockCoord heavy_first(bool heavy_is_high) {
   BlockCoord c;
   c.h = rem % nh;
   c.b = rem / nh;
+  c.t = heavy_is_high ? nt - 1 - rank : rank;
+  return c;
+}
+
+// XCD-grouped order (p.order == 1): workgroups are dealt to the 8 XCDs round-robin in flattened-id order
+// (lin % 8), each XCD with its own L2.  heavy_first() spreads the blocks of one (head, batch) -- which all
+// stream the SAME K/V (forward, dQ) or Q/dO (dK/dV) tiles -- over every XCD and over the whole launch, so
+// each re-read comes from HBM.  Here every (head, batch) group lives on one XCD (group g -> XCD g % 8) and
+// its blocks run back to back there, heaviest first, so the re-reads hit that XCD's L2.
+__device__ __forceinline__ BlockCoord block_order(bool heavy_is_high, int order) {
+  const int nt = gridDim.x, nh = gridDim.y, G = nh * gridDim.z;
+  if (order != 1 || (G & 7)) return heavy_first(heavy_is_high);
+  const int lin = blockIdx.x + nt * (blockIdx.y + nh * blockIdx.z);
+  const int j = lin >> 3, gi = j / nt, rank = j - gi * nt;
+  const int g = gi * 8 + (lin & 7);
+  BlockCoord c;
+  c.h = g % nh;
+  c.b = g / nh;
   c.t = heavy_is_high ? nt - 1 - rank : rank;
   return c;
 }
@@ -853,9 +874,10 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = heavy_first(true);
-  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
-  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
+  const BlockCoord bc = block_order(true, p.order);
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
+  const int qb = remap ? bc.t : (int)blockIdx.x;
   const int hk = hq / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
@@ -925,6 +947,122 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
         }
       }
     }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  store_row16<DT>(p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss, o, inv, h, qrow < p.Sq);
+  if (qrow < p.Sq && h == 0)
+    p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward v7 = v5's per-wave tile on a 512-thread workgroup: 8 waves x 32 query rows = 256 rows share every
+// staged K/V tile, twice v5's 128.  Each 64-key tile (32 KB of K and V) then feeds 2 x 128 x 64 x 128 x 2
+// FLOPs per 16 KB -- 256 FLOP/B instead of 128 -- which halves the L2 -> LDS tile traffic per FLOP: at
+// the GPT-2 1.3B shape v5 streamed ~3.9 TB/s of K/V for 460 TFLOP/s, i.e. it was fed, not computing.
+// One workgroup per CU (two waves per SIMD, the same register budget as v5's two 256-thread groups),
+// NBUF-deep LDS ring with counted vmcnt: tile t's DMA is waited for while tiles t+1 .. t+NBUF-2 stay in
+// flight (NBUF = 3: two tiles of latency cover instead of one).
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+// top of ring iteration t: this wave's DMA of tile t landed (later tiles may still fly), then the barrier
+// publishes every wave's part of tile t and retires all reads of the stage about to be refilled
+template <int PER_TILE, int NBUF>
+__device__ __forceinline__ void ring_wait(bool later_in_flight) {
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth 2 or 3");
+  if constexpr (NBUF == 3) {
+    if (later_in_flight) vm_wait<PER_TILE>();
+    else vm_wait<0>();
+  } else {
+    vm_wait<0>();
+  }
+  __syncthreads();
+}
+
+constexpr int NT8 = 512;
+
+template <int D, bool CAUSAL, int NBUF>
+__global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
+  using K = FwdV5<D, CAUSAL>;
+  constexpr int KS = K::KS, DT = K::DT, TE = K::TE, NW = 8, BM = 32 * NW;
+  using Dma = DmaLane<D, true, NW>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];   // [stage][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const BlockCoord bc = block_order(true, p.order);
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
+  const int qb = remap ? bc.t : (int)blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * BM, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + BM + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  Dma lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t)
+    if (t < ntiles) {
+      lk.issue(Kp, p.k_ss, t * TILE, p.Sk, smem + t * 2 * TE, w);
+      lv.issue(Vp, p.v_ss, t * TILE, p.Sk, smem + t * 2 * TE + TE, w);
+    }
+
+  int koff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int voff[DT][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int r1 = 4 * (g >> 1) + q;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
+      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
+    }
+  }
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+    }
+  }
+  retire(qf);
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  int stage = 0;   // stage of tile t; tile t + NBUF - 1 refills stage (t - 1) % NBUF
+  for (int t = 0; t < ntiles; ++t) {
+    ring_wait<2 * Dma::NI, NBUF>(t + 1 < ntiles);
+    if (t + NBUF - 1 < ntiles) {
+      const int ns = stage == 0 ? NBUF - 1 : stage - 1;
+      bf16_t* nb = smem + ns * 2 * TE;
+      lk.issue(Kp, p.k_ss, (t + NBUF - 1) * TILE, p.Sk, nb, w);
+      lv.issue(Vp, p.v_ss, (t + NBUF - 1) * TILE, p.Sk, nb + TE, w);
+    }
+    const int k0 = t * TILE;
+    if (!(CAUSAL && k0 > qw + 31 + off)) {
+      const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+      K::tile(smem + stage * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
+    }
+    stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -1581,9 +1719,10 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];    // [buf][lse | delta]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = heavy_first(false);   // causal: low key blocks see the most queries
-  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hk = CAUSAL ? bc.h : (int)blockIdx.y;
-  const int kb = CAUSAL ? bc.t : (int)blockIdx.x;
+  const BlockCoord bc = block_order(false, p.order);   // causal: low key blocks see the most queries
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
+  const int kb = remap ? bc.t : (int)blockIdx.x;
   const int group = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   const int kw = kb * 128 + w * 32, key = kw + c32;
@@ -1728,9 +1867,10 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = heavy_first(true);
-  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
-  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
+  const BlockCoord bc = block_order(true, p.order);
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
+  const int qb = remap ? bc.t : (int)blockIdx.x;
   const int hk = hq / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
@@ -1799,8 +1939,92 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
 }
 
+// dQ v4: dQ v3's per-wave tile on a 512-thread workgroup (8 waves x 32 query rows = 256 rows per staged
+// K/V tile, 384 instead of 192 FLOP per staged byte) with the NBUF-deep counted-vmcnt ring of forward v7.
+template <int D, bool CAUSAL, int NBUF>
+__global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D, NW = 8, BM = 32 * NW;
+  using Dma = DmaLane<D, true, NW>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];   // [stage][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const BlockCoord bc = block_order(true, p.order);
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
+  const int qb = remap ? bc.t : (int)blockIdx.x;
+  const int hk = hq / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * BM, qw = q0 + w * 32, qrow = qw + c32;
+  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  int kend = p.Sk;
+  if (CAUSAL) kend = min(p.Sk, q0 + BM + off);
+  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  Dma lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t)
+    if (t < ntiles) {
+      lk.issue(Kp, p.k_ss, t * TILE, p.Sk, smem + t * 2 * TE, w);
+      lv.issue(Vp, p.v_ss, t * TILE, p.Sk, smem + t * 2 * TE + TE, w);
+    }
+  u16x8 qf[KS], gf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < p.Sq) {
+      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
+    }
+  }
+  const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
+  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  retire(qf);
+  retire(gf);
+  asm volatile("" :: "v"(nlse2), "v"(dl));
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+  const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+
+  int stage = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    ring_wait<2 * Dma::NI, NBUF>(t + 1 < ntiles);
+    if (t + NBUF - 1 < ntiles) {
+      const int ns = stage == 0 ? NBUF - 1 : stage - 1;
+      bf16_t* nb = smem + ns * 2 * TE;
+      lk.issue(Kp, p.k_ss, (t + NBUF - 1) * TILE, p.Sk, nb, w);
+      lv.issue(Vp, p.v_ss, (t + NBUF - 1) * TILE, p.Sk, nb + TE, w);
+    }
+    const int k0 = t * TILE;
+    if (!(CAUSAL && k0 > qw + 31 + off)) {
+      const bf16_t* Ks = smem + stage * 2 * TE;
+      BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+    }
+    stage = stage + 1 == NBUF ? 0 : stage + 1;
+  }
+  store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
+}
+
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
-int g_fwd_variant = -1, g_bwd_variant = -1;
+int g_fwd_variant = -1, g_bwd_variant = -1, g_order = -1;
+int block_order_mode() {
+  if (g_order < 0) { const char* e = getenv("PDT_FA_ORDER"); g_order = e ? atoi(e) : 0; }
+  return g_order;
+}
 int fwd_variant() {
   if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 5; }
   return g_fwd_variant;
@@ -1822,6 +2046,15 @@ int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
   } else if (variant == 5) {
     if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else if (variant == 7 || variant == 8) {   // 8 waves x 32 rows; 7: 3-deep ring, 8: 2-deep
+    dim3 g8((p.Sq + 255) / 256, p.H, p.B);
+    if (variant == 7) {
+      if (causal) fa_fwd_v7_kernel<D, true, 3><<<g8, NT8, 0, st>>>(p);
+      else fa_fwd_v7_kernel<D, false, 3><<<g8, NT8, 0, st>>>(p);
+    } else {
+      if (causal) fa_fwd_v7_kernel<D, true, 2><<<g8, NT8, 0, st>>>(p);
+      else fa_fwd_v7_kernel<D, false, 2><<<g8, NT8, 0, st>>>(p);
+    }
   } else {
     if (causal) fa_fwd_v3_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v3_kernel<D, false><<<grid, NT, 0, st>>>(p);
@@ -1873,6 +2106,17 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
       fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
       fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(p);
     }
+  } else if (variant == 8 || variant == 9) {   // dK/dV v3 (one wave per SIMD) + dQ v4 (8 waves; 8: 3-deep ring)
+    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
+    if (causal) {
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
+      if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(p);
+      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(p);
+    } else {
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
+      if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(p);
+      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(p);
+    }
   } else if (variant == 3) {   // v3, one wave per SIMD for dK/dV (no spills)
     if (causal) {
       fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
@@ -1907,6 +2151,7 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
   p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
+  p.order = block_order_mode();
   const int variant = fwd_variant();
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
@@ -1929,7 +2174,14 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.dk_sb = strides[18]; p.dk_ss = strides[19]; p.dk_sh = strides[20];
   p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
+  p.order = block_order_mode();
   return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
+}
+
+// workgroup -> block order (0 heavy-first, 1 XCD-grouped; < 0 keeps the current one); returns the order in effect
+PDT_API int pdt_flash_attn_set_order(int order) {
+  if (order >= 0) g_order = order;
+  return block_order_mode();
 }
 
 // select kernel variants (<= 0 keeps the current choice); returns fwd * 16 + bwd now in effect

@@ -85,13 +85,19 @@ __device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint64_t budget = a.timeout_ticks;
     unsigned spins = 0;
-    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+    unsigned seen;
+    while ((int)((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) - a.epoch) < 0) {
       if ((++spins & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > budget) {
         // give up: record the failure, never hang the queue
         __hip_atomic_fetch_or((gu32*)(a.buf[a.rank] + ERR_OFF), 1u << b, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_SYSTEM);
-        if (a.host_err != nullptr)   // plain system-scope store (no PCIe atomics needed): any bit = failure
+        if (a.host_err != nullptr) {  // plain system-scope stores (no PCIe atomics needed): any bit = failure
+          // diagnosis words (last writer wins): the epoch waited for, barrier / late peer, the peer's last epoch
+          __hip_atomic_store(a.host_err + 1, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_err + 2, (unsigned)(b << 8 | t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_err + 3, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.host_err, 0x100u | (1u << b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         atomicOr(&timed_out, 1);
         break;
       }

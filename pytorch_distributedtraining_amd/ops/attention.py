@@ -182,5 +182,12 @@ def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:
     return r // 16, r % 16
 
 
+def set_block_order(order: int = -1) -> int:
+    """Workgroup -> block order of the flash-attention kernels: 0 heavy-first (longest causal blocks
+    dispatched first), 1 XCD-grouped (every (head, batch) on one XCD, its blocks back to back, so the K/V or
+    Q/dO re-reads hit that XCD's L2).  -1 keeps the current one.  Returns the order in effect."""
+    return int(_lib.require().pdt_flash_attn_set_order(int(order)))
+
+
 def supported(head_dim: int) -> bool:
     return head_dim in (64, 128)

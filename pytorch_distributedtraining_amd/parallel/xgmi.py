@@ -207,11 +207,21 @@ class XGMIComm:
         """Timeout bits recorded by the kernels so far (host-mapped word: no device sync)."""
         return ctypes.c_uint.from_address(self._host_flag.value).value
 
+    def diagnosis(self) -> dict:
+        """What the last timed-out wait saw: the epoch it waited for, the barrier, the late peer and that
+        peer's last signalled epoch (host-mapped words written by the kernel; no device sync)."""
+        w = (ctypes.c_uint * 4).from_address(self._host_flag.value)
+        return {"flag": w[0], "epoch": w[1], "barrier": w[2] >> 8, "peer": w[2] & 0xFF, "peer_epoch": w[3],
+                "issued_epoch": self.epoch}
+
     def raise_if_failed(self):
         v = self.failed()
         if v:
+            d = self.diagnosis()
             raise RuntimeError(f"xGMI collective timed out on rank {self.rank} (flag {v:#x}): a peer did not reach "
-                               "the same collective in time; its outputs were poisoned with NaN")
+                               f"the same collective in time; its outputs were poisoned with NaN -- waited at "
+                               f"barrier {d['barrier']} for epoch {d['epoch']}, peer {d['peer']} had signalled "
+                               f"{d['peer_epoch']}; this rank has issued up to epoch {d['issued_epoch']}")
 
     def check(self):
         """Synchronise the comm stream, then raise if any mesh wait timed out (tests / teardown)."""

@@ -24,7 +24,8 @@ MI355X-first design (not Fairscale's per-rank broadcasts and per-parameter reduc
     weight casts and no bf16->fp32 gradient casts (the autocast "cast storm").
   * ``ShardedDataParallel`` (ZeRO-2, ``reduce_mode="reduce"``): a rank keeps a persistent gradient buffer
     for its own segment only; gradients of other owners' parameters are produced by autograd, packed per
-    bucket (a window of one owner's segment) into a transient buffer, reduced (AVG) to the owner
+    bucket (a window of one owner's segment; the wire-dtype cast fused into the same kernel) into a slot of
+    a small ring of persistent staging buffers (no allocation per bucket), reduced (AVG) to the owner
     asynchronously from the grad hooks, and freed -- per-rank gradient memory is ~1/world of the model.
     ``reduce_mode="all_reduce"`` is the ZeRO-1 gradient path (DDP + OSS): full gradients, bucketed
     all-reduces over the same flat.
@@ -372,11 +373,15 @@ class ShardedDataParallel(nn.Module):
     """ZeRO-2: each gradient is reduced (averaged) only to the rank that owns its optimizer shard, and
     non-owners drop it.  ``reduce_mode="all_reduce"``: ZeRO-1 (full gradients all-reduced, DDP + OSS)."""
 
+
     def __init__(self, module: nn.Module, sharded_optimizer: OSS, comm: Comm | None = None,
                  broadcast_buffers: bool = True, sync_models_at_startup: bool = True,
                  reduce_buffer_size: int = 2 ** 23, reduce_fp16: bool = False, reduce_mode: str = "reduce",
-                 buffer_sync: str = "changed", **_ignored):
+                 buffer_sync: str = "changed", staging_slots: int = 4, **_ignored):
         super().__init__()
+        if staging_slots < 1:
+            raise ValueError(f"staging_slots must be >= 1, got {staging_slots}")
+        self.STAGING_SLOTS = staging_slots   # non-owned buckets in flight at once (ring of pack buffers)
         if reduce_mode not in ("reduce", "all_reduce"):
             raise ValueError(f"reduce_mode must be 'reduce' or 'all_reduce', got {reduce_mode}")
         self.module = module
@@ -396,6 +401,7 @@ class ShardedDataParallel(nn.Module):
                 self.comm.broadcast_coalesced(bufs)
         self.params = sharded_optimizer._all_params
         self._pad = {}
+        self._rings = {}            # (wire dtype, device) -> staging ring for non-owned buckets (_slot)
         # gradient storage: own segment only (ZeRO-2) or the full flat (ZeRO-1); buckets from the layout
         self._buckets = []          # (bank, owner, start, numel, [local idx])
         self._grad = {}             # bank id -> gradient flat
@@ -452,6 +458,10 @@ class ShardedDataParallel(nn.Module):
                     n += p.grad.numel() * p.grad.element_size()
         return n
 
+    def staging_bytes(self) -> int:
+        """Bytes of the persistent pack rings (bounded by STAGING_SLOTS x the largest non-owned bucket)."""
+        return sum(t.numel() * t.element_size() for r in self._rings.values() for t in r["bufs"])
+
     # ------------------------------------------------------------------ hooks / reduction
     def _zeros(self, n, dtype, device):
         z = self._pad.get((n, dtype, device))
@@ -459,8 +469,29 @@ class ShardedDataParallel(nn.Module):
             z = self._pad[(n, dtype, device)] = torch.zeros(n, dtype=dtype, device=device)
         return z
 
-    def _pack(self, bank, start, n, lidx):
-        """Non-owner: this bucket's gradients in the owner's segment layout, one cat (gaps = zeros)."""
+    def _slot(self, bank, n, dtype):
+        """A staging slot of ``n`` elements from the (dtype, device) ring of STAGING_SLOTS persistent buffers,
+        each as large as the largest non-owned bucket.  A slot is reused only after the reduce that last read
+        it was waited for (stream-ordered on device, so no host sync): ZeRO-2 keeps its memory bound -- the
+        ring is a few buckets, not the (W-1)/W of the gradients a buffer per bucket would pin -- while the
+        pack allocates nothing."""
+        key = (dtype, bank.device)
+        ring = self._rings.get(key)
+        if ring is None:
+            size = max(bn for bk, ow, _s, bn, _l in self._buckets
+                       if ow != bk.rank and bk.device == bank.device)
+            ring = self._rings[key] = {"bufs": [torch.empty(size, dtype=dtype, device=bank.device)
+                                                for _ in range(self.STAGING_SLOTS)],
+                                       "busy": [None] * self.STAGING_SLOTS, "next": 0}
+        i = ring["next"]
+        ring["next"] = (i + 1) % self.STAGING_SLOTS
+        if ring["busy"][i] is not None:
+            ring["busy"][i].wait()
+        return ring, i, ring["bufs"][i][:n]
+
+    def _pack(self, bank, start, n, lidx, dtype):
+        """Non-owner: this bucket's gradients in the owner's segment layout (gaps = zeros), cast to the wire
+        dtype in the same single ``cat`` kernel, written into a ring slot (no allocation per bucket)."""
         pieces, cur = [], start
         for li in sorted(lidx, key=lambda i: bank.offsets[i]):
             p = bank.params[li]
@@ -473,7 +504,9 @@ class ShardedDataParallel(nn.Module):
             cur = o + p.numel()
         if start + n > cur:
             pieces.append(self._zeros(start + n - cur, bank.dtype, bank.device))
-        return torch.cat(pieces) if len(pieces) > 1 else pieces[0].clone()
+        ring, i, slot = self._slot(bank, n, dtype)
+        torch.cat(pieces, out=slot)
+        return ring, i, slot
 
     def _launch(self, b):
         with prof.range(f"sddp.{self.reduce_mode}[bucket {b}]"):
@@ -481,23 +514,23 @@ class ShardedDataParallel(nn.Module):
 
     def _launch_bucket(self, b):
         bank, owner, start, n, lidx = self._buckets[b]
-        if self.reduce_mode == "all_reduce":
-            buf = self._grad[id(bank)][start:start + n]
-        elif owner == bank.rank:
-            o = start - bank.rank * bank.seg
+        wire = bank.dtype
+        if self.reduce_fp16 and bank.dtype == torch.float32:
+            wire = torch.bfloat16 if bank.device.type == "cuda" else torch.float16
+        if self.reduce_mode == "all_reduce" or owner == bank.rank:
+            o = start if self.reduce_mode == "all_reduce" else start - bank.rank * bank.seg
             buf = self._grad[id(bank)][o:o + n]
+            payload = buf if wire == buf.dtype else buf.to(wire)
+            if self.reduce_mode == "all_reduce":
+                h = self.comm.all_reduce(payload, "avg", async_op=True)
+            else:
+                h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
+            self._handles.append((h, buf if payload is not buf else None, payload))
         else:
-            buf = self._pack(bank, start, n, lidx)
-        payload = buf
-        if self.reduce_fp16 and buf.dtype == torch.float32:
-            payload = buf.to(torch.bfloat16 if buf.is_cuda else torch.float16)
-        if self.reduce_mode == "all_reduce":
-            h = self.comm.all_reduce(payload, "avg", async_op=True)
-            keep = True
-        else:
+            ring, i, payload = self._pack(bank, start, n, lidx, wire)
             h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
-            keep = owner == bank.rank
-        self._handles.append((h, buf if (keep and payload is not buf) else None, payload))
+            ring["busy"][i] = h
+            self._handles.append((h, None, payload))
 
     def _queue_finalize(self):
         if self._callback_queued:

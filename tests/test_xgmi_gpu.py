@@ -127,6 +127,7 @@ def _timeout_worker(rank, world):
     x.all_reduce(t, "sum")
     torch.cuda.synchronize()
     failed = x.failed()
+    diag = x.diagnosis()
     raised = False
     try:
         comm.check_errors()
@@ -135,10 +136,13 @@ def _timeout_worker(rank, world):
     nan = bool(torch.isnan(t).any())
     comm.barrier()
     x.close()
-    return failed, raised, nan
+    return failed, raised, nan, diag
 
 
 def test_xgmi_timeout_is_loud():
-    (f0, r0, n0), (f1, r1, n1) = run_workers(_timeout_worker, 2)
+    (f0, r0, n0, d0), (f1, r1, n1, _d1) = run_workers(_timeout_worker, 2)
     assert f0 != 0 and r0 and n0             # rank 0 timed out: flag set, check raises, output poisoned
     assert f1 == 0 and not r1 and not n1     # rank 1 found rank 0's signal and completed normally
+    # the diagnosis names the wait: barrier 0 of rank 0's last epoch, peer 1 still at an older epoch
+    assert d0["peer"] == 1 and d0["barrier"] == 0 and d0["epoch"] == d0["issued_epoch"]
+    assert d0["peer_epoch"] < d0["epoch"]
