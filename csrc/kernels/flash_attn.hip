@@ -1939,6 +1939,90 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
 }
 
+// dK/dV v5: dK/dV v3 (4 waves x 32 keys, one wave per SIMD: its 312 registers rule out a second wave) with
+// the NBUF-deep counted-vmcnt ring of forward v7, so the next Q / dO tile's DMA has two tiles of cover.
+template <int D, bool CAUSAL, int NBUF>
+__global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_v5_kernel(AttnParams p) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
+  using Dma = DmaLane<D, true, 4>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];        // [stage][Q | dO]
+  __shared__ __attribute__((aligned(16))) float sstat[NBUF][2][TILE];        // [stage][-lse log2e | delta]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const BlockCoord bc = block_order(false, p.order);
+  const bool remap = CAUSAL || p.order == 1;
+  const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
+  const int kb = remap ? bc.t : (int)blockIdx.x;
+  const int group = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int kw = kb * 128 + w * 32, key = kw + c32;
+  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
+  const float sl2 = p.scale * LOG2E;
+
+  const int qstart = CAUSAL ? max(0, kb * 128 - off) / TILE * TILE : 0;
+  const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
+  const int total = qtiles * group;
+  Dma lq, lg;
+  lq.init(p.q_ss, w, lane);
+  lg.init(p.do_ss, w, lane);
+  auto issue = [&](int it, int st) {
+    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
+    const int hq = hk * group + hi;
+    bf16_t* base = smem + st * 2 * TE;
+    lq.issue(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w);
+    lg.issue(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w);
+    if (w == 0) dma_f32_row(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[st][0], lane);
+    if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[st][1], lane);
+  };
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t)
+    if (t < total) issue(t, t);
+
+  u16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (key < p.Sk) {
+      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
+      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
+    }
+  }
+  retire(kf);
+  retire(vf);
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+
+  // waves 0 / 1 also carry the lse / delta row DMA: one more instruction per tile in their count
+  int stage = 0;
+  for (int it = 0; it < total; ++it) {
+    if (w < 2) ring_wait<2 * Dma::NI + 1, NBUF>(it + 1 < total);
+    else ring_wait<2 * Dma::NI, NBUF>(it + 1 < total);
+    if (it + NBUF - 1 < total) issue(it + NBUF - 1, stage == 0 ? NBUF - 1 : stage - 1);
+    const int q0 = qstart + (it % qtiles) * TILE;
+    if (!(CAUSAL && q0 + TILE - 1 + off < kw)) {
+      const bf16_t* Qs = smem + stage * 2 * TE;
+      const float* Ls = sstat[stage][0];
+      const int tmask = CAUSAL ? key - off - q0 - 4 * h : -1;
+      const int tsq = p.Sq - q0 - 4 * h;
+      BwdKVTile<D, CAUSAL>::run(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask, tsq, h);
+    }
+    stage = stage + 1 == NBUF ? 0 : stage + 1;
+  }
+  acc_fence();
+  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
+  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
+}
+
 // dQ v4: dQ v3's per-wave tile on a 512-thread workgroup (8 waves x 32 query rows = 256 rows per staged
 // K/V tile, 384 instead of 192 FLOP per staged byte) with the NBUF-deep counted-vmcnt ring of forward v7.
 template <int D, bool CAUSAL, int NBUF>
@@ -2021,21 +2105,32 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
 
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
 int g_fwd_variant = -1, g_bwd_variant = -1, g_order = -1;
-int block_order_mode() {
-  if (g_order < 0) { const char* e = getenv("PDT_FA_ORDER"); g_order = e ? atoi(e) : 0; }
-  return g_order;
+// block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ): PDT_FA_ORDER / pdt_flash_attn_set_order, else
+// per shape -- the forward groups (b, h) blocks per XCD while one group's K/V (2 x Sk x D bf16) stays well
+// inside an XCD's 4 MB L2 with the other groups in flight (GPT-2 1.3B B96: 438 -> 620 TFLOP/s; at Sk 4096
+// grouping lost 3 %); the backward kernels measured neutral (dK/dV v3) or slower (dQ v4) grouped
+// (profiles/r3_attn_ab.jsonl)
+int block_order_mode(int Sk, int D) {
+  if (g_order < 0) {
+    const char* e = getenv("PDT_FA_ORDER");
+    if (e) g_order = atoi(e);
+  }
+  if (g_order >= 0) return g_order;
+  return (int64_t)Sk * D * 4 <= (1 << 20) ? 1 : 0;
 }
 int fwd_variant() {
   if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 5; }
   return g_fwd_variant;
 }
 int bwd_variant() {
-  if (g_bwd_variant < 0) { const char* e = getenv("PDT_FA_BWD"); g_bwd_variant = e ? atoi(e) : 3; }
+  if (g_bwd_variant < 0) { const char* e = getenv("PDT_FA_BWD"); g_bwd_variant = e ? atoi(e) : 9; }
   return g_bwd_variant;
 }
 
 template <int D>
-int launch_fwd(const AttnParams& p, int causal, int variant, hipStream_t st) {
+int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
+  AttnParams p = p0;                       // p.order bit 0: forward block order
+  p.order = p0.order & 1;
   dim3 grid((p.Sq + 127) / 128, p.H, p.B);
   if (variant == 2) {
     if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
@@ -2069,69 +2164,81 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
   const int variant = bwd_variant();
+  AttnParams kv = p, qp = p;               // per-kernel block order (p.order bit 1: dK/dV, bit 2: dQ)
+  kv.order = (p.order >> 1) & 1;
+  qp.order = (p.order >> 2) & 1;
   if (variant == 1) {
     if (causal) {
-      fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     }
   } else if (variant == 2) {
     if (causal) {
-      fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     }
   } else if (variant == 5 || variant == 6) {   // mixed generations (kernel bisection in tests)
     if (causal) {
-      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
-      else fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(p);
-      if (variant == 5) fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(p);
-      else fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+      else fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
+      if (variant == 5) fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(qp);
+      else fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     } else {
-      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
-      else fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(p);
-      if (variant == 5) fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(p);
-      else fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+      else fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
+      if (variant == 5) fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(qp);
+      else fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     }
   } else if (variant == 7) {   // v3 with the dQ kernel at one wave per SIMD (inline-asm DMA, no spills):
                                // 4-8 % slower than variant 3's two waves per SIMD (profiles/r2_attn_experiments.txt)
     if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(qp);
     }
   } else if (variant == 8 || variant == 9) {   // dK/dV v3 (one wave per SIMD) + dQ v4 (8 waves; 8: 3-deep ring)
     dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
     if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
-      if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(p);
-      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+      if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
+      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
-      if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(p);
-      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+      if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
+      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
+    }
+  } else if (variant == 10) {   // dK/dV v5 (3-deep ring) + dQ v4 (8 waves, 2-deep ring)
+    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
+    if (causal) {
+      fa_bwd_dkdv_v5_kernel<D, true, 3><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
+    } else {
+      fa_bwd_dkdv_v5_kernel<D, false, 3><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
     }
   } else if (variant == 3) {   // v3, one wave per SIMD for dK/dV (no spills)
     if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     }
   } else {                     // v3, two waves per SIMD for dK/dV
     if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 2><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, true, 2><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 2><<<gkv, NT, 0, st>>>(p);
-      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(p);
+      fa_bwd_dkdv_v3_kernel<D, false, 2><<<gkv, NT, 0, st>>>(kv);
+      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     }
   }
   return (int)hipGetLastError();
@@ -2151,7 +2258,7 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
   p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  p.order = block_order_mode();
+  p.order = block_order_mode(Sk, D);
   const int variant = fwd_variant();
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
@@ -2174,19 +2281,20 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.dk_sb = strides[18]; p.dk_ss = strides[19]; p.dk_sh = strides[20];
   p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  p.order = block_order_mode();
+  p.order = block_order_mode(Sk, D);
   return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
 }
 
-// workgroup -> block order (0 heavy-first, 1 XCD-grouped; < 0 keeps the current one); returns the order in effect
+// workgroup -> block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ: 0 heavy-first, 1 XCD-grouped);
+// -2 restores the per-shape default, -1 keeps the current setting; returns the setting (-1: per shape)
 PDT_API int pdt_flash_attn_set_order(int order) {
-  if (order >= 0) g_order = order;
-  return block_order_mode();
+  if (order >= 0 || order == -2) g_order = order == -2 ? -1 : order;
+  return g_order;
 }
 
-// select kernel variants (<= 0 keeps the current choice); returns fwd * 16 + bwd now in effect
+// select kernel variants (<= 0 keeps the current choice); returns fwd * 32 + bwd now in effect
 PDT_API int pdt_flash_attn_set_variant(int fwd, int bwd) {
   if (fwd > 0) g_fwd_variant = fwd;
   if (bwd > 0) g_bwd_variant = bwd;
-  return fwd_variant() * 16 + bwd_variant();
+  return fwd_variant() * 32 + bwd_variant();
 }

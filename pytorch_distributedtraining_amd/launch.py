@@ -50,14 +50,35 @@ def spawn(fn, nprocs: int, args=(), join: bool = True):
     return mp.spawn(_worker_entry, args=(fn, nprocs, tuple(args), port), nprocs=nprocs, join=join)
 
 
+def _shared_gpu_queues(nproc: int) -> str | None:
+    """GPU_MAX_HW_QUEUES for ranks that must share GPUs (more ranks than devices: one-GPU rehearsals).  With
+    HIP's default 4 hardware queues per process, 4 ranks on one GPU oversubscribe the queues the command
+    processor keeps mapped, and a rank's collective kernel can wait unscheduled while a peer's mesh kernel
+    spins for it: the world-4 GPT-2 rehearsal timed out at its 3rd collective with 4 queues per rank and ran
+    clean with 2 (profiles/r3_rehearsal_gpt2_fsdp_w4_q4_vs_q2.log): keep <= 8 queues per GPU.  One rank per
+    GPU keeps HIP's default.  device_count() does not initialise the GPU in this (launcher) process."""
+    try:
+        import torch
+        ndev = torch.cuda.device_count()
+    except Exception:
+        return None
+    if not 0 < ndev < nproc:
+        return None
+    per_dev = -(-nproc // ndev)
+    return str(max(1, 8 // per_dev))
+
+
 def _launch_once(cmd, nproc, port, restart, use_local_rank_arg, grace_s):
     procs = []
+    queues = None if "GPU_MAX_HW_QUEUES" in os.environ else _shared_gpu_queues(nproc)
     for r in range(nproc):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    TORCHELASTIC_RESTART_COUNT=str(restart))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this platform
+        if queues is not None:
+            env["GPU_MAX_HW_QUEUES"] = queues
         c = list(cmd)
         if use_local_rank_arg:
             c.append(f"--local-rank={r}")

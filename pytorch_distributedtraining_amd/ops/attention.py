@@ -176,16 +176,20 @@ def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None):
 
 def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:
     """Select the flash-attention kernel generation (0 keeps the current one).  fwd: 2 register-staged,
-    3 LDS-DMA ring, 4 VALU-lean LDS-DMA, 5 (default) v4 + deferred rescale + read prefetch + 16-B epilogue.  bwd: 1 baseline, 2 LDS-DMA, 3 (default) hand-pipelined
-    dK/dV (v3).  Returns the (fwd, bwd) pair now in effect."""
+    3 LDS-DMA ring, 4 VALU-lean LDS-DMA, 5 (default) v4 + deferred rescale + read prefetch + 16-B epilogue,
+    7 / 8 v5's tile on 8-wave 256-row workgroups (3- / 2-deep ring).  bwd: 1 baseline, 2 LDS-DMA, 3
+    hand-pipelined dK/dV + dQ (v3), 8 / 9 (default) dK/dV v3 + dQ v4 (8-wave 256-row workgroups, 3- / 2-deep
+    ring), 10 dK/dV v5 (3-deep ring) + dQ v4.  Returns the (fwd, bwd) pair now in effect."""
     r = _lib.require().pdt_flash_attn_set_variant(int(fwd), int(bwd))
-    return r // 16, r % 16
+    return r // 32, r % 32
 
 
 def set_block_order(order: int = -1) -> int:
-    """Workgroup -> block order of the flash-attention kernels: 0 heavy-first (longest causal blocks
-    dispatched first), 1 XCD-grouped (every (head, batch) on one XCD, its blocks back to back, so the K/V or
-    Q/dO re-reads hit that XCD's L2).  -1 keeps the current one.  Returns the order in effect."""
+    """Workgroup -> block order of the flash-attention kernels, a bitmask (bit 0 forward, bit 1 dK/dV, bit 2
+    dQ): a set bit groups every (head, batch)'s blocks on one XCD, back to back, so the K/V (or Q/dO) re-reads
+    hit that XCD's L2; a clear bit dispatches the longest causal blocks first across the chip.  -2 restores the
+    per-shape default (forward grouped while one head's K/V fits comfortably in L2), -1 keeps the current
+    setting.  Returns the setting in effect (-1 = per-shape default)."""
     return int(_lib.require().pdt_flash_attn_set_order(int(order)))
 
 

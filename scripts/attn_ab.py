@@ -26,7 +26,8 @@ fwds = [int(x) for x in a.fwd.split(",")]
 bwds = [int(x) for x in a.bwd.split(",")]
 orders = [int(x) for x in a.order.split(",")]
 SHAPES = [("gpt2-1.3b-b96", 96, 1024, 16, 16, 128, True), ("gpt2-1.3b", 32, 1024, 16, 16, 128, True), ("gpt2-1.3b-full", 32, 1024, 16, 16, 128, False),
-          ("llama3-8b", 8, 1024, 32, 8, 128, True), ("long-4k", 8, 4096, 16, 16, 128, True)]
+          ("llama3-8b", 8, 1024, 32, 8, 128, True), ("long-4k", 8, 4096, 16, 16, 128, True),
+          ("gpt2-124m", 64, 1024, 12, 12, 64, True)]
 
 
 def timed(fn, iters):

@@ -173,3 +173,19 @@ def test_window_mask_label_cache_is_identity_checked():
         lb = _mask_labels(b)
         assert int(lb[0, 63]) == 40 and int(lb[0, 39]) == 0, (ptr == b.data_ptr())
         del b
+
+
+def test_launcher_limits_hw_queues_only_when_ranks_share_gpus(monkeypatch):
+    """More ranks than GPUs (one-GPU rehearsals): <= 8 HIP hardware queues per GPU in total, so no rank's
+    collective kernel waits unmapped behind peers' spinning mesh kernels; one rank per GPU keeps the default."""
+    import torch
+    from pytorch_distributedtraining_amd import launch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert launch._shared_gpu_queues(1) is None
+    assert launch._shared_gpu_queues(2) == "4"
+    assert launch._shared_gpu_queues(4) == "2"
+    assert launch._shared_gpu_queues(8) == "1"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert launch._shared_gpu_queues(8) is None
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert launch._shared_gpu_queues(4) is None

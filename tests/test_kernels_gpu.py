@@ -139,19 +139,23 @@ def _attn_ref(q, k, v, causal, scale):
     return (s.softmax(-1) @ vt).transpose(1, 2)
 
 
-@pytest.mark.parametrize("variant", [(4, 2), (4, 3), (5, 3)])
+# (fwd, bwd, block-order bitmask): the round-2 generations, the defaults (fwd 5 + bwd 9, order per shape: -2),
+# the 8-wave kernels (fwd 7 / 8, dQ v4 in bwd 8-10), the 3-deep-ring dK/dV (bwd 10), every kernel XCD-grouped (7)
+@pytest.mark.parametrize("variant", [(4, 2, 0), (4, 3, 0), (5, 3, 0), (5, 9, -2), (7, 8, 0), (8, 10, 0), (5, 9, 7)])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,S,H,Hkv", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 1024, 2, 1), (1, 77, 2, 2)])
 def test_flash_attn(D, causal, B, S, H, Hkv, variant):
     from pytorch_distributedtraining_amd.ops import flash_attn
-    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    from pytorch_distributedtraining_amd.ops.attention import set_block_order, set_kernel_variant
     prev = set_kernel_variant()
-    set_kernel_variant(*variant)
+    set_kernel_variant(variant[0], variant[1])
+    set_block_order(variant[2])
     try:
         _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv)
     finally:
         set_kernel_variant(*prev)
+        set_block_order(-2)
 
 
 def _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv):
@@ -207,16 +211,17 @@ def _check_flash_attn_tensors(flash_attn, q, k, v, causal):
     assert rel_err(v.grad, vr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("fwd", [4, 5])
-def test_flash_attn_full_grid_rows(fwd):
+@pytest.mark.parametrize("fwd,bwd,order", [(4, 3, 0), (5, 3, 0), (5, 9, -2), (8, 10, 0), (5, 9, 7)])
+def test_flash_attn_full_grid_rows(fwd, bwd, order):
     """The flagship shape (GPT-2 1.3B: B32 S1024 H16 D128 causal) keeps thousands of workgroups in flight,
     the load under which an LDS-DMA tile read before its DMA landed (a missing vmcnt wait before the ring
     barrier) corrupted the last query block's rows while every small-grid test passed.  Check every row of
     the first and last batch element, forward and all three gradients, against fp32."""
     from pytorch_distributedtraining_amd.ops import flash_attn
-    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
+    from pytorch_distributedtraining_amd.ops.attention import set_block_order, set_kernel_variant
     prev = set_kernel_variant()
-    set_kernel_variant(fwd=fwd)
+    set_kernel_variant(fwd=fwd, bwd=bwd)
+    set_block_order(order)
     try:
         B, S, H, D = 32, 1024, 16, 128
         q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
@@ -235,6 +240,7 @@ def test_flash_attn_full_grid_rows(fwd):
                 assert float(row_err.max()) < tol, (b, float(row_err.max()), int(row_err.argmax()))
     finally:
         set_kernel_variant(*prev)
+        set_block_order(-2)
 
 
 def test_flash_attn_qkvpacked_matches_unpacked():
