@@ -551,21 +551,27 @@ __device__ __forceinline__ BlockCoord heavy_first(bool heavy_is_high) {
 }
 
 // XCD-grouped order (p.order == 1): workgroups are dealt to the 8 XCDs round-robin in flattened-id order
-// (lin % 8), each XCD with its own L2.  heavy_first() spreads the blocks of one (head, batch) -- which all
-// stream the SAME K/V (forward, dQ) or Q/dO (dK/dV) tiles -- over every XCD and over the whole launch, so
-// each re-read comes from HBM.  Here every (head, batch) group lives on one XCD (group g -> XCD g % 8) and
-// its blocks run back to back there, heaviest first, so the re-reads hit that XCD's L2.
-__device__ __forceinline__ BlockCoord block_order(bool heavy_is_high, int order) {
-  const int nt = gridDim.x, nh = gridDim.y, G = nh * gridDim.z;
-  if (order != 1 || (G & 7)) return heavy_first(heavy_is_high);
-  const int lin = blockIdx.x + nt * (blockIdx.y + nh * blockIdx.z);
-  const int j = lin >> 3, gi = j / nt, rank = j - gi * nt;
-  const int g = gi * 8 + (lin & 7);
+// (lin % 8), each XCD with its own L2.  heavy_first() spreads the blocks that stream the SAME K/V tiles
+// (forward, dQ: every query head of one (batch, kv head) unit) or Q/dO tiles (dK/dV) over every XCD and over
+// the whole launch, so each re-read comes from HBM.  Here every unit lives on one XCD (unit u -> XCD u % 8)
+// and its blocks -- all its query heads', heaviest first -- run back to back there, so the re-reads hit that
+// XCD's L2.  grp = query heads per kv head for the query-side grids (1 for dK/dV's kv-head grid).
+__device__ __forceinline__ BlockCoord grouped_coord(int lin, int nt, int nh, int grp, bool heavy_is_high) {
+  const int per = grp * nt, j = lin >> 3, ui = j / per, r = j - ui * per;
+  const int u = ui * 8 + (lin & 7), rank = r / grp, hi = r - rank * grp, nkv = nh / grp;
   BlockCoord c;
-  c.h = g % nh;
-  c.b = g / nh;
+  c.b = u / nkv;
+  c.h = (u - c.b * nkv) * grp + hi;
   c.t = heavy_is_high ? nt - 1 - rank : rank;
   return c;
+}
+__device__ __forceinline__ bool grouped_ok(int order, int nh, int nb, int grp) {
+  return order == 1 && !(((nh / grp) * nb) & 7);
+}
+__device__ __forceinline__ BlockCoord block_order(bool heavy_is_high, int order, int grp) {
+  if (!grouped_ok(order, gridDim.y, gridDim.z, grp)) return heavy_first(heavy_is_high);
+  return grouped_coord(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y, grp,
+                       heavy_is_high);
 }
 
 template <int D, bool CAUSAL>
@@ -874,7 +880,7 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(true, p.order);
+  const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
   const int qb = remap ? bc.t : (int)blockIdx.x;
@@ -991,7 +997,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];   // [stage][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(true, p.order);
+  const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
   const int qb = remap ? bc.t : (int)blockIdx.x;
@@ -1069,6 +1075,145 @@ __global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
   store_row16<DT>(p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss, o, inv, h, qrow < p.Sq);
   if (qrow < p.Sq && h == 0)
     p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward v9 = v5's per-wave tile in a PERSISTENT grid: 2 workgroups per CU, each walks a static list of
+// 128-row blocks (block_of(L): the same heavy-first / XCD-grouped order as the one-block-per-workgroup
+// kernels, L = workgroup id + k * grid), and the block seams are pipelined: the next block's first K/V tile
+// is DMA'd into the free ring stage during the current block's last tile, and its Q rows are loaded into
+// the (then dead) Q registers before the current block's O epilogue, so a short causal block (2-16 tiles of
+// 64 keys at S = 1024) no longer pays a cold prologue.  grid % 8 == 0 keeps each workgroup on one XCD for
+// every block it takes, so XCD grouping still holds.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ BlockCoord block_of(int L, int nt, int nh, int nb, int grp, bool heavy_is_high, int order) {
+  if (grouped_ok(order, nh, nb, grp)) return grouped_coord(L, nt, nh, grp, heavy_is_high);
+  const int G = nh * nb, rank = L / G, g = L - rank * G;
+  BlockCoord c;
+  c.h = g % nh;
+  c.b = g / nh;
+  c.t = heavy_is_high ? nt - 1 - rank : rank;
+  return c;
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 2) void fa_fwd_v9_kernel(AttnParams p) {
+  using K = FwdV5<D, CAUSAL>;
+  constexpr int KS = K::KS, DT = K::DT, TE = K::TE;
+  using Dma = DmaLane<D, true, 4>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [stage 0/1][K | V]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int nt = (p.Sq + 127) / 128, G = p.H * p.B, total = nt * G;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * LOG2E;
+  const int grp = p.H / p.Hkv;
+  Dma lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
+  int koff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int voff[DT][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int r1 = 4 * (g >> 1) + q;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
+      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
+    }
+  }
+
+  struct Blk {
+    const bf16_t *Q, *K, *V;
+    int b, hq, q0, ntiles;
+  };
+  auto blk = [&](int L) {
+    const BlockCoord c = block_of(L, nt, p.H, p.B, p.H / p.Hkv, true, p.order);
+    Blk r;
+    r.b = c.b;
+    r.hq = c.h;
+    r.q0 = c.t * 128;
+    const int hk = c.h / grp;
+    r.Q = p.q + c.b * p.q_sb + c.h * p.q_sh;
+    r.K = p.k + c.b * p.k_sb + hk * p.k_sh;
+    r.V = p.v + c.b * p.v_sb + hk * p.v_sh;
+    int kend = p.Sk;
+    if (CAUSAL) kend = min(p.Sk, r.q0 + 128 + off);
+    r.ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+    return r;
+  };
+  auto load_q = [&](const Blk& B, u16x8 (&qf)[KS]) {
+    const int qrow = B.q0 + w * 32 + c32;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(B.Q + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+      else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
+      }
+    }
+  };
+
+  int L = blockIdx.x;
+  if (L >= total) return;
+  Blk cur = blk(L);
+  int stage = 0;
+  if (cur.ntiles > 0) {
+    lk.issue(cur.K, p.k_ss, 0, p.Sk, smem, w);
+    lv.issue(cur.V, p.v_ss, 0, p.Sk, smem + TE, w);
+  }
+  u16x8 qf[KS];
+  load_q(cur, qf);
+  retire(qf);
+  while (true) {
+    const int Ln = L + (int)gridDim.x;
+    const bool more = Ln < total;
+    Blk nxt = cur;
+    if (more) nxt = blk(Ln);
+    const int qw = cur.q0 + w * 32, qrow = qw + c32;
+    const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+    f32x16 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+    float m = -INFINITY, l = 0.f;
+    for (int t = 0; t < cur.ntiles; ++t) {
+      dma_barrier();   // tile t landed (and, at t = 0, the Q rows); the other stage is free
+      bf16_t* nb = smem + (stage ^ 1) * 2 * TE;
+      if (t + 1 < cur.ntiles) {
+        lk.issue(cur.K, p.k_ss, (t + 1) * TILE, p.Sk, nb, w);
+        lv.issue(cur.V, p.v_ss, (t + 1) * TILE, p.Sk, nb + TE, w);
+      } else if (more && nxt.ntiles > 0) {   // block seam: the next block's first tile
+        lk.issue(nxt.K, p.k_ss, 0, p.Sk, nb, w);
+        lv.issue(nxt.V, p.v_ss, 0, p.Sk, nb + TE, w);
+      }
+      const int k0 = t * TILE;
+      if (!(CAUSAL && k0 > qw + 31 + off)) {
+        const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+        K::tile(smem + stage * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
+      }
+      stage ^= 1;
+    }
+    if (more) load_q(nxt, qf);   // in flight under this block's epilogue
+    const float lt = l + __shfl_xor(l, 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    store_row16<DT>(p.o + cur.b * p.o_sb + cur.hq * p.o_sh + (int64_t)qrow * p.o_ss, o, inv, h, qrow < p.Sq);
+    if (qrow < p.Sq && h == 0)
+      p.lse[((int64_t)cur.b * p.H + cur.hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
+    if (!more) break;
+    // hipcc's wait for the Q loads lands here, behind the epilogue stores (it cannot see the inline-asm DMA,
+    // so a wait at the first use inside the tile loop would also drain the next tile's prefetch)
+    retire(qf);
+    if (cur.ntiles == 0 && nxt.ntiles > 0) {   // nothing was prefetched at the seam (degenerate Sk)
+      lk.issue(nxt.K, p.k_ss, 0, p.Sk, smem + stage * 2 * TE, w);
+      lv.issue(nxt.V, p.v_ss, 0, p.Sk, smem + stage * 2 * TE + TE, w);
+    }
+    L = Ln;
+    cur = nxt;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1719,7 +1864,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];    // [buf][lse | delta]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(false, p.order);   // causal: low key blocks see the most queries
+  const BlockCoord bc = block_order(false, p.order, 1);   // causal: low key blocks see the most queries
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
   const int kb = remap ? bc.t : (int)blockIdx.x;
@@ -1867,7 +2012,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(true, p.order);
+  const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
   const int qb = remap ? bc.t : (int)blockIdx.x;
@@ -1949,7 +2094,7 @@ __global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_v5_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float sstat[NBUF][2][TILE];        // [stage][-lse log2e | delta]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(false, p.order);
+  const BlockCoord bc = block_order(false, p.order, 1);
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
   const int kb = remap ? bc.t : (int)blockIdx.x;
@@ -2032,7 +2177,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];   // [stage][K | V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(true, p.order);
+  const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
   const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
   const int qb = remap ? bc.t : (int)blockIdx.x;
@@ -2105,6 +2250,15 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
 
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
 int g_fwd_variant = -1, g_bwd_variant = -1, g_order = -1;
+int num_cus() {   // persistent grids: 2 workgroups per CU (a multiple of 8: one XCD per workgroup for good)
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0, v = 0;
+    n = (hipGetDevice(&dev) == hipSuccess &&
+         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n;
+}
 // block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ): PDT_FA_ORDER / pdt_flash_attn_set_order, else
 // per shape -- the forward groups (b, h) blocks per XCD while one group's K/V (2 x Sk x D bf16) stays well
 // inside an XCD's 4 MB L2 with the other groups in flight (GPT-2 1.3B B96: 438 -> 620 TFLOP/s; at Sk 4096
@@ -2116,15 +2270,19 @@ int block_order_mode(int Sk, int D) {
     if (e) g_order = atoi(e);
   }
   if (g_order >= 0) return g_order;
-  return (int64_t)Sk * D * 4 <= (1 << 20) ? 1 : 0;
+  return (D == 128 && (int64_t)Sk * D * 4 <= (1 << 20)) ? 1 : 0;
 }
+// g_*_variant: -1 = not read yet (PDT_FA_FWD / PDT_FA_BWD env), 0 = the default, > 0 = pinned
 int fwd_variant() {
-  if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 5; }
-  return g_fwd_variant;
+  if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 0; }
+  return g_fwd_variant > 0 ? g_fwd_variant : 5;
 }
-int bwd_variant() {
-  if (g_bwd_variant < 0) { const char* e = getenv("PDT_FA_BWD"); g_bwd_variant = e ? atoi(e) : 9; }
-  return g_bwd_variant;
+// backward default: dQ v4 (variant 9) at head dim 128 (B96 S1024: 2.77 -> 2.58 ms), v3 at 64 where the 8-wave
+// dQ measured 1-3 % slower (profiles/r3_attn_ab2_bwd_orders.jsonl)
+int bwd_variant(int D = 128) {
+  if (g_bwd_variant < 0) { const char* e = getenv("PDT_FA_BWD"); g_bwd_variant = e ? atoi(e) : 0; }
+  if (g_bwd_variant > 0) return g_bwd_variant;
+  return D == 128 ? 9 : 3;
 }
 
 template <int D>
@@ -2141,6 +2299,12 @@ int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
   } else if (variant == 5) {
     if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else if (variant == 9) {   // persistent v5: 2 workgroups per CU walking the block list
+    const int total = ((p.Sq + 127) / 128) * p.H * p.B;
+    int g9 = 2 * num_cus();
+    g9 = total < g9 ? total : g9;
+    if (causal) fa_fwd_v9_kernel<D, true><<<g9, NT, 0, st>>>(p);
+    else fa_fwd_v9_kernel<D, false><<<g9, NT, 0, st>>>(p);
   } else if (variant == 7 || variant == 8) {   // 8 waves x 32 rows; 7: 3-deep ring, 8: 2-deep
     dim3 g8((p.Sq + 255) / 256, p.H, p.B);
     if (variant == 7) {
@@ -2163,7 +2327,7 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
-  const int variant = bwd_variant();
+  const int variant = bwd_variant(D);
   AttnParams kv = p, qp = p;               // per-kernel block order (p.order bit 1: dK/dV, bit 2: dQ)
   kv.order = (p.order >> 1) & 1;
   qp.order = (p.order >> 2) & 1;
@@ -2292,9 +2456,12 @@ PDT_API int pdt_flash_attn_set_order(int order) {
   return g_order;
 }
 
-// select kernel variants (<= 0 keeps the current choice); returns fwd * 32 + bwd now in effect
+// select kernel variants (0 keeps the current choice, -1 restores the default); returns fwd * 32 + bwd of the
+// pinned choices (0 = the default: forward v5, backward 9 at head dim 128 / 3 at 64)
 PDT_API int pdt_flash_attn_set_variant(int fwd, int bwd) {
-  if (fwd > 0) g_fwd_variant = fwd;
-  if (bwd > 0) g_bwd_variant = bwd;
-  return fwd_variant() * 32 + bwd_variant();
+  (void)fwd_variant();
+  (void)bwd_variant();                       // read the env once before overriding
+  if (fwd > 0 || fwd == -1) g_fwd_variant = fwd > 0 ? fwd : 0;
+  if (bwd > 0 || bwd == -1) g_bwd_variant = bwd > 0 ? bwd : 0;
+  return g_fwd_variant * 32 + g_bwd_variant;
 }

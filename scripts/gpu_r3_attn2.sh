@@ -8,7 +8,7 @@ mkdir -p $OUT
 timeout -k 10 420 python -u scripts/attn_ab.py --fwd 5 --bwd 3,9,10 --order=-2,0,2,3 --rounds 3 \
   > $OUT/r3_attn_ab2.jsonl 2> $OUT/r3_attn_ab2.err
 rc=$?; echo "attn_ab rc=$rc"; tail -n 3 $OUT/r3_attn_ab2.err; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "flash_attn" -x -q --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "flash_attn or hand_gemm_nt" -x -q --timeout 200 --timeout-method thread \
   -p no:cacheprovider > $OUT/r3_pytest_attn.log 2>&1
 rc=$?; echo "attn tests rc=$rc"; tail -n 3 $OUT/r3_pytest_attn.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py > $OUT/r3_bench_n1_attn.json 2> $OUT/r3_bench_n1_attn.err

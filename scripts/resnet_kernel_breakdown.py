@@ -12,7 +12,10 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+# the MIOpen find/perf database recorded on MI355X (as bench.py): without it a fresh box spends minutes in find
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(ROOT, "tuning", "miopen"))
 import torch  # noqa: E402
 
 CATS = [  # (category, substrings of the lower-cased kernel name), first match wins
@@ -65,9 +68,10 @@ def main():
         opt.step(grad_scale=coef)
         opt.zero_grad(set_to_none=True)
 
-    for _ in range(4):                       # MIOpen find + allocator warm-up
+    for i in range(4):                       # MIOpen find + allocator warm-up
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        print(json.dumps({"warmup_step": i}), flush=True)
     n = 10
     t0 = time.perf_counter()
     for _ in range(n):

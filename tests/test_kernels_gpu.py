@@ -140,22 +140,22 @@ def _attn_ref(q, k, v, causal, scale):
 
 
 # (fwd, bwd, block-order bitmask): the round-2 generations, the defaults (fwd 5 + bwd 9, order per shape: -2),
-# the 8-wave kernels (fwd 7 / 8, dQ v4 in bwd 8-10), the 3-deep-ring dK/dV (bwd 10), every kernel XCD-grouped (7)
-@pytest.mark.parametrize("variant", [(4, 2, 0), (4, 3, 0), (5, 3, 0), (5, 9, -2), (7, 8, 0), (8, 10, 0), (5, 9, 7)])
+# the 8-wave kernels (fwd 7 / 8, dQ v4 in bwd 8-10), the 3-deep-ring dK/dV (bwd 10), every kernel XCD-grouped (7),
+# the persistent forward (fwd 9: block seams pipelined, both orders)
+@pytest.mark.parametrize("variant", [(4, 2, 0), (4, 3, 0), (5, 3, 0), (5, 9, -2), (7, 8, 0), (8, 10, 0), (5, 9, 7),
+                                     (9, 9, -2), (9, 9, 0)])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,S,H,Hkv", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 1024, 2, 1), (1, 77, 2, 2)])
 def test_flash_attn(D, causal, B, S, H, Hkv, variant):
     from pytorch_distributedtraining_amd.ops import flash_attn
-    from pytorch_distributedtraining_amd.ops.attention import set_block_order, set_kernel_variant
-    prev = set_kernel_variant()
+    from pytorch_distributedtraining_amd.ops.attention import reset_kernel_variant, set_block_order, set_kernel_variant
     set_kernel_variant(variant[0], variant[1])
     set_block_order(variant[2])
     try:
         _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv)
     finally:
-        set_kernel_variant(*prev)
-        set_block_order(-2)
+        reset_kernel_variant()
 
 
 def _check_flash_attn(flash_attn, D, causal, B, S, H, Hkv):
@@ -181,8 +181,7 @@ def test_flash_attn_forced_rescale(fwd, causal):
     (cdna_hip_programming.md §5.4 rule 26): spike a few keys against chosen query rows so the running max
     jumps ~9.5 (log2 units, past the 8 threshold) at a late tile, and check O and the LSE-dependent gradients against fp32."""
     from pytorch_distributedtraining_amd.ops import flash_attn
-    from pytorch_distributedtraining_amd.ops.attention import set_kernel_variant
-    prev = set_kernel_variant()
+    from pytorch_distributedtraining_amd.ops.attention import reset_kernel_variant, set_kernel_variant
     set_kernel_variant(fwd=fwd)
     try:
         torch.manual_seed(0)
@@ -195,7 +194,7 @@ def test_flash_attn_forced_rescale(fwd, causal):
         q, k, v = (t.to(torch.bfloat16).requires_grad_() for t in (q, k, v))
         _check_flash_attn_tensors(flash_attn, q, k, v, causal)
     finally:
-        set_kernel_variant(*prev)
+        reset_kernel_variant()
 
 
 def _check_flash_attn_tensors(flash_attn, q, k, v, causal):
@@ -211,15 +210,14 @@ def _check_flash_attn_tensors(flash_attn, q, k, v, causal):
     assert rel_err(v.grad, vr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("fwd,bwd,order", [(4, 3, 0), (5, 3, 0), (5, 9, -2), (8, 10, 0), (5, 9, 7)])
+@pytest.mark.parametrize("fwd,bwd,order", [(4, 3, 0), (5, 3, 0), (5, 9, -2), (8, 10, 0), (5, 9, 7), (9, 9, -2)])
 def test_flash_attn_full_grid_rows(fwd, bwd, order):
     """The flagship shape (GPT-2 1.3B: B32 S1024 H16 D128 causal) keeps thousands of workgroups in flight,
     the load under which an LDS-DMA tile read before its DMA landed (a missing vmcnt wait before the ring
     barrier) corrupted the last query block's rows while every small-grid test passed.  Check every row of
     the first and last batch element, forward and all three gradients, against fp32."""
     from pytorch_distributedtraining_amd.ops import flash_attn
-    from pytorch_distributedtraining_amd.ops.attention import set_block_order, set_kernel_variant
-    prev = set_kernel_variant()
+    from pytorch_distributedtraining_amd.ops.attention import reset_kernel_variant, set_block_order, set_kernel_variant
     set_kernel_variant(fwd=fwd, bwd=bwd)
     set_block_order(order)
     try:
@@ -239,8 +237,7 @@ def test_flash_attn_full_grid_rows(fwd, bwd, order):
                 row_err = (got.float() - ref).norm(dim=-1) / torch.maximum(rn, rn.mean())   # [1, S, H]
                 assert float(row_err.max()) < tol, (b, float(row_err.max()), int(row_err.argmax()))
     finally:
-        set_kernel_variant(*prev)
-        set_block_order(-2)
+        reset_kernel_variant()
 
 
 def test_flash_attn_qkvpacked_matches_unpacked():
@@ -642,6 +639,51 @@ def test_hip_wgrad_full_grid_production_shapes(N, K, splits):
     err = (got - ref).abs()
     bad = err > 0.008 * ref.abs() + 0.01 * rms       # bf16 output rounding + fp32 accumulation order
     assert int(bad.sum()) == 0, (int(bad.sum()), float(err.max()), rms)
+
+
+def _gelu_tanh(x):
+    return torch.nn.functional.gelu(x, approximate="tanh")
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 1536), (4096, 768, 256), (512, 2048, 4096)])
+def test_hand_gemm_nt_epilogues(M, N, K):
+    """Hand MFMA GEMM, NT layout (y = a b^T, a [M, K], b [N, K]): plain, bias, bias+GELU (pre-activation kept)
+    and the backward dGELU epilogue (g = dy b * GELU'(h) with the bias gradient sum_rows g) vs fp32 torch."""
+    from pytorch_distributedtraining_amd.ops import gemm as G
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    ref = a.float() @ b.float().t()
+    assert rel_err(G.gemm_nt(a, b), ref) < 4e-3
+    assert rel_err(G.gemm_nt(a, b, bias), ref + bias.float()) < 4e-3
+    y, pre = G.gemm_nt_gelu(a, b, bias)
+    assert rel_err(pre, ref + bias.float()) < 4e-3
+    assert rel_err(y, _gelu_tanh(ref + bias.float())) < 6e-3
+    h = torch.randn(M, N, device=DEV).bfloat16()
+    g, db = G.gemm_nt_dgelu(a, b, h)
+    hr = h.float().requires_grad_()
+    _gelu_tanh(hr).backward(ref)
+    assert rel_err(g, hr.grad) < 6e-3
+    assert rel_err(db, hr.grad.sum(0)) < 6e-3
+
+
+def test_hand_gemm_nt_gelu_full_grid_production_shape():
+    """GPT-2 1.3B c_fc at 96 x 1024 tokens (98,304 x 8,192 x 2,048, the full grid of 256 x 256 tiles): every
+    element of the GELU output and the kept pre-activation against fp32."""
+    from pytorch_distributedtraining_amd.ops import gemm as G
+    M, N, K = 96 * 1024, 8192, 2048
+    torch.manual_seed(7)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    y, pre = G.gemm_nt_gelu(a, b, bias)
+    ref = torch.addmm(bias.float(), a.float(), b.float().t())
+    for got, want in ((pre, ref), (y, _gelu_tanh(ref))):
+        rms = float(want.square().mean().sqrt())
+        bad = (got.float() - want).abs() > 0.008 * want.abs() + 0.01 * rms
+        assert int(bad.sum()) == 0, int(bad.sum())
+        del want
 
 
 @pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60), (16384, 768, 768), (16384, 768, 3072),
