@@ -33,22 +33,43 @@ struct Tile {
   }
 };
 
-// MODE 0: (x, x^2)  MODE 1: (dy', dy' * xhat), dy' = dy * (y > 0) if RELU
-template <int MODE, bool RELU>
+// MODE 0: (x, x^2)  MODE 1: (dy', dy' * xhat), dy' = dy * relu'(.) per MASK:
+//   MASK 0: no ReLU;  1: mask = (y > 0) from the saved output (needed after a residual add);
+//   2: mask = (x * scale + shift > 0) recomputed from x with the forward's own coefficients (BN -> ReLU with
+//      no residual: y is then never read -- one bf16 stream less in both backward passes)
+template <int MASK>
+__device__ __forceinline__ void relu_mask(float (&g)[8], const float (&xv)[8], const float* yv, const float (&sc)[8],
+                                          const float (&sh)[8]) {
+  if constexpr (MASK == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+  } else if constexpr (MASK == 2) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = xv[k] * sc[k] + sh[k] > 0.f ? g[k] : 0.f;
+  }
+}
+
+template <int MODE, int MASK>
 __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                        const bf16_t* __restrict__ y, const float* __restrict__ mean,
-                                                       const float* __restrict__ invstd, int64_t R, int C,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ scsh, int64_t R, int C,
                                                        float* __restrict__ part) {
+  constexpr bool RELU = MASK == 1;   // y is read
   __shared__ __attribute__((aligned(16))) float sa[NT * 8];
   __shared__ __attribute__((aligned(16))) float sb[NT * 8];
   const Tile t(C);
-  float a[8], b[8], mu[8], is[8];
+  float a[8], b[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; is[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; is[k] = 0.f; sc[k] = 0.f; sh[k] = 0.f; }
   if (t.act) {
     if (MODE == 1) {
       Vec8<float>::load(mean + t.cg * 8, mu);
       Vec8<float>::load(invstd + t.cg * 8, is);
+    }
+    if (MASK == 2) {
+      Vec8<float>::load(scsh + t.cg * 8, sc);
+      Vec8<float>::load(scsh + C + t.cg * 8, sh);
     }
     const int64_t stride = (int64_t)gridDim.x * t.rpb;
     int64_t r = (int64_t)blockIdx.x * t.rpb + t.rl;
@@ -67,14 +88,10 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
 #pragma unroll
           for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
         } else {
-          float g[8];
+          float g[8], yv[8];
           Vec8<bf16_t>::unpack(u ? g1 : g0, g);
-          if (RELU) {
-            float yv[8];
-            Vec8<bf16_t>::unpack(u ? y1 : y0, yv);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-          }
+          if (RELU) Vec8<bf16_t>::unpack(u ? y1 : y0, yv);
+          relu_mask<MASK>(g, xv, yv, sc, sh);
 #pragma unroll
           for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
         }
@@ -88,14 +105,10 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
       } else {
-        float g[8];
+        float g[8], yv[8];
         Vec8<bf16_t>::load(dy + off, g);
-        if (RELU) {
-          float yv[8];
-          Vec8<bf16_t>::load(y + off, yv);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-        }
+        if (RELU) Vec8<bf16_t>::load(y + off, yv);
+        relu_mask<MASK>(g, xv, yv, sc, sh);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
       }
@@ -113,30 +126,37 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
   }
 }
 
-// [P, 2C] fp32 partials -> out[2C] fp64.  Workgroup = 64 outputs x 4 waves; each wave sums a quarter of
-// the P partial rows (lanes read consecutive outputs: coalesced), folded through LDS.
+// [P, 2C] fp32 partials -> out[2C] fp64.  Workgroup = 64 outputs x 16 waves; each wave sums a sixteenth of
+// the P partial rows (lanes read consecutive outputs: coalesced), 8 loads in flight per lane, folded through
+// LDS.  (4 waves and 4 loads left the ~100 combines of a ResNet-50 step latency-bound at ~11 us each: the
+// narrow layers have only 2-4 workgroups here.)
 //   count > 0: out[2C] = count (forward);  dw / db (nullable): fp32 copies of the two halves (backward)
-__global__ __launch_bounds__(256) void bn_combine_kernel(const float* __restrict__ part, int P, int C, double count,
-                                                         double* __restrict__ out, float* __restrict__ dw,
-                                                         float* __restrict__ db) {
-  __shared__ double red[4][64];
+constexpr int CW = 16;
+__global__ __launch_bounds__(64 * CW) void bn_combine_kernel(const float* __restrict__ part, int P, int C, double count,
+                                                             double* __restrict__ out, float* __restrict__ dw,
+                                                             float* __restrict__ db) {
+  __shared__ double red[CW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   double s = 0.0;
   if (i < 2 * C) {
-    const int per = (P + 3) / 4, j0 = wv * per, j1 = min(P, j0 + per);
+    const int per = (P + CW - 1) / CW, j0 = wv * per, j1 = min(P, j0 + per);
     int j = j0;
-    for (; j + 4 <= j1; j += 4) {
-      const float a0 = part[(int64_t)j * 2 * C + i], a1 = part[(int64_t)(j + 1) * 2 * C + i];
-      const float a2 = part[(int64_t)(j + 2) * 2 * C + i], a3 = part[(int64_t)(j + 3) * 2 * C + i];
-      s += (double)a0 + (double)a1 + (double)a2 + (double)a3;
+    for (; j + 8 <= j1; j += 8) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = part[(int64_t)(j + u) * 2 * C + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)a[u];
     }
     for (; j < j1; ++j) s += (double)part[(int64_t)j * 2 * C + i];
   }
   red[wv][lane] = s;
   __syncthreads();
   if (wv == 0 && i < 2 * C) {
-    const double t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < CW; ++q) t += red[q][lane];
     out[i] = t;
     if (i < C) { if (db) db[i] = (float)t; }
     else if (dw) dw[i - C] = (float)t;
@@ -210,18 +230,24 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__
   }
 }
 
-// dx = (dy' - s1 / M - xhat * s2 / M) * invstd * w ; dres = dy'
-template <bool RELU, bool DRES>
+// dx = (dy' - s1 / M - xhat * s2 / M) * invstd * w ; dres = dy'   (MASK as bn_reduce_kernel)
+template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, const float* __restrict__ w,
+                                                          const float* __restrict__ scsh,
                                                           const double* __restrict__ sums, const double* __restrict__ count,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t R,
                                                           int C) {
+  constexpr bool RELU = MASK == 1;
   const Tile t(C);
   if (!t.act) return;
   const double inv_m = 1.0 / count[0];
-  float mu[8], is[8], k1[8], k2[8], k3[8];
+  float mu[8], is[8], k1[8], k2[8], k3[8], sc[8], sh[8];
+  if (MASK == 2) {
+    Vec8<float>::load(scsh + t.cg * 8, sc);
+    Vec8<float>::load(scsh + C + t.cg * 8, sh);
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = t.cg * 8 + k;
@@ -236,15 +262,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
 #pragma unroll 2
   for (int64_t r = (int64_t)blockIdx.x * t.rpb + t.rl; r < R; r += stride) {
     const int64_t off = r * C + t.cg * 8;
-    float g[8], xv[8], o[8];
+    float g[8], xv[8], o[8], yv[8];
     Vec8<bf16_t>::load(dy + off, g);
     Vec8<bf16_t>::load(x + off, xv);
-    if (RELU) {
-      float yv[8];
-      Vec8<bf16_t>::load(y + off, yv);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-    }
+    if (RELU) Vec8<bf16_t>::load(y + off, yv);
+    relu_mask<MASK>(g, xv, yv, sc, sh);
     if (DRES) Vec8<bf16_t>::store(dres + off, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = g[k] * k1[k] - k2[k] - (xv[k] - mu[k]) * is[k] * k3[k];
@@ -278,8 +300,8 @@ PDT_API int pdt_bn_ok(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 : 
 PDT_API int pdt_bn_stats(const void* x, int64_t R, int C, float* ws, double* out, hipStream_t st) {
   if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
   const int P = reduce_grid(R, C);
-  bn_reduce_kernel<0, false><<<P, NT, 0, st>>>((const bf16_t*)x, nullptr, nullptr, nullptr, nullptr, R, C, ws);
-  bn_combine_kernel<<<(2 * C + 63) / 64, 256, 0, st>>>(ws, P, C, (double)R, out, nullptr, nullptr);
+  bn_reduce_kernel<0, 0><<<P, NT, 0, st>>>((const bf16_t*)x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, ws);
+  bn_combine_kernel<<<(2 * C + 63) / 64, 64 * CW, 0, st>>>(ws, P, C, (double)R, out, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -311,30 +333,34 @@ PDT_API int pdt_bn_apply(const void* x, const void* res, const float* scale, con
 }
 
 // backward sums: out[0:2C] = (sum dy', sum dy' * xhat) fp64 (local; caller all-reduces for SyncBN);
-// dw / db (fp32, nullable) receive the local parameter gradients
+// dw / db (fp32, nullable) receive the local parameter gradients.  relu: 0 none, 1 mask from y, 2 mask from
+// x * scale + shift (scsh = [scale C | shift C], the forward's coefficients; y is not read)
 PDT_API int pdt_bn_bwd_reduce(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
-                              int64_t R, int C, int relu, float* ws, double* out, float* dw, float* db,
-                              hipStream_t st) {
-  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+                              const float* scsh, int64_t R, int C, int relu, float* ws, double* out, float* dw,
+                              float* db, hipStream_t st) {
+  if (!pdt_bn_ok(C) || relu < 0 || relu > 2 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
   const int P = reduce_grid(R, C);
-  if (relu) bn_reduce_kernel<1, true><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)y, mean,
-                                                        invstd, R, C, ws);
-  else bn_reduce_kernel<1, false><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, nullptr, mean, invstd, R, C,
-                                                     ws);
-  bn_combine_kernel<<<(2 * C + 63) / 64, 256, 0, st>>>(ws, P, C, 0.0, out, dw, db);
+#define PDT_L(M) bn_reduce_kernel<1, M><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)y, mean, \
+                                                          invstd, scsh, R, C, ws)
+  if (relu == 1) PDT_L(1);
+  else if (relu == 2) PDT_L(2);
+  else PDT_L(0);
+#undef PDT_L
+  bn_combine_kernel<<<(2 * C + 63) / 64, 64 * CW, 0, st>>>(ws, P, C, 0.0, out, dw, db);
   return (int)hipGetLastError();
 }
 
 // dx (and dres = masked dy when dres != null); sums = global (sum dy', sum dy' xhat); count = global M
 PDT_API int pdt_bn_bwd_apply(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
-                             const float* w, const double* sums, const double* count, void* dx, void* dres, int64_t R,
-                             int C, int relu, hipStream_t st) {
-  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+                             const float* w, const float* scsh, const double* sums, const double* count, void* dx,
+                             void* dres, int64_t R, int C, int relu, hipStream_t st) {
+  if (!pdt_bn_ok(C) || relu < 0 || relu > 2 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
   const int g = apply_grid(R, C);
-#define PDT_L(RL, DR) bn_bwd_apply_kernel<RL, DR><<<g, NT, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, \
-      (const bf16_t*)x, mean, invstd, w, sums, count, (bf16_t*)dx, (bf16_t*)dres, R, C)
-  if (relu) { if (dres) PDT_L(true, true); else PDT_L(true, false); }
-  else { if (dres) PDT_L(false, true); else PDT_L(false, false); }
+#define PDT_L(M, DR) bn_bwd_apply_kernel<M, DR><<<g, NT, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, \
+      (const bf16_t*)x, mean, invstd, w, scsh, sums, count, (bf16_t*)dx, (bf16_t*)dres, R, C)
+  if (relu == 1) { if (dres) PDT_L(1, true); else PDT_L(1, false); }
+  else if (relu == 2) { if (dres) PDT_L(2, true); else PDT_L(2, false); }
+  else { if (dres) PDT_L(0, true); else PDT_L(0, false); }
 #undef PDT_L
   return (int)hipGetLastError();
 }

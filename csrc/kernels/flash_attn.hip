@@ -1078,145 +1078,6 @@ __global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// forward v9 = v5's per-wave tile in a PERSISTENT grid: 2 workgroups per CU, each walks a static list of
-// 128-row blocks (block_of(L): the same heavy-first / XCD-grouped order as the one-block-per-workgroup
-// kernels, L = workgroup id + k * grid), and the block seams are pipelined: the next block's first K/V tile
-// is DMA'd into the free ring stage during the current block's last tile, and its Q rows are loaded into
-// the (then dead) Q registers before the current block's O epilogue, so a short causal block (2-16 tiles of
-// 64 keys at S = 1024) no longer pays a cold prologue.  grid % 8 == 0 keeps each workgroup on one XCD for
-// every block it takes, so XCD grouping still holds.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ BlockCoord block_of(int L, int nt, int nh, int nb, int grp, bool heavy_is_high, int order) {
-  if (grouped_ok(order, nh, nb, grp)) return grouped_coord(L, nt, nh, grp, heavy_is_high);
-  const int G = nh * nb, rank = L / G, g = L - rank * G;
-  BlockCoord c;
-  c.h = g % nh;
-  c.b = g / nh;
-  c.t = heavy_is_high ? nt - 1 - rank : rank;
-  return c;
-}
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void fa_fwd_v9_kernel(AttnParams p) {
-  using K = FwdV5<D, CAUSAL>;
-  constexpr int KS = K::KS, DT = K::DT, TE = K::TE;
-  using Dma = DmaLane<D, true, 4>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [stage 0/1][K | V]
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int nt = (p.Sq + 127) / 128, G = p.H * p.B, total = nt * G;
-  const int off = p.Sk - p.Sq;
-  const float sl2 = p.scale * LOG2E;
-  const int grp = p.H / p.Hkv;
-  Dma lk, lv;
-  lk.init(p.k_ss, w, lane);
-  lv.init(p.v_ss, w, lane);
-  int koff[KS];
-  const int F = swz_f<D>(c32);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
-  int voff[DT][2];
-  {
-    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    const int r1 = 4 * (g >> 1) + q;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
-      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
-      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
-    }
-  }
-
-  struct Blk {
-    const bf16_t *Q, *K, *V;
-    int b, hq, q0, ntiles;
-  };
-  auto blk = [&](int L) {
-    const BlockCoord c = block_of(L, nt, p.H, p.B, p.H / p.Hkv, true, p.order);
-    Blk r;
-    r.b = c.b;
-    r.hq = c.h;
-    r.q0 = c.t * 128;
-    const int hk = c.h / grp;
-    r.Q = p.q + c.b * p.q_sb + c.h * p.q_sh;
-    r.K = p.k + c.b * p.k_sb + hk * p.k_sh;
-    r.V = p.v + c.b * p.v_sb + hk * p.v_sh;
-    int kend = p.Sk;
-    if (CAUSAL) kend = min(p.Sk, r.q0 + 128 + off);
-    r.ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-    return r;
-  };
-  auto load_q = [&](const Blk& B, u16x8 (&qf)[KS]) {
-    const int qrow = B.q0 + w * 32 + c32;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(B.Q + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-      else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
-      }
-    }
-  };
-
-  int L = blockIdx.x;
-  if (L >= total) return;
-  Blk cur = blk(L);
-  int stage = 0;
-  if (cur.ntiles > 0) {
-    lk.issue(cur.K, p.k_ss, 0, p.Sk, smem, w);
-    lv.issue(cur.V, p.v_ss, 0, p.Sk, smem + TE, w);
-  }
-  u16x8 qf[KS];
-  load_q(cur, qf);
-  retire(qf);
-  while (true) {
-    const int Ln = L + (int)gridDim.x;
-    const bool more = Ln < total;
-    Blk nxt = cur;
-    if (more) nxt = blk(Ln);
-    const int qw = cur.q0 + w * 32, qrow = qw + c32;
-    const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
-    f32x16 o[DT];
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
-    float m = -INFINITY, l = 0.f;
-    for (int t = 0; t < cur.ntiles; ++t) {
-      dma_barrier();   // tile t landed (and, at t = 0, the Q rows); the other stage is free
-      bf16_t* nb = smem + (stage ^ 1) * 2 * TE;
-      if (t + 1 < cur.ntiles) {
-        lk.issue(cur.K, p.k_ss, (t + 1) * TILE, p.Sk, nb, w);
-        lv.issue(cur.V, p.v_ss, (t + 1) * TILE, p.Sk, nb + TE, w);
-      } else if (more && nxt.ntiles > 0) {   // block seam: the next block's first tile
-        lk.issue(nxt.K, p.k_ss, 0, p.Sk, nb, w);
-        lv.issue(nxt.V, p.v_ss, 0, p.Sk, nb + TE, w);
-      }
-      const int k0 = t * TILE;
-      if (!(CAUSAL && k0 > qw + 31 + off)) {
-        const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
-        K::tile(smem + stage * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
-      }
-      stage ^= 1;
-    }
-    if (more) load_q(nxt, qf);   // in flight under this block's epilogue
-    const float lt = l + __shfl_xor(l, 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    store_row16<DT>(p.o + cur.b * p.o_sb + cur.hq * p.o_sh + (int64_t)qrow * p.o_ss, o, inv, h, qrow < p.Sq);
-    if (qrow < p.Sq && h == 0)
-      p.lse[((int64_t)cur.b * p.H + cur.hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
-    if (!more) break;
-    // hipcc's wait for the Q loads lands here, behind the epilogue stores (it cannot see the inline-asm DMA,
-    // so a wait at the first use inside the tile loop would also drain the next tile's prefetch)
-    retire(qf);
-    if (cur.ntiles == 0 && nxt.ntiles > 0) {   // nothing was prefetched at the seam (degenerate Sk)
-      lk.issue(nxt.K, p.k_ss, 0, p.Sk, smem + stage * 2 * TE, w);
-      lv.issue(nxt.V, p.v_ss, 0, p.Sk, smem + stage * 2 * TE + TE, w);
-    }
-    L = Ln;
-    cur = nxt;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // backward (a): delta[b, h, q] = sum_d dO * O
 // ------------------------------------------------------------------------------------------------
 template <int D>
@@ -2250,29 +2111,23 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
 
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
 int g_fwd_variant = -1, g_bwd_variant = -1, g_order = -1;
-int num_cus() {   // persistent grids: 2 workgroups per CU (a multiple of 8: one XCD per workgroup for good)
-  static int n = 0;
-  if (n <= 0) {
-    int dev = 0, v = 0;
-    n = (hipGetDevice(&dev) == hipSuccess &&
-         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
-  }
-  return n;
-}
 // block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ): PDT_FA_ORDER / pdt_flash_attn_set_order, else
-// per shape -- the forward groups (b, h) blocks per XCD while one group's K/V (2 x Sk x D bf16) stays well
-// inside an XCD's 4 MB L2 with the other groups in flight (GPT-2 1.3B B96: 438 -> 620 TFLOP/s; at Sk 4096
-// grouping lost 3 %); the backward kernels measured neutral (dK/dV v3) or slower (dQ v4) grouped
-// (profiles/r3_attn_ab.jsonl)
-int block_order_mode(int Sk, int D) {
+// per shape -- the forward groups (batch, kv head) units per XCD when the whole K/V no longer fits the 256 MB
+// Infinity Cache (so heavy-first re-reads go to HBM) but one unit's K/V (2 x Sk x D bf16) fits an XCD's L2
+// share: GPT-2 1.3B B96 (805 MB of K/V) 0.95 -> 0.68 ms; at B32 (268 MB), Llama-3 8B B8, GPT-2 124M B64 and
+// S4096 grouping lost 4-10 %.  The backward kernels measured neutral (dK/dV v3) or slower (dQ v4) grouped.
+// (profiles/r3_attn_ab*.jsonl; a persistent forward with pipelined block seams ran 5-45 % SLOWER than v5 in
+// every shape but one, profiles/r3_attn_ab3_persistent_fwd.jsonl -- removed)
+int block_order_mode(int B, int Hkv, int Sk, int D) {
   if (g_order < 0) {
     const char* e = getenv("PDT_FA_ORDER");
     if (e) g_order = atoi(e);
   }
   if (g_order >= 0) return g_order;
-  return (D == 128 && (int64_t)Sk * D * 4 <= (1 << 20)) ? 1 : 0;
+  const int64_t unit = (int64_t)Sk * D * 4, total = unit * B * Hkv;
+  return (unit <= (1 << 20) && total > ((int64_t)384 << 20)) ? 1 : 0;
 }
-// g_*_variant: -1 = not read yet (PDT_FA_FWD / PDT_FA_BWD env), 0 = the default, > 0 = pinned
+
 int fwd_variant() {
   if (g_fwd_variant < 0) { const char* e = getenv("PDT_FA_FWD"); g_fwd_variant = e ? atoi(e) : 0; }
   return g_fwd_variant > 0 ? g_fwd_variant : 5;
@@ -2299,12 +2154,6 @@ int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
   } else if (variant == 5) {
     if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
     else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
-  } else if (variant == 9) {   // persistent v5: 2 workgroups per CU walking the block list
-    const int total = ((p.Sq + 127) / 128) * p.H * p.B;
-    int g9 = 2 * num_cus();
-    g9 = total < g9 ? total : g9;
-    if (causal) fa_fwd_v9_kernel<D, true><<<g9, NT, 0, st>>>(p);
-    else fa_fwd_v9_kernel<D, false><<<g9, NT, 0, st>>>(p);
   } else if (variant == 7 || variant == 8) {   // 8 waves x 32 rows; 7: 3-deep ring, 8: 2-deep
     dim3 g8((p.Sq + 255) / 256, p.H, p.B);
     if (variant == 7) {
@@ -2422,7 +2271,7 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   p.v_sb = strides[6]; p.v_ss = strides[7]; p.v_sh = strides[8];
   p.o_sb = strides[9]; p.o_ss = strides[10]; p.o_sh = strides[11];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  p.order = block_order_mode(Sk, D);
+  p.order = block_order_mode(B, Hkv, Sk, D);
   const int variant = fwd_variant();
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
@@ -2445,7 +2294,7 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.dk_sb = strides[18]; p.dk_ss = strides[19]; p.dk_sh = strides[20];
   p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
-  p.order = block_order_mode(Sk, D);
+  p.order = block_order_mode(B, Hkv, Sk, D);
   return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
 }
 

@@ -71,6 +71,8 @@ def _shared_gpu_queues(nproc: int) -> str | None:
 def _launch_once(cmd, nproc, port, restart, use_local_rank_arg, grace_s):
     procs = []
     queues = None if "GPU_MAX_HW_QUEUES" in os.environ else _shared_gpu_queues(nproc)
+    if queues is not None:
+        print(f"[launch] {nproc} ranks share the GPUs: GPU_MAX_HW_QUEUES={queues} per rank", file=sys.stderr, flush=True)
     for r in range(nproc):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),

@@ -108,10 +108,10 @@ _SIGS = {
                         c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_eval_coef": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
-    "pdt_bn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p,
-                          c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_bn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_bwd_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_int64, c_int, c_int, c_void_p],
+                         c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_window_perm": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,
                       c_int, c_void_p],

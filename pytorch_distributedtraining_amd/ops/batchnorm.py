@@ -68,16 +68,19 @@ class _BNActFn(torch.autograd.Function):
         pg = torch.empty(2, c, dtype=torch.float32, device=dev)
         gw = pg[0] if ctx.has_w and ctx.needs_input_grad[2] else None
         gb = pg[1] if ctx.has_b and ctx.needs_input_grad[3] else None
+        # ReLU mask: recomputed from x with the forward's scale / shift when there is no residual (y is not
+        # read: one bf16 stream less in both passes); from the saved output after a residual add
+        mask = 0 if not ctx.relu else (1 if ctx.has_res else 2)
         _lib.call("pdt_bn_bwd_reduce", dy.data_ptr(), y.data_ptr(), x.data_ptr(), coef[0].data_ptr(),
-                  coef[1].data_ptr(), rows, c, 1 if ctx.relu else 0, ws.data_ptr(), sums.data_ptr(),
+                  coef[1].data_ptr(), coef[2].data_ptr(), rows, c, mask, ws.data_ptr(), sums.data_ptr(),
                   _lib.ptr(gw), _lib.ptr(gb), stream)
         if ctx.comm is not None and ctx.comm.world_size > 1:
             ctx.comm.all_reduce(sums, "sum")
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         _lib.call("pdt_bn_bwd_apply", dy.data_ptr(), y.data_ptr(), x.data_ptr(), coef[0].data_ptr(),
-                  coef[1].data_ptr(), _lib.ptr(weight), sums.data_ptr(), count.data_ptr(), dx.data_ptr(),
-                  _lib.ptr(dres), rows, c, 1 if ctx.relu else 0, stream)
+                  coef[1].data_ptr(), _lib.ptr(weight), coef[2].data_ptr(), sums.data_ptr(), count.data_ptr(),
+                  dx.data_ptr(), _lib.ptr(dres), rows, c, mask, stream)
         return dx, dres, gw, gb, None, None, None, None, None, None
 
 

@@ -21,11 +21,11 @@ import torch  # noqa: E402
 CATS = [  # (category, substrings of the lower-cased kernel name), first match wins
     ("bn_act", ("bn_", "batchnorm", "batch_norm")),
     ("optimizer", ("adamw", "multi_tensor", "clip", "norm_sq", "grad_norm")),
-    ("loss", ("softmax", "nll", "cross_entropy", "log_softmax")),
-    ("pooling", ("pool", "avg_pool", "max_pool")),
-    ("conv", ("conv", "igemm", "miopen", "winograd", "naive", "implicit", "fwd_", "bwd_", "wrw", "xdlops",
-              "gridwise", "ck::", "device_grouped", "direct")),
-    ("gemm", ("cijk", "gemm", "mfma", "matmul")),
+    ("gemm", ("cijk", "gemm_kernel", "matmul")),          # hipBLASLt: ResNet's channels-last 1x1 convs as GEMMs
+    ("conv", ("conv", "igemm", "miopen", "winograd", "naive", "implicit", "wrw", "xdlops", "gridwise", "ck::",
+              "device_grouped", "subtensorop")),
+    ("loss", ("softmax", "nll", "cross_entropy")),
+    ("pooling", ("pool",)),
     ("copy_cast", ("copy", "cast", "convert", "transpose", "fill", "memset", "memcpy")),
     ("elementwise", ("elementwise", "vectorized", "unrolled", "reduce", "add", "mul", "relu")),
 ]

@@ -17,7 +17,7 @@ import re
 import sys
 from collections import defaultdict
 
-KEYS = ("fa_", "win_attn", "bn_", "norm_", "adamw", "swin_mlp", "fp8_cast", "wgrad_kernel")
+KEYS = ("fa_", "win_attn", "bn_", "norm_", "adamw", "swin_mlp", "fp8_cast", "wgrad_kernel", "gemm_kernel", "Cijk")
 
 
 def load(d):
@@ -25,7 +25,7 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             full = r.get("Kernel_Name", "?")
-            m = re.search(r"((?:fa_|win_attn|bn_|norm_|adamw|swin_mlp|fp8_cast|wgrad_kernel)\w*)(<[^()]*>)?", full)
+            m = re.search(r"((?:fa_|win_attn|bn_|norm_|adamw|swin_mlp|fp8_cast|wgrad_kernel|gemm_kernel|Custom_Cijk|Cijk)\w*)(<[^()]*>)?", full)
             if m:
                 acc[(m.group(1) + (m.group(2) or ""))[:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
