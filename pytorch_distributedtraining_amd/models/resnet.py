@@ -72,6 +72,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        if self.fused and self.downsample is None and hasattr(self.conv1, "forward_fork"):
+            # conv1 and the identity share x: their two input gradients are summed inside conv1's dgrad GEMM
+            h, idt = self.conv1.forward_fork(x)
+            return self.bn3(self.conv3(self.bn2(self.conv2(self.bn1(h)))), residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused:
             out = self.bn2(self.conv2(self.bn1(self.conv1(x))))

@@ -242,6 +242,43 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw
 
 
+class _Conv1x1ForkFn(torch.autograd.Function):
+    """(conv1x1(x), x) for a ResNet bottleneck without downsample: x feeds both conv1 and the identity branch,
+    so autograd would sum two full-size input gradients in a separate add kernel (16 such adds were 1.3 ms of
+    a 32 ms ResNet-50 step, profiles/r3_resnet50_kernel_breakdown.jsonl).  Returning the identity from the same
+    Function hands both gradients to ONE backward, where the identity's is folded into the data-gradient GEMM
+    as its C operand: dX = dIdt + dY W in one in-place hipBLASLt call (beta = 1) on dIdt's buffer."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        key = ("f", tuple(x.shape), w.shape[0], x.device)
+        if _c1_pick(key, lambda: _c1_fwd_gemm(x, w), lambda: F.conv2d(x, w)):
+            y = _c1_fwd_gemm(x, w)
+        else:
+            y = F.conv2d(x, w)
+        ctx.save_for_backward(x, w)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, didt):
+        x, w = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        N, _, H, W = x.shape
+        dy2, x2 = _c1_rows(dy), _c1_rows(x)
+        w2 = w.view(w.shape[0], -1)
+        if didt is None:
+            dx2 = dy2 @ w2
+        else:
+            if not didt.is_contiguous(memory_format=torch.channels_last) or didt.dtype != dy.dtype:
+                didt = didt.contiguous(memory_format=torch.channels_last).to(dy.dtype)
+            # in place into the identity's gradient buffer (this backward is its only consumer): an
+            # out-of-place addmm first copies C into a fresh output (a full DtoD pass per block)
+            dx2 = _c1_rows(didt).addmm_(dy2, w2)
+        dw = wgrad(dy2, x2, w.dtype).view_as(w)
+        return _c1_from_rows(dx2, N, H, W), dw
+
+
 def conv1x1_ok(x, w) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[0] * x.shape[2] * x.shape[3] >= 4096)
@@ -266,3 +303,17 @@ class Conv2d1x1(nn.Conv2d):
         if conv1x1_ok(x, w):
             return _Conv1x1Fn.apply(x, w)
         return F.conv2d(x, w)
+
+    def forward_fork(self, x):
+        """(self(x), identity x) with the identity's gradient accumulated inside this conv's data-gradient GEMM
+        (``_Conv1x1ForkFn``); falls back to (self(x), x) where the GEMM form does not apply."""
+        w = self.weight
+        if x.is_cuda and x.dtype == torch.bfloat16 and torch.is_autocast_enabled("cuda") \
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            w = w.to(torch.bfloat16)
+            if conv1x1_ok(x, w):
+                with torch.autocast("cuda", enabled=False):
+                    return _Conv1x1ForkFn.apply(x, w)
+        elif conv1x1_ok(x, w):
+            return _Conv1x1ForkFn.apply(x, w)
+        return self(x), x

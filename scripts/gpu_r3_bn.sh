@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "batchnorm or flash_attn" -x -q --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "batchnorm or flash_attn or resnet or conv1x1" -q --timeout 200 --timeout-method thread \
   -p no:cacheprovider > $OUT/r3_pytest_bn_attn.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -n 3 $OUT/r3_pytest_bn_attn.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u scripts/resnet_kernel_breakdown.py > $OUT/r3_resnet50_kernel_breakdown_bn2.jsonl 2> $OUT/r3_resnet50_kernel_breakdown_bn2.err

@@ -886,6 +886,37 @@ def test_resnet50_fused_bn_matches_plain_model():
         assert rel_err(ga, gr) < 2 * rel_err(gb, gr) + 5e-2, name
 
 
+def test_resnet_bottleneck_fork_sums_identity_gradient_in_dgrad():
+    """Bottlenecks without downsample run conv1 + identity through one Function (the identity's input gradient
+    is the C operand of conv1's dgrad GEMM): gradients of the input and of every parameter vs fp32, with the
+    residual branch live (bn3 gamma != 0, unlike the zero-init default).  Three BNs deep, bf16 rounding alone
+    is several percent, so the bound is stock bf16 autocast's own error on the same block."""
+    from pytorch_distributedtraining_amd.models.resnet import Bottleneck
+    torch.manual_seed(3)
+    blk = Bottleneck(256, 64).to(DEV).to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+            torch.nn.init.uniform_(m.bias, -0.2, 0.2)
+    stock = Bottleneck(256, 64, fused=False).to(DEV).to(memory_format=torch.channels_last)
+    ref = Bottleneck(256, 64, fused=False).to(DEV).to(memory_format=torch.channels_last)
+    stock.load_state_dict(blk.state_dict())
+    ref.load_state_dict(blk.state_dict())
+    x0 = torch.randn(16, 256, 28, 28, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    g = None
+    grads = []
+    for m, amp in ((blk, True), (stock, True), (ref, False)):
+        x = (x0 if amp else x0.float()).detach().clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = m(x)
+        if g is None:
+            g = torch.randn_like(y.float())
+        (y.float() * g).sum().backward()
+        grads.append([x.grad] + [p.grad for p in m.parameters()])
+    for i, (a, b, r) in enumerate(zip(*grads)):
+        assert rel_err(a, r) < 2 * rel_err(b, r) + 1e-2, i
+
+
 @pytest.mark.parametrize("n", [60, 180, 12, 1020, 64, 2056])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_colsum_widths(n, dt):
