@@ -51,12 +51,13 @@ def spawn(fn, nprocs: int, args=(), join: bool = True):
 
 
 def _shared_gpu_queues(nproc: int) -> str | None:
-    """GPU_MAX_HW_QUEUES for ranks that must share GPUs (more ranks than devices: one-GPU rehearsals).  With
-    HIP's default 4 hardware queues per process, 4 ranks on one GPU oversubscribe the queues the command
-    processor keeps mapped, and a rank's collective kernel can wait unscheduled while a peer's mesh kernel
-    spins for it: the world-4 GPT-2 rehearsal timed out at its 3rd collective with 4 queues per rank and ran
-    clean with 2 (profiles/r3_rehearsal_gpt2_fsdp_w4_q4_vs_q2.log): keep <= 8 queues per GPU.  One rank per
-    GPU keeps HIP's default.  device_count() does not initialise the GPU in this (launcher) process."""
+    """GPU_MAX_HW_QUEUES for ranks that must share GPUs (more ranks than devices: one-GPU rehearsals), keeping
+    <= 8 HIP hardware queues per GPU.  With 4 queues per rank, 4 ranks on one GPU had a rank's 3rd xGMI
+    collective go unscheduled while peers' mesh kernels spun for it (profiles/r3_rehearsal_gpt2_fsdp_w4_q4_vs_q2.log);
+    2 queues per rank passed once and failed on a repeat (profiles/r3_rehearsal_gpt2_fsdp_w4_q2_repeat.log), so
+    several ranks spinning on one GPU stay a rehearsal-only configuration -- one rank per GPU keeps HIP's default.
+    device_count() does not initialise the GPU in this (launcher) process; on some boxes it reports the node's
+    GPUs rather than the ones this process can use, and then nothing is capped."""
     try:
         import torch
         ndev = torch.cuda.device_count()
