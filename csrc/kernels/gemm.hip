@@ -197,7 +197,10 @@ __device__ __forceinline__ void tile_of(const GemmArgs& p, int& tm, int& tn) {
 // A tile's DMA therefore has ~1.5 K-steps of MFMAs to land, no ds_read ever waits at a step boundary, and
 // the matrix pipe of a SIMD sees 128 MFMAs per barrier (cf. the 2-wave-per-SIMD staggered variant: 56 %
 // MFMA busy against hipBLASLt's 85 % at 8192^3, profiles/r3_pmc_gemm_v2_vs_hipblaslt.txt).
-template <int LAYOUT, int EPI>
+// DIAG (diagnostic builds only, pdt_gemm_diag_bf16 -- results are WRONG): 1 = no LDS-DMA in the main loop
+// (prologue tiles re-read: MFMA + ds_read ceiling), 2 = DMA issued but never waited for (issue cost without
+// the latency), 3 = no ds_reads in the main loop (MFMA + DMA only)
+template <int LAYOUT, int EPI, int DIAG = 0>
 __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STB];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -229,6 +232,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   // pieces [I0, I1) of BOTH operands of K-step t into slot t & 1
   auto issue = [&](auto i0, auto i1, int t) {
     constexpr int J0 = decltype(i0)::value, J1 = decltype(i1)::value;
+    if (DIAG == 1 && t >= 2) return;
     da.template issue<J0, J1>(Ab + a0 + t * astep, abytes, smem + (t & 1) * STB, w);
     db.template issue<J0, J1>(Bb + b0 + t * bstep, bbytes, smem + (t & 1) * STB + OPB, w);
   };
@@ -267,10 +271,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     // ---- A: substep 0 MFMAs || substep 1 reads (tile t) || second half of tile t+1's DMA
     if (t >= 1 && (!G || t + 1 < T)) issue(PH{}, PE{}, t + 1);
     // read order = order of first use: every B block (all of B1's MFMAs need them), then A blocks 0..7
+    if (DIAG != 3) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fb1[j] = fr.template read<1>(sa + OPB, 8 * wc + j);
+      for (int j = 0; j < 8; ++j) fb1[j] = fr.template read<1>(sa + OPB, 8 * wc + j);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa1[i] = fr.template read<1>(sa, 8 * wr + i);
+      for (int i = 0; i < 8; ++i) fa1[i] = fr.template read<1>(sa, 8 * wr + i);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { fb1[j] = fb0[j]; fa1[j] = fa0[j]; }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -287,14 +296,17 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (DIAG == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     // ---- B2: substep 1, rows 64-127 || tile t+1 substep-0 reads || first half of tile t+2's DMA
+    //      (issuing all of t+2 here -- a full K-step to land, as hipBLASLt's loop does -- made hipcc shuffle the
+    //      256 accumulators between AGPRs and VGPRs every step, with or without unrolling: kept split)
     if (!G || t + 2 < T) issue(P0{}, PH{}, t + 2);
-    const bool more = !G || t + 1 < T;
+    const bool more = (!G || t + 1 < T) && DIAG != 3;
     if (more) {   // the next step's A needs every B block first, then A blocks in order
 #pragma unroll
       for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(na + OPB, 8 * wc + j);
@@ -463,6 +475,25 @@ int launch_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
 
 // Shapes the kernel takes (checked by the host before any launch): M, N multiples of 256, K a multiple of
 // 32 * splits, 16-B aligned rows, every byte offset of a stage tile below 2^32 (buffer resources).
+// Diagnostic launches of the TT / plain kernel: diag 0 is the production kernel, 1-3 remove a part of the
+// main loop (see DIAG above; output garbage by construction).  For scripts/gemm_diag.py.
+PDT_API int pdt_gemm_diag_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                               hipStream_t s) {
+  if (M % TM || N % TN || K % KB || diag < 0 || diag > 3) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = M; a.ldb = N; a.ldc = N; a.k_per_split = (int)K;
+  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  dim3 grid((unsigned)((M / TM) * (N / TN)), 1);
+  switch (diag) {
+    case 0: gemm_kernel<L_TT, E_PLAIN, 0><<<grid, NTH, 0, s>>>(a); break;
+    case 1: gemm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a); break;
+    case 2: gemm_kernel<L_TT, E_PLAIN, 2><<<grid, NTH, 0, s>>>(a); break;
+    default: gemm_kernel<L_TT, E_PLAIN, 3><<<grid, NTH, 0, s>>>(a); break;
+  }
+  return (int)hipGetLastError();
+}
+
 PDT_API int pdt_gemm_ok(int layout, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int splits) {
   if (layout != L_NT && layout != L_TT) return 0;
   if (splits < 1 || M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % ((int64_t)KB * splits)) return 0;
