@@ -114,7 +114,8 @@ class Comm:
         self.tracer = rt.CollectiveTracer(4096) if rt is not None else None
         self.xgmi = None
         if xgmi is None:
-            xgmi = os.environ.get("PDT_XGMI", "0") == "1"
+            from ..run_config import xgmi_mode
+            xgmi = xgmi_mode() != "off"
         if xgmi and self.world_size > 1 and torch.cuda.is_available():
             from ..run_config import xgmi_kwargs
             self.enable_xgmi(**xgmi_kwargs())

@@ -23,9 +23,14 @@ Failure is loud: a mesh wait longer than ``timeout_us`` (wall clock, s_memrealti
 kernel poison its output with NaN and set a host-mapped error word; ``raise_if_failed()`` (called by every engine at its end-of-backward and
 optimizer sync points through ``Comm.check_errors``) reads that word without synchronising and raises.
 
-``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes eligible CUDA collectives here (fp32/bf16, sizes a multiple
-of 16 B, world <= 8); everything else stays on RCCL.  Ranks must issue collectives in the same order (the
-same contract as RCCL).
+``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes every eligible CUDA collective here (fp32/bf16, sizes a
+multiple of 16 B, world <= 8); ``PDT_XGMI=auto`` routes by SIZE CLASS: payloads in
+[``min_bytes``, ``max_bytes``] -- by default the latency class up to 1 MiB (grad-norm / found_inf scalars,
+SyncBN statistics, loss sync, small first buckets), where the one-shot mesh kernel is one barrier and one
+read of every peer -- go to the mesh, everything else stays on RCCL's pipelined rings
+(``PDT_XGMI_MIN_KB`` / ``PDT_XGMI_MAX_KB`` move the window; parity of the default window on a real 8-GPU node
+is unpinned: it has only run with several ranks on one GPU).  Ranks must issue collectives in the same order
+(the same contract as RCCL); the routing depends only on the payload size, so every rank routes alike.
 """
 from __future__ import annotations
 
@@ -40,11 +45,29 @@ SIG_BYTES = 4096
 MAX_WORLD = 8
 
 
+class SizeClass:
+    """Which payloads the mesh takes: [min_bytes, max_bytes] (None = unbounded), sizes a multiple of 16 B.
+    Pure function of the size, so every rank of a collective routes it the same way."""
+
+    def __init__(self, min_bytes: int = 0, max_bytes: int | None = None):
+        if min_bytes < 0 or (max_bytes is not None and max_bytes < min_bytes):
+            raise ValueError(f"bad xGMI size class [{min_bytes}, {max_bytes}]")
+        self.min_bytes, self.max_bytes = int(min_bytes), max_bytes
+
+    def __call__(self, nbytes: int) -> bool:
+        return (nbytes > 0 and nbytes % 16 == 0 and nbytes >= self.min_bytes
+                and (self.max_bytes is None or nbytes <= self.max_bytes))
+
+    def __repr__(self):
+        return f"SizeClass({self.min_bytes}, {self.max_bytes})"
+
+
 class XGMIComm:
     """Peer-mapped collectives for ``comm``'s ranks (one process per GPU of one node)."""
 
     def __init__(self, comm, slot_bytes: int = 256 << 20, oneshot_max_bytes: int = 256 << 10,
-                 timeout_us: int = 60_000_000, uncached: bool = True):
+                 timeout_us: int = 60_000_000, uncached: bool = True, min_bytes: int = 0,
+                 max_bytes: int | None = None):
         if comm.world_size > MAX_WORLD:
             raise ValueError(f"XGMIComm spans one node (<= {MAX_WORLD} GPUs), got world_size={comm.world_size}")
         self.comm = comm
@@ -54,6 +77,7 @@ class XGMIComm:
             # the kernels address a slot with 32-bit buffer-resource offsets
             raise ValueError(f"xGMI slot_bytes must be a positive multiple of 4 KiB below 2 GiB, got {slot_bytes}")
         self.oneshot_max_bytes = int(oneshot_max_bytes)
+        self.size_class = SizeClass(min_bytes, max_bytes)
         self.timeout_us = max(1, min(int(timeout_us), (1 << 32) - 1))
         self.wallclock_khz = int(_lib.require().pdt_xgmi_wallclock_khz())   # s_memrealtime rate (budget unit)
         self.device = torch.device("cuda", torch.cuda.current_device())
@@ -88,8 +112,8 @@ class XGMIComm:
 
     # ------------------------------------------------------------------ eligibility
     def eligible(self, nbytes: int, kind: str = "all_reduce") -> bool:
-        """Any fp32/bf16 payload that is a multiple of 16 B (larger ones are chunked)."""
-        return nbytes > 0 and nbytes % 16 == 0
+        """fp32/bf16 payloads that are a multiple of 16 B inside the size class (larger ones are chunked)."""
+        return self.size_class(nbytes)
 
     # ------------------------------------------------------------------ launch
     def _run(self, kind: str, inp: int, out: int, nbytes: int, pitch: int, dtype, scale: float):

@@ -7,7 +7,8 @@ fairscale_oss / fairscale_sddp, plus fsdp), precision, batch / accumulation / cl
 (safe loader) or JSON; ``apply_env_overrides`` lets a launcher retune communication without editing files:
 
     PDT_BUCKET_MB, PDT_FIRST_BUCKET_MB   DDP bucket cap / first bucket (MiB)
-    PDT_XGMI=1, PDT_XGMI_ONESHOT_KB      route eligible collectives through the xGMI peer kernels
+    PDT_XGMI=1|auto, PDT_XGMI_ONESHOT_KB route eligible collectives through the xGMI peer kernels (auto: by
+                                        size class, PDT_XGMI_MIN_KB / PDT_XGMI_MAX_KB)
     PDT_BATCH, PDT_STEPS, PDT_PRECISION  quick sweeps
 """
 from __future__ import annotations
@@ -91,10 +92,32 @@ def apply_env_overrides(cfg: RunConfig, env=None) -> RunConfig:
     return dataclasses.replace(cfg, **upd) if upd else cfg
 
 
+XGMI_AUTO_MAX_KB = 1024     # PDT_XGMI=auto: the mesh takes the latency class up to this size, RCCL the rest
+
+
+def xgmi_mode(env=None) -> str:
+    """PDT_XGMI: "0" (RCCL only, default), "1" / "all" (every eligible collective on the xGMI mesh), "auto"
+    (size classes: small payloads on the mesh, bulk on RCCL)."""
+    env = os.environ if env is None else env
+    v = env.get("PDT_XGMI", "0").strip().lower()
+    if v in ("1", "all", "true", "on"):
+        return "all"
+    if v == "auto":
+        return "auto"
+    return "off"
+
+
 def xgmi_kwargs(env=None) -> Dict[str, Any]:
-    """XGMIComm tuning from the environment (PDT_XGMI_ONESHOT_KB, PDT_XGMI_SLOT_MB, PDT_XGMI_TIMEOUT_S)."""
+    """XGMIComm tuning from the environment (PDT_XGMI_ONESHOT_KB, PDT_XGMI_SLOT_MB, PDT_XGMI_TIMEOUT_S, and the
+    size class PDT_XGMI_MIN_KB / PDT_XGMI_MAX_KB -- the latter defaulting to 1 MiB under PDT_XGMI=auto)."""
     env = os.environ if env is None else env
     kw = {}
+    if env.get("PDT_XGMI_MIN_KB"):
+        kw["min_bytes"] = int(float(env["PDT_XGMI_MIN_KB"]) * 1024)
+    if env.get("PDT_XGMI_MAX_KB"):
+        kw["max_bytes"] = int(float(env["PDT_XGMI_MAX_KB"]) * 1024)
+    elif xgmi_mode(env) == "auto":
+        kw["max_bytes"] = XGMI_AUTO_MAX_KB * 1024
     if env.get("PDT_XGMI_ONESHOT_KB"):
         kw["oneshot_max_bytes"] = int(float(env["PDT_XGMI_ONESHOT_KB"]) * 1024)
     if env.get("PDT_XGMI_SLOT_MB"):

@@ -189,3 +189,23 @@ def test_launcher_limits_hw_queues_only_when_ranks_share_gpus(monkeypatch):
     assert launch._shared_gpu_queues(8) is None
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
     assert launch._shared_gpu_queues(4) is None
+
+
+def test_xgmi_size_class_routing_policy():
+    """PDT_XGMI=auto routes by payload size alone (so every rank routes a collective alike): the latency class
+    (<= 1 MiB by default) to the xGMI mesh, bulk to RCCL; explicit windows via PDT_XGMI_MIN_KB / _MAX_KB."""
+    import pytest
+    from pytorch_distributedtraining_amd.parallel.xgmi import SizeClass
+    from pytorch_distributedtraining_amd.run_config import xgmi_kwargs, xgmi_mode
+    assert xgmi_mode({}) == "off" and xgmi_mode({"PDT_XGMI": "0"}) == "off"
+    assert xgmi_mode({"PDT_XGMI": "1"}) == "all" and xgmi_mode({"PDT_XGMI": "auto"}) == "auto"
+    assert "max_bytes" not in xgmi_kwargs({"PDT_XGMI": "1"})
+    kw = xgmi_kwargs({"PDT_XGMI": "auto"})
+    assert kw["max_bytes"] == 1 << 20
+    kw = xgmi_kwargs({"PDT_XGMI": "auto", "PDT_XGMI_MIN_KB": "4", "PDT_XGMI_MAX_KB": "256"})
+    sc = SizeClass(kw["min_bytes"], kw["max_bytes"])
+    assert not sc(1024) and sc(4096) and sc(256 << 10) and not sc((256 << 10) + 16)
+    assert not sc(4096 + 8)                       # the mesh kernels move 16-byte vectors
+    assert SizeClass()(16) and SizeClass()(1 << 30) and not SizeClass()(0)
+    with pytest.raises(ValueError):
+        SizeClass(100, 10)

@@ -146,3 +146,30 @@ def test_xgmi_timeout_is_loud():
     # the diagnosis names the wait: barrier 0 of rank 0's last epoch, peer 1 still at an older epoch
     assert d0["peer"] == 1 and d0["barrier"] == 0 and d0["epoch"] == d0["issued_epoch"]
     assert d0["peer_epoch"] < d0["epoch"]
+
+
+def _size_class_worker(rank, world):
+    from pytorch_distributedtraining_amd.parallel import Comm
+    torch.cuda.set_device(0)
+    comm = Comm(xgmi=False)
+    x = comm.enable_xgmi(slot_bytes=1 << 20, max_bytes=64 << 10)       # the PDT_XGMI=auto policy, 64 KiB class
+    small = torch.full((1024,), float(rank + 1), device="cuda")        # 4 KiB -> mesh
+    big = torch.full((1 << 18,), float(rank + 1), device="cuda")       # 1 MiB -> the c10d backend (gloo here)
+    c0 = x.calls
+    comm.all_reduce(small, "sum")
+    c1 = x.calls
+    comm.all_reduce(big, "sum")
+    c2 = x.calls
+    torch.cuda.synchronize()
+    comm.check_errors()
+    out = (c1 - c0, c2 - c1, float(small[0]), float(big[0]), float(big[-1]))
+    comm.barrier()
+    x.close()
+    return out
+
+
+def test_xgmi_size_class_routes_small_to_mesh_and_bulk_to_backend():
+    exp = float(sum(r + 1 for r in range(2)))
+    for mesh_small, mesh_big, s, b0, b1 in run_workers(_size_class_worker, 2):
+        assert mesh_small == 1 and mesh_big == 0
+        assert s == exp and b0 == exp and b1 == exp
