@@ -44,6 +44,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((address_space(3))) u16x8 lds_u16x8;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) const char lds_cchar;
 
 constexpr int TM = 256, TN = 256, KB = 64, NTH = 256;
 constexpr int OPB = TM * KB * 2;           // bytes of one operand tile of one K-step (32 KiB)
@@ -87,14 +88,14 @@ struct Dma {
     v4i rsrc;
     uint32_t lds0, rs;
   };
-  __device__ __forceinline__ Tile tile(const char* t, uint32_t nbytes, const char* lds_op, int w) const {
+  __device__ __forceinline__ Tile tile(const char* t, uint32_t nbytes, uint32_t lds_op, int w) const {
     const uint64_t addr = (uint64_t)(uintptr_t)t;
     Tile d;
     d.rsrc[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)addr);
     d.rsrc[1] = __builtin_amdgcn_readfirstlane((int)((addr >> 32) & 0xffff));
     d.rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
     d.rsrc[3] = 0x00020000;
-    d.lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_op + w * 1024);
+    d.lds0 = __builtin_amdgcn_readfirstlane(lds_op + w * 1024);
     d.rs = __builtin_amdgcn_readfirstlane(rowstep);
     return d;
   }
@@ -103,16 +104,16 @@ struct Dma {
     asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :: "s"(d.lds0 + I * 4096), "v"((I & 1) ? off1 : off0), "s"(d.rsrc), "s"(I * d.rs) : "memory");
   }
-  // pieces [I0, I1) of the tile at byte address `tile` (wave-uniform) into the LDS tile `lds_op`
+  // pieces [I0, I1) of the tile at byte address `tile` (wave-uniform) into the LDS tile at byte address `lds_op`
   template <int I0, int I1>
-  __device__ __forceinline__ void issue(const char* tile, uint32_t nbytes, const char* lds_op, int w) const {
+  __device__ __forceinline__ void issue(const char* tile, uint32_t nbytes, uint32_t lds_op, int w) const {
     const uint64_t addr = (uint64_t)(uintptr_t)tile;
     v4i rsrc;
     rsrc[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)addr);
     rsrc[1] = __builtin_amdgcn_readfirstlane((int)((addr >> 32) & 0xffff));
     rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
     rsrc[3] = 0x00020000;
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_op + w * 1024);
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_op + w * 1024);
     const uint32_t rs = __builtin_amdgcn_readfirstlane(rowstep);
 #pragma unroll
     for (int i = I0; i < I1; ++i) {
@@ -141,13 +142,13 @@ struct Frag {
     }
   }
   template <int S>
-  __device__ __forceinline__ u16x8 read(const char* op, int blk) const {
+  __device__ __forceinline__ u16x8 read(lds_cchar* op, int blk) const {
     if (LAYOUT == L_NT) {
-      return *(const lds_u16x8*)(lds_void*)(op + blk * 16 * 128 + (S ? o1 : o0));
+      return *(const lds_u16x8*)(op + blk * 16 * 128 + (S ? o1 : o0));
     } else {
       const uint32_t a = o0 + S * 32 * 512 + 16 * ((uint32_t)(2 * blk) ^ o1);
-      const v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds_void*)(op + a));
-      const v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds_void*)(op + a + 2048));
+      const v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(op + a));
+      const v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(op + a + 2048));
       return __builtin_bit_cast(u16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
     }
   }
@@ -167,12 +168,13 @@ struct GemmArgs {
   int xpr;                // XCD block cut (see tile_of)
 };
 
-__device__ __forceinline__ void tile_of(const GemmArgs& p, int& tm, int& tn) {
-  // XCD-aware tile order (speed only): workgroups b and b + 8 share an XCD under round-robin dispatch.
+__device__ __forceinline__ void tile_of(const GemmArgs& p, int id, int ntiles, int& tm, int& tn) {
+  // XCD-aware tile order (speed only): tile ids b and b + 8 share an XCD under round-robin dispatch (a
+  // persistent workgroup b walks ids b, b + G, ... with G % 8 == 0, so all of them stay on its XCD).
   // xpr > 0: the tile grid is cut into xpr x (8 / xpr) blocks, one per XCD (host picks the cut that
   // minimises the A + B panels an XCD's L2 holds); else each XCD takes a contiguous run of tiles.
-  const int mt = p.M / TM, nt = p.N / TN, ntiles = gridDim.x;
-  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int mt = p.M / TM, nt = p.N / TN;
+  const int xcd = id & 7, loc = id >> 3;
   if (p.xpr > 0) {
     const int xpc = 8 / p.xpr, rb = mt / p.xpr, cb = nt / xpc;
     tm = (xcd / xpc) * rb + loc / cb;
@@ -199,15 +201,27 @@ __device__ __forceinline__ void tile_of(const GemmArgs& p, int& tm, int& tn) {
 // MFMA busy against hipBLASLt's 85 % at 8192^3, profiles/r3_pmc_gemm_v2_vs_hipblaslt.txt).
 // DIAG (diagnostic builds only, pdt_gemm_diag_bf16 -- results are WRONG): 1 = no LDS-DMA in the main loop
 // (prologue tiles re-read: MFMA + ds_read ceiling), 2 = DMA issued but never waited for (issue cost without
-// the latency), 3 = no ds_reads in the main loop (MFMA + DMA only)
-template <int LAYOUT, int EPI, int DIAG = 0>
+// the latency), 3 = no ds_reads in the main loop (MFMA + DMA only), 4 = no epilogue stores (a store only where
+// an accumulator equals a sentinel: the tile-boundary cost without the C write)
+//
+// PERSIST (plain single-split launches; gridDim.x <= tiles, a multiple of 8): the workgroup walks tiles
+// id = blockIdx.x + i * gridDim.x.  The last K-step of a tile, right after its final barrier (both ring
+// slots are free then), issues the NEXT tile's first two K-steps, so their HBM latency hides behind the
+// tile's last MFMAs and its epilogue; the next tile's first wait counts the epilogue's stores as younger
+// (vmcnt(min(63, 16 + stores)), and its step 0 waits with vmcnt(min(63, stores))), so the C-tile stores
+// drain under the next tile's first K-steps instead of holding the CU at a workgroup boundary.
+template <int LAYOUT, int EPI, int DIAG = 0, bool PERSIST = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STB];
+  lds_cchar* const lds = (lds_cchar*)(lds_void*)smem;                 // the ring, LDS address space
+  const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;     // its LDS byte address (LDS-DMA m0)
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 1, wc = w & 1;
+  const int ntiles = PERSIST ? (p.M / TM) * (p.N / TN) : (int)gridDim.x;
+  int tile = blockIdx.x;
   int tm, tn;
-  tile_of(p, tm, tn);
-  const int m0 = tm * TM, n0 = tn * TN;
+  tile_of(p, tile, ntiles, tm, tn);
+  int m0 = tm * TM, n0 = tn * TN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int T = min(p.K - kbeg, p.k_per_split) / KB;
 
@@ -218,24 +232,41 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   fr.init(lane);
   const char* Ab = reinterpret_cast<const char*>(p.A);
   const char* Bb = reinterpret_cast<const char*>(p.B);
-  int64_t a0, b0, astep, bstep;
+  int64_t astep, bstep;
   uint32_t abytes, bbytes;
+  auto tile_base = [&](int mm, int nn, int64_t& ao, int64_t& bo) {
+    if (LAYOUT == L_NT) {
+      ao = ((int64_t)mm * p.lda + kbeg) * 2; bo = ((int64_t)nn * p.ldb + kbeg) * 2;
+    } else {
+      ao = ((int64_t)kbeg * p.lda + mm) * 2; bo = ((int64_t)kbeg * p.ldb + nn) * 2;
+    }
+  };
   if (LAYOUT == L_NT) {
-    a0 = ((int64_t)m0 * p.lda + kbeg) * 2; b0 = ((int64_t)n0 * p.ldb + kbeg) * 2;
     astep = bstep = KB * 2;
     abytes = (uint32_t)((TM - 1) * p.lda * 2 + KB * 2); bbytes = (uint32_t)((TN - 1) * p.ldb * 2 + KB * 2);
   } else {
-    a0 = ((int64_t)kbeg * p.lda + m0) * 2; b0 = ((int64_t)kbeg * p.ldb + n0) * 2;
     astep = KB * p.lda * 2; bstep = KB * p.ldb * 2;
     abytes = (uint32_t)((KB - 1) * p.lda * 2 + TM * 2); bbytes = (uint32_t)((KB - 1) * p.ldb * 2 + TN * 2);
   }
+  int64_t a0, b0;
+  tile_base(m0, n0, a0, b0);
   // pieces [I0, I1) of BOTH operands of K-step t into slot t & 1
   auto issue = [&](auto i0, auto i1, int t) {
     constexpr int J0 = decltype(i0)::value, J1 = decltype(i1)::value;
     if (DIAG == 1 && t >= 2) return;
-    da.template issue<J0, J1>(Ab + a0 + t * astep, abytes, smem + (t & 1) * STB, w);
-    db.template issue<J0, J1>(Bb + b0 + t * bstep, bbytes, smem + (t & 1) * STB + OPB, w);
+    da.template issue<J0, J1>(Ab + a0 + t * astep, abytes, lds_addr + (t & 1) * STB, w);
+    db.template issue<J0, J1>(Bb + b0 + t * bstep, bbytes, lds_addr + (t & 1) * STB + OPB, w);
   };
+  // PERSIST: the next tile (id, base offsets) and whether it exists
+  int ntile = tile + (int)gridDim.x;
+  int64_t na0 = 0, nb0 = 0;
+  int nm0 = 0, nn0 = 0;
+  if (PERSIST && ntile < ntiles) {
+    int a, b;
+    tile_of(p, ntile, ntiles, a, b);
+    nm0 = a * TM; nn0 = b * TN;
+    tile_base(nm0, nn0, na0, nb0);
+  }
   using P0 = std::integral_constant<int, 0>;
   using PH = std::integral_constant<int, PIECES / 2>;
   using PE = std::integral_constant<int, PIECES>;
@@ -254,10 +285,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  // VMEM ops the epilogue issues per wave (PERSIST's counted waits): stores, + the aux loads for DGELU
+  constexpr int EPI_VM = EPI == E_GELU ? 128 : EPI == E_DGELU ? 129 : EPI == E_F32 ? 64 : 64;
+  constexpr int W_FIRST = (2 * PIECES + EPI_VM) < 63 ? (2 * PIECES + EPI_VM) : 63;
+  constexpr int W_STEP0 = EPI_VM < 63 ? EPI_VM : 63;
+  bool later = false;   // PERSIST: this is not the workgroup's first tile
+  for (;;) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) fa0[i] = fr.template read<0>(smem, 8 * wr + i);
+  for (int i = 0; i < 8; ++i) fa0[i] = fr.template read<0>(lds, 8 * wr + i);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(smem + OPB, 8 * wc + j);
+  for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(lds + OPB, 8 * wc + j);
 
   // one K-step; G (guarded) only for the last two steps, so the steady state is branch-free and its
   // instruction interleave can be pinned with sched_group_barrier (hipcc otherwise issues a stage's reads
@@ -266,8 +303,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   // pieces between 8-MFMA groups by 8 % on the weight-gradient (TT) shapes (profiles/r3_gemm_variants.txt).
   auto kstep = [&](auto guarded, const int t) {
     constexpr bool G = decltype(guarded)::value;
-    const char* sa = smem + (t & 1) * STB;
-    const char* na = smem + ((t + 1) & 1) * STB;
+    lds_cchar* sa = lds + (t & 1) * STB;
+    lds_cchar* na = lds + ((t + 1) & 1) * STB;
     // ---- A: substep 0 MFMAs || substep 1 reads (tile t) || second half of tile t+1's DMA
     if (t >= 1 && (!G || t + 1 < T)) issue(PH{}, PE{}, t + 1);
     // read order = order of first use: every B block (all of B1's MFMAs need them), then A blocks 0..7
@@ -297,6 +334,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
     if (DIAG == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else if (PERSIST && t == 0 && later) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(W_STEP0) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -306,6 +344,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     //      (issuing all of t+2 here -- a full K-step to land, as hipBLASLt's loop does -- made hipcc shuffle the
     //      256 accumulators between AGPRs and VGPRs every step, with or without unrolling: kept split)
     if (!G || t + 2 < T) issue(P0{}, PH{}, t + 2);
+    if (PERSIST && G && t + 1 == T && ntile < ntiles) {
+      // both ring slots are free after this step's barrier: the next tile's K-steps 0 and 1 go out now
+      da.template issue<0, PIECES>(Ab + na0, abytes, lds_addr, w);
+      db.template issue<0, PIECES>(Bb + nb0, bbytes, lds_addr + OPB, w);
+      if (T > 1) {
+        da.template issue<0, PIECES>(Ab + na0 + astep, abytes, lds_addr + STB, w);
+        db.template issue<0, PIECES>(Bb + nb0 + bstep, bbytes, lds_addr + STB + OPB, w);
+      }
+    }
     const bool more = (!G || t + 1 < T) && DIAG != 3;
     if (more) {   // the next step's A needs every B block first, then A blocks in order
 #pragma unroll
@@ -332,6 +379,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   for (; t < T; ++t) kstep(Guarded{}, t);
 
   // ---------------------------------------------------------------- epilogue
+  {
   // acc[i][j][r] = C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
   const int mrow = m0 + 128 * wr + (lane & 15);
   const int ncol = n0 + 128 * wc + 4 * (lane >> 4);
@@ -342,7 +390,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         *reinterpret_cast<f32x4*>(C + (int64_t)(mrow + 16 * i) * p.N + ncol + 16 * j) = acc[i][j];
-    return;
   } else {
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
     float bj[8][4];
@@ -391,7 +438,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
             cs[j][r] += bf2f(gb);   // the bias gradient sums the gradient as stored
           }
         }
-        *reinterpret_cast<u16x4*>(C + e) = o;
+        if (DIAG != 4 || acc[i][j][0] == 1234.5f) *reinterpret_cast<u16x4*>(C + e) = o;
       }
     }
     if constexpr (EPI == E_DGELU) {
@@ -419,6 +466,34 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
       __syncthreads();
       p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
     }
+  }
+  }
+  if constexpr (PERSIST && EPI != E_DGELU) {   // (DGELU reuses the ring's LDS in its epilogue: not persistent)
+    if (ntile < ntiles) {
+      // next tile: its K-steps 0 / 1 were issued in the last K-step; wait for step 0 (the stores above are
+      // younger and may still drain), publish it, and run the main loop again
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W_FIRST) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      tile = ntile;
+      m0 = nm0; n0 = nn0; a0 = na0; b0 = nb0;
+      tm = m0 / TM; tn = n0 / TN;
+      ntile = tile + (int)gridDim.x;
+      if (ntile < ntiles) {
+        int a, b;
+        tile_of(p, ntile, ntiles, a, b);
+        nm0 = a * TM; nn0 = b * TN;
+        tile_base(nm0, nn0, na0, nb0);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      later = true;
+      continue;
+    }
+  }
+  break;
   }
 }
 
@@ -479,7 +554,7 @@ int launch_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
 // main loop (see DIAG above; output garbage by construction).  For scripts/gemm_diag.py.
 PDT_API int pdt_gemm_diag_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
                                hipStream_t s) {
-  if (M % TM || N % TN || K % KB || diag < 0 || diag > 3) return (int)hipErrorInvalidValue;
+  if (M % TM || N % TN || K % KB || diag < 0 || diag > 4) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = M; a.ldb = N; a.ldc = N; a.k_per_split = (int)K;
@@ -489,7 +564,65 @@ PDT_API int pdt_gemm_diag_bf16(int diag, const void* A, const void* B, void* C, 
     case 0: gemm_kernel<L_TT, E_PLAIN, 0><<<grid, NTH, 0, s>>>(a); break;
     case 1: gemm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a); break;
     case 2: gemm_kernel<L_TT, E_PLAIN, 2><<<grid, NTH, 0, s>>>(a); break;
-    default: gemm_kernel<L_TT, E_PLAIN, 3><<<grid, NTH, 0, s>>>(a); break;
+    case 3: gemm_kernel<L_TT, E_PLAIN, 3><<<grid, NTH, 0, s>>>(a); break;
+    default: gemm_kernel<L_TT, E_PLAIN, 4><<<grid, NTH, 0, s>>>(a); break;
+  }
+  return (int)hipGetLastError();
+}
+
+PDT_API int pdt_gemm_ok(int layout, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int splits);
+
+// persistent grid: one workgroup per CU (128 KiB of LDS each), a multiple of 8 (XCD affinity of tile ids)
+static int persist_grid(int ntiles) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      n = 256;
+    return n;
+  }();
+  int g = cus < ntiles ? cus : ntiles;
+  return g >= 8 ? g & ~7 : g;
+}
+
+// NT diagnostics (A [M, K], B [N, K] row-major): diag 0 = production plain kernel, 4 = no epilogue stores,
+// 5 = persistent plain kernel
+PDT_API int pdt_gemm_diag_nt_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                                  hipStream_t s) {
+  if (M % TM || N % TN || K % KB || K < 2 * KB || (diag != 0 && diag != 4 && diag != 5))
+    return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = K; a.ldb = K; a.ldc = N; a.k_per_split = (int)K;
+  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  const int ntiles = (int)((M / TM) * (N / TN));
+  dim3 grid((unsigned)ntiles, 1);
+  if (diag == 0) gemm_kernel<L_NT, E_PLAIN, 0><<<grid, NTH, 0, s>>>(a);
+  else if (diag == 4) gemm_kernel<L_NT, E_PLAIN, 4><<<grid, NTH, 0, s>>>(a);
+  else gemm_kernel<L_NT, E_PLAIN, 0, true><<<dim3(persist_grid(ntiles), 1), NTH, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+// Persistent NT GEMM (plain / bias / bias+GELU epilogues): C[M, N] = A[M, K] B[N, K]^T, one workgroup per CU
+// walking its tiles with the next tile's first K-steps in flight under the current epilogue.  Shapes as
+// pdt_gemm_ok(NT) and K >= 128.
+PDT_API int pdt_gemm_nt_persist_bf16(int epi, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                                     int64_t lda, int64_t ldb, int64_t ldc, const void* bias, void* aux_out,
+                                     hipStream_t s) {
+  if (!pdt_gemm_ok(L_NT, M, N, K, lda, ldb, 1) || K < 2 * KB || ldc < N || ldc % 4) return (int)hipErrorInvalidValue;
+  if (epi != E_PLAIN && epi != E_BIAS && epi != E_GELU) return (int)hipErrorInvalidValue;
+  if ((epi == E_BIAS || epi == E_GELU) && !bias) return (int)hipErrorInvalidValue;
+  if (epi == E_GELU && !aux_out) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.bias = (const bf16_t*)bias; a.aux_out = (bf16_t*)aux_out;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.k_per_split = (int)K;
+  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  const dim3 grid(persist_grid((int)((M / TM) * (N / TN))), 1);
+  switch (epi) {
+    case E_PLAIN: gemm_kernel<L_NT, E_PLAIN, 0, true><<<grid, NTH, 0, s>>>(a); break;
+    case E_BIAS: gemm_kernel<L_NT, E_BIAS, 0, true><<<grid, NTH, 0, s>>>(a); break;
+    default: gemm_kernel<L_NT, E_GELU, 0, true><<<grid, NTH, 0, s>>>(a); break;
   }
   return (int)hipGetLastError();
 }

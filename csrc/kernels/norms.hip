@@ -23,12 +23,12 @@ constexpr int RPB = NT / 64; // rows per block (one per wave)
 
 template <typename T, typename W, int ITERS, bool RMS>
 __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
-                                                      T* __restrict__ sum_out, const W* __restrict__ w,
-                                                      const W* __restrict__ b, T* __restrict__ y,
-                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                      int rows, int N, float eps) {
-  // optional fused residual: s = x + res is written to sum_out and normalised (saves one full pass of
-  // the residual stream per norm site)
+                                                      const W* __restrict__ rb, T* __restrict__ sum_out,
+                                                      const W* __restrict__ w, const W* __restrict__ b,
+                                                      T* __restrict__ y, float* __restrict__ mean_out,
+                                                      float* __restrict__ rstd_out, int rows, int N, float eps) {
+  // optional fused residual: s = x + res (+ rb[col], the bias of the Linear that produced res) is written to
+  // sum_out and normalised (saves one full pass of the residual stream per norm site)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float invN = 1.f / (float)N;
   for (int row = blockIdx.x * RPB + wid; row < rows; row += gridDim.x * RPB) {
@@ -43,6 +43,12 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
         if (res != nullptr) {
           float r8[8];
           Vec8<T>::load(res + (int64_t)row * N + col, r8);
+          if (rb != nullptr) {
+            float b8[8];
+            Vec8<W>::load(rb + col, b8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r8[k] += b8[k];
+          }
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[it][k] += r8[k];
           Vec8<T>::store(sum_out + (int64_t)row * N + col, v[it]);
@@ -107,13 +113,16 @@ __global__ __launch_bounds__(NT) void norm_fwd_kernel(const T* __restrict__ x, c
 // dgamma/dbeta partials accumulate in registers; at the end the 4 waves of a workgroup fold them
 // through one [2][N] LDS buffer (wave by wave, no atomics) and the workgroup writes ONE partial row;
 // a 2-level column reduce (reduce.h) finishes dgamma/dbeta.
-template <typename T, typename W, int ITERS, bool RMS, bool DRES, int OCC>
+// DSUM: also the column sums of dx as stored (-> ds_part): the gradient of a bias folded into the forward's
+// residual sum (norm_fwd's rb), so the producing Linear needs no separate column-sum pass over its dY.
+template <typename T, typename W, int ITERS, bool RMS, bool DRES, int OCC, bool DSUM>
 __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const W* __restrict__ w, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                       T* __restrict__ dx, float* __restrict__ dw_part,
-                                                      float* __restrict__ db_part, int rows, int N) {
-  extern __shared__ __attribute__((aligned(16))) float sacc[];   // [2][N]
+                                                      float* __restrict__ db_part, float* __restrict__ ds_part,
+                                                      int rows, int N) {
+  extern __shared__ __attribute__((aligned(16))) float sacc[];   // [2 or 3][N]
   typedef typename Vec8<T>::raw_t raw_t;
   typedef typename Vec8<W>::raw_t wraw_t;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -128,12 +137,12 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
     cv[it] = col < N;
     cc[it] = cv[it] ? col : N - 8;
   }
-  float dwa[ITERS][8], dba[ITERS][8];
+  float dwa[ITERS][8], dba[ITERS][8], dsa[DSUM ? ITERS : 1][8];
   wraw_t wr[ITERS];
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; }
+    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; if constexpr (DSUM) dsa[it][k] = 0.f; }
     wr[it] = Vec8<W>::load_raw(w + cc[it]);
   }
   const int stride = gridDim.x * RPB;
@@ -202,6 +211,11 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] += rv[k];
       }
+      if constexpr (DSUM) {   // the bias gradient sums dx as stored (masked lanes hold a clamped column)
+        const float m = cv[it] ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dsa[it][k] += m * to_f<T>(from_f<T>(o[k]));
+      }
       if (cv[it]) Vec8<T>::store(dxr + cc[it], o);
       cx[it] = nx[it];
       cg[it] = ng[it];
@@ -211,6 +225,7 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
   // fold the 4 waves' accumulators: wave 0 stores, waves 1..3 add in turn (no atomics)
   float* sdw = sacc;
   float* sdb = sacc + N;
+  float* sds = sacc + 2 * N;
 #pragma unroll
   for (int turn = 0; turn < RPB; ++turn) {
     if (wid == turn) {
@@ -220,8 +235,13 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
         if (col < N) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            if (turn == 0) { sdw[col + k] = dwa[it][k]; sdb[col + k] = dba[it][k]; }
-            else { sdw[col + k] += dwa[it][k]; sdb[col + k] += dba[it][k]; }
+            if (turn == 0) {
+              sdw[col + k] = dwa[it][k]; sdb[col + k] = dba[it][k];
+              if constexpr (DSUM) sds[col + k] = dsa[it][k];
+            } else {
+              sdw[col + k] += dwa[it][k]; sdb[col + k] += dba[it][k];
+              if constexpr (DSUM) sds[col + k] += dsa[it][k];
+            }
           }
         }
       }
@@ -231,13 +251,16 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
   for (int c = threadIdx.x * 4; c < N; c += NT * 4) {
     *reinterpret_cast<f32x4*>(dw_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdw + c);
     if (db_part) *reinterpret_cast<f32x4*>(db_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sdb + c);
+    if constexpr (DSUM)
+      *reinterpret_cast<f32x4*>(ds_part + (int64_t)blockIdx.x * N + c) = *reinterpret_cast<const f32x4*>(sds + c);
   }
 }
 
 // ---- fallback: one block per row, streamed from global memory ----
 template <typename T, typename W, bool RMS>
 __global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, const T* __restrict__ res,
-                                                       T* __restrict__ sum_out, const W* __restrict__ w,
+                                                       const W* __restrict__ rb, T* __restrict__ sum_out,
+                                                       const W* __restrict__ w,
                                                        const W* __restrict__ b, T* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                        int rows, int N, float eps) {
@@ -245,7 +268,8 @@ __global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, 
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     if (res != nullptr) {
       for (int c = threadIdx.x; c < N; c += NT)
-        sum_out[(int64_t)row * N + c] = from_f<T>(to_f<T>(x[(int64_t)row * N + c]) + to_f<T>(res[(int64_t)row * N + c]));
+        sum_out[(int64_t)row * N + c] = from_f<T>(to_f<T>(x[(int64_t)row * N + c]) +
+                                                  (to_f<T>(res[(int64_t)row * N + c]) + (rb ? to_f<W>(rb[c]) : 0.f)));
       __syncthreads();
     }
     const T* xr = (res != nullptr ? sum_out : x) + (int64_t)row * N;
@@ -281,12 +305,13 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
                                                        const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                        T* __restrict__ dx,
                                                        float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                       int rows, int N) {
+                                                       float* __restrict__ ds_part, int rows, int N) {
   // partial row per block: rows handled by this block are accumulated straight into it
   __shared__ float red[RPB];
   float* dwp = dw_part + (int64_t)blockIdx.x * N;
   float* dbp = db_part ? db_part + (int64_t)blockIdx.x * N : nullptr;
-  for (int c = threadIdx.x; c < N; c += NT) { dwp[c] = 0.f; if (dbp) dbp[c] = 0.f; }
+  float* dsp = ds_part ? ds_part + (int64_t)blockIdx.x * N : nullptr;
+  for (int c = threadIdx.x; c < N; c += NT) { dwp[c] = 0.f; if (dbp) dbp[c] = 0.f; if (dsp) dsp[c] = 0.f; }
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const T* xr = x + (int64_t)row * N;
     const T* gr = dy + (int64_t)row * N;
@@ -309,6 +334,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_generic(const T* __restrict__ dy,
       float o = rstd * (g - bs - xh * a);
       if (dres != nullptr) o += to_f<T>(dres[(int64_t)row * N + c]);
       dxr[c] = from_f<T>(o);
+      if (dsp) dsp[c] += to_f<T>(from_f<T>(o));
     }
   }
 }
@@ -348,19 +374,21 @@ __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes
 
 template <typename T, typename W, bool RMS>
 __global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, const T* __restrict__ res,
-                                                     T* __restrict__ sum_out, const W* __restrict__ w,
+                                                     const W* __restrict__ rb, T* __restrict__ sum_out,
+                                                     const W* __restrict__ w,
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int N, float eps) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
   const bool col_ok = c0 < N;
-  float wr[4] = {0, 0, 0, 0}, br[4] = {0, 0, 0, 0};
+  float wr[4] = {0, 0, 0, 0}, br[4] = {0, 0, 0, 0}, rbr[4] = {0, 0, 0, 0};
   if (col_ok) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       wr[k] = to_f<W>(w[c0 + k]);
       if (!RMS && b != nullptr) br[k] = to_f<W>(b[c0 + k]);
+      if (rb != nullptr) rbr[k] = to_f<W>(rb[c0 + k]);
     }
   }
   const float inv_n = 1.f / N;
@@ -374,7 +402,7 @@ __global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, co
         float r[4];
         Vec4<T>::load(res + row * N + c0, r);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = to_f<T>(from_f<T>(v[k] + r[k]));   // the stored sum, rounded
+        for (int k = 0; k < 4; ++k) v[k] = to_f<T>(from_f<T>(v[k] + (r[k] + rbr[k])));   // the stored sum, rounded
         Vec4<T>::store(sum_out + row * N + c0, v);
       }
     }
@@ -406,8 +434,9 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
                                                      const W* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                      T* __restrict__ dx, float* __restrict__ dw_part,
-                                                     float* __restrict__ db_part, int rows, int N) {
-  __shared__ __attribute__((aligned(16))) float sred[2][RPB][64];
+                                                     float* __restrict__ db_part, float* __restrict__ ds_part,
+                                                     int rows, int N) {
+  __shared__ __attribute__((aligned(16))) float sred[3][RPB][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
   const bool col_ok = c0 < N;
@@ -416,7 +445,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
 #pragma unroll
     for (int k = 0; k < 4; ++k) wr[k] = to_f<W>(w[c0 + k]);
   }
-  float dwa[4] = {0, 0, 0, 0}, dba[4] = {0, 0, 0, 0};
+  float dwa[4] = {0, 0, 0, 0}, dba[4] = {0, 0, 0, 0}, dsa[4] = {0, 0, 0, 0};
   const float inv_n = 1.f / N;
   for (int64_t base = ((int64_t)blockIdx.x * RPB + wv) * SM_RPW; base < rows; base += (int64_t)gridDim.x * SM_RPB) {
     const int64_t row = base + sub;
@@ -448,6 +477,8 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] += rstd * (gw[k] - bs - xh[k] * a);
       Vec4<T>::store(dx + row * N + c0, o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dsa[k] += to_f<T>(from_f<T>(o[k]));
     }
   }
   // fold the 4 row groups of the wave (lanes c, c+16, c+32, c+48 share columns), then the block's waves
@@ -455,18 +486,22 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
   for (int k = 0; k < 4; ++k) {
     dwa[k] += __shfl_xor(dwa[k], 16, 64); dwa[k] += __shfl_xor(dwa[k], 32, 64);
     dba[k] += __shfl_xor(dba[k], 16, 64); dba[k] += __shfl_xor(dba[k], 32, 64);
+    dsa[k] += __shfl_xor(dsa[k], 16, 64); dsa[k] += __shfl_xor(dsa[k], 32, 64);
   }
   if (sub == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { sred[0][wv][c0 + k] = dwa[k]; sred[1][wv][c0 + k] = dba[k]; }
+    for (int k = 0; k < 4; ++k) {
+      sred[0][wv][c0 + k] = dwa[k]; sred[1][wv][c0 + k] = dba[k]; sred[2][wv][c0 + k] = dsa[k];
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < N; c += NT) {
-    float s0 = 0.f, s1 = 0.f;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int q = 0; q < RPB; ++q) { s0 += sred[0][q][c]; s1 += sred[1][q][c]; }
+    for (int q = 0; q < RPB; ++q) { s0 += sred[0][q][c]; s1 += sred[1][q][c]; s2 += sred[2][q][c]; }
     dw_part[(int64_t)blockIdx.x * N + c] = s0;
     if (db_part) db_part[(int64_t)blockIdx.x * N + c] = s1;
+    if (ds_part) ds_part[(int64_t)blockIdx.x * N + c] = s2;
   }
 }
 
@@ -474,17 +509,17 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
 using red::col_reduce;
 
 template <typename T, typename W, bool RMS>
-int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y, float* mean,
-               float* rstd, int rows, int N, float eps, hipStream_t st) {
-  const T* X = (const T*)x; const T* R = (const T*)res; T* S = (T*)sum_out;
+int launch_fwd(const void* x, const void* res, const void* rb, void* sum_out, const void* w, const void* b, void* y,
+               float* mean, float* rstd, int rows, int N, float eps, hipStream_t st) {
+  const T* X = (const T*)x; const T* R = (const T*)res; T* S = (T*)sum_out; const W* RB = (const W*)rb;
   const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
   if (small_rows(N)) {
-    norm_fwd_small<T, W, RMS><<<grid_for(rows, SM_RPB, 256 * 16), NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N,
+    norm_fwd_small<T, W, RMS><<<grid_for(rows, SM_RPB, 256 * 16), NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N,
                                                                               eps);
   } else if (N % 8 == 0 && N <= 8192) {
     const int grid = grid_for(rows, RPB, 256 * 16);
     const int iters = (N + 511) / 512;
-#define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N, eps)
+#define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N, eps)
     if (iters <= 1) PDT_NF(1);
     else if (iters <= 2) PDT_NF(2);
     else if (iters <= 4) PDT_NF(4);
@@ -492,7 +527,7 @@ int launch_fwd(const void* x, const void* res, void* sum_out, const void* w, con
     else PDT_NF(16);
 #undef PDT_NF
   } else {
-    norm_fwd_generic<T, W, RMS><<<grid_for(rows, 1, 256 * 8), NT, 0, st>>>(X, R, S, Wt, B, Y, mean, rstd, rows, N, eps);
+    norm_fwd_generic<T, W, RMS><<<grid_for(rows, 1, 256 * 8), NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N, eps);
   }
   return (int)hipGetLastError();
 }
@@ -506,24 +541,28 @@ int bwd_partial_rows(int rows, int N) {
   return grid_for(rows, 1, 512);
 }
 
-// workspace: fp32, >= (2 * bwd_partial_rows(rows, N) + 128) * N floats
+// workspace: fp32, >= (3 * bwd_partial_rows(rows, N) + 192) * N floats
 template <typename T, typename W, bool RMS>
 int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
-               void* dx, void* dw, void* db, float* ws, int rows, int N, int accumulate, hipStream_t st) {
+               void* dx, void* dw, void* db, void* ds, float* ws, int rows, int N, int accumulate, hipStream_t st) {
   const T* DY = (const T*)dy; const T* X = (const T*)x; const W* Wt = (const W*)w; T* DX = (T*)dx;
   const T* DR = (const T*)dres;
   const int R = bwd_partial_rows(rows, N);
   float* dwp = ws;
   float* dbp = (db != nullptr) ? ws + (int64_t)R * N : nullptr;
+  float* dsp = (ds != nullptr) ? ws + (int64_t)2 * R * N : nullptr;
   if (small_rows(N)) {
-    norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N);
+    norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N);
   } else if (N % 8 == 0 && N <= 8192) {
     const int iters = (N + 511) / 512;
-    const size_t lds = 2 * (size_t)N * sizeof(float);
+    const size_t lds = (dsp ? 3 : 2) * (size_t)N * sizeof(float);
     static const int occ2 = [] { const char* e = getenv("PDT_LN_BWD_OCC"); return e && atoi(e) == 2; }();
-#define PDT_NB1(I, O)                                                                                                 \
-  if (DR) norm_bwd_kernel<T, W, I, RMS, true, O><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N); \
-  else norm_bwd_kernel<T, W, I, RMS, false, O><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N)
+#define PDT_NB2(I, O, S)                                                                                                \
+  if (DR) norm_bwd_kernel<T, W, I, RMS, true, O, S><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, \
+                                                                       rows, N);                                        \
+  else norm_bwd_kernel<T, W, I, RMS, false, O, S><<<R, NT, lds, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N)
+#define PDT_NB1(I, O) \
+  do { if (dsp) { PDT_NB2(I, O, true); } else { PDT_NB2(I, O, false); } } while (0)
 #define PDT_NB(I) \
   do { if (occ2) { PDT_NB1(I, 2); } else { PDT_NB1(I, 1); } } while (0)
     if (iters <= 1) PDT_NB(1);
@@ -533,12 +572,14 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
     else PDT_NB(16);
 #undef PDT_NB
 #undef PDT_NB1
+#undef PDT_NB2
   } else {
-    norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, rows, N);
+    norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N);
   }
-  float* ws2 = ws + (int64_t)2 * R * N;
+  float* ws2 = ws + (int64_t)3 * R * N;
   if (dw) col_reduce<W>(dwp, R, N, (W*)dw, ws2, accumulate, st);
   if (db) col_reduce<W>(dbp, R, N, (W*)db, ws2 + (int64_t)64 * N, accumulate, st);
+  if (ds) col_reduce<W>(dsp, R, N, (W*)ds, ws2 + (int64_t)128 * N, 0, st);
   return (int)hipGetLastError();
 }
 
@@ -546,30 +587,33 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
 
 // dtype codes: x/y in {kF32, kBF16}; w/b in {kF32, kBF16}.  rms=1 selects RMSNorm (b ignored, mean unused).
 // res/sum_out (nullable): fused residual -- sum_out = x + res is written and normalised.
-PDT_API int pdt_norm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
-                         float* mean, float* rstd, int rows, int N, float eps, int xdt, int wdt, int rms,
-                         hipStream_t st) {
+// res_bias (nullable, w/b dtype, [N]): added with res (the bias of the Linear that produced res).
+PDT_API int pdt_norm_fwd(const void* x, const void* res, const void* res_bias, void* sum_out, const void* w,
+                         const void* b, void* y, float* mean, float* rstd, int rows, int N, float eps, int xdt, int wdt,
+                         int rms, hipStream_t st) {
+  if (res_bias && !res) return (int)hipErrorInvalidValue;
 #define PDT_DISPATCH(R)                                                                                      \
-  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st); \
-  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);   \
-  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);     \
-  if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, res, sum_out, w, b, y, mean, rstd, rows, N, eps, st);
+  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);
   if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
 #undef PDT_DISPATCH
   return (int)hipErrorInvalidValue;
 }
 
-PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return (2 * bwd_partial_rows(rows, N) + 128) * N; }
+PDT_API int pdt_norm_bwd_workspace_floats(int rows, int N) { return (3 * bwd_partial_rows(rows, N) + 192) * N; }
 
 // dres (nullable): gradient arriving at the fused residual sum, added into dx.
+// ds (nullable, w dtype, [N]): column sums of dx -- the gradient of norm_fwd's res_bias (never accumulated).
 PDT_API int pdt_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                         const void* dres, void* dx, void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt,
-                         int rms, int accumulate, hipStream_t st) {
+                         const void* dres, void* dx, void* dw, void* db, void* ds, float* ws, int rows, int N, int xdt,
+                         int wdt, int rms, int accumulate, hipStream_t st) {
 #define PDT_DISPATCH(R)                                                                                         \
-  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st); \
-  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);   \
-  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);     \
-  if (xdt == kF32 && wdt == kBF16) return launch_bwd<float, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ws, rows, N, accumulate, st);
+  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ds, ws, rows, N, accumulate, st); \
+  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ds, ws, rows, N, accumulate, st);   \
+  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ds, ws, rows, N, accumulate, st);     \
+  if (xdt == kF32 && wdt == kBF16) return launch_bwd<float, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, ds, ws, rows, N, accumulate, st);
   if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
 #undef PDT_DISPATCH
   return (int)hipErrorInvalidValue;

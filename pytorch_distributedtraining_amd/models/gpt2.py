@@ -13,6 +13,7 @@ MI355X-first choices:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -54,6 +55,10 @@ GPT2_CONFIGS = {
 }
 
 
+# attention c_proj bias folded into ln_2's fused residual-add kernel (its gradient from the norm backward's pass)
+FOLD_PROJ_BIAS = os.environ.get("PDT_FOLD_PROJ_BIAS", "1") == "1"
+
+
 def gpt2_config(name: str, **overrides) -> GPT2Config:
     kw = dict(GPT2_CONFIGS[name])
     kw.update(overrides)
@@ -68,11 +73,16 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = Linear(cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x):
+    def forward(self, x, fold_bias: bool = False):
+        """Attention branch output; with ``fold_bias`` the pair (c_proj(y) without its bias, the bias) for a
+        consumer that adds the bias itself (the block's fused residual-add + LayerNorm, whose backward then
+        returns the bias gradient from its own pass instead of a separate column sum over dY)."""
         B, S, C = x.shape
         qkv = self.c_attn(x).view(B, S, 3, self.n_head, self.head_dim)
-        y = flash_attn_qkvpacked(qkv, causal=True)
-        return self.c_proj(y.reshape(B, S, C))
+        y = flash_attn_qkvpacked(qkv, causal=True).reshape(B, S, C)
+        if fold_bias:
+            return self.c_proj.matmul(y), self.c_proj.bias
+        return self.c_proj(y)
 
 
 class MLP(nn.Module):
@@ -108,7 +118,11 @@ class GPT2Block(nn.Module):
             h = self.ln_1(x)
         else:
             h, x = self.ln_1.forward_add(x, pending)
-        y, x = self.ln_2.forward_add(x, self.attn(h))
+        if FOLD_PROJ_BIAS:
+            a, a_bias = self.attn(h, fold_bias=True)   # c_proj's bias joins the residual sum in ln_2's kernel
+            y, x = self.ln_2.forward_add(x, a, a_bias)
+        else:
+            y, x = self.ln_2.forward_add(x, self.attn(h))
         return x, self.mlp(y)
 
 

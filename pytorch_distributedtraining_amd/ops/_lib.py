@@ -41,11 +41,11 @@ _SIGS = {
     "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "pdt_cast_f32_bf16_mt": [c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                     c_float, c_int, c_int, c_int, c_void_p],
+    "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                     c_int, c_float, c_int, c_int, c_int, c_void_p],
     "pdt_norm_bwd_workspace_floats": [c_int, c_int],
     "pdt_norm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_colsum_ws_floats": [c_int, c_int],
     "pdt_bias_gelu_bwd_db": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                              c_int, c_int, c_int, c_void_p],
@@ -128,6 +128,9 @@ _SIGS = {
                          c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p],
     "pdt_gemm_ok": [c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int],
     "pdt_gemm_diag_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "pdt_gemm_diag_nt_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "pdt_gemm_nt_persist_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                 c_int64, c_void_p, c_void_p, c_void_p],
     "pdt_gemm_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                       c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],

@@ -47,23 +47,36 @@ def _launch(layout, epi, a, b, c, m, n, k, bias=None, aux=None, aux_out=None, db
               _lib.ptr(ws), splits, _lib.stream_handle(a.device))
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
-    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N]."""
+def _launch_persist(epi, a, b, c, m, n, k, bias=None, aux_out=None):
+    _lib.call("pdt_gemm_nt_persist_bf16", epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
+              b.stride(0), c.stride(0), _lib.ptr(bias), _lib.ptr(aux_out), _lib.stream_handle(a.device))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None, persist: bool = False) -> torch.Tensor:
+    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N].  ``persist``: one workgroup per CU walking its tiles
+    (the next tile's first K-steps load under the current tile's epilogue; K >= 128)."""
     m, k = a.shape
     n = b.shape[0]
     c = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
-    _launch(L_NT, E_BIAS if bias is not None else E_PLAIN, a, b, c, m, n, k, bias=bias)
+    epi = E_BIAS if bias is not None else E_PLAIN
+    if persist:
+        _launch_persist(epi, a, b, c, m, n, k, bias=bias)
+    else:
+        _launch(L_NT, epi, a, b, c, m, n, k, bias=bias)
     return c
 
 
-def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor):
+def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor, persist: bool = False):
     """(gelu_tanh(a b^T + bias), a b^T + bias) -- both bf16 [M, N]; the GELU reads the stored (rounded)
     pre-activation, which is what the backward differentiates."""
     m, k = a.shape
     n = b.shape[0]
     y = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     pre = torch.empty_like(y)
-    _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
+    if persist:
+        _launch_persist(E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
+    else:
+        _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
     return y, pre
 
 

@@ -16,29 +16,31 @@ import torch.nn.functional as F
 from . import _lib
 
 
-def _norm_fwd(x2, w, b, eps, rms, res2=None):
+def _norm_fwd(x2, w, b, eps, rms, res2=None, rb=None):
     rows, n = x2.shape
     y = torch.empty_like(x2)
     s = torch.empty_like(x2) if res2 is not None else None
     rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
     mean = None if rms else torch.empty(rows, dtype=torch.float32, device=x2.device)
-    _lib.call("pdt_norm_fwd", x2.data_ptr(), _lib.ptr(res2), _lib.ptr(s), w.data_ptr(), _lib.ptr(b), y.data_ptr(),
-              _lib.ptr(mean), rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype),
+    _lib.call("pdt_norm_fwd", x2.data_ptr(), _lib.ptr(res2), _lib.ptr(rb), _lib.ptr(s), w.data_ptr(), _lib.ptr(b),
+              y.data_ptr(), _lib.ptr(mean), rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype),
               _lib.dtype_code(w.dtype), 1 if rms else 0, _lib.stream_handle(x2.device))
     return y, mean, rstd, s
 
 
-def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms, dres2=None):
+def _norm_bwd(dy2, x2, w, mean, rstd, need_b, rms, dres2=None, need_ds=False):
+    """(dx, dgamma, dbeta | None, colsum(dx) | None) -- the last is the gradient of a residual bias (rb)."""
     rows, n = x2.shape
     lib = _lib.require()
     dx = torch.empty_like(x2)
     dw = torch.empty_like(w)
     db = torch.empty_like(w) if need_b else None
+    ds = torch.empty_like(w) if need_ds else None
     ws = torch.empty(lib.pdt_norm_bwd_workspace_floats(rows, n), dtype=torch.float32, device=x2.device)
     _lib.call("pdt_norm_bwd", dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), _lib.ptr(mean), rstd.data_ptr(),
-              _lib.ptr(dres2), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(), rows, n,
+              _lib.ptr(dres2), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), _lib.ptr(ds), ws.data_ptr(), rows, n,
               _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype), 1 if rms else 0, 0, _lib.stream_handle(x2.device))
-    return dx, dw, db
+    return dx, dw, db, ds
 
 
 class _LayerNormFn(torch.autograd.Function):
@@ -55,7 +57,7 @@ class _LayerNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
         dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
-        dx, dw, db = _norm_bwd(dy2, x2, w, mean, rstd, ctx.has_bias, rms=False)
+        dx, dw, db, _ = _norm_bwd(dy2, x2, w, mean, rstd, ctx.has_bias, rms=False)
         return dx.view(dy.shape), dw, db, None
 
 
@@ -72,21 +74,23 @@ class _RMSNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, rstd = ctx.saved_tensors
         dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
-        dx, dw, _ = _norm_bwd(dy2, x2, w, None, rstd, False, rms=True)
+        dx, dw, _, _ = _norm_bwd(dy2, x2, w, None, rstd, False, rms=True)
         return dx.view(dy.shape), dw, None
 
 
 class _AddNormFn(torch.autograd.Function):
-    """(y, s) = (norm(x + r), x + r) in one pass; backward folds the residual gradient ds into dx."""
+    """(y, s) = (norm(x + r + rb), x + r + rb) in one pass; backward folds the residual gradient ds into dx and,
+    with a residual bias rb (the bias of the Linear that produced r), returns its gradient colsum(dx) from the
+    same pass -- the Linear then runs bias-free and skips its own column sum over dY."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, rms):
+    def forward(ctx, x, r, rb, weight, bias, eps, rms):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         r2 = r.reshape(-1, shape[-1]).contiguous()
-        y, mean, rstd, s = _norm_fwd(x2, weight, bias, eps, rms, res2=r2)
+        y, mean, rstd, s = _norm_fwd(x2, weight, bias, eps, rms, res2=r2, rb=rb)
         ctx.save_for_backward(s, weight, mean, rstd)
-        ctx.has_bias, ctx.rms = bias is not None, rms
+        ctx.has_bias, ctx.rms, ctx.has_rb = bias is not None, rms, rb is not None
         return y.view(shape), s.view(shape)
 
     @staticmethod
@@ -97,17 +101,20 @@ class _AddNormFn(torch.autograd.Function):
             dy = torch.zeros_like(s)
         dy2 = dy.reshape(-1, n).contiguous()
         ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
-        dx, dw, db = _norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2)
+        need_rb = ctx.has_rb and ctx.needs_input_grad[2]
+        dx, dw, db, drb = _norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2, need_ds=need_rb)
         dx = dx.view(dy.shape)
-        return dx, dx, dw, db, None, None
+        return dx, dx, drb, dw, db, None, None
 
 
-def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False):
-    """Fused residual add + LayerNorm/RMSNorm: returns (norm(x + r), x + r)."""
-    if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16) or r.dtype != x.dtype:
-        s = x + r
+def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False, r_bias=None):
+    """Fused residual add + LayerNorm/RMSNorm: returns (norm(x + r + r_bias), x + r + r_bias); ``r_bias``
+    (optional, [N], the norm's parameter dtype) is the bias of the Linear that produced r."""
+    if (not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16) or r.dtype != x.dtype
+            or (r_bias is not None and r_bias.dtype != weight.dtype)):
+        s = x + r if r_bias is None else x + (r + r_bias.to(r.dtype))
         return (rms_norm(s, weight, eps) if rms else layer_norm(s, weight, bias, eps)), s
-    return _AddNormFn.apply(x, r, weight, bias, eps, rms)
+    return _AddNormFn.apply(x, r, r_bias, weight, bias, eps, rms)
 
 
 def _use_native(x):
@@ -155,20 +162,20 @@ class LayerNorm(nn.Module):
                 return layer_norm(x, self.weight, self.bias, self.eps)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
-    def forward_add(self, x, r):
-        """(LN(x + r), x + r) with one kernel pass."""
-        return _ln_forward_add(self, x, r, rms=False)
+    def forward_add(self, x, r, r_bias=None):
+        """(LN(x + r + r_bias), x + r + r_bias) with one kernel pass."""
+        return _ln_forward_add(self, x, r, rms=False, r_bias=r_bias)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"
 
 
-def _ln_forward_add(mod, x, r, rms):
+def _ln_forward_add(mod, x, r, rms, r_bias=None):
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
-            return add_norm(x.to(dt), r.to(dt), mod.weight, getattr(mod, "bias", None), mod.eps, rms)
-    return add_norm(x, r, mod.weight, getattr(mod, "bias", None), mod.eps, rms)
+            return add_norm(x.to(dt), r.to(dt), mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias)
+    return add_norm(x, r, mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias)
 
 
 class RMSNorm(nn.Module):
@@ -184,5 +191,5 @@ class RMSNorm(nn.Module):
                 return rms_norm(x, self.weight, self.eps)
         return rms_norm(x, self.weight, self.eps)
 
-    def forward_add(self, x, r):
-        return _ln_forward_add(self, x, r, rms=True)
+    def forward_add(self, x, r, r_bias=None):
+        return _ln_forward_add(self, x, r, rms=True, r_bias=r_bias)

@@ -429,20 +429,26 @@ def test_ddp_bf16_engine_single_gpu_step():
     assert torch.equal(g.flat_param, params[0].detach().bfloat16())   # compute copy refreshed by the kernel
 
 
+@pytest.mark.parametrize("rbias", [False, True])
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("N", [2048, 96, 4096, 60])
-def test_fused_add_norm(rms, N):
+@pytest.mark.parametrize("N", [2048, 96, 4096, 60, 10240])
+def test_fused_add_norm(rms, N, rbias):
+    """Fused residual add (+ the producing Linear's bias, whose gradient is colsum(dx) from the same backward
+    pass) + LayerNorm / RMSNorm against fp32 torch; N = 10240 takes the generic (one block per row) kernels."""
     from pytorch_distributedtraining_amd.ops.norms import add_norm
-    x = torch.randn(300, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    r = torch.randn(300, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    rows = 3000 if N == 2048 else 300
+    x = torch.randn(rows, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(rows, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_()
     b = None if rms else (0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_()
-    y, s = add_norm(x, r, w, b, 1e-5, rms=rms)
+    rb = (0.5 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_() if rbias else None
+    y, s = add_norm(x, r, w, b, 1e-5, rms=rms, r_bias=rb)
     dy, ds = torch.randn_like(y), torch.randn_like(s)
     torch.autograd.backward([y, s], [dy, ds])
     xr, rr, wr = (t.detach().float().requires_grad_() for t in (x, r, w))
     br = None if rms else b.detach().float().requires_grad_()
-    sr = xr + rr
+    rbr = rb.detach().float().requires_grad_() if rbias else None
+    sr = xr + rr if rb is None else xr + rr + rbr
     if rms:
         yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
     else:
@@ -453,6 +459,10 @@ def test_fused_add_norm(rms, N):
     assert rel_err(w.grad, wr.grad) < 2e-2
     if not rms:
         assert rel_err(b.grad, br.grad) < 2e-2
+    if rbias:
+        assert rel_err(rb.grad, rbr.grad) < 2e-2
+        # exactly the column sum of the stored dx (fp32 accumulation of the bf16 values)
+        assert rel_err(rb.grad, x.grad.float().sum(0)) < 1e-2
 
 
 def test_llama_tiny_fsdp_step():
@@ -660,6 +670,11 @@ def test_hand_gemm_nt_epilogues(M, N, K):
     y, pre = G.gemm_nt_gelu(a, b, bias)
     assert rel_err(pre, ref + bias.float()) < 4e-3
     assert rel_err(y, _gelu_tanh(ref + bias.float())) < 6e-3
+    # persistent form: one workgroup per CU walking its tiles (next tile's loads under the epilogue)
+    assert rel_err(G.gemm_nt(a, b, persist=True), ref) < 4e-3
+    assert rel_err(G.gemm_nt(a, b, bias, persist=True), ref + bias.float()) < 4e-3
+    y2, pre2 = G.gemm_nt_gelu(a, b, bias, persist=True)
+    assert torch.equal(y2, y) and torch.equal(pre2, pre)
     h = torch.randn(M, N, device=DEV).bfloat16()
     g, db = G.gemm_nt_dgelu(a, b, h)
     hr = h.float().requires_grad_()
@@ -668,16 +683,17 @@ def test_hand_gemm_nt_epilogues(M, N, K):
     assert rel_err(db, hr.grad.sum(0)) < 6e-3
 
 
-def test_hand_gemm_nt_gelu_full_grid_production_shape():
-    """GPT-2 1.3B c_fc at 96 x 1024 tokens (98,304 x 8,192 x 2,048, the full grid of 256 x 256 tiles): every
-    element of the GELU output and the kept pre-activation against fp32."""
+@pytest.mark.parametrize("persist", [False, True])
+def test_hand_gemm_nt_gelu_full_grid_production_shape(persist):
+    """GPT-2 1.3B c_fc at 96 x 1024 tokens (98,304 x 8,192 x 2,048, the full grid of 256 x 256 tiles; persistent:
+    256 workgroups x 48 tiles each): every element of the GELU output and the kept pre-activation against fp32."""
     from pytorch_distributedtraining_amd.ops import gemm as G
     M, N, K = 96 * 1024, 8192, 2048
     torch.manual_seed(7)
     a = torch.randn(M, K, device=DEV).bfloat16()
     b = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
     bias = torch.randn(N, device=DEV).bfloat16()
-    y, pre = G.gemm_nt_gelu(a, b, bias)
+    y, pre = G.gemm_nt_gelu(a, b, bias, persist=persist)
     ref = torch.addmm(bias.float(), a.float(), b.float().t())
     for got, want in ((pre, ref), (y, _gelu_tanh(ref))):
         rms = float(want.square().mean().sqrt())
