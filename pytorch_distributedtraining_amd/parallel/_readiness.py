@@ -99,3 +99,29 @@ class Readiness:
         for h in self._handles:
             h.remove()
         self._handles = []
+
+
+class NullReadiness:
+    """One rank: no collective to launch, so no hook at all.  (Native hooks hold the parameters' AccumulateGrad
+    nodes, which remember the stream they were created on; a HIP-graph capture on another stream then has
+    autograd synchronise with that uncaptured stream -- torch 2.10 warns "AccumulateGrad node's stream does
+    not match" -- and ROCm faults ending such a capture.  Trainer.graph runs on exactly this one-rank path.)"""
+    kind = "none"
+    observing = False
+    enabled = False
+
+    def set_enabled(self, on: bool):
+        pass
+
+    def flush(self):
+        return []
+
+    def all_released(self) -> bool:
+        return True
+
+    def reset(self):
+        pass
+
+    def remove(self):
+        pass
+

@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from ..utils import profiling as prof
 from ..utils.native import require_runtime
-from ._readiness import Readiness
+from ._readiness import NullReadiness, Readiness
 from .comm import Comm, default_comm
 
 _DT_ID = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
@@ -215,6 +215,10 @@ class DistributedDataParallel(nn.Module):
         gradient order for the rebuild.  Callbacks hold the engine weakly (the C++ side is invisible to GC)."""
         if self._ready is not None:
             self._ready.remove()
+        if self.comm.world_size == 1:
+            self._ready = NullReadiness()
+            self._rebuild_pending = False       # bucket order only matters to the collectives
+            return
         ref = weakref.ref(self)
         self._ready = Readiness(
             self.params, [list(b.params) for b in self.plan],

@@ -44,7 +44,7 @@ from torch.optim import Optimizer
 from ..optim.clip import clip_grad_norm_
 from ..utils import profiling as prof
 from ..utils.native import require_runtime
-from ._readiness import Readiness
+from ._readiness import NullReadiness, Readiness
 from .comm import Comm, default_comm
 from .ddp import sync_buffers
 
@@ -426,8 +426,9 @@ class ShardedDataParallel(nn.Module):
         # bucket readiness on C++ AccumulateGrad post hooks (parallel/_readiness.py): Python runs once per ready
         # bucket; frozen parameters get no hook and their buckets are released at the end of backward
         ref = weakref.ref(self)
-        self._ready = Readiness(self.params, [gidx[b] for b in range(len(self._buckets))],
-                                on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b))
+        self._ready = NullReadiness() if self.comm.world_size == 1 else \
+            Readiness(self.params, [gidx[b] for b in range(len(self._buckets))],
+                      on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b))
         self._ready.set_enabled(self.comm.world_size > 1)
 
     # ------------------------------------------------------------------ gradient storage
