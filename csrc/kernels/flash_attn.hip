@@ -21,6 +21,7 @@
 // Used by the GPT-2 / Llama models (BASELINE.json configs 3-5; SURVEY.md K16 "flash attention
 // (causal, head_dim 64/128)").
 #include "common.h"
+#include "reduce.h"
 #include <stdlib.h>
 
 using namespace pdt;
@@ -151,6 +152,11 @@ struct AttnParams {
   int B, H, Hkv, Sq, Sk;
   float scale;   // softmax scale (natural domain)
   int order;     // workgroup -> block order: 0 heavy-first, 1 XCD-grouped (block_order)
+  // backward, nullable: per-workgroup column sums of the stored dQ / dK, dV rows (the bias gradient of the
+  // Linear that produced q, k, v -- GPT-2's c_attn -- without a separate column-sum pass over dqkv):
+  // cs_q [B * nqb][H * D] (nqb = query blocks of the dQ kernel), cs_kv [B * nkb][2][Hkv * D] (nkb = Sk / 128)
+  float* cs_q;
+  float* cs_kv;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -770,6 +776,89 @@ __device__ __forceinline__ void store_row16(bf16_t* row, const f32x16 (&acc)[DT]
         *reinterpret_cast<u32x4*>(row + dt * 32 + 16 * pr + 8 * h) = v;
       }
     }
+}
+
+// store_row16 that also returns the stored (bf16-rounded, scaled) values as floats, zero for a masked row:
+// v[(dt * 2 + pr) * 8 + k] is column dt * 32 + 16 * pr + 8 * h + k of this lane's row
+template <int DT>
+__device__ __forceinline__ void store_row16_vals(bf16_t* row, const f32x16 (&acc)[DT], float scale, int h, bool ok,
+                                                 float (&v)[DT * 16]) {
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      unsigned a[2], c[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int g0 = 2 * pr, g1 = 2 * pr + 1;
+        a[k] = (unsigned)f2bf(acc[dt][4 * g0 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g0 + 2 * k + 1] * scale) << 16);
+        c[k] = (unsigned)f2bf(acc[dt][4 * g1 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g1 + 2 * k + 1] * scale) << 16);
+        const auto r = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+        a[k] = r[0];
+        c[k] = r[1];
+      }
+      u32x4 q;
+      q[0] = a[0]; q[1] = a[1]; q[2] = c[0]; q[3] = c[1];
+      if (ok) *reinterpret_cast<u32x4*>(row + dt * 32 + 16 * pr + 8 * h) = q;
+      const float m = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[(dt * 2 + pr) * 8 + 2 * k] = m * __uint_as_float(q[k] << 16);
+        v[(dt * 2 + pr) * 8 + 2 * k + 1] = m * __uint_as_float(q[k] & 0xffff0000u);
+      }
+    }
+}
+
+// Column sums over the 32 rows (lanes c32 = 0..31) of a wave half: a reduce-scatter butterfly (each step halves
+// the values a lane keeps, 62 exchanges for 64 values instead of 320 for a full all-reduce).  In: N values per
+// lane (index i = the store_row16_vals layout); out: lane c32 holds the sums of indices c32 * (N / 32) + e.
+template <int NV, int M, int N>
+__device__ __forceinline__ void colsum32_step(float (&v)[N], int c32) {
+  // NV live values v[0, NV); exchange with lane ^ M (compile-time indices only: the array stays in registers)
+  const bool up = (c32 & M) != 0;   // this lane keeps the upper half
+#pragma unroll
+  for (int i = 0; i < NV / 2; ++i) {
+    const float send = up ? v[i] : v[i + NV / 2];
+    const float keep = up ? v[i + NV / 2] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+  if constexpr (M > 1) colsum32_step<NV / 2, M / 2, N>(v, c32);
+}
+template <int N>
+__device__ __forceinline__ void colsum32_scatter(float (&v)[N], int c32) {
+  static_assert(N == 32 || N == 64, "D 64 or 128");
+  colsum32_step<N, 16, N>(v, c32);
+}
+
+// one workgroup's partial column sums of its NW waves' stored rows -> out[0, D) (one fp32 row); lds: >= NW * D
+// floats of workgroup LDS no longer in use (every wave has passed its last read of it: barrier first)
+// Raw barriers (LDS counter only): __syncthreads() would also wait for this wave's just-issued dQ / dK / dV
+// row stores to complete (vmcnt(0)) -- measured +0.7 ms per flagship attention backward with it, 4x the
+// separate column-sum pass this replaces.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int D, int NW>
+__device__ __forceinline__ void wg_colsum_store(float (&v)[D / 2], float* lds, float* out, int w, int lane) {
+  constexpr int E = D / 64;             // values left per lane after the butterfly
+  const int h = lane >> 5, c32 = lane & 31;
+  colsum32_scatter<D / 2>(v, c32);
+  lds_barrier();                        // every wave is past its last read of the reused LDS
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = c32 * E + e;
+    lds[w * D + (i >> 4) * 32 + ((i >> 3) & 1) * 16 + 8 * h + (i & 7)] = v[e];
+  }
+  lds_barrier();
+  if ((int)threadIdx.x < D) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) t += lds[q * D + threadIdx.x];
+    out[threadIdx.x] = t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1796,8 +1885,20 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
     }
   }
   acc_fence();
-  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
-  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
+  if (p.cs_kv == nullptr) {
+    store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
+    store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
+  } else {   // + this workgroup's column sums of the stored dK / dV rows (the k / v parts of the bias gradient)
+    float vals[DT * 16];
+    float* row = p.cs_kv + ((int64_t)b * gridDim.x + kb) * 2 * p.Hkv * D + hk * D;
+    float* lds = reinterpret_cast<float*>(smem);
+    store_row16_vals<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk,
+                         vals);
+    wg_colsum_store<D, 4>(vals, lds, row, w, lane);
+    store_row16_vals<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk, vals);
+    lds_barrier();     // the k sums' LDS reads are done before the v sums overwrite it
+    wg_colsum_store<D, 4>(vals, lds, row + p.Hkv * D, w, lane);
+  }
 }
 
 template <int D, bool CAUSAL>
@@ -1942,7 +2043,15 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
       BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
   }
-  store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
+  if (p.cs_q == nullptr) {
+    store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
+  } else {
+    float vals[DT * 16];
+    store_row16_vals<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq,
+                         vals);
+    wg_colsum_store<D, 4>(vals, reinterpret_cast<float*>(smem),
+                          p.cs_q + ((int64_t)b * gridDim.x + qb) * p.H * D + hq * D, w, lane);
+  }
 }
 
 // dK/dV v5: dK/dV v3 (4 waves x 32 keys, one wave per SIMD: its 312 registers rule out a second wave) with
@@ -2106,7 +2215,15 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     }
     stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
-  store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
+  if (p.cs_q == nullptr) {
+    store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
+  } else {
+    float vals[DT * 16];
+    store_row16_vals<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq,
+                         vals);
+    wg_colsum_store<D, NW>(vals, reinterpret_cast<float*>(smem),
+                           p.cs_q + ((int64_t)b * gridDim.x + qb) * p.H * D + hq * D, w, lane);
+  }
 }
 
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
@@ -2276,12 +2393,47 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
 
+// rows of the backward's column-sum partials (cs_q, cs_kv) for the current kernel variant; 0 = the variant
+// does not produce them
+static void colsum_rows(int B, int Sq, int Sk, int D, int& rq, int& rkv) {
+  const int v = bwd_variant(D);
+  rq = rkv = 0;
+  if (v == 8 || v == 9) rq = B * ((Sq + 255) / 256);
+  else if (v == 3 || v == 4 || v == 7) rq = B * ((Sq + 127) / 128);
+  else return;
+  rkv = B * ((Sk + 127) / 128);
+}
+
+// fp32 workspace floats pdt_flash_attn_bwd needs for the bias-gradient column sums (0: unsupported by the
+// current backward variant -- the caller sums dqkv itself)
+PDT_API int64_t pdt_flash_attn_colsum_ws_floats(int B, int H, int Hkv, int Sq, int Sk, int D) {
+  if (D != 64 && D != 128) return 0;
+  int rq, rkv;
+  colsum_rows(B, Sq, Sk, D, rq, rkv);
+  if (rq == 0) return 0;
+  const int64_t hd = (int64_t)H * D, kd = (int64_t)2 * Hkv * D;
+  return (int64_t)rq * hd + (int64_t)rkv * kd + 64 * (hd + kd);
+}
+
 // strides[0..23]: q k v o dout dq dk dv, each (b, s, h).  delta: fp32 workspace of B*H*Sq.
+// dbias (nullable; dtype code dbias_dt: bf16 or fp32): column sums of the stored dq | dk | dv rows -> [H*D |
+// Hkv*D | Hkv*D] (the bias gradient of a packed qkv projection), from per-workgroup partials the dQ / dK-dV
+// kernels write into cs_ws (pdt_flash_attn_colsum_ws_floats) and a deterministic column reduce.
 PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
                                const void* dout, void* dq, void* dk, void* dv, float* delta, const int64_t* strides,
-                               int B, int H, int Hkv, int Sq, int Sk, int D, float scale, int causal, hipStream_t st) {
+                               int B, int H, int Hkv, int Sq, int Sk, int D, float scale, int causal, float* cs_ws,
+                               void* dbias, int dbias_dt, hipStream_t st) {
   if (H % Hkv != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  int rq = 0, rkv = 0;
+  if (dbias) {
+    colsum_rows(B, Sq, Sk, D, rq, rkv);
+    if (rq == 0 || !cs_ws || (dbias_dt != kBF16 && dbias_dt != kF32)) return (int)hipErrorInvalidValue;
+  }
   AttnParams p{};
+  if (dbias) {
+    p.cs_q = cs_ws;
+    p.cs_kv = cs_ws + (int64_t)rq * H * D;
+  }
   p.q = (const bf16_t*)q; p.k = (const bf16_t*)k; p.v = (const bf16_t*)v; p.o = (bf16_t*)o;
   p.lse = const_cast<float*>(lse); p.dout = (const bf16_t*)dout;
   p.dq = (bf16_t*)dq; p.dk = (bf16_t*)dk; p.dv = (bf16_t*)dv; p.delta = delta;
@@ -2295,7 +2447,18 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.dv_sb = strides[21]; p.dv_ss = strides[22]; p.dv_sh = strides[23];
   p.B = B; p.H = H; p.Hkv = Hkv; p.Sq = Sq; p.Sk = Sk; p.scale = scale;
   p.order = block_order_mode(B, Hkv, Sk, D);
-  return D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
+  const int err = D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
+  if (err || !dbias) return err;
+  const int hd = H * D, kd = 2 * Hkv * D;
+  float* ws2 = p.cs_kv + (int64_t)rkv * kd;
+  if (dbias_dt == kBF16) {
+    red::col_reduce<bf16_t>(p.cs_q, rq, hd, (bf16_t*)dbias, ws2, 0, st);
+    red::col_reduce<bf16_t>(p.cs_kv, rkv, kd, (bf16_t*)dbias + hd, ws2 + (int64_t)64 * hd, 0, st);
+  } else {
+    red::col_reduce<float>(p.cs_q, rq, hd, (float*)dbias, ws2, 0, st);
+    red::col_reduce<float>(p.cs_kv, rkv, kd, (float*)dbias + hd, ws2 + (int64_t)64 * hd, 0, st);
+  }
+  return (int)hipGetLastError();
 }
 
 // workgroup -> block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ: 0 heavy-first, 1 XCD-grouped);

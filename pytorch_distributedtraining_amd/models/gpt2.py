@@ -79,7 +79,9 @@ class CausalSelfAttention(nn.Module):
         returns the bias gradient from its own pass instead of a separate column sum over dY)."""
         B, S, C = x.shape
         qkv = self.c_attn(x).view(B, S, 3, self.n_head, self.head_dim)
-        y = flash_attn_qkvpacked(qkv, causal=True).reshape(B, S, C)
+        # c_attn's bias gradient comes out of the attention backward kernels (per-workgroup column sums of the
+        # dq / dk / dv rows they store), not from a separate pass over the [tokens, 3C] gradient
+        y = flash_attn_qkvpacked(qkv, causal=True, bias_grad=self.c_attn.bias is not None).reshape(B, S, C)
         if fold_bias:
             return self.c_proj.matmul(y), self.c_proj.bias
         return self.c_proj(y)

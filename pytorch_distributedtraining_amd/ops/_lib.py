@@ -75,7 +75,8 @@ _SIGS = {
                            c_int, c_int, c_float, c_int, c_void_p],
     "pdt_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
-                           c_void_p],
+                           c_void_p, c_void_p, c_int, c_void_p],
+    "pdt_flash_attn_colsum_ws_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "pdt_flash_attn_set_variant": [c_int, c_int],
     "pdt_flash_attn_set_order": [c_int],
     "pdt_win_attn_grid": [c_int],
@@ -143,7 +144,7 @@ _SIGS = {
                              c_int64, c_int, c_int64, c_int, c_int, c_void_p],
 }
 
-_RET64 = {"pdt_swin_mlp_ws_floats", "pdt_fp8_gelu_bwd_ws_floats"}
+_RET64 = {"pdt_swin_mlp_ws_floats", "pdt_fp8_gelu_bwd_ws_floats", "pdt_flash_attn_colsum_ws_floats"}
 
 F32, BF16, F16 = 0, 1, 2
 

@@ -43,16 +43,27 @@ def _fwd(q, k, v, causal, scale):
     return o, lse
 
 
-def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale):
+def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, bias_grad=False):
+    """dq, dk, dv; with ``bias_grad`` also returns the fp32 column sums of the stored dq | dk | dv rows
+    ([H*D + 2*Hkv*D], the bias gradient of the packed qkv projection) from per-workgroup partials of the
+    backward kernels themselves, or None where the current kernel variant does not produce them."""
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     delta = torch.empty((2, B, H, Sq), dtype=torch.float32, device=q.device)   # [delta | -lse*log2e]
     do = do if (do.stride(-1) == 1 and all(s % 8 == 0 for s in do.stride()[:-1])) else do.contiguous()
     strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
                            + _strides(dk) + _strides(dv), dtype=torch.int64)
+    ws = db = None
+    if bias_grad:
+        n = int(_lib.require().pdt_flash_attn_colsum_ws_floats(B, H, Hkv, Sq, Sk, D))
+        if n > 0:
+            ws = torch.empty(n, dtype=torch.float32, device=q.device)
+            db = torch.empty((H + 2 * Hkv) * D, dtype=torch.float32, device=q.device)
     _lib.call("pdt_flash_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), delta.data_ptr(), strides.data_ptr(),
-              B, H, Hkv, Sq, Sk, D, float(scale), 1 if causal else 0, _lib.stream_handle(q.device))
+              B, H, Hkv, Sq, Sk, D, float(scale), 1 if causal else 0, _lib.ptr(ws), _lib.ptr(db),
+              _lib.dtype_code(torch.float32), _lib.stream_handle(q.device))
+    return db
 
 
 class _FlashAttnFn(torch.autograd.Function):
@@ -77,21 +88,48 @@ class _FlashAttnFn(torch.autograd.Function):
 
 class _FlashAttnPackedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, causal, scale):
+    def forward(ctx, qkv, causal, scale, bias_grad):
         _check(qkv, "qkv")
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         o, lse = _fwd(q, k, v, causal, scale)
         ctx.save_for_backward(qkv, o, lse)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.bias_grad = causal, scale, bias_grad
         return o
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse = ctx.saved_tensors
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
-        _bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
-             ctx.causal, ctx.scale)
-        return dqkv, None, None
+        db = _bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
+                  ctx.causal, ctx.scale, bias_grad=ctx.bias_grad)
+        if db is not None:
+            stash_bias_grad(dqkv, db)
+        return dqkv, None, None, None
+
+
+_BIAS_GRADS: dict = {}
+
+
+def stash_bias_grad(grad, colsum):
+    """Hand the column sums of the gradient buffer ``grad`` (computed by the kernel that wrote it) to the Linear
+    whose output received that gradient: its backward takes them (``take_bias_grad``) instead of summing dY
+    again.  Keyed by the buffer's storage; the entry holds the buffer weakly and dies with it."""
+    for key in [k for k, (ref, _) in _BIAS_GRADS.items() if ref() is None]:
+        del _BIAS_GRADS[key]
+    _BIAS_GRADS[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum)
+
+
+def take_bias_grad(dy):
+    """The stashed column sums for ``dy`` (a 2-D [rows, N] view of a stashed gradient buffer), once; else None."""
+    ent = _BIAS_GRADS.pop(dy.untyped_storage().data_ptr(), None)
+    if ent is None:
+        return None
+    src, colsum = ent[0](), ent[1]
+    if (src is None or src.untyped_storage().data_ptr() != dy.untyped_storage().data_ptr()
+            or src.numel() != dy.numel() or dy.dim() != 2 or colsum.numel() != dy.shape[1]
+            or dy.data_ptr() != src.data_ptr()):
+        return None
+    return colsum
 
 
 _FRESH_GRADS = weakref.WeakValueDictionary()
@@ -166,12 +204,14 @@ def flash_attn(q, k, v, causal: bool = True, scale: float | None = None):
     return _FlashAttnFn.apply(q, k, v, causal, scale)
 
 
-def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None):
-    """qkv [B, S, 3, H, D] -> o [B, S, H, D]."""
+def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None, bias_grad: bool = False):
+    """qkv [B, S, 3, H, D] -> o [B, S, H, D].  ``bias_grad``: qkv is the output of a Linear with a bias (GPT-2's
+    c_attn) -- the backward kernels also sum their dq / dk / dv rows per column and hand that bias gradient to the
+    Linear's backward (``take_bias_grad``), which then skips its own column-sum pass over dqkv."""
     scale = 1.0 / math.sqrt(qkv.shape[-1]) if scale is None else scale
     if not qkv.is_cuda:
         return _reference(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal, scale)
-    return _FlashAttnPackedFn.apply(qkv, causal, scale)
+    return _FlashAttnPackedFn.apply(qkv, causal, scale, bias_grad)
 
 
 def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:

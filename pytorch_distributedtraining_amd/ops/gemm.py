@@ -109,12 +109,15 @@ def tt_splits(m: int, n: int, k: int, cus: int = 256) -> int:
     return best
 
 
-def gemm_tt(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> torch.Tensor:
-    """a[K, M]^T @ b[K, N] -> bf16 [M, N] (dW = dY^T X with a = dY, b = X)."""
+def gemm_tt(a: torch.Tensor, b: torch.Tensor, splits: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """a[K, M]^T @ b[K, N] -> bf16 [M, N] (dW = dY^T X with a = dY, b = X); ``out``: a contiguous bf16 [M, N]
+    to write into (e.g. the leading rows of a larger weight gradient)."""
     k, m = a.shape
     n = b.shape[1]
     s = splits or tt_splits(m, n, k)
-    c = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
+    if out is not None:
+        assert out.shape == (m, n) and out.dtype == torch.bfloat16 and out.is_contiguous()
+    c = out if out is not None else torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     ws = torch.empty(s * m * n, dtype=torch.float32, device=a.device) if s > 1 else None
     _launch(L_TT, E_PLAIN, a, b, c, m, n, k, ws=ws, splits=s)
     return c

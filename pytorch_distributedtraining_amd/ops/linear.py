@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .activations import _colsum, colsum_ok
+from .attention import take_bias_grad
 from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 from .gemm import gemm_tt, tt_ok, tt_splits
@@ -70,7 +71,7 @@ def _timed_ms(fn, iters: int = 3) -> float:
     return e0.elapsed_time(e1)
 
 
-def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, ragged: bool = False) -> bool:
     """Hand kernel vs hipBLASLt for this weight-gradient shape.  Measured, not assumed: the two trade places
     by shape and by box (GPT-2 1.3B attention projection +12 %, fc1 +3 %, Llama-3 8B qkv -14 % on one box;
     the flagship gained 3 % on another, profiles/r2_wgrad_hip_vs_hipblaslt.jsonl)."""
@@ -82,7 +83,8 @@ def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
         if torch.cuda.is_current_stream_capturing():
             return True
         # against the path wgrad() would otherwise take (split-K batched GEMM for small outputs, else one GEMM)
-        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip_wgrad(dy2, x2)) < \
+        hip = hip_wgrad_ragged if ragged else hip_wgrad
+        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip(dy2, x2)) < \
             _timed_ms(lambda: _library_wgrad(dy2, x2, torch.bfloat16))
     return c
 
@@ -109,15 +111,42 @@ def hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int | None = None) ->
     return gemm_tt(dy2, x2, splits or hip_wgrad_splits(m, n, k))
 
 
+def _ragged_rows(n: int) -> int:
+    """Rows of an N-row weight gradient the 256-row hand-kernel tiles cover (the rest go to hipBLASLt)."""
+    return n // 256 * 256
+
+
+def hip_wgrad_ragged_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> bool:
+    """Weight gradients whose row count is not a multiple of 256 but large (GPT-2's tied LM head: 50,304 vocab
+    rows): the leading 256-multiple on the hand kernel, a < 256-row remainder on hipBLASLt."""
+    m, n = dy2.shape
+    k = x2.shape[1]
+    nm = _ragged_rows(n)
+    return (HIP_WGRAD != "0" and dy2.is_cuda and out_dtype == torch.bfloat16 and m >= 4096 and nm >= 4096
+            and nm < n and tt_ok(dy2[:, :nm], x2, hip_wgrad_splits(m, nm, k)))
+
+
+def hip_wgrad_ragged(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    m, n = dy2.shape
+    k = x2.shape[1]
+    nm = _ragged_rows(n)
+    out = torch.empty(n, k, dtype=torch.bfloat16, device=dy2.device)
+    gemm_tt(dy2[:, :nm], x2, hip_wgrad_splits(m, nm, k), out=out[:nm])
+    torch.mm(dy2[:, nm:].t(), x2, out=out[nm:])
+    return out
+
+
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
     """dW = dy2^T @ x2 ([M, N]^T [M, K] -> [N, K]) in ``out_dtype``; the hand MFMA kernel for large bf16
-    shapes, row-split batched GEMM for tall-skinny M."""
+    shapes (a ragged row count split between it and hipBLASLt), row-split batched GEMM for tall-skinny M."""
     m, n = dy2.shape
     k = x2.shape[1]
     if not dy2.is_cuda:
         return torch.mm(dy2.t(), x2).to(out_dtype)
     if hip_wgrad_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2):
         return hip_wgrad(dy2, x2)
+    if hip_wgrad_ragged_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2, ragged=True):
+        return hip_wgrad_ragged(dy2, x2)
     return _library_wgrad(dy2, x2, out_dtype)
 
 
@@ -213,7 +242,11 @@ class _LinearFn(torch.autograd.Function):
                 dx = torch.mm(dy2, w)
             dx = dx.view(*dy.shape[:-1], w.shape[1])
         if want_db:
-            db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
+            db = take_bias_grad(dy2)      # summed by the kernel that produced dY (flash attention's backward)
+            if db is not None:
+                db = db.to(w.dtype)
+            else:
+                db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
         return dx, dw, db
 
 

@@ -253,6 +253,45 @@ def test_flash_attn_qkvpacked_matches_unpacked():
     assert torch.equal(qkv.grad, x.grad)
 
 
+@pytest.mark.parametrize("bwd", [0, 3, 8])
+@pytest.mark.parametrize("D,S,B", [(128, 1024, 3), (64, 300, 2), (128, 200, 2)])
+def test_attn_bias_grad_from_backward_kernels(D, S, B, bwd):
+    """The qkv projection's bias gradient summed by the attention backward kernels (per-workgroup column sums
+    of the stored dq / dk / dv rows + a column reduce) equals the column sum of the gradient they stored; through
+    a biased Linear (GPT-2's c_attn) the Linear takes it instead of summing dY, and its bias gradient matches."""
+    from pytorch_distributedtraining_amd.ops import attention as A
+    from pytorch_distributedtraining_amd.ops.linear import Linear
+    H = 4
+    try:
+        A.set_kernel_variant(0, bwd if bwd else -1)
+        torch.manual_seed(D + S)
+        qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+        scale = D ** -0.5
+        o, lse = A._fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], True, scale)
+        dqkv = torch.empty_like(qkv)
+        got = A._bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, torch.randn_like(o), dqkv[:, :, 0],
+                     dqkv[:, :, 1], dqkv[:, :, 2], True, scale, bias_grad=True)
+        assert got is not None and got.dtype == torch.float32
+        want = dqkv.float().reshape(B * S, 3 * H * D).sum(0)
+        assert rel_err(got, want) < 1e-5, rel_err(got, want)
+        # end to end through a biased Linear: the stash is consumed, the bias gradient matches the column sum
+        C = H * D
+        lin = Linear(C, 3 * C).to(DEV).bfloat16()
+        x = torch.randn(B, S, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        y = A.flash_attn_qkvpacked(lin(x).view(B, S, 3, H, D), causal=True, bias_grad=True)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        assert not [e for e in A._BIAS_GRADS.values() if e[0]() is not None]      # taken by the Linear
+        lin2 = Linear(C, 3 * C).to(DEV).bfloat16()
+        lin2.load_state_dict(lin.state_dict())
+        y2 = A.flash_attn_qkvpacked(lin2(x.detach()).view(B, S, 3, H, D), causal=True, bias_grad=False)
+        y2.backward(dy)
+        assert rel_err(lin.bias.grad, lin2.bias.grad) < 1e-2
+        assert torch.equal(lin.weight.grad, lin2.weight.grad)
+    finally:
+        A.reset_kernel_variant()
+
+
 def test_flash_attn_cross_length():
     from pytorch_distributedtraining_amd.ops import flash_attn
     q = torch.randn(1, 64, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -649,6 +688,26 @@ def test_hip_wgrad_full_grid_production_shapes(N, K, splits):
     err = (got - ref).abs()
     bad = err > 0.008 * ref.abs() + 0.01 * rms       # bf16 output rounding + fp32 accumulation order
     assert int(bad.sum()) == 0, (int(bad.sum()), float(err.max()), rms)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 4096 + 128, 512), (96 * 1024, 50304, 2048)])
+def test_hip_wgrad_ragged_rows(M, N, K):
+    """Weight gradient with a row count off the 256 grid (the GPT-2 LM head: 50,304 vocab rows at the flagship's
+    96 x 1024 tokens): leading 256-multiple on the hand TT kernel (A read with the full row stride), remainder
+    on hipBLASLt, every element against fp32."""
+    from pytorch_distributedtraining_amd.ops.linear import hip_wgrad_ragged, hip_wgrad_ragged_ok
+    torch.manual_seed(N)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    assert hip_wgrad_ragged_ok(dy, x, torch.bfloat16)
+    got = hip_wgrad_ragged(dy, x).float()
+    xf = x.float()
+    for r0 in range(0, N, 8192):          # fp32 reference in row chunks (the full one would be 6.6 GB of inputs)
+        r1 = min(N, r0 + 8192)
+        ref = dy[:, r0:r1].float().t() @ xf
+        rms = float(ref.square().mean().sqrt())
+        bad = (got[r0:r1] - ref).abs() > 0.008 * ref.abs() + 0.01 * rms
+        assert int(bad.sum()) == 0, (r0, int(bad.sum()))
 
 
 def _gelu_tanh(x):
