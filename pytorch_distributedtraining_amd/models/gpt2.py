@@ -113,13 +113,14 @@ class GPT2Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
         self.mlp = MLP(cfg)
 
-    def forward(self, x, pending=None):
+    def forward(self, x, pending=None, pending_colsum=False):
         """(x, pending) -> (x', mlp_out): the residual adds are fused into the following LayerNorm
-        kernels (``pending`` is the previous block's branch output not yet added to the stream)."""
+        kernels (``pending`` is the previous block's branch output not yet added to the stream;
+        ``pending_colsum``: it came from a biased Linear, whose bias gradient ln_1's backward sums)."""
         if pending is None:
             h = self.ln_1(x)
         else:
-            h, x = self.ln_1.forward_add(x, pending)
+            h, x = self.ln_1.forward_add(x, pending, r_colsum=pending_colsum and FOLD_PROJ_BIAS)
         if FOLD_PROJ_BIAS:
             a, a_bias = self.attn(h, fold_bias=True)   # c_proj's bias joins the residual sum in ln_2's kernel
             y, x = self.ln_2.forward_add(x, a, a_bias)
@@ -140,6 +141,8 @@ class GPT2LMHeadModel(nn.Module):
         self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
         self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_epsilon)
+        # which blocks' MLP c_proj carries a bias (read at build time: FSDP later swaps parameters in and out)
+        self._mlp_proj_bias = [blk.mlp.c_proj.bias is not None for blk in self.h]
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -176,11 +179,15 @@ class GPT2LMHeadModel(nn.Module):
         pending = self.wpe(pos).unsqueeze(0).expand(B, S, -1)
         n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.h)
         for i, blk in enumerate(self.h):
+            # block i > 0 receives the previous MLP's c_proj output (biased Linear): ln_1 sums its gradient
+            colsum = i > 0 and self._mlp_proj_bias[i - 1] and not fp8_enabled()
             if self.config.activation_checkpointing and self.training and i < n_ckpt:
-                x, pending = torch.utils.checkpoint.checkpoint(fp8_recompute_safe(blk), x, pending, use_reentrant=False)
+                x, pending = torch.utils.checkpoint.checkpoint(fp8_recompute_safe(blk), x, pending, colsum,
+                                                               use_reentrant=False)
             else:
-                x, pending = blk(x, pending)
-        x, _ = self.ln_f.forward_add(x, pending)
+                x, pending = blk(x, pending, colsum)
+        last = self._mlp_proj_bias[-1] and not fp8_enabled() and FOLD_PROJ_BIAS
+        x, _ = self.ln_f.forward_add(x, pending, r_colsum=last)
         logits = linear(x, self.wte.weight)     # tied head (framework linear: transposed-layout dgrad)
         if labels is None:
             return logits

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .attention import stash_bias_grad
 
 
 def _norm_fwd(x2, w, b, eps, rms, res2=None, rb=None):
@@ -84,13 +85,13 @@ class _AddNormFn(torch.autograd.Function):
     same pass -- the Linear then runs bias-free and skips its own column sum over dY."""
 
     @staticmethod
-    def forward(ctx, x, r, rb, weight, bias, eps, rms):
+    def forward(ctx, x, r, rb, weight, bias, eps, rms, r_colsum):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         r2 = r.reshape(-1, shape[-1]).contiguous()
         y, mean, rstd, s = _norm_fwd(x2, weight, bias, eps, rms, res2=r2, rb=rb)
         ctx.save_for_backward(s, weight, mean, rstd)
-        ctx.has_bias, ctx.rms, ctx.has_rb = bias is not None, rms, rb is not None
+        ctx.has_bias, ctx.rms, ctx.has_rb, ctx.r_colsum = bias is not None, rms, rb is not None, r_colsum
         return y.view(shape), s.view(shape)
 
     @staticmethod
@@ -102,19 +103,26 @@ class _AddNormFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, n).contiguous()
         ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
         need_rb = ctx.has_rb and ctx.needs_input_grad[2]
-        dx, dw, db, drb = _norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2, need_ds=need_rb)
+        stash = ctx.r_colsum and not need_rb and ctx.needs_input_grad[1]
+        dx, dw, db, drb = _norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2,
+                                    need_ds=need_rb or stash)
+        if stash:   # r came from a biased Linear in another FSDP unit: its backward takes colsum(dx) from here
+            stash_bias_grad(dx, drb)
+            drb = None
         dx = dx.view(dy.shape)
-        return dx, dx, drb, dw, db, None, None
+        return dx, dx, drb, dw, db, None, None, None
 
 
-def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False, r_bias=None):
+def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False, r_bias=None, r_colsum=False):
     """Fused residual add + LayerNorm/RMSNorm: returns (norm(x + r + r_bias), x + r + r_bias); ``r_bias``
-    (optional, [N], the norm's parameter dtype) is the bias of the Linear that produced r."""
+    (optional, [N], the norm's parameter dtype) is the bias of the Linear that produced r.  ``r_colsum``: r came
+    from a biased Linear whose bias cannot be passed here (another FSDP unit's parameter): the backward still
+    sums its dx per column in the same pass and stashes it for that Linear (``ops.attention.take_bias_grad``)."""
     if (not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16) or r.dtype != x.dtype
             or (r_bias is not None and r_bias.dtype != weight.dtype)):
         s = x + r if r_bias is None else x + (r + r_bias.to(r.dtype))
         return (rms_norm(s, weight, eps) if rms else layer_norm(s, weight, bias, eps)), s
-    return _AddNormFn.apply(x, r, r_bias, weight, bias, eps, rms)
+    return _AddNormFn.apply(x, r, r_bias, weight, bias, eps, rms, bool(r_colsum))
 
 
 def _use_native(x):
@@ -162,20 +170,21 @@ class LayerNorm(nn.Module):
                 return layer_norm(x, self.weight, self.bias, self.eps)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
-    def forward_add(self, x, r, r_bias=None):
-        """(LN(x + r + r_bias), x + r + r_bias) with one kernel pass."""
-        return _ln_forward_add(self, x, r, rms=False, r_bias=r_bias)
+    def forward_add(self, x, r, r_bias=None, r_colsum=False):
+        """(LN(x + r + r_bias), x + r + r_bias) with one kernel pass (``add_norm``)."""
+        return _ln_forward_add(self, x, r, rms=False, r_bias=r_bias, r_colsum=r_colsum)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"
 
 
-def _ln_forward_add(mod, x, r, rms, r_bias=None):
+def _ln_forward_add(mod, x, r, rms, r_bias=None, r_colsum=False):
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
-            return add_norm(x.to(dt), r.to(dt), mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias)
-    return add_norm(x, r, mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias)
+            return add_norm(x.to(dt), r.to(dt), mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias,
+                            r_colsum)
+    return add_norm(x, r, mod.weight, getattr(mod, "bias", None), mod.eps, rms, r_bias, r_colsum)
 
 
 class RMSNorm(nn.Module):
@@ -191,5 +200,5 @@ class RMSNorm(nn.Module):
                 return rms_norm(x, self.weight, self.eps)
         return rms_norm(x, self.weight, self.eps)
 
-    def forward_add(self, x, r, r_bias=None):
-        return _ln_forward_add(self, x, r, rms=True, r_bias=r_bias)
+    def forward_add(self, x, r, r_bias=None, r_colsum=False):
+        return _ln_forward_add(self, x, r, rms=True, r_bias=r_bias, r_colsum=r_colsum)

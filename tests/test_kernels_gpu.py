@@ -410,6 +410,29 @@ def test_gpt2_fsdp_step_matches_fp32_reference():
     assert set(sd2) == set(sd)
 
 
+def test_gpt2_every_grad_matches_fp32_reference():
+    """Per-parameter gradients of the bf16 GPT-2 on the HIP kernels vs the fp32 torch model -- in particular the
+    biases whose gradients come from fused passes: c_attn (attention backward column sums), attention c_proj
+    (ln_2's residual-bias backward), MLP c_proj (the next ln_1 / ln_f backward's column sums, stashed for the
+    Linear), c_fc (bias-GELU backward)."""
+    from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.ops import attention as A
+    torch.manual_seed(0)
+    ref = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=3)
+    x = torch.randint(0, 512, (4, 129))
+    ref(x[:, :-1], labels=x[:, 1:]).backward()
+    m = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=3)
+    m.load_state_dict(ref.state_dict())
+    m = m.to(DEV).bfloat16()
+    xd = x.to(DEV)
+    m(xd[:, :-1], labels=xd[:, 1:]).backward()
+    assert not [e for e in A._BIAS_GRADS.values() if e[0]() is not None]      # every stashed colsum consumed
+    grads = dict(ref.named_parameters())
+    for n, p in m.named_parameters():
+        g, want = p.grad.float().cpu(), grads[n].grad
+        assert rel_err(g, want) < 4e-2, (n, rel_err(g, want))
+
+
 @pytest.mark.parametrize("layout", ["nchw", "nhwc"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C", [64, 24, 3])
