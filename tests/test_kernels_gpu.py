@@ -66,7 +66,7 @@ def test_rms_norm(N):
 
 @pytest.mark.parametrize("approx", ["tanh", "none"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("rows,N", [(300, 1024), (301, 4096)])
+@pytest.mark.parametrize("rows,N", [(300, 1024), (301, 4096), (40003, 8192)])
 def test_bias_gelu(approx, dt, rows, N):
     from pytorch_distributedtraining_amd.ops import bias_gelu
     h = torch.randn(rows, N, device=DEV).to(dt).requires_grad_()
