@@ -157,7 +157,35 @@ struct AttnParams {
   // cs_q [B * nqb][H * D] (nqb = query blocks of the dQ kernel), cs_kv [B * nkb][2][Hkv * D] (nkb = Sk / 128)
   float* cs_q;
   float* cs_kv;
+  // backward: the dQ kernel computes delta = rowsum(dO * O) and the log2-domain lse for its rows itself (from
+  // the dO fragments it holds anyway) and writes them for the dK/dV kernel, which then runs after it -- no
+  // separate delta pass re-reading O and dO
+  int fuse_delta;
 };
+
+// delta of this lane's query row from its dO fragments (gf, already in registers) and the O row; written with
+// the log2-domain lse for the dK/dV kernel by the h == 0 lane.  Returns delta (both halves of the row).
+template <int KS>
+__device__ __forceinline__ float row_delta(const AttnParams& p, const u16x8 (&gf)[KS], int b, int hq, int qrow,
+                                           int h) {
+  float acc = 0.f;
+  if (qrow < p.Sq) {
+    const bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 of = *reinterpret_cast<const u16x8*>(Op + 16 * ks);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += bf2f(of[e]) * bf2f(gf[ks][e]);
+    }
+  }
+  acc += __shfl_xor(acc, 32, 64);
+  if (qrow < p.Sq && h == 0) {
+    const int64_t idx = ((int64_t)b * p.H + hq) * p.Sq + qrow;
+    p.delta[idx] = acc;
+    p.delta[(int64_t)p.B * p.H * p.Sq + idx] = -p.lse[idx] * LOG2E;
+  }
+  return acc;
+}
 
 // ------------------------------------------------------------------------------------------------
 // forward
@@ -2011,7 +2039,8 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
     }
   }
   const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
-  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  const float dl = p.fuse_delta ? row_delta<KS>(p, gf, b, hq, qrow, h)
+                                : (qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f);
   retire(qf);
   retire(gf);
   asm volatile("" :: "v"(nlse2), "v"(dl));
@@ -2184,7 +2213,8 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     }
   }
   const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
-  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
+  const float dl = p.fuse_delta ? row_delta<KS>(p, gf, b, hq, qrow, h)
+                                : (qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f);
   retire(qf);
   retire(gf);
   asm volatile("" :: "v"(nlse2), "v"(dl));
@@ -2290,13 +2320,34 @@ int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
 template <int D>
 int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.Sq;
-  fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
   const int variant = bwd_variant(D);
   AttnParams kv = p, qp = p;               // per-kernel block order (p.order bit 1: dK/dV, bit 2: dQ)
   kv.order = (p.order >> 1) & 1;
   qp.order = (p.order >> 2) & 1;
+  kv.fuse_delta = qp.fuse_delta = 0;
+  // dQ v3 / v4 + dK/dV v3 (variants 3, 7, 8, 9 -- the defaults): dQ first, computing delta itself
+  static const bool fuse = [] { const char* e = getenv("PDT_FA_FUSE_DELTA"); return !e || atoi(e) != 0; }();
+  if (fuse && (variant == 3 || variant == 7 || variant == 8 || variant == 9)) {
+    qp.fuse_delta = 1;
+    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
+    if (causal) {
+      if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
+      else if (variant == 7) fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(qp);
+      else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
+      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
+      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+    } else {
+      if (variant == 3) fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
+      else if (variant == 7) fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(qp);
+      else if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
+      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
+      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+    }
+    return (int)hipGetLastError();
+  }
+  fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
   if (variant == 1) {
     if (causal) {
       fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
