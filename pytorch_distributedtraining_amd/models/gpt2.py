@@ -174,9 +174,10 @@ class GPT2LMHeadModel(nn.Module):
 
     def forward(self, input_ids, labels=None):
         B, S = input_ids.shape
-        pos = torch.arange(S, device=input_ids.device)
         x = self.wte(input_ids)
-        pending = self.wpe(pos).unsqueeze(0).expand(B, S, -1)
+        # positions are 0..S-1: the first S rows of the table, no gather (its backward was a sort-based
+        # embedding_dense_backward over B*S indices; now a slice copy of S rows)
+        pending = self.wpe.weight[:S].unsqueeze(0).expand(B, S, -1)
         n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.h)
         for i, blk in enumerate(self.h):
             # block i > 0 receives the previous MLP's c_proj output (biased Linear): ln_1 sums its gradient

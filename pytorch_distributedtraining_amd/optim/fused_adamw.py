@@ -128,6 +128,10 @@ class FusedAdamW(Optimizer):
                 ms = [self.state[p]["exp_avg"] for p in ps]
                 vs = [self.state[p]["exp_avg_sq"] for p in ps]
                 lps = [getattr(p, "_pdt_lp_shard", None) for p in ps]
+                # the kernel's epilogue writes bf16 compute copies; an fp32 "copy" (a DDP compute-copy model's
+                # batch-norm group) is refreshed by a plain copy after the step
+                lp_other = [(p, x) for p, x in zip(ps, lps) if x is not None and x.dtype != torch.bfloat16]
+                lps = [x if (x is not None and x.dtype == torch.bfloat16) else None for x in lps]
                 has_lp = any(x is not None for x in lps)
                 table = None
                 if dev.type == "cuda":
@@ -137,6 +141,9 @@ class FusedAdamW(Optimizer):
                               weight_decay=group["weight_decay"], step=max(step, 1),
                               decoupled=group.get("decoupled", True), grad_scale=grad_scale, found_inf=found_inf,
                               out_bf16=lps if has_lp else None, table=table, dstep=dstep if step < 0 else None)
+                with torch.no_grad():
+                    for p, x in lp_other:
+                        x.copy_(p)
                 for p in ps:
                     if getattr(p, "_pdt_lp_shard", None) is not None:
                         p._pdt_lp_version = p._version   # compute copy already refreshed by the kernel

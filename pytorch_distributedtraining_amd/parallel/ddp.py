@@ -130,7 +130,8 @@ class DistributedDataParallel(nn.Module):
         find_unused_parameters: allow parameters that receive no gradient (flushed as zeros).
         compute_dtype: e.g. torch.bfloat16 -> the module runs in bf16, gradients are bf16 and
             all-reduced in bf16, and ``optimizer_parameters()`` returns the fp32 master flat(s)
-            (the optimizer writes the bf16 compute copy back).  None -> classic fp32 params + autocast.
+            (the optimizer writes the bf16 compute copy back); batch-norm layers stay fp32.  None -> classic
+            fp32 params + autocast.
         reduce_dtype: optional dtype for the all-reduce payload (bf16 compression of fp32 grads).
         rebuild_buckets: after the first backward, re-plan buckets in the observed gradient order.
     """
@@ -170,6 +171,11 @@ class DistributedDataParallel(nn.Module):
         module.to(self.device)
         if compute_dtype is not None:
             module.to(compute_dtype)
+            # batch norms keep fp32 affine parameters and running statistics (their own fp32 flat group):
+            # bf16 running stats drift, and the fused BN kernels take fp32 parameters with bf16 activations
+            for m in module.modules():
+                if isinstance(m, nn.modules.batchnorm._BatchNorm):
+                    m.float()
         self.params = [p for p in module.parameters() if p.requires_grad]
         if self.comm.world_size > 1:
             self.comm.broadcast_coalesced([p.data for p in self.params] + [b for b in module.buffers()])

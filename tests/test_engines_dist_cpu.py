@@ -106,6 +106,39 @@ def test_ddp_compute_dtype_master_matches_single_process(world):
         assert torch.allclose(outs[0][k], ref[k], atol=2e-5), k
 
 
+def _w_ddp_bf16_bn(rank, world):
+    """DDP bf16 compute copy on a model with batch norm (bench.py's ResNet-50 path): Linear weights become bf16
+    views of the flat compute copy, the batch norm keeps fp32 parameters / running stats in its own fp32 group,
+    and the fused AdamW refreshes both copies from the fp32 masters."""
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(16, 32), nn.BatchNorm1d(32), nn.Tanh(), nn.Linear(32, 4))
+    bn0 = m[1].weight.detach().clone()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.001, first_bucket_mb=0.0005, compute_dtype=torch.bfloat16)
+    assert m[0].weight.dtype == torch.bfloat16 and m[3].weight.dtype == torch.bfloat16
+    assert m[1].weight.dtype == torch.float32 and m[1].running_mean.dtype == torch.float32
+    opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    for s in range(STEPS):
+        x, y = _data(s, world)
+        loss = nn.functional.mse_loss(ddp(_shard(x, rank, world).bfloat16()).float(), _shard(y, rank, world))
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    assert not torch.equal(m[1].weight.detach(), bn0)           # the fp32 group's copy was refreshed
+    return {k: v.detach().float().clone() for k, v in ddp.full_state_dict().items()}
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_ddp_bf16_compute_copy_keeps_batchnorm_fp32(world):
+    outs = run_workers(_w_ddp_bf16_bn, world)
+    for k in outs[0]:
+        if "running" in k or "num_batches" in k:
+            continue            # per-rank batch statistics after the last forward (rank 0's are broadcast next)
+        for r in range(1, world):
+            assert torch.equal(outs[0][k], outs[r][k]), k
+
+
 def _w_zero(rank, world, sddp, bcast16):
     from pytorch_distributedtraining_amd.optim import FusedAdamW
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel

@@ -410,6 +410,41 @@ def test_gpt2_fsdp_step_matches_fp32_reference():
     assert set(sd2) == set(sd)
 
 
+def test_resnet_ddp_bf16_compute_copy_keeps_batchnorm_fp32():
+    """DDP's bf16 compute copy on a ResNet (bench.py's ResNet-50 path): convs / fc on bf16 parameters, batch norms
+    with fp32 parameters and running statistics (fused BN kernels), fp32 masters stepped by FusedAdamW; the first
+    steps track the fp32-parameter + autocast form of the same model."""
+    import copy
+    from pytorch_distributedtraining_amd.models.resnet import resnet18
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    base = resnet18().to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 64, 64, device=DEV).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (16,), device=DEV)
+    crit = torch.nn.CrossEntropyLoss()
+    losses = {}
+    for mode in ("copy", "autocast"):
+        m = copy.deepcopy(base)
+        ddp = DistributedDataParallel(m, compute_dtype=torch.bfloat16 if mode == "copy" else None)
+        opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-3)
+        if mode == "copy":
+            assert m.conv1.weight.dtype == torch.bfloat16 and m.fc.weight.dtype == torch.bfloat16
+            assert m.bn1.weight.dtype == torch.float32 and m.bn1.running_mean.dtype == torch.float32
+        out = []
+        for _ in range(3):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "autocast"):
+                loss = crit(ddp(x.bfloat16() if mode == "copy" else x).float(), y)
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            out.append(float(loss))
+        losses[mode] = out
+    assert losses["copy"][-1] < losses["copy"][0]
+    for a, b in zip(losses["copy"], losses["autocast"]):
+        assert abs(a - b) < 3e-2 * abs(b), losses
+
+
 def test_gpt2_every_grad_matches_fp32_reference():
     """Per-parameter gradients of the bf16 GPT-2 on the HIP kernels vs the fp32 torch model -- in particular the
     biases whose gradients come from fused passes: c_attn (attention backward column sums), attention c_proj
