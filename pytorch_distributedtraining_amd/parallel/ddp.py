@@ -70,6 +70,12 @@ def _running_stat_ids(module):
     return ids
 
 
+def _pview(flat, p, o):
+    """Parameter ``p``'s region of a flat buffer at offset ``o``, with p's own strides (a channels_last conv weight
+    keeps channels_last memory order in the flat: MIOpen then takes it as is, no per-call layout change)."""
+    return torch.as_strided(flat, p.shape, p.stride(), o)
+
+
 class _FlatGroup:
     """All parameters of one storage dtype, laid out bucket after bucket."""
 
@@ -98,11 +104,9 @@ class _FlatGroup:
             self.flat_param = torch.zeros(total, dtype=dtype, device=device)
             with torch.no_grad():
                 for li, p in enumerate(params):
-                    o = self.offset_of[li]
-                    self.flat_param[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                    _pview(self.flat_param, p, self.offset_of[li]).copy_(p.detach())
             for li, p in enumerate(params):
-                o = self.offset_of[li]
-                p.data = self.flat_param[o:o + p.numel()].view(p.shape)
+                p.data = _pview(self.flat_param, p, self.offset_of[li])
             m = nn.Parameter(self.flat_param.detach().to(torch.float32))
             m._pdt_lp_shard = self.flat_param
             m._pdt_lp_version = m._version
@@ -368,8 +372,7 @@ class DistributedDataParallel(nn.Module):
         for g in self.groups:
             for li, gi in enumerate(g.idxs):
                 p = self.params[gi]
-                o = g.offset_of[li]
-                sd[name_of[id(p)]] = g.master.detach()[o:o + p.numel()].view(p.shape).clone()
+                sd[name_of[id(p)]] = _pview(g.master.detach(), p, g.offset_of[li]).clone()
         return sd
 
     def full_optim_state_dict(self, optimizer):
@@ -390,7 +393,7 @@ class DistributedDataParallel(nn.Module):
                 ent = {}
                 for k, v in st.items():
                     if torch.is_tensor(v) and v.dim() == 1 and v.numel() == g.master.numel():
-                        ent[k] = v.detach()[o:o + p.numel()].view(p.shape).clone()
+                        ent[k] = _pview(v.detach(), p, o).clone()
                     else:
                         ent[k] = v.detach().clone() if torch.is_tensor(v) else v
                 state[idx_of[id(p)]] = ent
@@ -425,7 +428,7 @@ class DistributedDataParallel(nn.Module):
                     if torch.is_tensor(v) and v.dim() > 0:
                         if k not in new:
                             new[k] = torch.zeros_like(g.master, dtype=torch.float32)
-                        new[k][o:o + p.numel()].copy_(v.reshape(-1))
+                        _pview(new[k], p, o).copy_(v.reshape(p.shape))
                     elif k == "step":
                         step = v
             if new:
@@ -444,7 +447,6 @@ class DistributedDataParallel(nn.Module):
                 for g in self.groups:
                     for li, gi in enumerate(g.idxs):
                         p = self.params[gi]
-                        o = g.offset_of[li]
-                        g.master[o:o + p.numel()].copy_(sd[name_of[id(p)]].reshape(-1).float())
+                        _pview(g.master, p, g.offset_of[li]).copy_(sd[name_of[id(p)]].float())
                     g.master._pdt_lp_version = g.master._version
         return res

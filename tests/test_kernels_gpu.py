@@ -431,6 +431,8 @@ def test_resnet_ddp_bf16_compute_copy_keeps_batchnorm_fp32():
         if mode == "copy":
             assert m.conv1.weight.dtype == torch.bfloat16 and m.fc.weight.dtype == torch.bfloat16
             assert m.bn1.weight.dtype == torch.float32 and m.bn1.running_mean.dtype == torch.float32
+            # conv weights keep channels_last memory order inside the flat compute copy
+            assert m.conv1.weight.is_contiguous(memory_format=torch.channels_last)
         out = []
         for _ in range(3):
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "autocast"):
