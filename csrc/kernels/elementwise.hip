@@ -16,19 +16,25 @@ namespace {
 
 constexpr int NT = 256;
 // y = gelu(h + bias); N % 8 == 0 (vector path).  bias may be null.
-// (4 vectors per thread per pass with every load issued first measured 4 % SLOWER at the GPT-2 1.3B c_fc shape:
-// 17.2 -> 17.8 ms per step; the kernel is not load-latency-bound)
+// The bias column advances incrementally (one compare-subtract per pass): a 64-bit `e % N` per vector is a
+// ~40-instruction software division.  (4 vectors per thread per pass with every load issued first measured 4 %
+// SLOWER at the GPT-2 1.3B c_fc shape; the kernel is not load-latency-bound.)
 template <typename T, typename B, bool TANH>
 __global__ __launch_bounds__(NT) void bias_gelu_fwd_kernel(const T* __restrict__ h, const B* __restrict__ bias,
                                                            T* __restrict__ y, int64_t n8, int N) {
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+  const int64_t i0 = blockIdx.x * (int64_t)NT + threadIdx.x, stride = (int64_t)gridDim.x * NT;
+  int col = (int)((i0 * 8) % N);
+  const int inc = (int)((stride * 8) % N);
+  for (int64_t i = i0; i < n8; i += stride) {
     const int64_t e = i * 8;
     float v[8], b[8];
     Vec8<T>::load(h + e, v);
-    if (bias) Vec8<B>::load(bias + (int)(e % N), b);
+    if (bias) Vec8<B>::load(bias + col, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = gelu_f<TANH>(bias ? v[k] + b[k] : v[k]);
     Vec8<T>::store(y + e, v);
+    col += inc;
+    if (col >= N) col -= N;
   }
 }
 
@@ -36,12 +42,15 @@ template <typename T, typename B, bool TANH>
 __global__ __launch_bounds__(NT) void bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ h,
                                                            const B* __restrict__ bias, T* __restrict__ dh,
                                                            int64_t n8, int N) {
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+  const int64_t i0 = blockIdx.x * (int64_t)NT + threadIdx.x, stride = (int64_t)gridDim.x * NT;
+  int col = (int)((i0 * 8) % N);
+  const int inc = (int)((stride * 8) % N);
+  for (int64_t i = i0; i < n8; i += stride, col = col + inc >= N ? col + inc - N : col + inc) {
     const int64_t e = i * 8;
     float v[8], g[8], b[8];
     Vec8<T>::load(h + e, v);
     Vec8<T>::load(dy + e, g);
-    if (bias) Vec8<B>::load(bias + (int)(e % N), b);
+    if (bias) Vec8<B>::load(bias + col, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] *= gelu_grad<TANH>(bias ? v[k] + b[k] : v[k]);
     Vec8<T>::store(dh + e, g);
