@@ -96,7 +96,16 @@ def tt_splits(m: int, n: int, k: int, cus: int = 256) -> int:
     """Token split (1, 2, 4, 8, 16) whose tiles x slices fill whole waves of the CUs best (>= 4096 tokens
     per slice); outputs of at least one wave of tiles are not split (the fp32 slab pass costs more)."""
     tiles = (m // 256) * (n // 256)
-    if tiles == 0 or tiles >= cus:
+    if tiles == 0:
+        return 1
+    if tiles >= cus:
+        # a full wave already; split only to rescue a badly quantised last wave (GPT-2's LM-head weight gradient:
+        # 1,568 tiles = 6.125 waves of 256 CUs run as 7; 2 slices = 12.25 -> 13, 94 % vs 87.5 % of the rounds busy)
+        eff1 = tiles / (-(-tiles // cus) * cus)
+        if eff1 < 0.9 and k % (32 * 2) == 0 and k // 2 >= 4096:
+            eff2 = 2 * tiles / (-(-(2 * tiles) // cus) * cus)
+            if eff2 > eff1 + 0.05:
+                return 2
         return 1
     best, best_eff = 1, 0.0
     for s in (1, 2, 4, 8, 16):
