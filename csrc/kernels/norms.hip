@@ -577,9 +577,20 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
     norm_bwd_generic<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N);
   }
   float* ws2 = ws + (int64_t)3 * R * N;
-  if (dw) col_reduce<W>(dwp, R, N, (W*)dw, ws2, accumulate, st);
-  if (db) col_reduce<W>(dbp, R, N, (W*)db, ws2 + (int64_t)64 * N, accumulate, st);
-  if (ds) col_reduce<W>(dsp, R, N, (W*)ds, ws2 + (int64_t)128 * N, 0, st);
+  // dgamma / dbeta / residual-bias partials sit at ws + z * R * N: reduced together (one launch per level)
+  red::ColOuts3 outs{};
+  int nz = 0;
+  if (dw) { outs.out[nz] = dw; outs.accumulate[nz] = accumulate; ++nz; }
+  if (db) { outs.out[nz] = db; outs.accumulate[nz] = accumulate; ++nz; }
+  if (ds) { outs.out[nz] = ds; outs.accumulate[nz] = 0; ++nz; }
+  const bool packed = (!db || dbp == ws + (int64_t)R * N) && (!ds || dsp == ws + (int64_t)(db ? 2 : 1) * R * N);
+  if (packed && nz > 0) {
+    red::col_reduce3<W>(ws, R, N, nz, outs, ws2, st);
+  } else {
+    if (dw) col_reduce<W>(dwp, R, N, (W*)dw, ws2, accumulate, st);
+    if (db) col_reduce<W>(dbp, R, N, (W*)db, ws2 + (int64_t)64 * N, accumulate, st);
+    if (ds) col_reduce<W>(dsp, R, N, (W*)ds, ws2 + (int64_t)128 * N, 0, st);
+  }
   return (int)hipGetLastError();
 }
 

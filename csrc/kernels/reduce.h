@@ -56,6 +56,54 @@ __global__ __launch_bounds__(NT) void col_reduce_kernel(const float* __restrict_
   }
 }
 
+// Up to 3 [R, N] partial matrices at part + z * R * N reduced in the same launches (blockIdx.z = matrix): the
+// norm backward's dgamma / dbeta / residual-bias sums are ~5 us launches each, launch-bound.
+struct ColOuts3 {
+  void* out[3];
+  int accumulate[3];
+};
+template <typename W, bool FINAL>
+__global__ __launch_bounds__(NT) void col_reduce3_kernel(const float* __restrict__ part, int R, int N, ColOuts3 outs,
+                                                         float* __restrict__ part2) {
+  __shared__ float sred[4][64];
+  const int z = blockIdx.z;
+  part += (int64_t)z * R * N;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int per = (R + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
+  float s = 0.f;
+  if (col < N)
+    for (int r = r0 + wid; r < r1; r += 4) s += part[(int64_t)r * N + col];
+  sred[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && col < N) {
+    float t = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
+    if (FINAL) {
+      W* out = reinterpret_cast<W*>(outs.out[z]);
+      if (outs.accumulate[z]) t += to_f<W>(out[col]);
+      out[col] = from_f<W>(t);
+    } else {
+      part2[((int64_t)z * gridDim.y + blockIdx.y) * N + col] = t;
+    }
+  }
+}
+
+// nz (<= 3) matrices part[z][R, N] -> outs.out[z][N]; ws2 must hold >= nz * 64 * N floats.  The same two-level
+// fixed-order reduction as col_reduce (bitwise equal results).
+template <typename W>
+inline void col_reduce3(const float* part, int R, int N, int nz, const ColOuts3& outs, float* ws2, hipStream_t st) {
+  const int cg = (N + 63) / 64;
+  int rs = 1;
+  while (rs < 64 && cg * rs < 512 && R / (rs * 2) >= 8) rs *= 2;
+  if (rs == 1) {
+    col_reduce3_kernel<W, true><<<dim3(cg, 1, nz), NT, 0, st>>>(part, R, N, outs, nullptr);
+  } else {
+    col_reduce3_kernel<W, false><<<dim3(cg, rs, nz), NT, 0, st>>>(part, R, N, outs, ws2);
+    col_reduce3_kernel<W, true><<<dim3(cg, 1, nz), NT, 0, st>>>(ws2, rs, N, outs, nullptr);
+  }
+}
+
 // part[R, N] -> out[N] (+= if accumulate).  ws2 must hold >= 64 * N floats.
 template <typename W>
 inline void col_reduce(const float* part, int R, int N, W* out, float* ws2, int accumulate, hipStream_t st) {

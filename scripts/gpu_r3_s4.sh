@@ -23,7 +23,7 @@ if [ "${PROFILE:-1}" == "1" ]; then
   mkdir -p $OUT/s4_prof
   run s4_prof 400 rocprofv3 --kernel-trace --stats -d $OUT/s4_prof -o flagship -- python3 bench.py --steps 3 --warmup 2 --secondary 0 || exit $?
   db=$(find $OUT/s4_prof -name "*.db" | head -n 1)
-  python scripts/prof_db_stats.py "$db" --step-kernel adamw_mt_kernel --skip 2 -o $OUT/s4_kernel_stats.csv > $OUT/s4_kernel_table.txt 2>&1 || true
+  python scripts/prof_db_stats.py "$db" --step-kernel adamw_mt_kernel --skip 2 --gaps 25 -o $OUT/s4_kernel_stats.csv > $OUT/s4_kernel_table.txt 2>&1 || true
   rm -f "$db"
   head -n 30 $OUT/s4_kernel_stats.csv
 fi

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--step-kernel", default="")
     ap.add_argument("--skip", type=int, default=0, help="once-per-step dispatches to skip (warm-up steps)")
     ap.add_argument("--top", type=int, default=0)
+    ap.add_argument("--gaps", type=int, default=0, help="also report idle time between dispatches (N largest)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, duration from kernels order by start").fetchall()
@@ -64,6 +65,19 @@ def main():
         span = (hi - lo) / 1e6
         print(f"# window {span:.1f} ms over {steps} steps = {span / steps:.1f} ms/step; kernel time "
               f"{total / 1e6 / steps:.1f} ms/step", file=sys.stderr)
+    if a.gaps:
+        # idle time between consecutive dispatches (one stream: the next kernel starts after the previous ends)
+        gaps, last_end, last_name = [], None, None
+        for name, st, en, _d in rows:
+            if last_end is not None and st > last_end:
+                gaps.append((st - last_end, last_name, name))
+            if last_end is None or en > last_end:
+                last_end, last_name = en, name
+        tot = sum(g[0] for g in gaps)
+        print(f"# idle between dispatches: {tot / 1e6 / max(steps or 1, 1):.2f} ms/step over {len(gaps)} gaps",
+              file=sys.stderr)
+        for g, before, after in sorted(gaps, reverse=True)[:a.gaps]:
+            print(f"#   {g / 1e3:9.1f} us  after {short(before)[:70]}  before {short(after)[:70]}", file=sys.stderr)
 
 
 if __name__ == "__main__":
