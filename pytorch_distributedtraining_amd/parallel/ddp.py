@@ -70,10 +70,18 @@ def _running_stat_ids(module):
     return ids
 
 
+def _dense_stride(p):
+    """p's strides when p is dense (contiguous or channels_last: its numel elements fill one span), else the
+    contiguous strides of its shape."""
+    if p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last)):
+        return p.stride()
+    return torch.empty(p.shape, device="meta").stride()
+
+
 def _pview(flat, p, o):
-    """Parameter ``p``'s region of a flat buffer at offset ``o``, with p's own strides (a channels_last conv weight
-    keeps channels_last memory order in the flat: MIOpen then takes it as is, no per-call layout change)."""
-    return torch.as_strided(flat, p.shape, p.stride(), o)
+    """Parameter ``p``'s region of a flat buffer at offset ``o``, with p's own (dense) strides: a channels_last conv
+    weight keeps channels_last memory order in the flat, so MIOpen takes it as is, no per-call layout change."""
+    return torch.as_strided(flat, p.shape, _dense_stride(p), o)
 
 
 class _FlatGroup:
@@ -118,7 +126,7 @@ class _FlatGroup:
         for li, p in enumerate(self.params):
             o = self.offset_of[li]
             # same strides as the parameter (channels_last convs): autograd accumulates in place
-            p.grad = torch.as_strided(self.flat_grad, p.shape, p.stride(), o)
+            p.grad = _pview(self.flat_grad, p, o)
 
 
 class DistributedDataParallel(nn.Module):
