@@ -51,6 +51,26 @@ def test_bench_world2_reports_topology_and_secondary_headline():
     assert sec["collectives_per_step"] >= 2
 
 
+def test_bench_under_torchrun_driver_command():
+    """The driver's own launch form for N > 1 (torch.distributed.run, one rank per device, env:// on 127.0.0.1):
+    exactly one JSON line from rank 0 with the real world size."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--device", "cpu", "--workload", "gpt2-fsdp", "--model", "gpt2-tiny", "--micro-batch", "2",
+                        "--seq", "64", "--steps", "2", "--warmup", "1", "--secondary-micro-batch", "2"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_ranks"] == 2 and res["topology"]["c10d_world"] == 2 and res["steps"] == 2
+    assert res["secondary"]["config"]["parallelism"] == "dp2"
+
+
 def test_bench_refuses_mismatched_world_size():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--workload", "resnet18-cpu"], cwd=ROOT,
                        env=_env(WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
