@@ -15,13 +15,13 @@ run() {  # name, seconds, cmd...
   return $rc
 }
 K=${K:-"bias_grad or ragged or fused_add_norm or hand_gemm or flash_attn or trainer_graph"}
-run s5_pytest_new 600 python -u -m pytest tests/test_kernels_gpu.py -m gpu -q -x -k "$K" --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
+run s5_pytest_new 600 python -u -m pytest ${FILES:-tests/test_kernels_gpu.py} -m gpu -q -x -k "$K" --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
 run s5_bench 400 python bench.py --steps 10 --warmup 3 || exit $?
 if [ "${PROFILE:-1}" == "1" ]; then
   mkdir -p $OUT/s5_prof
   run s5_prof 400 rocprofv3 --kernel-trace --stats -d $OUT/s5_prof -o flagship -- python3 bench.py --steps 3 --warmup 2 --secondary 0 || exit $?
   db=$(find $OUT/s5_prof -name "*.db" | head -n 1)
-  python scripts/prof_db_stats.py "$db" --step-kernel adamw_mt_kernel --skip 2 -o $OUT/s5_kernel_stats.csv > $OUT/s5_kernel_table.txt 2>&1 || true
+  python scripts/prof_db_stats.py "$db" --step-kernel adamw_mt_kernel --skip 2 --gaps 25 -o $OUT/s5_kernel_stats.csv > $OUT/s5_kernel_table.txt 2>&1 || true
   rm -f "$db"
   head -n 24 $OUT/s5_kernel_stats.csv | cut -c1-150
 fi

@@ -39,6 +39,13 @@ def _entry(rank, world, port, fn, args, outdir):
                 pass
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump((res, err), f)
+    # The result is on disk: leave without running C++ static destructors.  Under a loaded host (pytest -n 4)
+    # a gloo background thread still joinable at interpreter teardown aborts the worker ("terminate called
+    # without an active exception") and spawn reports SIGABRT for a run that had succeeded.
+    import sys
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 def run_workers(fn, world=2, *args, timeout=240):
