@@ -1,6 +1,6 @@
 // Fused BatchNorm (+ residual add) (+ ReLU) for channels-last (NHWC) activations on gfx950 -- the
 // ResNet-50 DDP config (BASELINE.json config 2).  A bf16 ResNet-50 step spends ~35 % of
-// its time in BatchNorm and another ~8 % in ReLU (scripts/resnet_breakdown.py: 42.2 ms -> 27.3 ms without
+// its time in BatchNorm and another ~8 % in ReLU (scripts/bench_resnet_breakdown.py: 42.2 ms -> 27.3 ms without
 // BN, -> 24.0 ms without BN and ReLU); stock PyTorch runs BN, the residual add and ReLU as separate
 // passes over HBM.  Here:
 //

@@ -1,6 +1,6 @@
 // hipBLASLt GEMMs with fused epilogues, called directly (host code; the GEMM kernels are hipBLASLt's).
 //
-// What this build of hipBLASLt offers on gfx950 was probed per epilogue (scripts/probe_lt_epilogues.py,
+// What this build of hipBLASLt offers on gfx950 was probed per epilogue (scripts/bench_lt_epilogues.py,
 // profiles/r2_hipblaslt_epilogue_probe.txt): BIAS, GELU_BIAS and BGRADB (B transposed) have algorithms;
 // GELU_AUX_BIAS, DGELU and DGELU_BGRAD have none -- so the transformer MLP keeps the framework's own bias-GELU
 // kernels, and what moves into the GEMM is the bias gradient of every biased Linear:

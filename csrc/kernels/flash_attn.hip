@@ -896,7 +896,7 @@ __device__ __forceinline__ void wg_colsum_store(float (&v)[D / 2], float* lds, f
 // (2) the K row fragments stream two MFMA steps ahead of their use and the V transposed fragments one
 // step ahead, each step its own scheduling region, so an LDS read's latency hides behind the MFMAs
 // instead of stalling every pair; (3) the 16-byte permlane epilogue.
-// Measured and NOT adopted (scripts/attn_ab.py, one process, interleaved rounds): an in-wave pipeline
+// Measured and NOT adopted (scripts/bench_attn_ab.py, one process, interleaved rounds): an in-wave pipeline
 // across tiles (QK(t+1) MFMAs under the softmax VALU of tile t, PV(t) under the row max of t+1, K and V
 // on separate rings) ran 555 vs 571 TFLOP/s causal and tied non-causal -- the co-resident wave of the
 // other workgroup already fills this wave's softmax gaps; likewise two-step-ahead fragment reads in the

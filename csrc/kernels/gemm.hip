@@ -551,7 +551,7 @@ int launch_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
 // Shapes the kernel takes (checked by the host before any launch): M, N multiples of 256, K a multiple of
 // 32 * splits, 16-B aligned rows, every byte offset of a stage tile below 2^32 (buffer resources).
 // Diagnostic launches of the TT / plain kernel: diag 0 is the production kernel, 1-3 remove a part of the
-// main loop (see DIAG above; output garbage by construction).  For scripts/gemm_diag.py.
+// main loop (see DIAG above; output garbage by construction).  For scripts/bench_gemm_diag.py.
 PDT_API int pdt_gemm_diag_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
                                hipStream_t s) {
   if (M % TM || N % TN || K % KB || diag < 0 || diag > 4) return (int)hipErrorInvalidValue;

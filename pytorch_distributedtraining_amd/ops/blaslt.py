@@ -3,7 +3,7 @@ fastest of hipBLASLt's heuristic candidates picked by timing on a shape's first 
 
 Used for the Linear weight gradient with the bias gradient reduced inside the same GEMM (epilogue BGRADB):
 dW = dY^T X and db = colsum(dY) read dY once instead of twice, and the separate column-sum launches
-(2 per biased Linear per step) disappear.  The probe in scripts/probe_lt_epilogues.py
+(2 per biased Linear per step) disappear.  The probe in scripts/bench_lt_epilogues.py
 (profiles/r2_hipblaslt_epilogue_probe.txt) shows which epilogues this hipBLASLt build has gfx950 algorithms
 for: BIAS, GELU_BIAS and BGRADB (with B transposed) yes; GELU_AUX_BIAS, DGELU and DGELU_BGRAD no -- so the
 GELU stays in the framework's own bias-GELU kernels.

@@ -2,7 +2,7 @@
 """A/B the flash-attention kernel generations in ONE process, interleaved rounds (cdna_hip_programming.md
 §5.4 rule 24): forward and backward ms + TFLOP/s on the flagship (GPT-2 1.3B: B32 S1024 H16 D128 causal),
 Llama-3 8B (B8 S1024 H32/8 D128 causal) and a long-sequence shape, plus the max |diff| of each variant's
-output against the first one.  Usage: python scripts/attn_ab.py --fwd 4,5 --bwd 3"""
+output against the first one.  Usage: python scripts/bench_attn_ab.py --fwd 4,5 --bwd 3"""
 import argparse
 import json
 import os

@@ -4,7 +4,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT/prof_r3b
-timeout -k 10 240 python -u scripts/gemm_diag.py > $OUT/r3_gemm_diag.jsonl 2> $OUT/r3_gemm_diag.err
+timeout -k 10 240 python -u scripts/bench_gemm_diag.py > $OUT/r3_gemm_diag.jsonl 2> $OUT/r3_gemm_diag.err
 rc=$?; echo "gemm diag rc=$rc"; cat $OUT/r3_gemm_diag.jsonl; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -p no:cacheprovider \
   > $OUT/r3_pytest_gpu_full.log 2>&1

@@ -7,7 +7,7 @@ OUT=gpurun_out
 mkdir -p $OUT/prof_r3
 STEP=${STEP:-all}
 if [ "$STEP" = all ] || [ "$STEP" = attn ]; then
-  timeout -k 10 420 python -u scripts/attn_ab.py --shapes gpt2-1.3b-b96,gpt2-1.3b,gpt2-1.3b-full,long-4k \
+  timeout -k 10 420 python -u scripts/bench_attn_ab.py --shapes gpt2-1.3b-b96,gpt2-1.3b,gpt2-1.3b-full,long-4k \
     --fwd 5,7,8 --bwd 3,8,9 --order 0,1 --rounds 3 > $OUT/r3_attn_ab.jsonl 2> $OUT/r3_attn_ab.err
   rc=$?; echo "attn_ab rc=$rc"; tail -3 $OUT/r3_attn_ab.err; [ $rc -eq 0 ] || exit $rc
 fi

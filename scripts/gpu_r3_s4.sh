@@ -18,7 +18,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   run s4_smoke 200 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
 run s4_bench 400 python bench.py --steps 10 --warmup 3 || exit $?
-[ "${DIAG:-0}" == "1" ] && { run s4_gemm_diag_nt 300 python -u scripts/gemm_diag_nt.py || exit $?; }
+[ "${DIAG:-0}" == "1" ] && { run s4_gemm_diag_nt 300 python -u scripts/bench_gemm_nt_diag.py || exit $?; }
 if [ "${PROFILE:-1}" == "1" ]; then
   mkdir -p $OUT/s4_prof
   run s4_prof 400 rocprofv3 --kernel-trace --stats -d $OUT/s4_prof -o flagship -- python3 bench.py --steps 3 --warmup 2 --secondary 0 || exit $?
