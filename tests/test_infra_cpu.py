@@ -209,3 +209,20 @@ def test_xgmi_size_class_routing_policy():
     assert SizeClass()(16) and SizeClass()(1 << 30) and not SizeClass()(0)
     with pytest.raises(ValueError):
         SizeClass(100, 10)
+
+
+def test_multi_tensor_table_layout():
+    """The multi-tensor table (meta rows + packed (tensor, chunk) int32 pairs in ONE buffer, built without a
+    per-chunk loop) lists every chunk of every tensor in order; empty tensors get no chunk, an empty list one dummy."""
+    from pytorch_distributedtraining_amd.ops.multi_tensor import META, TensorTable
+    ts = [torch.zeros(100000), torch.zeros(5), torch.zeros(0), torch.zeros(70000), torch.zeros(32768)]
+    gs = [torch.zeros_like(t) for t in ts]
+    tab = TensorTable([ts, gs], chunk=32768)
+    want = [[i, c] for i, t in enumerate(ts) for c in range((t.numel() + 32767) // 32768)]
+    assert tab.nblocks == len(want) and tab.blk.tolist() == want
+    assert tab.blk.dtype == torch.int32 and tab.meta.shape == (len(ts), META)
+    assert tab.meta[:, 5].tolist() == [t.numel() for t in ts]
+    assert tab.meta[:, 0].tolist() == [t.data_ptr() for t in ts]
+    assert tab.meta[:, 1].tolist() == [g.data_ptr() for g in gs]
+    empty = TensorTable([[torch.zeros(0)]])
+    assert empty.nblocks == 0 and empty.blk.tolist() == [[0, 0]]
