@@ -211,7 +211,12 @@ def timed_loop(step_fn, args, comm, dev):
     if dev.type == "cuda":
         timed_loop.comm["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     if comm.world_size > 1 and dev.type == "cuda" and args.overlap_probe:
-        timed_loop.comm.update(overlap_probe(step_fn, comm, dev, float(t.item()) * 1000 / args.steps))
+        # diagnostics only, after the measurement: a failure here must not cost the run its JSON line
+        try:
+            timed_loop.comm.update(overlap_probe(step_fn, comm, dev, float(t.item()) * 1000 / args.steps))
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] overlap probe skipped: {type(e).__name__}: {e}")
+            timed_loop.comm["overlap_probe_error"] = f"{type(e).__name__}: {e}"[:200]
     return float(t.item())
 
 
