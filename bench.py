@@ -231,15 +231,24 @@ def overlap_probe(step_fn, comm, dev, step_ms):
     step_fn()
     exposed = C.stop_wait_timing()
     ops, comm.op_log = comm.op_log, None
-    bufs = []
-    for op, n, dt, d in ops:
-        kind = op.split(":")[0]
-        if kind == "all_gather":
-            bufs.append((kind, op, torch.empty(n, dtype=dt, device=d), torch.empty(n * comm.world_size, dtype=dt, device=d)))
-        elif kind == "reduce_scatter":
-            bufs.append((kind, op, torch.empty(n // comm.world_size, dtype=dt, device=d), torch.empty(n, dtype=dt, device=d)))
-        else:
-            bufs.append((kind, op, torch.zeros(n, dtype=dt, device=d), None))
+    bufs, err = [], None
+    try:
+        for op, n, dt, d in ops:
+            kind = op.split(":")[0]
+            if kind == "all_gather":
+                bufs.append((kind, op, torch.empty(n, dtype=dt, device=d), torch.empty(n * comm.world_size, dtype=dt, device=d)))
+            elif kind == "reduce_scatter":
+                bufs.append((kind, op, torch.empty(n // comm.world_size, dtype=dt, device=d), torch.empty(n, dtype=dt, device=d)))
+            else:
+                bufs.append((kind, op, torch.zeros(n, dtype=dt, device=d), None))
+    except RuntimeError as e:  # e.g. out of memory on one rank only
+        err, bufs = e, []
+    # every rank agrees before the replay, so a local failure skips the probe everywhere instead of
+    # leaving the other ranks blocked in a collective this rank never enters
+    flag = torch.tensor([0.0 if err is None else 1.0], device=dev)
+    comm.all_reduce(flag, "max")
+    if flag.item() > 0:
+        raise RuntimeError(f"replay buffers unavailable on some rank ({err})")
 
     def replay():
         for kind, op, a, b in bufs:
