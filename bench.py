@@ -132,8 +132,9 @@ def main():
     if args.secondary and args.workload == "gpt2-fsdp":
         # BASELINE.json names TWO headline metrics (GPT-2-1.3B FSDP tokens/s and ResNet-50 DDP samples/s, both
         # "at 1/2/4/8"): every run also measures the second one at the SAME world size, so each point of the
-        # driver's scaling curve records both.  Outside the primary's timed region; a failure here is reported
-        # and never loses the primary line.
+        # driver's scaling curve records both.  Outside the primary's timed region; its setup and first step
+        # are guarded phases (bench_resnet guarded=True): a failure on any rank skips it on every rank together
+        # and the primary line is still printed.
         import copy
         import gc
         gc.collect()
@@ -143,17 +144,59 @@ def main():
             a2.workload, a2.micro_batch, a2.steps, a2.warmup = "resnet50-ddp", args.secondary_micro_batch, 10, 3
             if dev.type == "cpu":
                 a2.steps, a2.warmup = 1, 1
-            sec = bench_resnet(a2, comm, dev, world, rank)
+            sec = bench_resnet(a2, comm, dev, world, rank, guarded=True)
             result["secondary"] = {k: sec[k] for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "steps",
                                                        "warmup", "dtype", "config", "collectives_per_step",
                                                        "comm_bytes_per_step") if k in sec}
-        except Exception as e:   # pragma: no cover - reported, primary result kept
+        except SecondarySkipped as e:   # every rank raised this together: no rank is left in a collective
+            log(f"[bench] secondary ResNet-50 measurement skipped on every rank: {e}")
+            result["secondary_error"] = str(e)[:200]
+        except Exception as e:  # noqa: BLE001 - one rank: nobody to strand, keep the primary line
+            if world > 1:
+                raise
             log(f"[bench] secondary ResNet-50 measurement failed: {e!r}")
+            result["secondary_error"] = f"{type(e).__name__}: {e}"[:200]
+    if not headline_ok(result, args, dev, world):
+        sys.exit(3)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+class SecondarySkipped(RuntimeError):
+    """Raised on EVERY rank at the same agreement point when any rank failed a guarded phase."""
+
+
+def agree(comm, dev, err, phase):
+    """Phase boundary of a guarded measurement: every rank contributes whether it failed; all raise
+    together, so a failure on one rank never leaves the others blocked in the next collective."""
+    import torch
+    flag = torch.tensor([0.0 if err is None else 1.0], device=dev)
+    if comm.world_size > 1:
+        comm.all_reduce(flag, "max")
+    if float(flag.item()) > 0:
+        raise SecondarySkipped(f"{phase}: " + (f"{type(err).__name__}: {err}" if err is not None else "failed on another rank"))
+
+
+def headline_ok(result, args, dev, world) -> bool:
+    """N > 1 on GPUs: print a headline only if the process group really spans N ranks on N distinct devices
+    (a run whose ranks shared a GPU, or whose c10d world disagrees, would be a mislabelled scaling point).
+    PDT_BENCH_REHEARSAL=1 (the one-GPU multi-rank plumbing rehearsal) prints it, marked as a rehearsal."""
+    topo = result.get("topology", {})
+    if dev.type != "cuda" or world <= 1:
+        return True
+    ok = topo.get("c10d_world") == world == args.gpus and topo.get("distinct_devices") == world
+    if ok:
+        return True
+    if os.environ.get("PDT_BENCH_REHEARSAL") == "1":
+        result["rehearsal"] = True
+        result["metric"] += " [REHEARSAL: ranks share GPUs -- not a measurement]"
+        return True
+    log(f"[bench] refusing to print a headline: c10d_world={topo.get('c10d_world')} n_gpus={args.gpus} "
+        f"WORLD_SIZE={world} distinct_devices={topo.get('distinct_devices')}")
+    return False
 
 
 def topology(comm, dev):
@@ -407,36 +450,50 @@ def bench_gpt2(args, comm, dev, world, rank):
                           if ckpt_on else {})}}
 
 
-def bench_resnet(args, comm, dev, world, rank):
+def bench_resnet(args, comm, dev, world, rank, guarded=False):
+    """``guarded`` (the secondary measurement after the GPT-2 headline): model / data are built and one local
+    step (forward, backward under ``no_sync``, optimizer step -- no collective) runs before the timed loop,
+    with an agreement of all ranks after each phase (``agree``), so an OOM or kernel error on one rank skips
+    the measurement on every rank instead of blocking the others in a DDP collective."""
     import torch
     from pytorch_distributedtraining_amd.models.resnet import resnet50
     from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
     from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
 
     cpu = dev.type == "cpu"
+    fail_rank = int(os.environ.get("PDT_BENCH_SECONDARY_FAIL_RANK", "-1")) if guarded else -1
     if not cpu and os.environ.get("PDT_CONV_BENCHMARK", "1") == "1":
         # MIOpen find per conv shape in the first (untimed) step instead of its immediate-mode heuristic:
         # 7,133 -> 7,999 samples/s (profiles/r1_v9_miopen_modes.log; exhaustive search adds nothing)
         torch.backends.cudnn.benchmark = True
     mb = args.micro_batch or (16 if cpu else 256)
-    if cpu:
-        from pytorch_distributedtraining_amd.models.resnet import resnet18
-        model = resnet18().to(memory_format=torch.channels_last)
-    else:
-        model = resnet50().to(dev).to(memory_format=torch.channels_last)
     # PDT_RESNET_AUTOCAST=0: the DDP bf16 compute copy instead of fp32 parameters under autocast (convs / fc on
     # bf16 parameters the fused AdamW epilogue rewrites from fp32 masters, channels_last inside the flat, batch
     # norms fp32).  Measured equal (8,624-8,728 vs 8,722 samples/s, profiles/r3_s4_resnet50_compute_copy_ab.log):
     # the ~250 weight-cast / fp32 gradient-add launches it removes are not on the critical path -- autocast kept
     autocast = cpu or os.environ.get("PDT_RESNET_AUTOCAST", "1") == "1"
+    err = None
+    try:   # phase 1 (local): module, inputs
+        if cpu:
+            from pytorch_distributedtraining_amd.models.resnet import resnet18
+            model = resnet18().to(memory_format=torch.channels_last)
+        else:
+            model = resnet50().to(dev).to(memory_format=torch.channels_last)
+        x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+        if not autocast:
+            x = x.bfloat16()
+        y = torch.randint(0, 1000, (mb,), device=dev)
+    except Exception as e:  # noqa: BLE001
+        if not guarded:
+            raise
+        err = e
+    if guarded:
+        agree(comm, dev, err, "build")
+    # phase 2: the DDP wrap (startup broadcast: every rank is here), then one local step
     model = DistributedDataParallel(model, comm=comm, reduce_dtype=None if cpu else torch.bfloat16,
                                     compute_dtype=None if autocast else torch.bfloat16)
     params = model.optimizer_parameters()
     opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
-    x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
-    if not autocast:
-        x = x.bfloat16()
-    y = torch.randint(0, 1000, (mb,), device=dev)
     crit = torch.nn.CrossEntropyLoss()
 
     def step():
@@ -446,6 +503,24 @@ def bench_resnet(args, comm, dev, world, rank):
         _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
         opt.step(grad_scale=coef)
         opt.zero_grad(set_to_none=True)
+
+    if guarded:
+        try:
+            if rank == fail_rank:
+                raise RuntimeError("injected secondary failure (PDT_BENCH_SECONDARY_FAIL_RANK)")
+            # no collective at all: gradient buckets held (no_sync), buffers not broadcast -- a local failure
+            # here cannot strand a peer
+            bb, model.broadcast_buffers = model.broadcast_buffers, False
+            try:
+                with model.no_sync():
+                    step()
+            finally:
+                model.broadcast_buffers = bb
+            if not cpu:
+                torch.cuda.synchronize(dev)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        agree(comm, dev, err, "first step")
 
     dt = timed_loop(step, args, comm, dev)
     sps = world * mb * args.steps / dt

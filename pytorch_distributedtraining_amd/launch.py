@@ -50,20 +50,39 @@ def spawn(fn, nprocs: int, args=(), join: bool = True):
     return mp.spawn(_worker_entry, args=(fn, nprocs, tuple(args), port), nprocs=nprocs, join=join)
 
 
+def visible_gpu_count() -> int | None:
+    """GPUs this process may use, counted WITHOUT touching HIP (the launcher forks ranks; a parent that has
+    initialised the GPU must not): the first of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES that is set, else the GPU nodes of the KFD topology in sysfs (CPU nodes report
+    gfx_target_version 0).  None when neither says (then nothing is capped)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    for line in f:
+                        k, _, val = line.partition(" ")
+                        if k == "gfx_target_version" and int(val) > 0:
+                            n += 1
+                            break
+            except (OSError, ValueError):
+                continue
+        return n or None
+    except OSError:
+        return None
+
+
 def _shared_gpu_queues(nproc: int) -> str | None:
     """GPU_MAX_HW_QUEUES for ranks that must share GPUs (more ranks than devices: one-GPU rehearsals), keeping
-    <= 8 HIP hardware queues per GPU.  With 4 queues per rank, 4 ranks on one GPU had a rank's 3rd xGMI
-    collective go unscheduled while peers' mesh kernels spun for it (profiles/r3_rehearsal_gpt2_fsdp_w4_q4_vs_q2.log);
-    2 queues per rank passed once and failed on a repeat (profiles/r3_rehearsal_gpt2_fsdp_w4_q2_repeat.log), so
-    several ranks spinning on one GPU stay a rehearsal-only configuration -- one rank per GPU keeps HIP's default.
-    device_count() does not initialise the GPU in this (launcher) process; on some boxes it reports the node's
-    GPUs rather than the ones this process can use, and then nothing is capped."""
-    try:
-        import torch
-        ndev = torch.cuda.device_count()
-    except Exception:
-        return None
-    if not 0 < ndev < nproc:
+    <= 8 HIP hardware queues per GPU (each rank's compute, comm and copy streams).  One rank per GPU keeps
+    HIP's default.  Counted by ``visible_gpu_count`` (no HIP initialisation in the launcher)."""
+    ndev = visible_gpu_count()
+    if ndev is None or not 0 < ndev < nproc:
         return None
     per_dev = -(-nproc // ndev)
     return str(max(1, 8 // per_dev))

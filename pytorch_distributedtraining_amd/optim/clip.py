@@ -12,12 +12,23 @@ from ..ops import multi_tensor as mt
 from ._grads import grad_of
 
 
+def _device(parameters, comm):
+    if parameters:
+        return parameters[0].device
+    if comm is not None and comm.backend == "nccl" and torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def grad_norm_sq(parameters, comm=None, sharded=False) -> torch.Tensor:
+    parameters = list(parameters)
     grads = [grad_of(p) for p in parameters if grad_of(p) is not None]
-    if not grads:
-        dev = next(iter(parameters)).device if parameters else torch.device("cpu")
-        return torch.zeros(1, dtype=torch.float32, device=dev)
-    total = mt.l2norm_sq(grads)
+    if grads:
+        total = mt.l2norm_sq(grads)
+    else:
+        # a rank that owns no gradient (more ranks than sharded tensors) still joins the all-reduce below,
+        # or every other rank would wait for it forever
+        total = torch.zeros(1, dtype=torch.float32, device=_device(parameters, comm))
     if sharded and comm is not None and comm.world_size > 1:
         comm.all_reduce(total, "sum")
     return total
@@ -35,13 +46,16 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, comm=No
     parameters = list(parameters)
     if norm_type != 2.0:
         grads = [grad_of(p) for p in parameters if grad_of(p) is not None]
+        dev = _device(parameters, comm)
         if norm_type == float("inf"):
-            local = torch.stack([g.detach().abs().max().float() for g in grads]).max().reshape(1)
+            local = torch.stack([g.detach().abs().max().float() for g in grads]).max().reshape(1) if grads \
+                else torch.zeros(1, device=dev)
             if sharded and comm is not None:
                 comm.all_reduce(local, "max")
             total = local
         else:
-            local = sum(g.detach().float().abs().pow(norm_type).sum() for g in grads).reshape(1)
+            local = sum((g.detach().float().abs().pow(norm_type).sum() for g in grads),
+                        torch.zeros((), device=dev)).reshape(1)
             if sharded and comm is not None:
                 comm.all_reduce(local, "sum")
             total = local.pow(1.0 / norm_type)

@@ -129,6 +129,19 @@ class _FlatGroup:
             p.grad = _pview(self.flat_grad, p, o)
 
 
+def _cast_except_batchnorm(module: nn.Module, dtype: torch.dtype) -> None:
+    """``module.to(dtype)`` for every floating parameter / buffer except those owned by batch norms."""
+    for m in module.modules():
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            continue
+        for p in m.parameters(recurse=False):
+            if p.is_floating_point() and p.dtype != dtype:
+                p.data = p.data.to(dtype)
+        for name, b in list(m.named_buffers(recurse=False)):
+            if b is not None and b.is_floating_point() and b.dtype != dtype:
+                m._buffers[name] = b.to(dtype)
+
+
 class DistributedDataParallel(nn.Module):
     """Data parallel wrapper.
 
@@ -182,12 +195,10 @@ class DistributedDataParallel(nn.Module):
 
         module.to(self.device)
         if compute_dtype is not None:
-            module.to(compute_dtype)
             # batch norms keep fp32 affine parameters and running statistics (their own fp32 flat group):
-            # bf16 running stats drift, and the fused BN kernels take fp32 parameters with bf16 activations
-            for m in module.modules():
-                if isinstance(m, nn.modules.batchnorm._BatchNorm):
-                    m.float()
+            # bf16 running stats drift, and the fused BN kernels take fp32 parameters with bf16 activations.
+            # They are never cast at all (a round trip through bf16 would round values loaded before wrapping).
+            _cast_except_batchnorm(module, compute_dtype)
         self.params = [p for p in module.parameters() if p.requires_grad]
         if self.comm.world_size > 1:
             self.comm.broadcast_coalesced([p.data for p in self.params] + [b for b in module.buffers()])

@@ -369,10 +369,31 @@ class OSS(Optimizer):
         self.optim.load_state_dict(local)
 
 
-class ShardedDataParallel(nn.Module):
-    """ZeRO-2: each gradient is reduced (averaged) only to the rank that owns its optimizer shard, and
-    non-owners drop it.  ``reduce_mode="all_reduce"``: ZeRO-1 (full gradients all-reduced, DDP + OSS)."""
+class _Window:
+    """ZeRO-2 reduce-scatter bucket: the window [lo, lo + n) of EVERY owner's segment of one bank.  Packed
+    owner-major ([owner 0's window | owner 1's | ...]) into one staging slot, a single reduce-scatter (AVG)
+    leaves owner r's reduced window in rank r's persistent gradient segment."""
 
+    __slots__ = ("bank", "lo", "n", "members", "drop")
+
+    def __init__(self, bank, lo, n):
+        self.bank, self.lo, self.n = bank, lo, n
+        self.members = []   # (slot offset, local param idx, param-local start a, end b), sorted by slot offset
+        self.drop = []      # non-owned local param idx whose LAST window this is (gradient freed after packing)
+
+
+class ShardedDataParallel(nn.Module):
+    """ZeRO-2: gradients are reduce-scattered (averaged) onto the ranks that own their optimizer shard, and
+    non-owners drop them.  ``reduce_mode="all_reduce"``: ZeRO-1 (full gradients all-reduced, DDP + OSS).
+
+    Fairscale's ShardedDDP reduces every parameter to its owner (``dist.reduce`` per parameter or small-param
+    bucket).  On a full xGMI mesh a reduce into ONE destination loads that destination's inbound
+    links only, and W owners mean W collectives per gradient region.  Here a bucket is the same window of every
+    owner's segment (``_Window``): one reduce-scatter per window moves every rank's share at once over all
+    links, and each rank's reduced gradient lands directly in its persistent segment.  Readiness: a parameter
+    belongs to the FIRST window it touches and windows are released strictly in order, so a window is launched
+    only when every parameter intersecting it has its gradient (a parameter spanning windows keeps its
+    gradient until the last of them is packed)."""
 
     def __init__(self, module: nn.Module, sharded_optimizer: OSS, comm: Comm | None = None,
                  broadcast_buffers: bool = True, sync_models_at_startup: bool = True,
@@ -381,7 +402,7 @@ class ShardedDataParallel(nn.Module):
         super().__init__()
         if staging_slots < 1:
             raise ValueError(f"staging_slots must be >= 1, got {staging_slots}")
-        self.STAGING_SLOTS = staging_slots   # non-owned buckets in flight at once (ring of pack buffers)
+        self.STAGING_SLOTS = staging_slots   # windows in flight at once (ring of pack buffers)
         if reduce_mode not in ("reduce", "all_reduce"):
             raise ValueError(f"reduce_mode must be 'reduce' or 'all_reduce', got {reduce_mode}")
         self.module = module
@@ -401,24 +422,30 @@ class ShardedDataParallel(nn.Module):
                 self.comm.broadcast_coalesced(bufs)
         self.params = sharded_optimizer._all_params
         self._pad = {}
-        self._rings = {}            # (wire dtype, device) -> staging ring for non-owned buckets (_slot)
-        # gradient storage: own segment only (ZeRO-2) or the full flat (ZeRO-1); buckets from the layout
-        self._buckets = []          # (bank, owner, start, numel, [local idx])
+        self._rings = {}            # (wire dtype, device) -> staging ring (_slot)
+        # gradient storage: own segment only (ZeRO-2) or the full flat (ZeRO-1)
         self._grad = {}             # bank id -> gradient flat
+        self._buckets = []          # all_reduce: (bank, owner, start, numel, [local idx]); reduce: _Window
+        readiness = []              # global parameter indices per bucket, in release order
         for bank in sharded_optimizer.banks():
-            if reduce_mode == "reduce":
-                self._grad[id(bank)] = torch.zeros(bank.seg, dtype=bank.dtype, device=bank.device)
-            else:
-                self._grad[id(bank)] = torch.zeros(bank.total, dtype=bank.dtype, device=bank.device)
-            esz = torch.tensor([], dtype=bank.dtype).element_size()
-            for b in bank.layout(reduce_buffer_size // esz).buckets:
-                self._buckets.append((bank, int(b.owner), int(b.start), int(b.numel), list(b.params)))
-        self._buckets.sort(key=lambda b: -min(b[0].idxs[li] for li in b[4]))
+            n = bank.seg if reduce_mode == "reduce" else bank.total
+            self._grad[id(bank)] = torch.zeros(n, dtype=bank.dtype, device=bank.device)
+        if reduce_mode == "reduce":
+            for bank in sharded_optimizer.banks():
+                wins, first = self._plan_windows(bank, reduce_buffer_size)
+                for k, w in enumerate(wins):
+                    self._buckets.append(w)
+                    readiness.append([bank.idxs[li] for li in first.get(k, [])])
+        else:
+            tmp = []
+            for bank in sharded_optimizer.banks():
+                esz = torch.tensor([], dtype=bank.dtype).element_size()
+                for b in bank.layout(reduce_buffer_size // esz).buckets:
+                    tmp.append((bank, int(b.owner), int(b.start), int(b.numel), list(b.params)))
+            tmp.sort(key=lambda b: -min(b[0].idxs[li] for li in b[4]))
+            self._buckets = tmp
+            readiness = [[bank.idxs[li] for li in lidx] for bank, _o, _s, _n, lidx in tmp]
         self._attach()
-        gidx = {}
-        for bi, (bank, _o, _s, _n, lidx) in enumerate(self._buckets):
-            for li in lidx:
-                gidx.setdefault(bi, []).append(bank.idxs[li])
         self._bank_li = {}
         for bank in sharded_optimizer.banks():
             for li, gi in enumerate(bank.idxs):
@@ -427,9 +454,43 @@ class ShardedDataParallel(nn.Module):
         # bucket; frozen parameters get no hook and their buckets are released at the end of backward
         ref = weakref.ref(self)
         self._ready = NullReadiness() if self.comm.world_size == 1 else \
-            Readiness(self.params, [gidx[b] for b in range(len(self._buckets))],
-                      on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b))
+            Readiness(self.params, readiness, on_first=lambda: ref()._queue_finalize(),
+                      on_ready=lambda b: ref()._launch(b))
         self._ready.set_enabled(self.comm.world_size > 1)
+
+    def _wire_dtype(self, bank):
+        if self.reduce_fp16 and bank.dtype == torch.float32:
+            return torch.bfloat16 if bank.device.type == "cuda" else torch.float16
+        return bank.dtype
+
+    def _plan_windows(self, bank, reduce_buffer_size):
+        """Windows over the segment coordinate.  Window length: the whole bucket (every owner's window) is
+        about ``reduce_buffer_size`` bytes on the wire, in 16-element granules.  Segments list their owner's
+        parameters in reverse registration order (native ZeroLayout), so window 0 holds each owner's
+        last-layer gradients -- the first ones backward produces."""
+        W = bank.world
+        esz = torch.tensor([], dtype=self._wire_dtype(bank)).element_size()
+        w = max(ALIGN, (reduce_buffer_size // (esz * W)) // ALIGN * ALIGN)
+        nwin = max(1, -(-bank.seg // w))
+        wins = [_Window(bank, k * w, min(w, bank.seg - k * w)) for k in range(nwin)]
+        first, last = {}, {}
+        for li, p in enumerate(bank.params):
+            r = bank.owners[li]
+            s0 = bank.offsets[li] - r * bank.seg          # segment coordinate of the parameter's first element
+            s1 = s0 + p.numel()
+            k0, k1 = s0 // w, (s1 - 1) // w
+            for k in range(k0, k1 + 1):
+                win = wins[k]
+                a, b = max(s0, win.lo), min(s1, win.lo + win.n)
+                win.members.append((r * win.n + (a - win.lo), li, a - s0, b - s0))
+            first.setdefault(k0, []).append(li)
+            last[li] = k1
+        for win in wins:
+            win.members.sort()
+        for li, k in last.items():
+            if bank.owners[li] != bank.rank:
+                wins[k].drop.append(li)
+        return wins, first
 
     # ------------------------------------------------------------------ gradient storage
     def _grad_view(self, bank, li):
@@ -460,8 +521,12 @@ class ShardedDataParallel(nn.Module):
         return n
 
     def staging_bytes(self) -> int:
-        """Bytes of the persistent pack rings (bounded by STAGING_SLOTS x the largest non-owned bucket)."""
+        """Bytes of the persistent pack rings (STAGING_SLOTS x world x the longest window, per wire dtype)."""
         return sum(t.numel() * t.element_size() for r in self._rings.values() for t in r["bufs"])
+
+    def collectives_per_backward(self) -> int:
+        """Collectives one synchronised backward issues (one per bucket)."""
+        return len(self._buckets) if self.comm.world_size > 1 else 0
 
     # ------------------------------------------------------------------ hooks / reduction
     def _zeros(self, n, dtype, device):
@@ -472,15 +537,14 @@ class ShardedDataParallel(nn.Module):
 
     def _slot(self, bank, n, dtype):
         """A staging slot of ``n`` elements from the (dtype, device) ring of STAGING_SLOTS persistent buffers,
-        each as large as the largest non-owned bucket.  A slot is reused only after the reduce that last read
-        it was waited for (stream-ordered on device, so no host sync): ZeRO-2 keeps its memory bound -- the
-        ring is a few buckets, not the (W-1)/W of the gradients a buffer per bucket would pin -- while the
-        pack allocates nothing."""
+        each world x the longest window.  A slot is reused only after the collective that last read it was
+        waited for (stream-ordered on device, so no host sync): ZeRO-2 keeps its memory bound -- the ring is a
+        few buckets, not the (W-1)/W of the gradients a buffer per bucket would pin -- while the pack
+        allocates nothing."""
         key = (dtype, bank.device)
         ring = self._rings.get(key)
         if ring is None:
-            size = max(bn for bk, ow, _s, bn, _l in self._buckets
-                       if ow != bk.rank and bk.device == bank.device)
+            size = max(w.bank.world * w.n for w in self._buckets if w.bank.device == bank.device)
             ring = self._rings[key] = {"bufs": [torch.empty(size, dtype=dtype, device=bank.device)
                                                 for _ in range(self.STAGING_SLOTS)],
                                        "busy": [None] * self.STAGING_SLOTS, "next": 0}
@@ -488,50 +552,56 @@ class ShardedDataParallel(nn.Module):
         ring["next"] = (i + 1) % self.STAGING_SLOTS
         if ring["busy"][i] is not None:
             ring["busy"][i].wait()
+            ring["busy"][i] = None
         return ring, i, ring["bufs"][i][:n]
 
-    def _pack(self, bank, start, n, lidx, dtype):
-        """Non-owner: this bucket's gradients in the owner's segment layout (gaps = zeros), cast to the wire
-        dtype in the same single ``cat`` kernel, written into a ring slot (no allocation per bucket)."""
-        pieces, cur = [], start
-        for li in sorted(lidx, key=lambda i: bank.offsets[i]):
-            p = bank.params[li]
-            o = bank.offsets[li]
-            if o > cur:
-                pieces.append(self._zeros(o - cur, bank.dtype, bank.device))
-            g = p.grad
-            pieces.append(g.reshape(-1) if g is not None else self._zeros(p.numel(), bank.dtype, bank.device))
-            p.grad = None                                # ZeRO-2: a non-owner drops the gradient
-            cur = o + p.numel()
-        if start + n > cur:
-            pieces.append(self._zeros(start + n - cur, bank.dtype, bank.device))
-        ring, i, slot = self._slot(bank, n, dtype)
+    def _pack_window(self, win, dtype):
+        """Every owner's window of this bucket, owner-major, into one ring slot: the rank's own window is one
+        contiguous slice of its persistent segment, peers' windows are (pieces of) the autograd gradients of
+        their parameters (gaps = zeros); the wire-dtype cast is fused into the single ``cat``."""
+        bank, n, W, r = win.bank, win.n, win.bank.world, win.bank.rank
+        own = self._grad[id(bank)][win.lo:win.lo + n]
+        parts = [(r * n, own)]
+        for off, li, a, b in win.members:
+            if bank.owners[li] != r:
+                g = bank.params[li].grad
+                parts.append((off, g.reshape(-1)[a:b] if g is not None else self._zeros(b - a, bank.dtype,
+                                                                                        bank.device)))
+        parts.sort(key=lambda x: x[0])
+        pieces, cur = [], 0
+        for off, t in parts:
+            if off > cur:
+                pieces.append(self._zeros(off - cur, bank.dtype, bank.device))
+            pieces.append(t)
+            cur = off + t.numel()
+        if W * n > cur:
+            pieces.append(self._zeros(W * n - cur, bank.dtype, bank.device))
+        ring, i, slot = self._slot(bank, W * n, dtype)
         torch.cat(pieces, out=slot)
-        return ring, i, slot
+        for li in win.drop:                             # ZeRO-2: a non-owner drops the gradient once packed
+            bank.params[li].grad = None
+        return ring, i, slot, own
 
     def _launch(self, b):
         with prof.range(f"sddp.{self.reduce_mode}[bucket {b}]"):
             self._launch_bucket(b)
 
     def _launch_bucket(self, b):
-        bank, owner, start, n, lidx = self._buckets[b]
-        wire = bank.dtype
-        if self.reduce_fp16 and bank.dtype == torch.float32:
-            wire = torch.bfloat16 if bank.device.type == "cuda" else torch.float16
-        if self.reduce_mode == "all_reduce" or owner == bank.rank:
-            o = start if self.reduce_mode == "all_reduce" else start - bank.rank * bank.seg
-            buf = self._grad[id(bank)][o:o + n]
+        if self.reduce_mode == "all_reduce":
+            bank, _owner, start, n, _lidx = self._buckets[b]
+            wire = self._wire_dtype(bank)
+            buf = self._grad[id(bank)][start:start + n]
             payload = buf if wire == buf.dtype else buf.to(wire)
-            if self.reduce_mode == "all_reduce":
-                h = self.comm.all_reduce(payload, "avg", async_op=True)
-            else:
-                h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
+            h = self.comm.all_reduce(payload, "avg", async_op=True)
             self._handles.append((h, buf if payload is not buf else None, payload))
-        else:
-            ring, i, payload = self._pack(bank, start, n, lidx, wire)
-            h = self.comm.reduce(payload, dst=owner, op="avg", async_op=True)
-            ring["busy"][i] = h
-            self._handles.append((h, None, payload))
+            return
+        win = self._buckets[b]
+        wire = self._wire_dtype(win.bank)
+        ring, i, slot, own = self._pack_window(win, wire)
+        out = own if wire == own.dtype else torch.empty(win.n, dtype=wire, device=own.device)
+        h = self.comm.reduce_scatter(out, slot, "avg", async_op=True)
+        ring["busy"][i] = h
+        self._handles.append((h, own if out is not own else None, out))
 
     def _queue_finalize(self):
         if self._callback_queued:
@@ -549,6 +619,8 @@ class ShardedDataParallel(nn.Module):
             if dst is not None:
                 dst.copy_(payload)
         self._handles.clear()
+        for ring in self._rings.values():
+            ring["busy"] = [None] * self.STAGING_SLOTS
         self._ready.reset()
 
     # ------------------------------------------------------------------ forward

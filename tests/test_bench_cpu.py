@@ -76,3 +76,47 @@ def test_bench_refuses_mismatched_world_size():
                        env=_env(WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_secondary_failure_on_one_rank_keeps_primary_line():
+    """a failure of the secondary ResNet measurement on ONE rank must not strand the other rank in
+    a DDP collective: the ranks agree at the guarded phase boundaries, skip the secondary together, and rank 0
+    still prints the primary GPT-2 line (with the reason in 'secondary_error')."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--workload", "gpt2-fsdp",
+                        "--model", "gpt2-tiny", "--micro-batch", "2", "--seq", "64", "--steps", "1", "--warmup", "1",
+                        "--secondary-micro-batch", "2"], cwd=ROOT, env=_env(PDT_BENCH_SECONDARY_FAIL_RANK="1"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["config"]["parallelism"] == "fsdp2" and res["value"] > 0
+    assert "secondary" not in res
+    assert "injected secondary failure" in res["secondary_error"] or "another rank" in res["secondary_error"]
+
+
+def test_headline_guard_refuses_shared_gpus():
+    """A GPU run at N > 1 prints a headline only when c10d world == --gpus == distinct devices."""
+    import importlib.util
+    import types
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    dev = types.SimpleNamespace(type="cuda")
+    args = types.SimpleNamespace(gpus=4)
+    good = {"metric": "m", "topology": {"c10d_world": 4, "distinct_devices": 4}}
+    assert bench.headline_ok(good, args, dev, 4)
+    shared = {"metric": "m", "topology": {"c10d_world": 4, "distinct_devices": 1}}
+    assert not bench.headline_ok(shared, args, dev, 4)
+    wrong_world = {"metric": "m", "topology": {"c10d_world": 2, "distinct_devices": 2}}
+    assert not bench.headline_ok(wrong_world, args, dev, 4)
+    old = os.environ.get("PDT_BENCH_REHEARSAL")
+    os.environ["PDT_BENCH_REHEARSAL"] = "1"
+    try:
+        assert bench.headline_ok(shared, args, dev, 4) and shared["rehearsal"] and "REHEARSAL" in shared["metric"]
+    finally:
+        if old is None:
+            del os.environ["PDT_BENCH_REHEARSAL"]
+        else:
+            os.environ["PDT_BENCH_REHEARSAL"] = old
+    assert bench.headline_ok({"metric": "m", "topology": {}}, types.SimpleNamespace(gpus=1), dev, 1)

@@ -1,4 +1,4 @@
-"""Engine equivalence on CPU / gloo, world_size 2: every engine must reproduce single-process training
+"""Engine equivalence on CPU / gloo, world_size 2, 4 and 8 (the reference ran 4 ranks, the MI355X node has 8): every engine must reproduce single-process training
 on the concatenated global batch (DDP, ZeRO-1 OSS, ZeRO-2 ShardedDDP, FSDP full-shard / grad-op),
 plus no_sync accumulation, SyncBN statistics and checkpoint consolidation."""
 import copy
@@ -69,7 +69,7 @@ def _w_ddp(rank, world, accum):
     return {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
-@pytest.mark.parametrize("world,accum", [(2, 1), (2, 2), (4, 1), (4, 2)])
+@pytest.mark.parametrize("world,accum", [(2, 1), (2, 2), (4, 1), (4, 2), (8, 1), (8, 2)])
 def test_ddp_matches_single_process(world, accum):
     ref = _reference(world, accum=accum)
     outs = run_workers(_w_ddp, world, accum)
@@ -163,7 +163,7 @@ def _w_zero(rank, world, sddp, bcast16):
     return {k: v.detach().clone() for k, v in m.state_dict().items()}, sd, list(opt.owner)
 
 
-@pytest.mark.parametrize("world,sddp", [(2, False), (2, True), (4, False), (4, True)])
+@pytest.mark.parametrize("world,sddp", [(2, False), (2, True), (4, False), (4, True), (8, False), (8, True)])
 def test_zero_oss_sddp_match_single_process(world, sddp):
     ref = _reference(world)
     outs = run_workers(_w_zero, world, sddp, False)
@@ -176,7 +176,8 @@ def test_zero_oss_sddp_match_single_process(world, sddp):
     assert sorted(sd["state"].keys()) == list(range(6))
     assert set(sd["state"][0].keys()) == {"step", "exp_avg", "exp_avg_sq"}
     assert sd["param_groups"][0]["params"] == list(range(6))
-    assert set(owner) == set(range(world))      # the greedy partition gives every rank a segment
+    # the greedy partition gives every rank a segment (world 8: only 6 tensors -> 6 owners)
+    assert len(set(owner)) == min(world, 6) and set(owner) <= set(range(world))
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -209,7 +210,7 @@ def _w_fsdp(rank, world, strategy):
 
 
 @pytest.mark.parametrize("world,strategy", [(2, "full_shard"), (2, "shard_grad_op"), (4, "full_shard"),
-                                            (4, "shard_grad_op")])
+                                            (4, "shard_grad_op"), (8, "full_shard"), (8, "shard_grad_op")])
 def test_fsdp_matches_single_process(world, strategy):
     ref = _reference(world)
     outs = run_workers(_w_fsdp, world, strategy)
@@ -236,7 +237,7 @@ def _w_syncbn(rank, world):
     return y.detach(), xs.grad, sbn.running_mean.clone(), sbn.running_var.clone(), sbn.weight.grad.clone()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_syncbn_matches_full_batch_bn(world):
     outs = run_workers(_w_syncbn, world)
     torch.manual_seed(0)
@@ -281,9 +282,9 @@ def _w_sharded_load(rank, world, path):
     return f.state_dict(), f.full_optim_state_dict(opt), extras
 
 
-@pytest.mark.parametrize("save_world,load_worlds", [(2, (1, 2, 4)), (4, (2, 4))])
+@pytest.mark.parametrize("save_world,load_worlds", [(2, (1, 2, 4, 8)), (4, (2, 4)), (8, (2,))])
 def test_sharded_checkpoint_resharding(tmp_path, save_world, load_worlds):
-    """save on N ranks -> load on M ranks (2->1, 2->2, 2->4, 4->2, 4->4) -> identical model + optimizer state."""
+    """save on N ranks -> load on M ranks (2->1/2/4/8, 4->2/4, 8->2) -> identical model + optimizer state."""
     from pytorch_distributedtraining_amd.utils.sharded_checkpoint import consolidate_to_full
     (sd, osd) = run_workers(_w_sharded_save, save_world, str(tmp_path))[0]
     for world in load_worlds:
@@ -360,7 +361,8 @@ def _w_zero2(rank, world, mode, accum, compute_bf16):
 
 
 @pytest.mark.parametrize("world,mode,accum", [(2, "reduce", 1), (2, "reduce", 2), (2, "all_reduce", 1),
-                                              (4, "reduce", 1), (4, "reduce", 2), (4, "all_reduce", 1)])
+                                              (4, "reduce", 1), (4, "reduce", 2), (4, "all_reduce", 1),
+                                              (8, "reduce", 1), (8, "reduce", 2), (8, "all_reduce", 1)])
 def test_zero2_reduce_to_owner_matches_and_shards_gradients(world, mode, accum):
     ref = _reference(world, accum=accum)
     outs = run_workers(_w_zero2, world, mode, accum, False)
@@ -442,7 +444,7 @@ def _w_zero2_mem(rank, world):
     return held, live, sum(p.numel() * 4 for p in m.parameters())
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_zero2_gradient_memory(world):
     bound = 1.0 / world + 0.05
     for held, live, total in run_workers(_w_zero2_mem, world):
@@ -451,15 +453,15 @@ def test_zero2_gradient_memory(world):
 
 
 def _w_zero2_ring(rank, world, reduce_fp16):
-    """ZeRO-2 non-owned buckets go through a ring of STAGING_SLOTS persistent pack buffers: with many more
-    buckets than slots, every slot is reused within one backward (after its reduce was waited for), and no
-    buffer is allocated after the first backward."""
+    """ZeRO-2 reduce-scatter windows are packed into a ring of STAGING_SLOTS persistent buffers: with many more
+    windows than slots, every slot is reused within one backward (after its reduce-scatter was waited for),
+    and no buffer is allocated after the first backward."""
     from pytorch_distributedtraining_amd.optim import FusedAdamW
     from pytorch_distributedtraining_amd.parallel.zero import OSS, ShardedDataParallel
     m = _deep_model()
     opt = OSS(m.parameters(), optim=FusedAdamW, lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
     model = ShardedDataParallel(m, opt, reduce_buffer_size=64, reduce_fp16=reduce_fp16, staging_slots=2)
-    nonowned = sum(1 for bk, ow, _s, _n, _l in model._buckets if ow != bk.rank)
+    nwin = len(model._buckets)                    # reduce-scatter windows (one collective each)
     ptrs = None
     for s in range(STEPS):
         x, y = _data(s, world)
@@ -469,18 +471,18 @@ def _w_zero2_ring(rank, world, reduce_fp16):
         ptrs = now
         opt.step()
         model.zero_grad()
-    biggest = max(n for bk, ow, _s, n, _l in model._buckets if ow != bk.rank)
+    longest = max(w.n for w in model._buckets)
     esz = 2 if reduce_fp16 else 4
-    return ({k: v.detach().clone() for k, v in m.state_dict().items()}, nonowned, model.staging_bytes(),
-            model.STAGING_SLOTS * biggest * esz)
+    return ({k: v.detach().clone() for k, v in m.state_dict().items()}, nwin, model.staging_bytes(),
+            model.STAGING_SLOTS * world * longest * esz)
 
 
-@pytest.mark.parametrize("world,reduce_fp16", [(2, False), (4, False), (2, True)])
+@pytest.mark.parametrize("world,reduce_fp16", [(2, False), (4, False), (8, False), (2, True)])
 def test_zero2_staging_ring_reuse(world, reduce_fp16):
     ref = _reference(world, model_fn=_deep_model)
     outs = run_workers(_w_zero2_ring, world, reduce_fp16)
     for o in outs:
-        assert o[1] > 2                       # more non-owned buckets than ring slots
+        assert o[1] > 2                       # more windows than ring slots
         assert o[2] == o[3]                   # the ring is the only staging memory
     for k in ref:
         for r in range(1, world):
@@ -547,3 +549,69 @@ def test_fsdp_rank0_only_offloaded_state_dicts():
     (n0, same0, none0, os0), (n1, same1, none1, os1) = run_workers(_w_fsdp_rank0, 2)
     assert n0 == 6 and same0 and not none0 and os0       # rank 0: the full dicts, on the host
     assert n1 == 0 and none1                             # rank 1: nothing materialised
+
+
+def test_ddp_bf16_compute_copy_never_rounds_batchnorm_through_bf16():
+    """with compute_dtype=bf16 the batch norms stay fp32 and are never cast at all -- affine
+    parameters and running statistics loaded before wrapping keep every bit (a round trip through bf16
+    would keep ~3 significant digits)."""
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 16), nn.BatchNorm1d(16), nn.Linear(16, 2))
+    bn = m[1]
+    with torch.no_grad():
+        bn.weight.copy_(1.0 + torch.rand(16) * 1e-3)
+        bn.bias.copy_(torch.randn(16) * 0.123456789)
+        bn.running_mean.copy_(torch.randn(16) * 3.14159265)
+        bn.running_var.copy_(1.0 + torch.rand(16) * 1.2345678)
+    want = {k: v.detach().clone() for k, v in bn.state_dict().items()}
+    DistributedDataParallel(m, compute_dtype=torch.bfloat16)
+    assert m[0].weight.dtype == torch.bfloat16 and m[2].weight.dtype == torch.bfloat16
+    for k, v in bn.state_dict().items():
+        assert v.dtype == want[k].dtype and torch.equal(v, want[k]), k
+
+
+def _w_fsdp_reduce_drift(rank, world, rdtype_name):
+    """One FSDP step (fp32 params, SGD lr 1) with the gradient reduce-scatter in ``rdtype``: the parameter
+    change IS the reduced (averaged) gradient."""
+    from pytorch_distributedtraining_amd.parallel.fsdp import FullyShardedDataParallel, MixedPrecision
+    rdtype = getattr(torch, rdtype_name)
+    m = _deep_model()
+    init = {k: v.detach().clone().double() for k, v in m.state_dict().items()}
+    f = FullyShardedDataParallel(m, wrap_classes=(nn.Linear,), mixed_precision=MixedPrecision(torch.float32, rdtype),
+                                 device="cpu")
+    opt = torch.optim.SGD(f.parameters(), lr=1.0)
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(world * 64, 16, generator=g)
+    y = torch.randn(world * 64, 4, generator=g)
+    nn.functional.mse_loss(f(_shard(x, rank, world)), _shard(y, rank, world)).backward()
+    opt.step()
+    sd = f.state_dict()
+    return {k: (init[k] - sd[k].double()) for k in init}
+
+
+def test_fsdp_bf16_gradient_reduce_drift_at_world8():
+    """the flagship reduces FSDP gradients in bf16 (MixedPrecision.reduce_dtype), so every
+    ring hop rounds to 8 significant bits.  Pinned at world 8 (the MI355X node) against the fp64 gradient of
+    the global batch: bf16 reduce relative L2 error <= 1.5e-2 per tensor (measured 4.1e-3 worst tensor), fp32
+    reduce <= 1e-4 (measured 3.7e-5: the fp32 parameter subtraction that exposes the gradient).  The gloo ring sums in the payload dtype like RCCL, so
+    this is the drift the 8-GPU run sees; at ~0.5 % per step, below AdamW's own eps/bias noise, bf16
+    (half the bytes on the xGMI links) stays the default reduce dtype."""
+    world = 8
+    m = _deep_model().double()
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(world * 64, 16, generator=g).double()
+    y = torch.randn(world * 64, 4, generator=g).double()
+    # per-rank mean losses averaged == the mean of the per-shard means (equal shard sizes)
+    loss = sum(nn.functional.mse_loss(m(_shard(x, r, world)), _shard(y, r, world)) for r in range(world)) / world
+    loss.backward()
+    truth = {k: p.grad for k, p in m.named_parameters()}
+    errs = {}
+    for name in ("bfloat16", "float32"):
+        got = run_workers(_w_fsdp_reduce_drift, world, name)[0]
+        errs[name] = max(float((got[k] - truth[k]).norm() / truth[k].norm()) for k in truth)
+    assert errs["float32"] <= 1e-4, errs
+    assert errs["bfloat16"] <= 1.5e-2, errs
+    assert errs["bfloat16"] > errs["float32"]
+    from pytorch_distributedtraining_amd.parallel.fsdp import MixedPrecision
+    assert MixedPrecision().reduce_dtype == torch.bfloat16

@@ -176,19 +176,31 @@ def test_window_mask_label_cache_is_identity_checked():
 
 
 def test_launcher_limits_hw_queues_only_when_ranks_share_gpus(monkeypatch):
-    """More ranks than GPUs (one-GPU rehearsals): <= 8 HIP hardware queues per GPU in total, so no rank's
-    collective kernel waits unmapped behind peers' spinning mesh kernels; one rank per GPU keeps the default."""
+    """More ranks than GPUs (one-GPU rehearsals): <= 8 HIP hardware queues per GPU in total; one rank per GPU
+    keeps the default.  The launcher counts GPUs from the env / sysfs and never through HIP (torch's
+    device_count() can fall back to a HIP-initialising query) -- a HIP query here makes the test fail."""
     import torch
     from pytorch_distributedtraining_amd import launch
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+
+    def no_hip():
+        raise AssertionError("the launcher must not query HIP")
+    monkeypatch.setattr(torch.cuda, "device_count", no_hip)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", no_hip, raising=False)
+    for var in ("ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
     assert launch._shared_gpu_queues(1) is None
     assert launch._shared_gpu_queues(2) == "4"
     assert launch._shared_gpu_queues(4) == "2"
     assert launch._shared_gpu_queues(8) == "1"
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    assert launch.visible_gpu_count() == 8
     assert launch._shared_gpu_queues(8) is None
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert launch._shared_gpu_queues(4) is None
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    n = launch.visible_gpu_count()          # sysfs KFD topology: this container has no GPU node
+    assert n is None or n >= 1
 
 
 def test_xgmi_size_class_routing_policy():
