@@ -497,6 +497,275 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   }
 }
 
+// ============================================================================================================
+// Hand-scheduled main loop (round 4): the whole K-loop is ONE inline-asm statement generated by
+// gen_gemm_kloop.py (gemm_kloop.inc) -- same tile, LDS images and DMA pieces as gemm_kernel above, but every
+// MFMA, LDS read, LDS-DMA piece, wait and barrier placed by hand with the accumulators pinned in a[0:255].
+// Epilogue: accumulator tiles are read back (v_accvgpr_read), the epilogue math runs in fp32, and bf16 results
+// are staged through LDS (528-byte rows) so every global store is a full 512-byte row segment
+// (32 lanes x 16 B; the compiler-scheduled kernel's 8-byte stores touched 16 rows per instruction).
+// ============================================================================================================
+}  // namespace
+#include "gemm_kloop.inc"
+namespace {
+
+constexpr int EROW = 528;                   // staging image row stride (bytes): 512 + 16 (2-way ds_write_b64)
+constexpr int SMEM2 = TM * EROW;            // 135,168 B >= the 128 KiB ring
+
+template <int I, int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+// accumulator tile k = 8 i + j (4 fp32) out of a[4k .. 4k + 3]
+template <int K>
+__device__ __forceinline__ f32x4 acc_tile() {
+  float x, y, z, w;
+  asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+               "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+               : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
+               : "i"(4 * K), "i"(4 * K + 1), "i"(4 * K + 2), "i"(4 * K + 3));
+  return f32x4{x, y, z, w};
+}
+
+// store phase of the staging image: wave w writes rows 64 w .. 64 w + 63, two rows (2 x 512 B) per instruction
+__device__ __forceinline__ void stage_store(const char* smem, bf16_t* dst, int64_t ldc, int m0, int n0, int w,
+                                            int lane) {
+  const int half = lane >> 5, c16 = lane & 31;
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int row = 64 * w + 2 * it + half;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(smem + row * EROW + c16 * 16);
+    *reinterpret_cast<u16x8*>(dst + (int64_t)(m0 + row) * ldc + n0 + 8 * c16) = v;
+  }
+}
+
+// load phase (DGELU's aux tile): the same mapping, global -> staging image
+__device__ __forceinline__ void stage_load(char* smem, const bf16_t* src, int64_t ldc, int m0, int n0, int w,
+                                           int lane) {
+  const int half = lane >> 5, c16 = lane & 31;
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int row = 64 * w + 2 * it + half;
+    *reinterpret_cast<u16x8*>(smem + row * EROW + c16 * 16) =
+        *reinterpret_cast<const u16x8*>(src + (int64_t)(m0 + row) * ldc + n0 + 8 * c16);
+  }
+}
+
+template <int LAYOUT, int EPI>
+__global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wr = w >> 1, wc = w & 1;
+  int tm, tn;
+  tile_of(p, blockIdx.x, (int)gridDim.x, tm, tn);
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int T = min(p.K - kbeg, p.k_per_split) / KB;
+
+  // ---- main-loop operands (see gen_gemm_kloop.py for the register map and schedule)
+  const char* Ab = reinterpret_cast<const char*>(p.A);
+  const char* Bb = reinterpret_cast<const char*>(p.B);
+  uint64_t a0, b0, astep, bstep;
+  uint32_t abytes, bbytes, rsa, rsb;
+  uint32_t voa0, voa1, vob0, vob1, rd0, rd1;
+  int32_t db;
+  if (LAYOUT == L_NT) {
+    a0 = (uint64_t)(uintptr_t)Ab + ((uint64_t)m0 * p.lda + kbeg) * 2;
+    b0 = (uint64_t)(uintptr_t)Bb + ((uint64_t)n0 * p.ldb + kbeg) * 2;
+    astep = bstep = KB * 2;
+    abytes = (uint32_t)((TM - 1) * p.lda * 2 + KB * 2);
+    bbytes = (uint32_t)((TN - 1) * p.ldb * 2 + KB * 2);
+    rsa = (uint32_t)(32 * p.lda * 2);
+    rsb = (uint32_t)(32 * p.ldb * 2);
+    const int row = 8 * w + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    voa0 = voa1 = (uint32_t)(row * p.lda * 2 + c * 16);
+    vob0 = vob1 = (uint32_t)(row * p.ldb * 2 + c * 16);
+    const int x = lane & 15, g = lane >> 4, h = (x >> 1) & 7;
+    rd0 = lds_addr + 16384 * wr + (uint32_t)(x * 128 + 16 * (g ^ h));
+    rd1 = lds_addr + 16384 * wr + (uint32_t)(x * 128 + 16 * ((4 + g) ^ h));
+    db = OPB + 16384 * (wc - wr);
+  } else {
+    a0 = (uint64_t)(uintptr_t)Ab + ((uint64_t)kbeg * p.lda + m0) * 2;
+    b0 = (uint64_t)(uintptr_t)Bb + ((uint64_t)kbeg * p.ldb + n0) * 2;
+    astep = (uint64_t)KB * p.lda * 2;
+    bstep = (uint64_t)KB * p.ldb * 2;
+    abytes = (uint32_t)((KB - 1) * p.lda * 2 + TM * 2);
+    bbytes = (uint32_t)((KB - 1) * p.ldb * 2 + TN * 2);
+    rsa = (uint32_t)(8 * p.lda * 2);
+    rsb = (uint32_t)(8 * p.ldb * 2);
+    const int r0 = 2 * w + (lane >> 5);
+    voa0 = (uint32_t)(r0 * p.lda * 2 + ((lane & 31) ^ tt_f(r0)) * 16);
+    voa1 = (uint32_t)(r0 * p.lda * 2 + ((lane & 31) ^ tt_f(r0 + 8)) * 16);
+    vob0 = (uint32_t)(r0 * p.ldb * 2 + ((lane & 31) ^ tt_f(r0)) * 16);
+    vob1 = (uint32_t)(r0 * p.ldb * 2 + ((lane & 31) ^ tt_f(r0 + 8)) * 16);
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    rd0 = lds_addr + 256 * wr + (uint32_t)((8 * g + q) * 512 + 16 * (pp >> 1) + 8 * (pp & 1));
+    rd1 = (uint32_t)tt_f(8 * g + q);     // the block XOR term
+    db = OPB + 256 * (wc - wr);
+  }
+  // buffer resources: {base lo, base hi (stride 0), num_records, dword3} assembled in the statement from 32-bit
+  // scalar operands (every value here is wave-uniform: kernel arguments, blockIdx and the wave index)
+  const uint32_t alo = (uint32_t)a0, ahi = (uint32_t)(a0 >> 32) & 0xffffu;
+  const uint32_t blo = (uint32_t)b0, bhi = (uint32_t)(b0 >> 32) & 0xffffu;
+  const uint32_t m0b = __builtin_amdgcn_readfirstlane(lds_addr + w * 1024);
+  const int dbs = __builtin_amdgcn_readfirstlane(db);
+  const uint32_t asl = (uint32_t)astep, ash = (uint32_t)(astep >> 32);
+  const uint32_t bsl = (uint32_t)bstep, bsh = (uint32_t)(bstep >> 32);
+  const int cnt = __builtin_amdgcn_readfirstlane(T);
+
+#define PDT_KLOOP_CLOBBERS                                                                                      \
+  "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",   \
+  "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78",     \
+  "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93",     \
+  "v94", "v95", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", \
+  "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152",      \
+  "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165",      \
+  "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178",      \
+  "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191",      \
+  "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204",      \
+  "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217",      \
+  "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230",      \
+  "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243",      \
+  "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255",              \
+  PDT_AGPR_CLOBBERS
+  if constexpr (LAYOUT == L_NT) {
+    asm volatile(PDT_GEMM_KLOOP_NT
+                 :
+                 : [alo] "s"(alo), [ahi] "s"(ahi), [anr] "s"(abytes), [blo] "s"(blo), [bhi] "s"(bhi), [bnr] "s"(bbytes),
+                   [cnt] "s"(cnt),
+                   [m0b] "s"(m0b), [rsa] "s"(rsa), [rsb] "s"(rsb), [asl] "s"(asl), [ash] "s"(ash), [bsl] "s"(bsl),
+                   [bsh] "s"(bsh), [voa] "v"(voa0), [vob] "v"(vob0), [rd0] "v"(rd0), [rd1] "v"(rd1), [db] "s"(dbs)
+                 : PDT_KLOOP_CLOBBERS);
+  } else {
+    asm volatile(PDT_GEMM_KLOOP_TT
+                 :
+                 : [alo] "s"(alo), [ahi] "s"(ahi), [anr] "s"(abytes), [blo] "s"(blo), [bhi] "s"(bhi), [bnr] "s"(bbytes),
+                   [cnt] "s"(cnt),
+                   [m0b] "s"(m0b), [rsa] "s"(rsa), [rsb] "s"(rsb), [asl] "s"(asl), [ash] "s"(ash), [bsl] "s"(bsl),
+                   [bsh] "s"(bsh), [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),
+                   [rd0] "v"(rd0), [rdx] "v"(rd1), [db] "s"(dbs)
+                 : PDT_KLOOP_CLOBBERS);
+  }
+#undef PDT_KLOOP_CLOBBERS
+  (void)voa1; (void)vob1;
+
+  // ---------------------------------------------------------------- epilogue
+  // acc tile (i, j): C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
+  const int lrow = 128 * wr + (lane & 15);
+  const int lcol = 128 * wc + 4 * (lane >> 4);
+  if constexpr (EPI == E_F32) {
+    float* C = p.ws + (int64_t)blockIdx.y * p.M * p.N;
+    sfor<0, 64>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const f32x4 v = acc_tile<k>();
+      *reinterpret_cast<f32x4*>(C + (int64_t)(m0 + lrow + 16 * (k >> 3)) * p.N + n0 + lcol + 16 * (k & 7)) = v;
+    });
+    return;
+  } else {
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+    char* img = smem;
+    __syncthreads();                         // every wave done with the ring: reuse its LDS as the staging image
+    if constexpr (EPI == E_DGELU) {
+      stage_load(img, p.aux, p.ldc, m0, n0, w, lane);
+      __syncthreads();
+    }
+    float bj[8][4];
+    if constexpr (EPI == E_BIAS || EPI == E_GELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const u16x4 b = *reinterpret_cast<const u16x4*>(p.bias + n0 + lcol + 16 * j);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(b[r]);
+      }
+    }
+    float cs[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+    // pass 0: the result (PLAIN / BIAS / DGELU) or the pre-activation (GELU) into the image
+    sfor<0, 64>([&](auto kc) {
+      constexpr int k = decltype(kc)::value, i = k >> 3, j = k & 7;
+      const f32x4 v = acc_tile<k>();
+      char* at = img + (lrow + 16 * i) * EROW + (lcol + 16 * j) * 2;
+      u16x4 o;
+      if constexpr (EPI == E_DGELU) {
+        const u16x4 hh = *reinterpret_cast<const u16x4*>(at);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bf16_t gb = f2bf(v[r] * gelu_grad<true>(bf2f(hh[r])));
+          o[r] = gb;
+          cs[j][r] += bf2f(gb);            // the bias gradient sums the gradient as stored
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf((EPI == E_BIAS || EPI == E_GELU) ? v[r] + bj[j][r] : v[r]);
+      }
+      *reinterpret_cast<u16x4*>(at) = o;
+    });
+    __syncthreads();
+    stage_store(img, EPI == E_GELU ? p.aux_out : C, p.ldc, m0, n0, w, lane);
+    if constexpr (EPI == E_GELU) {
+      // pass 1: GELU of the stored (rounded) pre-activation
+      __syncthreads();
+      sfor<0, 64>([&](auto kc) {
+        constexpr int k = decltype(kc)::value, i = k >> 3, j = k & 7;
+        const f32x4 v = acc_tile<k>();
+        char* at = img + (lrow + 16 * i) * EROW + (lcol + 16 * j) * 2;
+        u16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(gelu_f<true>(bf2f(f2bf(v[r] + bj[j][r]))));
+        *reinterpret_cast<u16x4*>(at) = o;
+      });
+      __syncthreads();
+      stage_store(img, C, p.ldc, m0, n0, w, lane);
+    }
+    if constexpr (EPI == E_DGELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = cs[j][r];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          cs[j][r] = v;
+        }
+      __syncthreads();                                   // the image is stored: reuse its LDS
+      float* red = reinterpret_cast<float*>(smem);       // [2 wave rows][256 columns]
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wr * 256 + lcol + 16 * j + r] = cs[j][r];
+      }
+      __syncthreads();
+      p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
+    }
+  }
+}
+
+template <int LAYOUT>
+int launch_asm_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
+  const dim3 grid((a.M / TM) * (a.N / TN), splits);
+  switch (epi) {
+    case E_PLAIN: gemm_asm_kernel<LAYOUT, E_PLAIN><<<grid, NTH, 0, s>>>(a); break;
+    case E_BIAS: gemm_asm_kernel<LAYOUT, E_BIAS><<<grid, NTH, 0, s>>>(a); break;
+    case E_GELU: gemm_asm_kernel<LAYOUT, E_GELU><<<grid, NTH, 0, s>>>(a); break;
+    case E_DGELU: gemm_asm_kernel<LAYOUT, E_DGELU><<<grid, NTH, 0, s>>>(a); break;
+    case E_F32: gemm_asm_kernel<LAYOUT, E_F32><<<grid, NTH, 0, s>>>(a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 // out[e] = sum over S slices of part[s][e] (fp32 slabs) -> bf16, 4 elements per thread
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ part,
                                                                  bf16_t* __restrict__ out, int64_t n4, int S,
@@ -666,6 +935,40 @@ PDT_API int pdt_gemm_bf16(int layout, int epi, const void* A, const void* B, voi
     const int64_t n4 = M * N / 4;
     gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, s>>>(ws, (bf16_t*)C, n4, splits, M * N);
     if (ldc != N) return (int)hipErrorInvalidValue;   // slab reduce writes a dense [M, N]
+  }
+  if (epi == E_DGELU) {
+    colpart_reduce_kernel<<<(int)((N + 255) / 256), 256, 0, s>>>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias);
+  }
+  return (int)hipGetLastError();
+}
+
+// The hand-scheduled main loop (gemm_asm_kernel): same contract as pdt_gemm_bf16, plus K / splits >= 128 and
+// ldc % 8 == 0 (16-byte epilogue stores).
+PDT_API int pdt_gemm2_bf16(int layout, int epi, const void* A, const void* B, void* C, int64_t M, int64_t N,
+                           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const void* bias, const void* aux,
+                           void* aux_out, void* dbias, float* ws, int splits, hipStream_t s) {
+  if (!pdt_gemm_ok(layout, M, N, K, lda, ldb, splits) || ldc < N || ldc % 8) return (int)hipErrorInvalidValue;
+  if (K / splits < 2 * KB) return (int)hipErrorInvalidValue;
+  if (epi < 0 || epi > E_DGELU) return (int)hipErrorInvalidValue;
+  if (splits > 1 && (epi != E_PLAIN || !ws)) return (int)hipErrorInvalidValue;
+  if ((epi == E_BIAS || epi == E_GELU) && !bias) return (int)hipErrorInvalidValue;
+  if (epi == E_GELU && !aux_out) return (int)hipErrorInvalidValue;
+  if (epi == E_DGELU && (!aux || !ws || !dbias)) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.bias = (const bf16_t*)bias; a.aux = (const bf16_t*)aux; a.aux_out = (bf16_t*)aux_out; a.ws = ws;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.k_per_split = (int)(K / splits);
+  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  const int run_epi = splits > 1 ? E_F32 : epi;
+  if (splits > 1) a.ldc = N;
+  int err = layout == L_NT ? launch_asm_layout<L_NT>(run_epi, a, splits, s)
+                           : launch_asm_layout<L_TT>(run_epi, a, splits, s);
+  if (err) return err;
+  if (splits > 1) {
+    if (ldc != N) return (int)hipErrorInvalidValue;
+    const int64_t n4 = M * N / 4;
+    gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, s>>>(ws, (bf16_t*)C, n4, splits, M * N);
   }
   if (epi == E_DGELU) {
     colpart_reduce_kernel<<<(int)((N + 255) / 256), 256, 0, s>>>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias);

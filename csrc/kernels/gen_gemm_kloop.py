@@ -1,0 +1,294 @@
+#!/usr/bin/env python
+"""Generates ``gemm_kloop.inc``: the whole MFMA main loop of the 256 x 256 x 64 bf16 GEMM (csrc/kernels/gemm.hip)
+as ONE inline-asm statement per operand layout, with every instruction placed by hand.
+
+Why asm: the compiler-scheduled loop of round 3 (same tile, same LDS images, same MFMA count) held the matrix
+pipe busy 0.61 of the time against hipBLASLt's 0.78-0.85 at the same 4-wave / one-wave-per-SIMD structure
+(profiles/r3_pmc_attention_tt_gemm_hipblaslt.txt).  With one wave per SIMD nobody hides a stall of the wave
+that owns the MFMA pipe, so the order of LDS reads, LDS-DMA pieces, waits and barriers between the MFMAs is
+the whole game; hipcc neither keeps 256 accumulators in place across a hand-placed schedule nor counts the
+inline-asm DMA it cannot see.
+
+Structure (per workgroup: 4 waves as 2 x 2, each wave 128 x 128 = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16,
+accumulators a[0:255]; LDS: two 64 KiB stages, A tile then B tile, filled by buffer_load ... lds):
+
+  K-step t reads stage s = t & 1 (tile t); fragments double-buffered: F0 = substep 0 (k 0..31), F1 = substep 1
+  Q1  32 MFMA F0.A[0..3] x F0.B        || F1 reads (tile t, stage s)          -> lgkmcnt(0), barrier
+  Q2  32 MFMA F0.A[4..7] x F0.B        || DMA of tile t+2, A pieces -> stage s (every wave done reading it)
+  Q3  32 MFMA F1.A[0..3] x F1.B        || DMA of tile t+2, B pieces           -> vmcnt(16) (= tile t+1 landed),
+                                                                                barrier
+  Q4  32 MFMA F1.A[4..7] x F1.B        || F0 reads of tile t+1 (stage s ^ 1)
+
+  Every tile's DMA has a full K-step of MFMAs to land; no MFMA waits for an LDS read issued in its own quarter;
+  the only two barriers per K-step sit where an LDS stage changes hands.
+
+Register map inside the statement (clobbered): v[128:255] fragments (F0.A, F0.B, F1.A, F1.B, 8 x 4 VGPRs
+each), v[64:95] LDS read addresses, s[80:91] buffer resources / counters, m0.  MFMA operand order is
+(B fragment, A fragment), so accumulator tile (i, j) holds C^T: lane l has 4 consecutive columns
+n = 16 j + 4 (l >> 4) + r of row m = 16 i + (l & 15) in a[4 (8 i + j) + r].
+
+Hazards handled here (hipcc pads nothing inside asm, cdna_hip_programming.md §5.7): an MFMA separates every
+m0 / soffset write from the DMA reading it; fragment registers are overwritten >= 8 MFMAs after their last
+MFMA read; the statement ends with s_nop padding so the compiler's v_accvgpr_read of the accumulators sits
+behind the last MFMA's result latency.
+
+Run ``python csrc/kernels/gen_gemm_kloop.py`` (the build does it when this file is newer than the .inc).
+"""
+import os
+
+NT, TT = 0, 1
+STB = 65536            # one LDS stage: A tile (32 KiB) then B tile
+OPB = 32768
+F0A, F0B, F1A, F1B = 128, 160, 192, 224
+RD = 64                # read-address registers
+S_RA, S_RB, S_CNT, S_OA, S_OB = 80, 84, 88, 89, 90
+
+
+def frag(base, i):
+    return f"v[{base + 4 * i}:{base + 4 * i + 3}]"
+
+
+def acc(i, j):
+    k = 4 * (8 * i + j)
+    return f"a[{k}:{k + 3}]"
+
+
+class Gen:
+    def __init__(self, layout):
+        self.layout = layout
+        self.lines = []
+
+    def emit(self, s):
+        self.lines.append(s)
+
+    # ---------------------------------------------------------------- pieces of work
+    def rd_reg(self, stage, op, sub_or_blk):
+        """NT: one address register per (stage, operand, substep); TT: one per (stage, operand, block)."""
+        if self.layout == NT:
+            return f"v{RD + stage * 4 + op * 2 + sub_or_blk}"
+        return f"v{RD + stage * 16 + op * 8 + sub_or_blk}"
+
+    def read_ops(self, stage, sub, which):
+        """LDS reads of one fragment set: list of instruction strings.  which = [(op, blk, dst_base)]."""
+        out = []
+        for op, blk, dst in which:
+            if self.layout == NT:
+                out.append(f"ds_read_b128 {frag(dst, blk)}, {self.rd_reg(stage, op, sub)} offset:{blk * 2048}")
+            else:
+                r = self.rd_reg(stage, op, blk)
+                o = sub * 16384
+                out.append(f"ds_read_b64_tr_b16 v[{dst + 4 * blk}:{dst + 4 * blk + 1}], {r} offset:{o}")
+                out.append(f"ds_read_b64_tr_b16 v[{dst + 4 * blk + 2}:{dst + 4 * blk + 3}], {r} offset:{o + 2048}")
+        return out
+
+    def dma_ops(self, stage, op):
+        """8 LDS-DMA pieces of one operand of one tile into `stage` (each piece: SALU set-up, then the load
+        one MFMA later), followed by the buffer-resource advance to the next tile."""
+        s_rs = S_RA if op == 0 else S_RB
+        s_off = S_OA if op == 0 else S_OB
+        ops = []
+        for i in range(8):
+            setup = [f"s_add_u32 m0, %[m0b], {stage * STB + op * OPB + i * 4096}"]
+            if i > 0:
+                setup.append(f"s_add_u32 s{s_off}, s{s_off}, %[{'rsa' if op == 0 else 'rsb'}]")
+            if self.layout == NT:
+                voff = "%[voa]" if op == 0 else "%[vob]"
+            else:
+                voff = (("%[voa1]" if op == 0 else "%[vob1]") if i & 1 else ("%[voa0]" if op == 0 else "%[vob0]"))
+            load = f"buffer_load_dwordx4 {voff}, s[{s_rs}:{s_rs + 3}], s{s_off} offen lds"
+            ops.append((setup, load))
+        tail = [f"s_add_u32 s{s_rs}, s{s_rs}, %[{'asl' if op == 0 else 'bsl'}]",
+                f"s_addc_u32 s{s_rs + 1}, s{s_rs + 1}, %[{'ash' if op == 0 else 'bsh'}]",
+                f"s_mov_b32 s{s_off}, 0"]
+        return ops, tail
+
+    def mfmas(self, fa, fb, rows, zero=False):
+        """zero: the accumulator's first MFMA (C = 0: no separate zeroing pass over a[0:255])."""
+        return [f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {frag(fb, j)}, {frag(fa, i)}, {0 if zero else acc(i, j)}"
+                for i in rows for j in range(8)]
+
+    # ---------------------------------------------------------------- schedule helpers
+    def interleave_reads(self, mf, reads, per):
+        """`per` reads after each MFMA from the first one on, all reads issued in the first part of the
+        quarter so their latency hides under the rest of it."""
+        k = 0
+        for m in mf:
+            self.emit(m)
+            for _ in range(per):
+                if k < len(reads):
+                    self.emit(reads[k])
+                    k += 1
+        while k < len(reads):
+            self.emit(reads[k])
+            k += 1
+
+    def interleave_dma(self, mf, pieces, tail):
+        """SALU set-up of a piece after one MFMA, its load after the next: 8 pieces over 16 MFMAs of the
+        quarter, the remaining MFMAs let the TA drain."""
+        k = 0
+        pending = None
+        for m in mf:
+            self.emit(m)
+            if pending is not None:
+                self.emit(pending)
+                pending = None
+            elif k < len(pieces):
+                setup, load = pieces[k]
+                for s in setup:
+                    self.emit(s)
+                pending = load
+                k += 1
+        if pending is not None:
+            self.emit(pending)
+        for s in tail:
+            self.emit(s)
+
+    # ---------------------------------------------------------------- one K-step
+    def step(self, stage, dma, has_next, vm, first=False):
+        nxt = stage ^ 1
+        self.emit(f"; ---- K-step: stage {stage} dma {dma} next {has_next} first {first}")
+        self.emit("s_waitcnt lgkmcnt(0)")
+        # Q1: F0.A[0..3] x F0.B, F1 reads of this tile.  Order: A blocks 0-3 (last MFMA read a quarter ago), B
+        # blocks, A blocks 4-7 -- each register is rewritten >= 8 MFMAs after the previous K-step's last MFMA
+        # that read it (Q4 reads F1.A[4..7] and every F1.B block)
+        f1 = self.read_ops(stage, 1, [(0, i, F1A) for i in range(4)] + [(1, j, F1B) for j in range(8)] +
+                           [(0, i, F1A) for i in range(4, 8)])
+        self.interleave_reads(self.mfmas(F0A, F0B, range(0, 4), first), f1, 1 if self.layout == NT else 2)
+        self.emit("s_waitcnt lgkmcnt(0)")
+        self.emit("s_barrier")
+        # Q2 / Q3: the DMA of tile t+2 into this stage (free: every wave passed the barrier above after its reads)
+        q2 = self.mfmas(F0A, F0B, range(4, 8), first)
+        q3 = self.mfmas(F1A, F1B, range(0, 4))
+        if dma:
+            pa, ta = self.dma_ops(stage, 0)
+            pb, tb = self.dma_ops(stage, 1)
+            self.interleave_dma(q2, pa, ta)
+            self.interleave_dma(q3, pb, tb)
+        else:
+            for m in q2 + q3:
+                self.emit(m)
+        if has_next:
+            self.emit(f"s_waitcnt vmcnt({vm})")      # tile t+1 (issued a K-step ago) landed in stage s^1
+            self.emit("s_barrier")
+        # Q4: F1.A[4..7] x F1.B, F0 reads of tile t+1 (A block 0 and every B block first: Q1 order)
+        q4 = self.mfmas(F1A, F1B, range(4, 8))
+        if has_next:
+            f0 = self.read_ops(nxt, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
+                               [(0, i, F0A) for i in range(1, 8)])
+            self.interleave_reads(q4, f0, 1 if self.layout == NT else 2)
+        else:
+            for m in q4:
+                self.emit(m)
+
+    def tile_dma(self, stage):
+        for op in (0, 1):
+            pieces, tail = self.dma_ops(stage, op)
+            for setup, load in pieces:
+                for s in setup:
+                    self.emit(s)
+                self.emit("s_nop 0")
+                self.emit(load)
+            for s in tail:
+                self.emit(s)
+
+    def program(self):
+        L = self.layout
+        e = self.emit
+        e("; pdt gemm main loop (generated by gen_gemm_kloop.py)")
+        for base, x in ((S_RA, "a"), (S_RB, "b")):     # {base lo, base hi | stride 0, num_records, dword3}
+            e(f"s_mov_b32 s{base}, %[{x}lo]")
+            e(f"s_mov_b32 s{base + 1}, %[{x}hi]")
+            e(f"s_mov_b32 s{base + 2}, %[{x}nr]")
+            e(f"s_mov_b32 s{base + 3}, 0x20000")
+        e(f"s_mov_b32 s{S_CNT}, %[cnt]")
+        e(f"s_mov_b32 s{S_OA}, 0")
+        e(f"s_mov_b32 s{S_OB}, 0")
+        # LDS read addresses
+        if L == NT:
+            # %[ra0] / %[ra1]: A fragment address for substep 0 / 1 (stage 0, block 0); B = A + %[db]
+            for stage in (0, 1):
+                for op in (0, 1):
+                    for sub in (0, 1):
+                        dst = self.rd_reg(stage, op, sub)
+                        src = "%[rd0]" if sub == 0 else "%[rd1]"
+                        off = stage * STB
+                        if op == 0:
+                            e(f"v_add_u32 {dst}, {off}, {src}")
+                        else:
+                            e(f"v_add_u32 {dst}, %[db], {src}")
+                            if off:
+                                e(f"v_add_u32 {dst}, {off}, {dst}")
+        else:
+            # block i address: %[rd0] + 16 * ((2 i) ^ %[rdx]);  B = A + %[db]
+            for i in range(8):
+                a0 = self.rd_reg(0, 0, i)
+                e(f"v_xor_b32 {a0}, {2 * i}, %[rdx]")
+                e(f"v_lshl_add_u32 {a0}, {a0}, 4, %[rd0]")
+                e(f"v_add_u32 {self.rd_reg(0, 1, i)}, %[db], {a0}")
+                e(f"v_add_u32 {self.rd_reg(1, 0, i)}, {STB}, {a0}")
+                e(f"v_add_u32 {self.rd_reg(1, 1, i)}, {STB}, {self.rd_reg(0, 1, i)}")
+        # prologue: tiles 0 and 1 in flight, tile 0 landed, its substep-0 fragments read
+        self.tile_dma(0)
+        self.tile_dma(1)
+        e("s_waitcnt vmcnt(16)")
+        e("s_barrier")
+        for r in self.read_ops(0, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
+                               [(0, i, F0A) for i in range(1, 8)]):
+            e(r)
+        # K-step 0 peeled (its substep-0 MFMAs start every accumulator from C = 0), then two K-steps per
+        # iteration (stage 1, stage 0); s88 = K-steps left including the current one
+        e(f"s_cmp_le_u32 s{S_CNT}, 2")
+        e("s_cbranch_scc1 pdtk%=_first_tail")
+        self.step(0, True, True, 16, first=True)
+        e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+        e(f"s_cmp_le_u32 s{S_CNT}, 2")
+        e("s_cbranch_scc1 pdtk%=_tail1")
+        e("pdtk%=_loop:")
+        self.step(1, True, True, 16)
+        e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+        e(f"s_cmp_le_u32 s{S_CNT}, 2")
+        e("s_cbranch_scc1 pdtk%=_tail0")
+        self.step(0, True, True, 16)
+        e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+        e(f"s_cmp_le_u32 s{S_CNT}, 2")
+        e("s_cbranch_scc0 pdtk%=_loop")
+        e("s_branch pdtk%=_tail1")
+        e("pdtk%=_tail0:")
+        self.step(0, False, True, 0)
+        self.step(1, False, False, 0)
+        e("s_branch pdtk%=_done")
+        e("pdtk%=_tail1:")
+        self.step(1, False, True, 0)
+        self.step(0, False, False, 0)
+        e("s_branch pdtk%=_done")
+        e("pdtk%=_first_tail:")                 # K = 128: both K-steps without DMA, the first from C = 0
+        self.step(0, False, True, 0, first=True)
+        self.step(1, False, False, 0)
+        e("pdtk%=_done:")
+        e("s_nop 15")
+        e("s_nop 15")
+        return self.lines
+
+
+def render(name, lines):
+    return f"#define {name} \\\n" + " \\\n".join(f'  "{ln}\\n"' for ln in lines) + "\n"
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = ["// GENERATED by gen_gemm_kloop.py -- do not edit.  The hand-scheduled main loops of gemm.hip.",
+           "#pragma once", ""]
+    for L, name in ((NT, "PDT_GEMM_KLOOP_NT"), (TT, "PDT_GEMM_KLOOP_TT")):
+        g = Gen(L)
+        lines = g.program()
+        n_mfma = sum(1 for ln in lines if ln.startswith("v_mfma"))
+        out.append(f"// {name}: {len(lines)} lines, {n_mfma} MFMAs")
+        out.append(render(name, lines))
+    out.append("#define PDT_AGPR_CLOBBERS " + ", ".join(f'"a{i}"' for i in range(256)))
+    out.append("")
+    with open(os.path.join(here, "gemm_kloop.inc"), "w") as f:
+        f.write("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -65,8 +65,14 @@ def _run(cmd, verbose):
 
 
 def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
+    # generated sources (hand-scheduled asm main loops): regenerate when the generator changed
+    for gen in sorted(glob.glob(os.path.join(KERNEL_DIR, "gen_*.py"))):
+        inc = os.path.join(KERNEL_DIR, os.path.basename(gen)[4:-3] + ".inc")
+        if _newer(inc, [gen]):
+            _run([sys.executable, gen], verbose)
     srcs = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.hip")))
     headers = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.h")))
+    incs = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.inc")))
     os.makedirs(BUILD_DIR, exist_ok=True)
     os.makedirs(os.path.dirname(KERNEL_LIB), exist_ok=True)
     hipcc = _hipcc()
@@ -74,7 +80,10 @@ def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
     for s in srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s)[:-4] + f".{ARCH}.o")
         objs.append(o)
-        if _newer(o, [s] + headers + [__file__]):
+        with open(s) as f:
+            text = f.read()
+        deps = [s] + headers + [i for i in incs if os.path.basename(i) in text] + [__file__]
+        if _newer(o, deps):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
     if todo:

@@ -15,6 +15,8 @@ otherwise.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -41,8 +43,14 @@ def tt_ok(a: torch.Tensor, b: torch.Tensor, splits: int = 1) -> bool:
             and gemm_ok(L_TT, a.shape[1], b.shape[1], a.shape[0], a.stride(0), b.stride(0), splits))
 
 
+# kernel generation: "asm" = the hand-scheduled main loop (gemm_asm_kernel, round 4), "hip" = the
+# compiler-scheduled one (gemm_kernel, round 3)
+KERNEL = {"name": os.environ.get("PDT_GEMM_KERNEL", "asm")}
+
+
 def _launch(layout, epi, a, b, c, m, n, k, bias=None, aux=None, aux_out=None, dbias=None, ws=None, splits=1):
-    _lib.call("pdt_gemm_bf16", layout, epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
+    fn = "pdt_gemm2_bf16" if KERNEL["name"] == "asm" else "pdt_gemm_bf16"
+    _lib.call(fn, layout, epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
               b.stride(0), c.stride(0), _lib.ptr(bias), _lib.ptr(aux), _lib.ptr(aux_out), _lib.ptr(dbias),
               _lib.ptr(ws), splits, _lib.stream_handle(a.device))
 

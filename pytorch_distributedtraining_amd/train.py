@@ -159,7 +159,7 @@ def run(cfg: RunConfig) -> dict:
         i = step - cfg.warmup
         maybe_save(step + 1)
         if (i + 1) % cfg.log_every == 0 or step + 1 == total:
-            last = tr.detach_and_sync_loss(loss)       # one host sync per log line only
+            last = float(tr.detach_and_sync_loss(loss))       # one host sync per log line only
             rate = meter.rate()
             rec = {"step": step + 1, "loss": last, "samples_per_s": rate["samples_per_s"]}
             if kind == "lm":

@@ -42,6 +42,86 @@ def _val(x):
     return x.value if hasattr(x, "value") else x
 
 
+class SyncedLoss:
+    """A rank-local device scalar whose cross-rank mean is taken lazily (``Trainer.detach_and_sync_loss``).
+
+    Linear arithmetic keeps it on the device and unsynchronised: ``+``/``-`` with another SyncedLoss or a number,
+    ``*``/``/`` by a number (the mean over ranks commutes with these).  Reading it -- ``float()``, ``item()``,
+    formatting, comparisons -- runs ONE all-reduce (AVG) and one host read, then caches the value.  A number
+    added to it is treated as already rank-uniform (e.g. the ``0.0`` a running sum starts from)."""
+
+    __slots__ = ("t", "comm", "_value")
+
+    def __init__(self, t, comm):
+        self.t, self.comm, self._value = t, comm, None
+
+    # -- lazy linear arithmetic ------------------------------------------------------------------------
+    def _other(self, o):
+        if isinstance(o, SyncedLoss):
+            return o.t
+        if isinstance(o, (int, float)):
+            return float(o)
+        return NotImplemented
+
+    def __add__(self, o):
+        v = self._other(o)
+        return NotImplemented if v is NotImplemented else SyncedLoss(self.t + v, self.comm)
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        v = self._other(o)
+        return NotImplemented if v is NotImplemented else SyncedLoss(self.t - v, self.comm)
+
+    def __rsub__(self, o):
+        v = self._other(o)
+        return NotImplemented if v is NotImplemented else SyncedLoss(v - self.t, self.comm)
+
+    def __mul__(self, o):
+        if isinstance(o, (int, float)):
+            return SyncedLoss(self.t * float(o), self.comm)
+        return NotImplemented
+
+    __rmul__ = __mul__
+
+    def __truediv__(self, o):
+        if isinstance(o, (int, float)):
+            return SyncedLoss(self.t / float(o), self.comm)
+        return NotImplemented
+
+    def __neg__(self):
+        return SyncedLoss(-self.t, self.comm)
+
+    # -- materialisation (collective) ------------------------------------------------------------------
+    def item(self) -> float:
+        if self._value is None:
+            t = self.t.clone()
+            self.comm.all_reduce(t, "avg")
+            self._value = float(t.item())
+        return self._value
+
+    def __float__(self):
+        return self.item()
+
+    def __format__(self, spec):
+        return format(self.item(), spec)
+
+    def __repr__(self):
+        return f"SyncedLoss({self.item()!r})" if self._value is not None else "SyncedLoss(<not synced>)"
+
+    def __lt__(self, o):
+        return self.item() < float(o)
+
+    def __le__(self, o):
+        return self.item() <= float(o)
+
+    def __gt__(self, o):
+        return self.item() > float(o)
+
+    def __ge__(self, o):
+        return self.item() >= float(o)
+
+
 class Trainer:
     def __init__(self, model: nn.Module, optimizer, loss, batch_size_per_device: int, grad_accum_steps: int = 1,
                  grad_clip=None, gpu: bool = False, fp16=None, distributed=None, fairscale_oss: bool = False,
@@ -359,16 +439,22 @@ class Trainer:
 
     # ------------------------------------------------------------------ loss sync / printing
     def detach_and_sync_loss(self, loss, device=None):
-        t = loss.detach().float().reshape(1).clone()
-        self.comm.all_reduce(t, "avg")
-        return float(t.item())
+        """The loss averaged over ranks, as a ``SyncedLoss``: a device scalar that is NOT synchronised yet.
+        Stoke returns a float (an all-reduce plus a host read on every micro-batch, Stoke-DDP.py:86); here
+        ``sum_loss += t.detach_and_sync_loss(loss)`` stays on the device (sums of rank-local values), and the
+        one all-reduce + host read happen when the value is read (``float()``, formatting, comparisons) --
+        on log steps only.  Every rank must read it at the same point (it is a collective)."""
+        return SyncedLoss(loss.detach().float().reshape(1).clone(), self.comm)
 
     def print_ema_loss(self, prepend_msg: str = "Current EMA Loss", postpend_msg: str = ""):
+        """Collective (every rank calls it): one device all-reduce of the EMA; only the printing rank reads the
+        value back to the host."""
         if self._ema is None:
             return
         t = self._ema.reshape(1).clone()
         self.comm.all_reduce(t, "avg")
-        self.logger.print(f"{prepend_msg}: {float(t.item()):.5f} {postpend_msg}".rstrip())
+        if self.logger.will_print():
+            self.logger.print(f"{prepend_msg}: {float(t.item()):.5f} {postpend_msg}".rstrip())
 
     def print_on_devices(self, msg, rank=None):
         self.logger.print(msg, ranks=None if rank is None else (rank if isinstance(rank, (list, tuple)) else [rank]))

@@ -34,6 +34,14 @@ class RankLogger:
         if ranks == "all" or r in ranks:
             print(f"[rank {r}] {msg}" if ranks == "all" or len(ranks) > 1 else msg, file=self.stream, flush=True)
 
+    def will_print(self, ranks=None) -> bool:
+        """Whether ``print(msg, ranks)`` on this rank would print (callers skip building the message -- and
+        any host read it needs -- otherwise)."""
+        r = _rank()
+        if ranks is None:
+            ranks = [self.info_rank] if not isinstance(self.info_rank, (list, tuple)) else self.info_rank
+        return ranks == "all" or r in ranks
+
     def info(self, msg):
         if self.verbose:
             self.print(msg)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: hand-scheduled GEMM main loop -- correctness vs the compiler-scheduled kernel / fp32, then timing.
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out/r4_gemm${TAG:-}
+mkdir -p $OUT
+echo "=== check"; date
+MODE=check timeout -k 10 300 python -u scripts/bench_gemm_asm.py > $OUT/check.jsonl 2> $OUT/check.err
+rc=$?; echo "check rc=$rc"; cat $OUT/check.jsonl; tail -5 $OUT/check.err
+[ $rc -eq 0 ] || exit $rc
+echo "=== bench"; date
+MODE=bench ROUNDS=${ROUNDS:-5} timeout -k 10 500 python -u scripts/bench_gemm_asm.py > $OUT/bench.jsonl 2> $OUT/bench.err
+rc=$?; echo "bench rc=$rc"; cat $OUT/bench.jsonl; tail -5 $OUT/bench.err
+exit $rc

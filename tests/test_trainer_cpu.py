@@ -48,7 +48,7 @@ def test_single_process_accumulation_and_checkpoint(tmp_path):
     assert t.step() is True
     assert not torch.equal(w0, t.model_access[0].weight)
     assert t.backward_steps == 2 and t.optimizer_steps == 1
-    assert isinstance(t.detach_and_sync_loss(loss), float)
+    assert isinstance(float(t.detach_and_sync_loss(loss)), float)
     t.print_ema_loss(prepend_msg="EMA")
     path, tag = t.save(str(tmp_path), name="m1", extras={"epoch": 3})
     assert tag == "stoke-m1-backward-step-2"
@@ -99,7 +99,7 @@ def _w_trainer(rank, world, tmp):
         total += t.detach_and_sync_loss(loss)
     path, tag = t.save(tmp, name="dist")
     sd = {k: v.clone() for k, v in t.model_access.state_dict().items()}
-    return sd, t.optimizer_steps, type(t.model_access[1]).__name__, tag, total
+    return sd, t.optimizer_steps, type(t.model_access[1]).__name__, tag, float(total)
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -200,3 +200,38 @@ def _w_trainer_debug(rank, world, diverge_at):
 def test_trainer_debug_mode_catches_divergent_collective():
     assert run_workers(_w_trainer_debug, 2, -1) == [("ok", None)] * 2            # consistent run: no false alarm
     assert run_workers(_w_trainer_debug, 2, 2) == [("mismatch", 2)] * 2          # caught at that very step
+
+
+def _w_lazy_loss(rank, world):
+    """the facade's loss sync is lazy -- summing SyncedLoss values issues no collective and no host
+    read; reading the sum issues ONE all-reduce, and equals the sum of the eagerly synced per-step means."""
+    from pytorch_distributedtraining_amd.trainer import SyncedLoss, Trainer
+    torch.manual_seed(0)
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, distributed="ddp", verbose=False)
+    eager, lazy = 0.0, 0.0
+    calls = []
+    for step in range(5):
+        g = torch.Generator().manual_seed(10 * step + rank)
+        x, y = torch.randn(2, 3, 8, 8, generator=g), torch.randn(2, 3, 8, 8, generator=g)
+        loss = t.loss(t.model(x), y)
+        t.backward(loss)
+        t.step()
+        c0 = t.comm.stats["calls"]
+        lazy = lazy + t.detach_and_sync_loss(loss) * 2
+        calls.append(t.comm.stats["calls"] - c0)                  # no collective while summing
+        d = loss.detach().reshape(1).clone()
+        torch.distributed.all_reduce(d)
+        eager += 2 * float(d) / world
+    assert isinstance(lazy, SyncedLoss) and sum(calls) == 0
+    c0 = t.comm.stats["calls"]
+    v = float(lazy / 5)
+    return v, eager / 5, t.comm.stats["calls"] - c0
+
+
+@pytest.mark.parametrize("world", [2])
+def test_lazy_synced_loss_matches_eager(world):
+    outs = run_workers(_w_lazy_loss, world)
+    for v, e, n in outs:
+        assert abs(v - e) < 1e-5 * max(1.0, abs(e)), (v, e)
+        assert n == 1                                               # one all-reduce for the whole sum
+    assert outs[0][0] == outs[1][0]
