@@ -42,6 +42,19 @@ class BucketReadiness : public std::enable_shared_from_this<BucketReadiness> {
     reset();
   }
 
+  // The last owner can be a hook lambda's temporary on the autograd thread (Python dropped the engine while a
+  // backward was in flight): release the Python callables under the GIL, never without it.
+  ~BucketReadiness() {
+    if (!Py_IsInitialized()) {
+      on_first_.release();   // interpreter gone: leak rather than touch its heap
+      on_ready_.release();
+      return;
+    }
+    py::gil_scoped_acquire gil;
+    on_first_ = py::object();
+    on_ready_ = py::object();
+  }
+
   // attach to parameter i's gradient accumulator (params that do not require grad get none)
   void attach(const std::vector<at::Tensor>& params) {
     if ((int)params.size() != (int)param_bucket_.size())
@@ -73,7 +86,10 @@ class BucketReadiness : public std::enable_shared_from_this<BucketReadiness> {
     std::lock_guard<std::mutex> g(mu_);
     enabled_ = on;
   }
-  bool enabled() const { return enabled_; }
+  bool enabled() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return enabled_;
+  }
 
   // buckets not yet released (parameters that got no gradient), in plan order; marks them released
   std::vector<int> flush() {
@@ -91,8 +107,14 @@ class BucketReadiness : public std::enable_shared_from_this<BucketReadiness> {
     ready_ = 0;
   }
 
-  int ready_count() const { return ready_; }
-  bool all_released() const { return next_ == (int)pending_.size(); }
+  int ready_count() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return ready_;
+  }
+  bool all_released() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return next_ == (int)pending_.size();
+  }
   int hooks() const { return (int)accumulators_.size(); }
 
  private:
@@ -117,7 +139,7 @@ class BucketReadiness : public std::enable_shared_from_this<BucketReadiness> {
     for (int b : launch) on_ready_(b);
   }
 
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::vector<int> param_bucket_, pending_init_, pending_, seen_;
   int next_ = 0, ready_ = 0;
   bool enabled_ = true;

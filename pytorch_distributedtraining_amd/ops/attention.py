@@ -113,21 +113,23 @@ _BIAS_GRADS: dict = {}
 def stash_bias_grad(grad, colsum):
     """Hand the column sums of the gradient buffer ``grad`` (computed by the kernel that wrote it) to the Linear
     whose output received that gradient: its backward takes them (``take_bias_grad``) instead of summing dY
-    again.  Keyed by the buffer's storage; the entry holds the buffer weakly and dies with it."""
-    for key in [k for k, (ref, _) in _BIAS_GRADS.items() if ref() is None]:
+    again.  Keyed by the buffer's storage; the entry holds the buffer weakly and dies with it, and records the
+    buffer's version counter (shared by its views), so an in-place write between stash and take voids it."""
+    for key in [k for k, (ref, _, _) in _BIAS_GRADS.items() if ref() is None]:
         del _BIAS_GRADS[key]
-    _BIAS_GRADS[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum)
+    _BIAS_GRADS[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum, grad._version)
 
 
 def take_bias_grad(dy):
-    """The stashed column sums for ``dy`` (a 2-D [rows, N] view of a stashed gradient buffer), once; else None."""
+    """The stashed column sums for ``dy`` (a 2-D [rows, N] view of a stashed gradient buffer, unmodified since
+    the stash), once; else None (the caller sums dY itself)."""
     ent = _BIAS_GRADS.pop(dy.untyped_storage().data_ptr(), None)
     if ent is None:
         return None
-    src, colsum = ent[0](), ent[1]
+    src, colsum, version = ent[0](), ent[1], ent[2]
     if (src is None or src.untyped_storage().data_ptr() != dy.untyped_storage().data_ptr()
             or src.numel() != dy.numel() or dy.dim() != 2 or colsum.numel() != dy.shape[1]
-            or dy.data_ptr() != src.data_ptr()):
+            or dy.data_ptr() != src.data_ptr() or src._version != version or dy._version != version):
         return None
     return colsum
 

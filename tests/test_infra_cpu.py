@@ -238,3 +238,16 @@ def test_multi_tensor_table_layout():
     assert tab.meta[:, 1].tolist() == [g.data_ptr() for g in gs]
     empty = TensorTable([[torch.zeros(0)]])
     assert empty.nblocks == 0 and empty.blk.tolist() == [[0, 0]]
+
+
+def test_stashed_bias_grad_voided_by_in_place_write():
+    """ops.attention.take_bias_grad hands back the producer's column sums only while the gradient buffer is
+    unmodified since the stash (version counter shared by its views); otherwise the Linear sums dY itself."""
+    from pytorch_distributedtraining_amd.ops.attention import stash_bias_grad, take_bias_grad
+    g = torch.randn(4, 3, 6)
+    stash_bias_grad(g, g.reshape(-1, 6).sum(0))
+    assert torch.equal(take_bias_grad(g.reshape(-1, 6)), g.reshape(-1, 6).sum(0))
+    assert take_bias_grad(g.reshape(-1, 6)) is None           # taken once
+    stash_bias_grad(g, g.reshape(-1, 6).sum(0))
+    g.reshape(-1, 6).add_(1.0)                                # e.g. a second consumer's gradient accumulated in place
+    assert take_bias_grad(g.reshape(-1, 6)) is None
