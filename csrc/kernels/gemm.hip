@@ -199,29 +199,19 @@ __device__ __forceinline__ void tile_of(const GemmArgs& p, int id, int ntiles, i
 // A tile's DMA therefore has ~1.5 K-steps of MFMAs to land, no ds_read ever waits at a step boundary, and
 // the matrix pipe of a SIMD sees 128 MFMAs per barrier (cf. the 2-wave-per-SIMD staggered variant: 56 %
 // MFMA busy against hipBLASLt's 85 % at 8192^3, profiles/r3_pmc_gemm_v2_vs_hipblaslt.txt).
-// DIAG (diagnostic builds only, pdt_gemm_diag_bf16 -- results are WRONG): 1 = no LDS-DMA in the main loop
-// (prologue tiles re-read: MFMA + ds_read ceiling), 2 = DMA issued but never waited for (issue cost without
-// the latency), 3 = no ds_reads in the main loop (MFMA + DMA only), 4 = no epilogue stores (a store only where
-// an accumulator equals a sentinel: the tile-boundary cost without the C write)
-//
-// PERSIST (plain single-split launches; gridDim.x <= tiles, a multiple of 8): the workgroup walks tiles
-// id = blockIdx.x + i * gridDim.x.  The last K-step of a tile, right after its final barrier (both ring
-// slots are free then), issues the NEXT tile's first two K-steps, so their HBM latency hides behind the
-// tile's last MFMAs and its epilogue; the next tile's first wait counts the epilogue's stores as younger
-// (vmcnt(min(63, 16 + stores)), and its step 0 waits with vmcnt(min(63, stores))), so the C-tile stores
-// drain under the next tile's first K-steps instead of holding the CU at a workgroup boundary.
-template <int LAYOUT, int EPI, int DIAG = 0, bool PERSIST = false>
+// (This compiler-scheduled kernel is the alternative path -- PDT_GEMM_KERNEL=hip -- and the bitwise reference
+// of the hand-scheduled gemm_asm_kernel below: the same MFMA order per accumulator.)
+template <int LAYOUT, int EPI>
 __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STB];
   lds_cchar* const lds = (lds_cchar*)(lds_void*)smem;                 // the ring, LDS address space
   const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;     // its LDS byte address (LDS-DMA m0)
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 1, wc = w & 1;
-  const int ntiles = PERSIST ? (p.M / TM) * (p.N / TN) : (int)gridDim.x;
-  int tile = blockIdx.x;
+  const int ntiles = (int)gridDim.x;
   int tm, tn;
-  tile_of(p, tile, ntiles, tm, tn);
-  int m0 = tm * TM, n0 = tn * TN;
+  tile_of(p, blockIdx.x, ntiles, tm, tn);
+  const int m0 = tm * TM, n0 = tn * TN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int T = min(p.K - kbeg, p.k_per_split) / KB;
 
@@ -253,20 +243,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   // pieces [I0, I1) of BOTH operands of K-step t into slot t & 1
   auto issue = [&](auto i0, auto i1, int t) {
     constexpr int J0 = decltype(i0)::value, J1 = decltype(i1)::value;
-    if (DIAG == 1 && t >= 2) return;
     da.template issue<J0, J1>(Ab + a0 + t * astep, abytes, lds_addr + (t & 1) * STB, w);
     db.template issue<J0, J1>(Bb + b0 + t * bstep, bbytes, lds_addr + (t & 1) * STB + OPB, w);
   };
-  // PERSIST: the next tile (id, base offsets) and whether it exists
-  int ntile = tile + (int)gridDim.x;
-  int64_t na0 = 0, nb0 = 0;
-  int nm0 = 0, nn0 = 0;
-  if (PERSIST && ntile < ntiles) {
-    int a, b;
-    tile_of(p, ntile, ntiles, a, b);
-    nm0 = a * TM; nn0 = b * TN;
-    tile_base(nm0, nn0, na0, nb0);
-  }
   using P0 = std::integral_constant<int, 0>;
   using PH = std::integral_constant<int, PIECES / 2>;
   using PE = std::integral_constant<int, PIECES>;
@@ -285,12 +264,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  // VMEM ops the epilogue issues per wave (PERSIST's counted waits): stores, + the aux loads for DGELU
-  constexpr int EPI_VM = EPI == E_GELU ? 128 : EPI == E_DGELU ? 129 : EPI == E_F32 ? 64 : 64;
-  constexpr int W_FIRST = (2 * PIECES + EPI_VM) < 63 ? (2 * PIECES + EPI_VM) : 63;
-  constexpr int W_STEP0 = EPI_VM < 63 ? EPI_VM : 63;
-  bool later = false;   // PERSIST: this is not the workgroup's first tile
-  for (;;) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa0[i] = fr.template read<0>(lds, 8 * wr + i);
 #pragma unroll
@@ -308,15 +281,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     // ---- A: substep 0 MFMAs || substep 1 reads (tile t) || second half of tile t+1's DMA
     if (t >= 1 && (!G || t + 1 < T)) issue(PH{}, PE{}, t + 1);
     // read order = order of first use: every B block (all of B1's MFMAs need them), then A blocks 0..7
-    if (DIAG != 3) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) fb1[j] = fr.template read<1>(sa + OPB, 8 * wc + j);
+    for (int j = 0; j < 8; ++j) fb1[j] = fr.template read<1>(sa + OPB, 8 * wc + j);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) fa1[i] = fr.template read<1>(sa, 8 * wr + i);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { fb1[j] = fb0[j]; fa1[j] = fa0[j]; }
-    }
+    for (int i = 0; i < 8; ++i) fa1[i] = fr.template read<1>(sa, 8 * wr + i);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -333,9 +301,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
-    if (DIAG == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else if (PERSIST && t == 0 && later) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(W_STEP0) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -344,16 +310,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     //      (issuing all of t+2 here -- a full K-step to land, as hipBLASLt's loop does -- made hipcc shuffle the
     //      256 accumulators between AGPRs and VGPRs every step, with or without unrolling: kept split)
     if (!G || t + 2 < T) issue(P0{}, PH{}, t + 2);
-    if (PERSIST && G && t + 1 == T && ntile < ntiles) {
-      // both ring slots are free after this step's barrier: the next tile's K-steps 0 and 1 go out now
-      da.template issue<0, PIECES>(Ab + na0, abytes, lds_addr, w);
-      db.template issue<0, PIECES>(Bb + nb0, bbytes, lds_addr + OPB, w);
-      if (T > 1) {
-        da.template issue<0, PIECES>(Ab + na0 + astep, abytes, lds_addr + STB, w);
-        db.template issue<0, PIECES>(Bb + nb0 + bstep, bbytes, lds_addr + STB + OPB, w);
-      }
-    }
-    const bool more = (!G || t + 1 < T) && DIAG != 3;
+    const bool more = !G || t + 1 < T;
     if (more) {   // the next step's A needs every B block first, then A blocks in order
 #pragma unroll
       for (int j = 0; j < 8; ++j) fb0[j] = fr.template read<0>(na + OPB, 8 * wc + j);
@@ -438,7 +395,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
             cs[j][r] += bf2f(gb);   // the bias gradient sums the gradient as stored
           }
         }
-        if (DIAG != 4 || acc[i][j][0] == 1234.5f) *reinterpret_cast<u16x4*>(C + e) = o;
+        *reinterpret_cast<u16x4*>(C + e) = o;
       }
     }
     if constexpr (EPI == E_DGELU) {
@@ -468,33 +425,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
     }
   }
   }
-  if constexpr (PERSIST && EPI != E_DGELU) {   // (DGELU reuses the ring's LDS in its epilogue: not persistent)
-    if (ntile < ntiles) {
-      // next tile: its K-steps 0 / 1 were issued in the last K-step; wait for step 0 (the stores above are
-      // younger and may still drain), publish it, and run the main loop again
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W_FIRST) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      tile = ntile;
-      m0 = nm0; n0 = nn0; a0 = na0; b0 = nb0;
-      tm = m0 / TM; tn = n0 / TN;
-      ntile = tile + (int)gridDim.x;
-      if (ntile < ntiles) {
-        int a, b;
-        tile_of(p, ntile, ntiles, a, b);
-        nm0 = a * TM; nn0 = b * TN;
-        tile_base(nm0, nn0, na0, nb0);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      later = true;
-      continue;
-    }
-  }
-  break;
-  }
 }
 
 // ============================================================================================================
@@ -509,8 +439,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #include "gemm_kloop.inc"
 namespace {
 
-constexpr int EROW = 528;                   // staging image row stride (bytes): 512 + 16 (2-way ds_write_b64)
-constexpr int SMEM2 = TM * EROW;            // 135,168 B >= the 128 KiB ring
+constexpr int RING = 2 * STB;                // the two ring stages (128 KiB)
+constexpr int STAGE_BYTES = 32768;          // epilogue staging: LDS past the ring, 64 rows x 512 B per round
+constexpr int SMEM3 = RING + STAGE_BYTES;   // 160 KiB: all of the CU's LDS
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -531,52 +462,110 @@ __device__ __forceinline__ f32x4 acc_tile() {
   return f32x4{x, y, z, w};
 }
 
-// store phase of the staging image: wave w writes rows 64 w .. 64 w + 63, two rows (2 x 512 B) per instruction
-__device__ __forceinline__ void stage_store(const char* smem, bf16_t* dst, int64_t ldc, int m0, int n0, int w,
-                                            int lane) {
-  const int half = lane >> 5, c16 = lane & 31;
-#pragma unroll 4
-  for (int it = 0; it < 32; ++it) {
-    const int row = 64 * w + 2 * it + half;
-    const u16x8 v = *reinterpret_cast<const u16x8*>(smem + row * EROW + c16 * 16);
-    *reinterpret_cast<u16x8*>(dst + (int64_t)(m0 + row) * ldc + n0 + 8 * c16) = v;
+// Epilogue staging (round r = 0..3): every wave's accumulator tiles i = 2r, 2r + 1 (32 rows x 128 columns), i.e.
+// rows {32 r .. 32 r + 31} and {128 + 32 r ..} of the 256 x 256 tile: 64 rows x 512 B at LDS offset RING.  Image row
+// q = 32 wr + (row & 31); its 16-byte chunks are XOR-swizzled with (q & 15) (the 16 lanes of an accumulator
+// column write 16 consecutive rows: without the swizzle one bank).  Each wave then reads 16 whole rows back (two
+// rows = 1 KiB per instruction) and stores them as full 512-byte row segments.
+__device__ __forceinline__ uint32_t stg_off(int q, int col) {   // byte offset of (image row q, column col)
+  return (uint32_t)(q * 512 + ((((col >> 3) ^ q) & 15) | ((col >> 3) & 16)) * 16 + (col & 7) * 2);
+}
+// global row of image row q in round r
+__device__ __forceinline__ int stg_row(int r, int q) { return 128 * (q >> 5) + 32 * r + (q & 31); }
+__device__ __forceinline__ void stg_read(const char* img, u16x8 (&buf)[8], int w, int lane) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int q = 16 * w + 2 * it + (lane >> 5), c16 = lane & 31;
+    buf[it] = *reinterpret_cast<const u16x8*>(img + q * 512 + ((c16 ^ (q & 15)) & 15 | (c16 & 16)) * 16);
+  }
+}
+__device__ __forceinline__ void stg_write_out(const u16x8 (&buf)[8], bf16_t* dst, int64_t ldc, int m0, int n0, int r,
+                                              int w, int lane) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int q = 16 * w + 2 * it + (lane >> 5);
+    *reinterpret_cast<u16x8*>(dst + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31)) = buf[it];
+  }
+}
+// DGELU: the aux rows of round r into the image (the same mapping as the write-out, reversed)
+__device__ __forceinline__ void stg_load(char* img, const bf16_t* src, int64_t ldc, int m0, int n0, int r, int w,
+                                         int lane) {
+  u16x8 t[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int q = 16 * w + 2 * it + (lane >> 5);
+    t[it] = *reinterpret_cast<const u16x8*>(src + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31));
+  }
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int q = 16 * w + 2 * it + (lane >> 5), c16 = lane & 31;
+    *reinterpret_cast<u16x8*>(img + q * 512 + ((c16 ^ (q & 15)) & 15 | (c16 & 16)) * 16) = t[it];
   }
 }
 
-// load phase (DGELU's aux tile): the same mapping, global -> staging image
-__device__ __forceinline__ void stage_load(char* smem, const bf16_t* src, int64_t ldc, int m0, int n0, int w,
-                                           int lane) {
-  const int half = lane >> 5, c16 = lane & 31;
-#pragma unroll 4
-  for (int it = 0; it < 32; ++it) {
-    const int row = 64 * w + 2 * it + half;
-    *reinterpret_cast<u16x8*>(smem + row * EROW + c16 * 16) =
-        *reinterpret_cast<const u16x8*>(src + (int64_t)(m0 + row) * ldc + n0 + 8 * c16);
+// Per-item operands of the main-loop / next-item statements (gen_gemm_kloop.py): buffer resources of the item's
+// A and B K-tile 0 (every value wave-uniform: kernel arguments, blockIdx, the item index, the wave index).
+template <int LAYOUT>
+struct ItemOps {
+  int tm, tn, m0, n0, split, T;
+  uint32_t alo, ahi, blo, bhi;
+  __device__ __forceinline__ void init(const GemmArgs& p, int item, int ntiles) {
+    split = item / ntiles;
+    tile_of(p, item - split * ntiles, ntiles, tm, tn);
+    m0 = tm * TM; n0 = tn * TN;
+    const int kbeg = split * p.k_per_split;
+    T = min(p.K - kbeg, p.k_per_split) / KB;
+    uint64_t a0, b0;
+    if (LAYOUT == L_NT) {
+      a0 = (uint64_t)(uintptr_t)p.A + ((uint64_t)m0 * p.lda + kbeg) * 2;
+      b0 = (uint64_t)(uintptr_t)p.B + ((uint64_t)n0 * p.ldb + kbeg) * 2;
+    } else {
+      a0 = (uint64_t)(uintptr_t)p.A + ((uint64_t)kbeg * p.lda + m0) * 2;
+      b0 = (uint64_t)(uintptr_t)p.B + ((uint64_t)kbeg * p.ldb + n0) * 2;
+    }
+    alo = (uint32_t)a0; ahi = (uint32_t)(a0 >> 32) & 0xffffu;
+    blo = (uint32_t)b0; bhi = (uint32_t)(b0 >> 32) & 0xffffu;
   }
+  // the same item's K-tile n (skip2: its tiles 0 and 1 were issued by the previous item's epilogue)
+  __device__ __forceinline__ void skip2(uint64_t astep, uint64_t bstep) { skipn(2 * astep, 2 * bstep); }
+  __device__ __forceinline__ void skip1(uint64_t astep, uint64_t bstep) { skipn(astep, bstep); }
+  __device__ __forceinline__ void skipn(uint64_t da, uint64_t dbb) {
+    const uint64_t a = (((uint64_t)ahi << 32) | alo) + da, b = (((uint64_t)bhi << 32) | blo) + dbb;
+    alo = (uint32_t)a; ahi = (uint32_t)(a >> 32) & 0xffffu;
+    blo = (uint32_t)b; bhi = (uint32_t)(b >> 32) & 0xffffu;
+  }
+};
+
+// Persistent: a workgroup walks items (tile, K split) id = blockIdx.x + i * gridDim.x.  When the K-step count is
+// even, an item's last two K-steps DMA the NEXT item's K-tiles 0 and 1 into the ring (gen_gemm_kloop.py
+// next_tail), so those loads fly under this item's last MFMAs and its epilogue; the epilogue stages its bf16
+// results through the 32 KiB of LDS past the ring (4 rounds of 64 rows, full-row 16-byte stores) and the stores
+// drain under the next item's first K-steps (its first wait counts them: vmcnt(16 + stores)).
+// DIAG = 1 (diagnostic builds only, pdt_gemm_stamps_bf16): wave 0 stamps s_memtime at each item's start, after
+// its main loop and after its epilogue into p.aux_out (uint64 [item][4], the 4th = s_memrealtime at item start)
+// -- for the phase shares of an item, never for timing the production kernel.
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
 }
 
-template <int LAYOUT, int EPI>
+template <int LAYOUT, int EPI, int DIAG = 0>
 __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM3];
   const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 1, wc = w & 1;
-  int tm, tn;
-  tile_of(p, blockIdx.x, (int)gridDim.x, tm, tn);
-  const int m0 = tm * TM, n0 = tn * TN;
-  const int kbeg = blockIdx.y * p.k_per_split;
-  const int T = min(p.K - kbeg, p.k_per_split) / KB;
+  const int ntiles = (p.M / TM) * (p.N / TN);
+  const int splits = (p.K + p.k_per_split - 1) / p.k_per_split;
+  const int nall = ntiles * splits;
 
-  // ---- main-loop operands (see gen_gemm_kloop.py for the register map and schedule)
-  const char* Ab = reinterpret_cast<const char*>(p.A);
-  const char* Bb = reinterpret_cast<const char*>(p.B);
-  uint64_t a0, b0, astep, bstep;
+  // ---- item-independent operands
+  uint64_t astep, bstep;
   uint32_t abytes, bbytes, rsa, rsb;
   uint32_t voa0, voa1, vob0, vob1, rd0, rd1;
   int32_t db;
   if (LAYOUT == L_NT) {
-    a0 = (uint64_t)(uintptr_t)Ab + ((uint64_t)m0 * p.lda + kbeg) * 2;
-    b0 = (uint64_t)(uintptr_t)Bb + ((uint64_t)n0 * p.ldb + kbeg) * 2;
     astep = bstep = KB * 2;
     abytes = (uint32_t)((TM - 1) * p.lda * 2 + KB * 2);
     bbytes = (uint32_t)((TN - 1) * p.ldb * 2 + KB * 2);
@@ -591,8 +580,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     rd1 = lds_addr + 16384 * wr + (uint32_t)(x * 128 + 16 * ((4 + g) ^ h));
     db = OPB + 16384 * (wc - wr);
   } else {
-    a0 = (uint64_t)(uintptr_t)Ab + ((uint64_t)kbeg * p.lda + m0) * 2;
-    b0 = (uint64_t)(uintptr_t)Bb + ((uint64_t)kbeg * p.ldb + n0) * 2;
     astep = (uint64_t)KB * p.lda * 2;
     bstep = (uint64_t)KB * p.ldb * 2;
     abytes = (uint32_t)((KB - 1) * p.lda * 2 + TM * 2);
@@ -609,18 +596,19 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     rd1 = (uint32_t)tt_f(8 * g + q);     // the block XOR term
     db = OPB + 256 * (wc - wr);
   }
-  // buffer resources: {base lo, base hi (stride 0), num_records, dword3} assembled in the statement from 32-bit
-  // scalar operands (every value here is wave-uniform: kernel arguments, blockIdx and the wave index)
-  const uint32_t alo = (uint32_t)a0, ahi = (uint32_t)(a0 >> 32) & 0xffffu;
-  const uint32_t blo = (uint32_t)b0, bhi = (uint32_t)(b0 >> 32) & 0xffffu;
   const uint32_t m0b = __builtin_amdgcn_readfirstlane(lds_addr + w * 1024);
   const int dbs = __builtin_amdgcn_readfirstlane(db);
   const uint32_t asl = (uint32_t)astep, ash = (uint32_t)(astep >> 32);
   const uint32_t bsl = (uint32_t)bstep, bsh = (uint32_t)(bstep >> 32);
-  const int cnt = __builtin_amdgcn_readfirstlane(T);
+  // global stores an epilogue issues after the next item's first DMA (the next main loop's first wait skips them)
+  constexpr int NST = EPI == E_F32 ? 64 : EPI == E_GELU ? 64 : 32;
+  constexpr int WNX = 16 + NST < 63 ? 16 + NST : 63;
+  const int lrow = 128 * wr + (lane & 15);
+  const int lcol = 128 * wc + 4 * (lane >> 4);
+  char* const img = smem + RING;
 
 #define PDT_KLOOP_CLOBBERS                                                                                      \
-  "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",   \
+  "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",         \
   "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78",     \
   "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93",     \
   "v94", "v95", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", \
@@ -634,127 +622,178 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
   "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243",      \
   "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255",              \
   PDT_AGPR_CLOBBERS
-  if constexpr (LAYOUT == L_NT) {
-    asm volatile(PDT_GEMM_KLOOP_NT
-                 :
-                 : [alo] "s"(alo), [ahi] "s"(ahi), [anr] "s"(abytes), [blo] "s"(blo), [bhi] "s"(bhi), [bnr] "s"(bbytes),
-                   [cnt] "s"(cnt),
-                   [m0b] "s"(m0b), [rsa] "s"(rsa), [rsb] "s"(rsb), [asl] "s"(asl), [ash] "s"(ash), [bsl] "s"(bsl),
-                   [bsh] "s"(bsh), [voa] "v"(voa0), [vob] "v"(vob0), [rd0] "v"(rd0), [rd1] "v"(rd1), [db] "s"(dbs)
-                 : PDT_KLOOP_CLOBBERS);
-  } else {
-    asm volatile(PDT_GEMM_KLOOP_TT
-                 :
-                 : [alo] "s"(alo), [ahi] "s"(ahi), [anr] "s"(abytes), [blo] "s"(blo), [bhi] "s"(bhi), [bnr] "s"(bbytes),
-                   [cnt] "s"(cnt),
-                   [m0b] "s"(m0b), [rsa] "s"(rsa), [rsb] "s"(rsb), [asl] "s"(asl), [ash] "s"(ash), [bsl] "s"(bsl),
-                   [bsh] "s"(bsh), [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),
-                   [rd0] "v"(rd0), [rdx] "v"(rd1), [db] "s"(dbs)
-                 : PDT_KLOOP_CLOBBERS);
-  }
-#undef PDT_KLOOP_CLOBBERS
-  (void)voa1; (void)vob1;
+#define PDT_ITEM_OPS                                                                                            \
+  [alo] "s"(lo.alo), [ahi] "s"(lo.ahi), [anr] "s"(abytes), [blo] "s"(lo.blo), [bhi] "s"(lo.bhi),               \
+      [bnr] "s"(bbytes), [m0b] "s"(m0b), [rsa] "s"(rsa), [rsb] "s"(rsb), [asl] "s"(asl), [ash] "s"(ash),         \
+      [bsl] "s"(bsl), [bsh] "s"(bsh), [cnt] "s"(cnt), [first] "s"(first), [wnx] "i"(WNX), [hnx] "s"(hnx),        \
+      [nalo] "s"(nxt.alo), [nahi] "s"(nxt.ahi), [nblo] "s"(nxt.blo), [nbhi] "s"(nxt.bhi), [db] "s"(dbs)
+#define PDT_KLOOP_NT_ASM(MAC)                                                                                     \
+  asm volatile(MAC : : PDT_ITEM_OPS, [voa] "v"(voa0), [vob] "v"(vob0), [rd0] "v"(rd0), [rd1] "v"(rd1)           \
+               : PDT_KLOOP_CLOBBERS)
+#define PDT_KLOOP_TT_ASM(MAC)                                                                                     \
+  asm volatile(MAC : : PDT_ITEM_OPS, [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),    \
+               [rd0] "v"(rd0), [rdx] "v"(rd1) : PDT_KLOOP_CLOBBERS)
 
-  // ---------------------------------------------------------------- epilogue
-  // acc tile (i, j): C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
-  const int lrow = 128 * wr + (lane & 15);
-  const int lcol = 128 * wc + 4 * (lane >> 4);
-  if constexpr (EPI == E_F32) {
-    float* C = p.ws + (int64_t)blockIdx.y * p.M * p.N;
-    sfor<0, 64>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      const f32x4 v = acc_tile<k>();
-      *reinterpret_cast<f32x4*>(C + (int64_t)(m0 + lrow + 16 * (k >> 3)) * p.N + n0 + lcol + 16 * (k & 7)) = v;
-    });
-    return;
-  } else {
-    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-    char* img = smem;
-    __syncthreads();                         // every wave done with the ring: reuse its LDS as the staging image
-    if constexpr (EPI == E_DGELU) {
-      stage_load(img, p.aux, p.ldc, m0, n0, w, lane);
-      __syncthreads();
-    }
-    float bj[8][4];
-    if constexpr (EPI == E_BIAS || EPI == E_GELU) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const u16x4 b = *reinterpret_cast<const u16x4*>(p.bias + n0 + lcol + 16 * j);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(b[r]);
-      }
-    }
-    float cs[8][4];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
-    // pass 0: the result (PLAIN / BIAS / DGELU) or the pre-activation (GELU) into the image
-    sfor<0, 64>([&](auto kc) {
-      constexpr int k = decltype(kc)::value, i = k >> 3, j = k & 7;
-      const f32x4 v = acc_tile<k>();
-      char* at = img + (lrow + 16 * i) * EROW + (lcol + 16 * j) * 2;
-      u16x4 o;
-      if constexpr (EPI == E_DGELU) {
-        const u16x4 hh = *reinterpret_cast<const u16x4*>(at);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16_t gb = f2bf(v[r] * gelu_grad<true>(bf2f(hh[r])));
-          o[r] = gb;
-          cs[j][r] += bf2f(gb);            // the bias gradient sums the gradient as stored
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf((EPI == E_BIAS || EPI == E_GELU) ? v[r] + bj[j][r] : v[r]);
-      }
-      *reinterpret_cast<u16x4*>(at) = o;
-    });
-    __syncthreads();
-    stage_store(img, EPI == E_GELU ? p.aux_out : C, p.ldc, m0, n0, w, lane);
-    if constexpr (EPI == E_GELU) {
-      // pass 1: GELU of the stored (rounded) pre-activation
-      __syncthreads();
+  ItemOps<LAYOUT> cur;
+  int item = blockIdx.x;
+  cur.init(p, item, ntiles);
+  int first = 1;
+  while (true) {
+    const int next_item = item + (int)gridDim.x;
+    const bool has_next = next_item < nall;
+    ItemOps<LAYOUT> nxt = cur;
+    if (has_next) nxt.init(p, next_item, ntiles);
+    // the last two K-steps load the next item's first two K-tiles (even K-step counts only: stage parity)
+    // integer arithmetic, not a select: a bool-derived operand can be rematerialised as a VGPR v_cndmask
+    const int hnx = __builtin_amdgcn_readfirstlane((((nall - 1 - next_item) >> 31) + 1) & ~cur.T & 1);
+    const int cnt = __builtin_amdgcn_readfirstlane(cur.T);
+    first = __builtin_amdgcn_readfirstlane(first);
+    // the main loop's own DMA starts at K-tile 2 when the previous item's last K-steps issued tiles 0 and 1
+    ItemOps<LAYOUT> lo = cur;
+    if (!first) lo.skip2(astep, bstep);
+    lo.alo = __builtin_amdgcn_readfirstlane(lo.alo); lo.ahi = __builtin_amdgcn_readfirstlane(lo.ahi);
+    lo.blo = __builtin_amdgcn_readfirstlane(lo.blo); lo.bhi = __builtin_amdgcn_readfirstlane(lo.bhi);
+    uint64_t st0 = 0, st1 = 0, rt0 = 0;
+    if (DIAG) { st0 = stamp(); rt0 = __builtin_amdgcn_s_memrealtime(); }
+    // ---------------------------------------------------------------- main loop
+    if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM(PDT_GEMM_KLOOP_NT);
+    else PDT_KLOOP_TT_ASM(PDT_GEMM_KLOOP_TT);
+    if (DIAG) st1 = stamp();
+    const int m0 = cur.m0, n0 = cur.n0, tm = cur.tm;
+
+    // ---------------------------------------------------------------- epilogue
+    // acc tile (i, j): C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
+    if constexpr (EPI == E_F32) {
+      float* C = p.ws + (int64_t)cur.split * p.M * p.N;
       sfor<0, 64>([&](auto kc) {
-        constexpr int k = decltype(kc)::value, i = k >> 3, j = k & 7;
+        constexpr int k = decltype(kc)::value;
         const f32x4 v = acc_tile<k>();
-        char* at = img + (lrow + 16 * i) * EROW + (lcol + 16 * j) * 2;
-        u16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(gelu_f<true>(bf2f(f2bf(v[r] + bj[j][r]))));
-        *reinterpret_cast<u16x4*>(at) = o;
+        *reinterpret_cast<f32x4*>(C + (int64_t)(m0 + lrow + 16 * (k >> 3)) * p.N + n0 + lcol + 16 * (k & 7)) = v;
       });
-      __syncthreads();
-      stage_store(img, C, p.ldc, m0, n0, w, lane);
-    }
-    if constexpr (EPI == E_DGELU) {
+    } else {
+      bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+      u16x8 buf[8];
+      float bj[8][4];
+      if constexpr (EPI == E_BIAS || EPI == E_GELU) {
+        // (the wait for these loads also drains the next item's first DMA that the main loop left in flight:
+        // a bias epilogue gives up that overlap)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const u16x4 b = *reinterpret_cast<const u16x4*>(p.bias + n0 + lcol + 16 * j);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(b[r]);
+        }
+      }
+      float cs[8][4];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = cs[j][r];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          cs[j][r] = v;
+        for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+      // round r: this wave's accumulator tiles i = 2 r, 2 r + 1 -> image rows q = 32 wr + 16 (i & 1) + (lane & 15)
+      sfor<0, 4>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if constexpr (EPI == E_DGELU) {
+          __syncthreads();                   // the previous round's image is read
+          stg_load(img, p.aux, p.ldc, m0, n0, r, w, lane);
         }
-      __syncthreads();                                   // the image is stored: reuse its LDS
-      float* red = reinterpret_cast<float*>(smem);       // [2 wave rows][256 columns]
-      if ((lane & 15) == 0) {
+        __syncthreads();
+        sfor<0, 16>([&](auto kc) {
+          constexpr int k = 16 * r + decltype(kc)::value, i = k >> 3, j = k & 7;
+          const f32x4 v = acc_tile<k>();
+          const uint32_t at = stg_off(32 * wr + 16 * (i & 1) + (lane & 15), lcol + 16 * j);
+          u16x4 o;
+          if constexpr (EPI == E_DGELU) {
+            const u16x4 hh = *reinterpret_cast<const u16x4*>(img + at);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bf16_t gb = f2bf(v[e] * gelu_grad<true>(bf2f(hh[e])));
+              o[e] = gb;
+              cs[j][e] += bf2f(gb);          // the bias gradient sums the gradient as stored
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = f2bf((EPI == E_BIAS || EPI == E_GELU) ? v[e] + bj[j][e] : v[e]);
+          }
+          *reinterpret_cast<u16x4*>(img + at) = o;
+        });
+        __syncthreads();
+        stg_read(img, buf, w, lane);
+        stg_write_out(buf, EPI == E_GELU ? p.aux_out : C, p.ldc, m0, n0, r, w, lane);
+        if constexpr (EPI == E_GELU) {       // then GELU of the stored (rounded) pre-activation, same rows
+          __syncthreads();
+          sfor<0, 16>([&](auto kc) {
+            constexpr int k = 16 * r + decltype(kc)::value, i = k >> 3, j = k & 7;
+            const f32x4 v = acc_tile<k>();
+            const uint32_t at = stg_off(32 * wr + 16 * (i & 1) + (lane & 15), lcol + 16 * j);
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = f2bf(gelu_f<true>(bf2f(f2bf(v[e] + bj[j][e]))));
+            *reinterpret_cast<u16x4*>(img + at) = o;
+          });
+          __syncthreads();
+          stg_read(img, buf, w, lane);
+          stg_write_out(buf, C, p.ldc, m0, n0, r, w, lane);
+        }
+      });
+      if constexpr (EPI == E_DGELU) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[wr * 256 + lcol + 16 * j + r] = cs[j][r];
+          for (int e = 0; e < 4; ++e) {
+            float v = cs[j][e];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            cs[j][e] = v;
+          }
+        __syncthreads();                                   // the last round's image is read
+        float* red = reinterpret_cast<float*>(img);        // [2 wave rows][256 columns]
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[wr * 256 + lcol + 16 * j + e] = cs[j][e];
+        }
+        __syncthreads();
+        p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
       }
-      __syncthreads();
-      p.ws[(int64_t)tm * p.N + n0 + tid] = red[tid] + red[256 + tid];
+      __syncthreads();                       // the staging image is free for the next item's epilogue
     }
+    if (DIAG) {
+      const uint64_t st2 = stamp();
+      if (tid == 0) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(p.aux_out) + 4 * (int64_t)item;
+        d[0] = st0; d[1] = st1; d[2] = st2; d[3] = rt0;
+      }
+    }
+    if (!has_next) break;
+    item = next_item;
+    first = 1 - hnx;
+    cur = nxt;
   }
+#undef PDT_KLOOP_CLOBBERS
+#undef PDT_ITEM_OPS
+#undef PDT_KLOOP_NT_ASM
+#undef PDT_KLOOP_TT_ASM
+}
+
+// one workgroup per CU (all 160 KiB of LDS each) walking its items; a multiple of 8 (tile ids b, b + 8 share an XCD)
+static int persist_grid(int nitems) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      n = 256;
+    return n;
+  }();
+  int g = cus < nitems ? cus : nitems;
+  return g >= 8 ? g & ~7 : g;
 }
 
 template <int LAYOUT>
 int launch_asm_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
-  const dim3 grid((a.M / TM) * (a.N / TN), splits);
+  const dim3 grid(persist_grid((a.M / TM) * (a.N / TN) * splits), 1);
   switch (epi) {
     case E_PLAIN: gemm_asm_kernel<LAYOUT, E_PLAIN><<<grid, NTH, 0, s>>>(a); break;
     case E_BIAS: gemm_asm_kernel<LAYOUT, E_BIAS><<<grid, NTH, 0, s>>>(a); break;
@@ -819,83 +858,6 @@ int launch_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
 
 // Shapes the kernel takes (checked by the host before any launch): M, N multiples of 256, K a multiple of
 // 32 * splits, 16-B aligned rows, every byte offset of a stage tile below 2^32 (buffer resources).
-// Diagnostic launches of the TT / plain kernel: diag 0 is the production kernel, 1-3 remove a part of the
-// main loop (see DIAG above; output garbage by construction).  For scripts/bench_gemm_diag.py.
-PDT_API int pdt_gemm_diag_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
-                               hipStream_t s) {
-  if (M % TM || N % TN || K % KB || diag < 0 || diag > 4) return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
-  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = M; a.ldb = N; a.ldc = N; a.k_per_split = (int)K;
-  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
-  dim3 grid((unsigned)((M / TM) * (N / TN)), 1);
-  switch (diag) {
-    case 0: gemm_kernel<L_TT, E_PLAIN, 0><<<grid, NTH, 0, s>>>(a); break;
-    case 1: gemm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a); break;
-    case 2: gemm_kernel<L_TT, E_PLAIN, 2><<<grid, NTH, 0, s>>>(a); break;
-    case 3: gemm_kernel<L_TT, E_PLAIN, 3><<<grid, NTH, 0, s>>>(a); break;
-    default: gemm_kernel<L_TT, E_PLAIN, 4><<<grid, NTH, 0, s>>>(a); break;
-  }
-  return (int)hipGetLastError();
-}
-
-PDT_API int pdt_gemm_ok(int layout, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int splits);
-
-// persistent grid: one workgroup per CU (128 KiB of LDS each), a multiple of 8 (XCD affinity of tile ids)
-static int persist_grid(int ntiles) {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess)
-      n = 256;
-    return n;
-  }();
-  int g = cus < ntiles ? cus : ntiles;
-  return g >= 8 ? g & ~7 : g;
-}
-
-// NT diagnostics (A [M, K], B [N, K] row-major): diag 0 = production plain kernel, 4 = no epilogue stores,
-// 5 = persistent plain kernel
-PDT_API int pdt_gemm_diag_nt_bf16(int diag, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
-                                  hipStream_t s) {
-  if (M % TM || N % TN || K % KB || K < 2 * KB || (diag != 0 && diag != 4 && diag != 5))
-    return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
-  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = K; a.ldb = K; a.ldc = N; a.k_per_split = (int)K;
-  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
-  const int ntiles = (int)((M / TM) * (N / TN));
-  dim3 grid((unsigned)ntiles, 1);
-  if (diag == 0) gemm_kernel<L_NT, E_PLAIN, 0><<<grid, NTH, 0, s>>>(a);
-  else if (diag == 4) gemm_kernel<L_NT, E_PLAIN, 4><<<grid, NTH, 0, s>>>(a);
-  else gemm_kernel<L_NT, E_PLAIN, 0, true><<<dim3(persist_grid(ntiles), 1), NTH, 0, s>>>(a);
-  return (int)hipGetLastError();
-}
-
-// Persistent NT GEMM (plain / bias / bias+GELU epilogues): C[M, N] = A[M, K] B[N, K]^T, one workgroup per CU
-// walking its tiles with the next tile's first K-steps in flight under the current epilogue.  Shapes as
-// pdt_gemm_ok(NT) and K >= 128.
-PDT_API int pdt_gemm_nt_persist_bf16(int epi, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
-                                     int64_t lda, int64_t ldb, int64_t ldc, const void* bias, void* aux_out,
-                                     hipStream_t s) {
-  if (!pdt_gemm_ok(L_NT, M, N, K, lda, ldb, 1) || K < 2 * KB || ldc < N || ldc % 4) return (int)hipErrorInvalidValue;
-  if (epi != E_PLAIN && epi != E_BIAS && epi != E_GELU) return (int)hipErrorInvalidValue;
-  if ((epi == E_BIAS || epi == E_GELU) && !bias) return (int)hipErrorInvalidValue;
-  if (epi == E_GELU && !aux_out) return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
-  a.bias = (const bf16_t*)bias; a.aux_out = (bf16_t*)aux_out;
-  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.k_per_split = (int)K;
-  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
-  const dim3 grid(persist_grid((int)((M / TM) * (N / TN))), 1);
-  switch (epi) {
-    case E_PLAIN: gemm_kernel<L_NT, E_PLAIN, 0, true><<<grid, NTH, 0, s>>>(a); break;
-    case E_BIAS: gemm_kernel<L_NT, E_BIAS, 0, true><<<grid, NTH, 0, s>>>(a); break;
-    default: gemm_kernel<L_NT, E_GELU, 0, true><<<grid, NTH, 0, s>>>(a); break;
-  }
-  return (int)hipGetLastError();
-}
-
 PDT_API int pdt_gemm_ok(int layout, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int splits) {
   if (layout != L_NT && layout != L_TT) return 0;
   if (splits < 1 || M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % ((int64_t)KB * splits)) return 0;
@@ -973,5 +935,20 @@ PDT_API int pdt_gemm2_bf16(int layout, int epi, const void* A, const void* B, vo
   if (epi == E_DGELU) {
     colpart_reduce_kernel<<<(int)((N + 255) / 256), 256, 0, s>>>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias);
   }
+  return (int)hipGetLastError();
+}
+
+// Instrumented build (results unchanged): the plain-epilogue kernel with phase stamps (DIAG above) into `stamps`
+// (uint64 [items][4]) -- scripts/gemm_stamps.py.
+PDT_API int pdt_gemm_stamps_bf16(int layout, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                                 int64_t lda, int64_t ldb, void* stamps, hipStream_t s) {
+  if (!pdt_gemm_ok(layout, M, N, K, lda, ldb, 1) || K < 2 * KB || !stamps) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux_out = (bf16_t*)stamps;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = N; a.k_per_split = (int)K;
+  a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  const dim3 grid(persist_grid((int)((M / TM) * (N / TN))), 1);
+  if (layout == L_NT) gemm_asm_kernel<L_NT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
+  else gemm_asm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
   return (int)hipGetLastError();
 }

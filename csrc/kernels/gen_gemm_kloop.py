@@ -53,10 +53,24 @@ def acc(i, j):
     return f"a[{k}:{k + 3}]"
 
 
+# Schedule knobs (a variant = one set; VARIANTS[0] is the production schedule and the only one emitted -- the
+# others are the measured alternatives, profiles/r4/r4_gemm_variants_v1.jsonl, kept to re-run the A/B):
+#   rd1  MFMAs of Q1 over which the F1 reads are spread      dma  MFMAs per quarter over which 8 DMA pieces spread
+#   rd0  MFMAs of Q4 over which the F0 reads are spread      bar  Q2 MFMAs issued before Q1's lgkmcnt(0) + barrier
+VARIANTS = [
+    dict(rd1=16, rd0=16, dma=32, bar=0),     # production: one DMA piece per 4 MFMAs (+2.5-5.6 % over dma=16,
+                                             # profiles/r4/r4_gemm_variants_v1.jsonl)
+    dict(rd1=16, rd0=16, dma=16, bar=0),     # round-4 first schedule
+    dict(rd1=16, rd0=24, dma=32, bar=0),
+    dict(rd1=12, rd0=12, dma=32, bar=0),
+]
+
+
 class Gen:
-    def __init__(self, layout):
+    def __init__(self, layout, sched=None):
         self.layout = layout
         self.lines = []
+        self.sc = dict(VARIANTS[0] if sched is None else sched)
 
     def emit(self, s):
         self.lines.append(s)
@@ -108,40 +122,39 @@ class Gen:
                 for i in rows for j in range(8)]
 
     # ---------------------------------------------------------------- schedule helpers
-    def interleave_reads(self, mf, reads, per):
-        """`per` reads after each MFMA from the first one on, all reads issued in the first part of the
-        quarter so their latency hides under the rest of it."""
-        k = 0
-        for m in mf:
+    def interleave_reads(self, mf, reads, span):
+        """The reads spread evenly over the first `span` MFMAs of the quarter (at least one MFMA between two
+        read slots; several reads per slot when there are more reads than MFMAs in the span)."""
+        slots = [[] for _ in mf]
+        span = max(1, min(span, len(mf)))
+        for k, r in enumerate(reads):
+            slots[min(span - 1, (k * span) // len(reads))].append(r)
+        for m, sl in zip(mf, slots):
             self.emit(m)
-            for _ in range(per):
-                if k < len(reads):
-                    self.emit(reads[k])
-                    k += 1
-        while k < len(reads):
-            self.emit(reads[k])
-            k += 1
+            for r in sl:
+                self.emit(r)
 
-    def interleave_dma(self, mf, pieces, tail):
-        """SALU set-up of a piece after one MFMA, its load after the next: 8 pieces over 16 MFMAs of the
-        quarter, the remaining MFMAs let the TA drain."""
-        k = 0
+    def interleave_dma(self, mf, pieces, tail, span):
+        """Piece k: SALU set-up after MFMA p_k, its load after MFMA p_k + 1, with p_k spread evenly over the first
+        `span` MFMAs of the quarter (>= 2 apart)."""
+        n = len(pieces)
+        span = max(2 * n, min(span, len(mf)))
+        pos = {(k * span) // n: k for k in range(n)}
         pending = None
-        for m in mf:
+        for idx, m in enumerate(mf):
             self.emit(m)
             if pending is not None:
                 self.emit(pending)
                 pending = None
-            elif k < len(pieces):
-                setup, load = pieces[k]
-                for s in setup:
-                    self.emit(s)
+            if idx in pos:
+                setup, load = pieces[pos[idx]]
+                for x in setup:
+                    self.emit(x)
                 pending = load
-                k += 1
         if pending is not None:
             self.emit(pending)
-        for s in tail:
-            self.emit(s)
+        for x in tail:
+            self.emit(x)
 
     # ---------------------------------------------------------------- one K-step
     def step(self, stage, dma, has_next, vm, first=False):
@@ -153,17 +166,22 @@ class Gen:
         # that read it (Q4 reads F1.A[4..7] and every F1.B block)
         f1 = self.read_ops(stage, 1, [(0, i, F1A) for i in range(4)] + [(1, j, F1B) for j in range(8)] +
                            [(0, i, F1A) for i in range(4, 8)])
-        self.interleave_reads(self.mfmas(F0A, F0B, range(0, 4), first), f1, 1 if self.layout == NT else 2)
+        sc = self.sc
+        self.interleave_reads(self.mfmas(F0A, F0B, range(0, 4), first), f1, sc["rd1"])
+        # Q2 / Q3: the DMA of tile t+2 into this stage (free once every wave passed the barrier after its F1 reads;
+        # the barrier sits `bar` MFMAs into Q2 so the last F1 reads have landed when it is reached)
+        q2 = self.mfmas(F0A, F0B, range(4, 8), first)
+        for m in q2[:sc["bar"]]:
+            self.emit(m)
         self.emit("s_waitcnt lgkmcnt(0)")
         self.emit("s_barrier")
-        # Q2 / Q3: the DMA of tile t+2 into this stage (free: every wave passed the barrier above after its reads)
-        q2 = self.mfmas(F0A, F0B, range(4, 8), first)
+        q2 = q2[sc["bar"]:]
         q3 = self.mfmas(F1A, F1B, range(0, 4))
         if dma:
             pa, ta = self.dma_ops(stage, 0)
             pb, tb = self.dma_ops(stage, 1)
-            self.interleave_dma(q2, pa, ta)
-            self.interleave_dma(q3, pb, tb)
+            self.interleave_dma(q2, pa, ta, sc["dma"])
+            self.interleave_dma(q3, pb, tb, sc["dma"])
         else:
             for m in q2 + q3:
                 self.emit(m)
@@ -175,10 +193,31 @@ class Gen:
         if has_next:
             f0 = self.read_ops(nxt, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
                                [(0, i, F0A) for i in range(1, 8)])
-            self.interleave_reads(q4, f0, 1 if self.layout == NT else 2)
+            self.interleave_reads(q4, f0, sc["rd0"])
         else:
             for m in q4:
                 self.emit(m)
+
+    def next_tail(self, first):
+        """The last two K-steps (stages 0, 1) of an item whose K-step count is even.  With %[hnx] set they DMA the
+        workgroup's NEXT item's K-tiles 0 and 1 into stages 0 and 1 in their Q2 / Q3 DMA slots (buffer resources
+        from %[nalo] .. %[nbhi]), so the next item's first loads are in flight under this item's last MFMAs and
+        its epilogue (which stages through the LDS past the ring)."""
+        e = self.emit
+        e("s_cmp_eq_u32 %[hnx], 0")
+        e("s_cbranch_scc1 pdtk%=_tl" + ("f" if first else "0"))
+        for base, x in ((S_RA, "na"), (S_RB, "nb")):
+            e(f"s_mov_b32 s{base}, %[{x}lo]")
+            e(f"s_mov_b32 s{base + 1}, %[{x}hi]")
+        e(f"s_mov_b32 s{S_OA}, 0")
+        e(f"s_mov_b32 s{S_OB}, 0")
+        self.step(0, True, True, 16, first=first)
+        self.step(1, True, False, 0)
+        e("s_branch pdtk%=_done")
+        e("pdtk%=_tl" + ("f" if first else "0") + ":")
+        self.step(0, False, True, 0, first=first)
+        self.step(1, False, False, 0)
+        e("s_branch pdtk%=_done")
 
     def tile_dma(self, stage):
         for op in (0, 1):
@@ -227,10 +266,18 @@ class Gen:
                 e(f"v_add_u32 {self.rd_reg(0, 1, i)}, %[db], {a0}")
                 e(f"v_add_u32 {self.rd_reg(1, 0, i)}, {STB}, {a0}")
                 e(f"v_add_u32 {self.rd_reg(1, 1, i)}, {STB}, {self.rd_reg(0, 1, i)}")
-        # prologue: tiles 0 and 1 in flight, tile 0 landed, its substep-0 fragments read
+        # prologue: tiles 0 and 1 in flight, tile 0 landed, its substep-0 fragments read.  A persistent
+        # workgroup's later items (%[first] = 0) find tiles 0 / 1 already issued by the previous item's last two
+        # K-steps (next_tail): then only the wait, counted past the previous epilogue's global stores (%[wnx])
+        e("s_cmp_eq_u32 %[first], 0")
+        e("s_cbranch_scc1 pdtk%=_issued")
         self.tile_dma(0)
         self.tile_dma(1)
         e("s_waitcnt vmcnt(16)")
+        e("s_branch pdtk%=_landed")
+        e("pdtk%=_issued:")
+        e("s_waitcnt vmcnt(%[wnx])")
+        e("pdtk%=_landed:")
         e("s_barrier")
         for r in self.read_ops(0, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
                                [(0, i, F0A) for i in range(1, 8)]):
@@ -253,17 +300,14 @@ class Gen:
         e(f"s_cmp_le_u32 s{S_CNT}, 2")
         e("s_cbranch_scc0 pdtk%=_loop")
         e("s_branch pdtk%=_tail1")
-        e("pdtk%=_tail0:")
-        self.step(0, False, True, 0)
-        self.step(1, False, False, 0)
-        e("s_branch pdtk%=_done")
-        e("pdtk%=_tail1:")
+        e("pdtk%=_tail0:")                      # 2 K-steps left, stage 0 (T even)
+        self.next_tail(False)
+        e("pdtk%=_tail1:")                      # 2 K-steps left, stage 1 (T odd: the next item loads itself)
         self.step(1, False, True, 0)
         self.step(0, False, False, 0)
         e("s_branch pdtk%=_done")
-        e("pdtk%=_first_tail:")                 # K = 128: both K-steps without DMA, the first from C = 0
-        self.step(0, False, True, 0, first=True)
-        self.step(1, False, False, 0)
+        e("pdtk%=_first_tail:")                 # K = 128: both K-steps, the first from C = 0
+        self.next_tail(True)
         e("pdtk%=_done:")
         e("s_nop 15")
         e("s_nop 15")
@@ -279,10 +323,10 @@ def main():
     out = ["// GENERATED by gen_gemm_kloop.py -- do not edit.  The hand-scheduled main loops of gemm.hip.",
            "#pragma once", ""]
     for L, name in ((NT, "PDT_GEMM_KLOOP_NT"), (TT, "PDT_GEMM_KLOOP_TT")):
-        g = Gen(L)
-        lines = g.program()
+        sched = VARIANTS[int(os.environ.get("PDT_GEMM_SCHEDULE", "0"))]
+        lines = Gen(L, sched).program()
         n_mfma = sum(1 for ln in lines if ln.startswith("v_mfma"))
-        out.append(f"// {name}: {len(lines)} lines, {n_mfma} MFMAs")
+        out.append(f"// {name} {sched}: {len(lines)} lines, {n_mfma} MFMAs")
         out.append(render(name, lines))
     out.append("#define PDT_AGPR_CLOBBERS " + ", ".join(f'"a{i}"' for i in range(256)))
     out.append("")

@@ -128,12 +128,10 @@ _SIGS = {
     "pdt_swin_mlp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p],
     "pdt_gemm_ok": [c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int],
-    "pdt_gemm_diag_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
-    "pdt_gemm_diag_nt_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
-    "pdt_gemm_nt_persist_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
-                                 c_int64, c_void_p, c_void_p, c_void_p],
     "pdt_gemm_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                       c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "pdt_gemm_stamps_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                             c_void_p, c_void_p],
     "pdt_gemm2_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
@@ -148,7 +146,7 @@ _SIGS = {
 
 _RET64 = {"pdt_swin_mlp_ws_floats", "pdt_fp8_gelu_bwd_ws_floats", "pdt_flash_attn_colsum_ws_floats"}
 
-F32, BF16, F16 = 0, 1, 2
+F32, BF16, F16, F64 = 0, 1, 2, 3
 
 
 def dtype_code(dt: torch.dtype) -> int:
@@ -158,6 +156,8 @@ def dtype_code(dt: torch.dtype) -> int:
         return BF16
     if dt == torch.float16:
         return F16
+    if dt == torch.float64:
+        return F64
     raise TypeError(f"unsupported dtype for HIP kernel: {dt}")
 
 

@@ -49,42 +49,32 @@ KERNEL = {"name": os.environ.get("PDT_GEMM_KERNEL", "asm")}
 
 
 def _launch(layout, epi, a, b, c, m, n, k, bias=None, aux=None, aux_out=None, dbias=None, ws=None, splits=1):
-    fn = "pdt_gemm2_bf16" if KERNEL["name"] == "asm" else "pdt_gemm_bf16"
+    # the hand-scheduled loop needs >= 2 K-steps per split and 16-byte epilogue rows; the compiler-scheduled
+    # kernel takes the rest (same results: the MFMA order per accumulator is identical)
+    asm = KERNEL["name"] == "asm" and k // splits >= 128 and c.stride(0) % 8 == 0
+    fn = "pdt_gemm2_bf16" if asm else "pdt_gemm_bf16"
     _lib.call(fn, layout, epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
               b.stride(0), c.stride(0), _lib.ptr(bias), _lib.ptr(aux), _lib.ptr(aux_out), _lib.ptr(dbias),
               _lib.ptr(ws), splits, _lib.stream_handle(a.device))
 
 
-def _launch_persist(epi, a, b, c, m, n, k, bias=None, aux_out=None):
-    _lib.call("pdt_gemm_nt_persist_bf16", epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0),
-              b.stride(0), c.stride(0), _lib.ptr(bias), _lib.ptr(aux_out), _lib.stream_handle(a.device))
-
-
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None, persist: bool = False) -> torch.Tensor:
-    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N].  ``persist``: one workgroup per CU walking its tiles
-    (the next tile's first K-steps load under the current tile's epilogue; K >= 128)."""
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N]."""
     m, k = a.shape
     n = b.shape[0]
     c = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
-    epi = E_BIAS if bias is not None else E_PLAIN
-    if persist:
-        _launch_persist(epi, a, b, c, m, n, k, bias=bias)
-    else:
-        _launch(L_NT, epi, a, b, c, m, n, k, bias=bias)
+    _launch(L_NT, E_BIAS if bias is not None else E_PLAIN, a, b, c, m, n, k, bias=bias)
     return c
 
 
-def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor, persist: bool = False):
+def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor):
     """(gelu_tanh(a b^T + bias), a b^T + bias) -- both bf16 [M, N]; the GELU reads the stored (rounded)
     pre-activation, which is what the backward differentiates."""
     m, k = a.shape
     n = b.shape[0]
     y = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     pre = torch.empty_like(y)
-    if persist:
-        _launch_persist(E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
-    else:
-        _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
+    _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
     return y, pre
 
 

@@ -50,7 +50,7 @@ def timeit(fn, iters=10):
 
 def check():
     torch.manual_seed(0)
-    for (M, N, K) in ((512, 512, 128), (2048, 1024, 1536), (1024, 768, 4096)):
+    for (M, N, K) in ((512, 512, 128), (2048, 1024, 1536), (1024, 768, 4096), (1024, 768, 4160)):
         a = torch.randn(M, K, device=dev).bfloat16()
         b = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
         bias = torch.randn(N, device=dev).bfloat16()
@@ -73,7 +73,7 @@ def check():
         bt = torch.randn(K * 2, N, device=dev).bfloat16()
         reft = at.float().t() @ bt.float()
         for s in (1, 2, 4):
-            if (2 * K) // s < 128:
+            if (2 * K) // s < 128 or (2 * K) % (64 * s):
                 continue
             t_asm = with_kernel("asm", lambda: G.gemm_tt(at, bt, splits=s))
             t_hip = with_kernel("hip", lambda: G.gemm_tt(at, bt, splits=s))
