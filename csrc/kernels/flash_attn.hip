@@ -11,12 +11,13 @@
 // staged TRANSPOSED in LDS with a +4-element row pad (136-B stride: conflict-free 8-B reads), and the
 // row-major operands (K, V, Q, dO) are staged with a 16-B-chunk XOR swizzle (conflict-free b128 reads).
 //
-// Forward: workgroup = 4 waves x 32 query rows (BM = 128), 64-key tiles, register-staged prefetch
-// of the next K/V tile overlapping the current tile's MFMAs (T14), heavy (diagonal-rich) blocks
-// launched first under the causal mask.
-// Backward: FA2-style split into (a) delta = rowsum(dO*O), (b) dK/dV kernel (workgroup owns 128
-// keys of one kv head and sweeps every query head of its GQA group, so dK/dV need no cross-workgroup
-// sum), (c) dQ kernel (workgroup owns 128 query rows).  No atomics: bitwise deterministic.
+// Forward (v5, default): workgroup = 4 waves x 32 query rows (BM = 128), 64-key tiles DMA'd into an LDS
+// ring overlapping the current tile's MFMAs, heavy (diagonal-rich) blocks launched first under the causal
+// mask; alternative v7: the same tile on 8 waves x 32 rows (256 rows share each staged K/V tile).
+// Backward: FA2-style split into (a) the dQ kernel (workgroup owns 128 / 256 query rows; it also computes
+// delta = rowsum(dO*O) for its rows and hands it on), (b) the dK/dV kernel (workgroup owns 128 keys of one
+// kv head and sweeps every query head of its GQA group, so dK/dV need no cross-workgroup sum).  No
+// atomics: bitwise deterministic.  Selection: ops/attention.py set_kernel_variant.
 //
 // Used by the GPT-2 / Llama models (BASELINE.json configs 3-5; SURVEY.md K16 "flash attention
 // (causal, head_dim 64/128)").
@@ -78,54 +79,6 @@ __device__ __forceinline__ int swz(int r, int c) {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-template <int D>
-struct TileIO {
-  static constexpr int CH = D / 8;                // 16-B chunks per row
-  static constexpr int NCH = TILE * CH / NT;      // chunks per thread per tile
-  // global -> registers (zero rows >= nrows)
-  __device__ __forceinline__ static void load(const bf16_t* base, int64_t row_stride, int row0, int nrows,
-                                              u16x8 (&r)[NCH]) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = threadIdx.x + i * NT;
-      const int row = c / CH, ch = c % CH;
-      if (row0 + row < nrows) {
-        r[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + row) * row_stride + ch * 8);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r[i][k] = 0;
-      }
-    }
-  }
-  // registers -> swizzled LDS image (16-B writes)
-  __device__ __forceinline__ static void store(bf16_t* lds, const u16x8 (&r)[NCH]) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = threadIdx.x + i * NT;
-      const int row = c / CH, ch = c % CH;
-      *reinterpret_cast<u16x8*>(lds + swz<D>(row, ch)) = r[i];
-    }
-  }
-  // row fragment: row `row`, k-step ks, lane half h -> elements d = 16ks + 8h .. +7
-  __device__ __forceinline__ static u16x8 row_frag(const bf16_t* lds, int row, int ks, int h) {
-    return *reinterpret_cast<const u16x8*>(lds + swz<D>(row, 2 * ks + h));
-  }
-  // transposed fragment (A operand for the permuted-k MFMA): lane l gets column d = 32dt + (l&31) of
-  // rows {kb + 4h + j} (j<4) and {kb + 8 + 4h + j-4} (j>=4), via two ds_read_b64_tr_b16.
-  __device__ __forceinline__ static u16x8 tr_frag(const bf16_t* lds, int dt, int kb, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int col = 32 * dt + 16 * (g & 1) + 4 * p;
-    const int r1 = kb + 4 * (g >> 1) + q;
-    const int o1 = swz<D>(r1, col >> 3) + (col & 7);
-    const int o2 = swz<D>(r1 + 8, col >> 3) + (col & 7);
-    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + o1));
-    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + o2));
-    u16x8 r;
-    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-    return r;
-  }
-};
 
 // pack registers 8s..8s+7 of an fp32 accumulator into a bf16 fragment
 __device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
@@ -187,135 +140,11 @@ __device__ __forceinline__ float row_delta(const AttnParams& p, const u16x8 (&gf
   return acc;
 }
 
-// ------------------------------------------------------------------------------------------------
-// forward
-// ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT) void fa_fwd_kernel(AttnParams p) {
-  using IO = TileIO<D>;
-  constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
-  bf16_t* Ks = smem;
-  bf16_t* Vs = smem + TILE * D;
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
-  const int off = p.Sk - p.Sq;  // bottom-right aligned causal mask
-  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
-  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  u16x8 qf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-    else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
-    }
-  }
-  f32x16 o[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
-  float m = -INFINITY, l = 0.f;
-
-  int kend = p.Sk;
-  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
-  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-
-  u16x8 kr[IO::NCH], vr[IO::NCH];
-  if (ntiles > 0) {
-    IO::load(Kp, p.k_ss, 0, p.Sk, kr);
-    IO::load(Vp, p.v_ss, 0, p.Sk, vr);
-  }
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    IO::store(Ks, kr);
-    IO::store(Vs, vr);
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
-      IO::load(Vp, p.v_ss, (t + 1) * TILE, p.Sk, vr);
-    }
-    const int k0 = t * TILE;
-    if (CAUSAL && k0 > qw + 31 + off) continue;  // every key of the tile is in this wave's future
-
-    f32x16 s[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = zero16();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[kt] = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s[kt]);
-    }
-    const bool need_mask = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[kt][r] * sl2;
-        if (need_mask) {
-          const int key = k0 + kt * 32 + acc_row(r, h);
-          if (key >= p.Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
-        }
-        s[kt][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float msub = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = fast_exp2(m - msub);
-    float ls = 0.f;
-    u16x8 pf[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = fast_exp2(s[kt][r] - msub);
-        s[kt][r] = pv;
-        ls += pv;
-      }
-      pf[kt][0] = pack8(s[kt], 0);
-      pf[kt][1] = pack8(s[kt], 1);
-    }
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-          o[dt] = mfma32(IO::tr_frag(Vs, dt, kt * 32 + 16 * ss, lane), pf[kt][ss], o[dt]);
-    }
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < p.Sq) {
-    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
-        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
-      }
-    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
-// forward v3: K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into a 2-deep LDS ring -- no
-// staging registers, ONE barrier per 64-key tile (the barrier's vmcnt(0) retires the tile this
-// iteration reads; the DMA for tile t+1 is issued right after it and overlaps tile t's MFMAs).
+// LDS-DMA operand staging shared by every kernel below: K/V (Q/dO) tiles arrive by buffer_load ... lds into
+// an LDS ring -- no staging registers, ONE barrier per 64-row tile (the barrier's vmcnt wait retires the tile
+// this iteration reads; the DMA for the next tile is issued right after it and overlaps this tile's MFMAs).
 // The XOR swizzle is applied on the per-lane SOURCE address (the DMA destination is lane-linear,
 // cdna_hip_programming.md §5.4 rule 21); rows past Sk are clamped to a real row and masked.
 // ------------------------------------------------------------------------------------------------
@@ -337,24 +166,6 @@ __device__ __forceinline__ void dma_barrier() {
   __syncthreads();
 }
 
-template <int D>
-__device__ __forceinline__ void dma_tile(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
-                                         int w, int lane) {
-  constexpr int RPI = 1024 / (D * 2);   // rows per wave-instruction (1 KiB per instruction)
-  constexpr int NI = 16 / RPI;          // instructions per wave (each wave fills 16 rows)
-  constexpr int LPR = 64 / RPI;         // lanes per row
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int row = 16 * w + RPI * i + lane / LPR;
-    const int pc = lane % LPR;
-    const int c = pc ^ swz_f<D>(row);
-    int g = row0 + row;
-    g = g < nrows ? g : nrows - 1;
-    const bf16_t* src = base + (int64_t)g * row_stride + c * 8;
-    bf16_t* dst = lds + (16 * w + RPI * i) * D;   // wave-uniform base; lane l lands at +16 B * l
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
-  }
-}
 
 // LDS-DMA of a TILE-row window through a buffer resource (T8): the per-lane byte offset of this lane's
 // 16-B chunk (row-major, XOR-swizzled) is computed once per kernel; per tile only the wave-uniform
@@ -435,129 +246,10 @@ struct DmaLane {
   }
 };
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void fa_fwd_v3_kernel(AttnParams p) {
-  using IO = TileIO<D>;
-  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
-  const int off = p.Sk - p.Sq;
-  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
-  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  int kend = p.Sk;
-  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
-  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  if (ntiles > 0) {
-    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
-    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
-  }
-
-  u16x8 qf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-    else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
-    }
-  }
-  f32x16 o[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
-  float m = -INFINITY, l = 0.f;
-
-  for (int t = 0; t < ntiles; ++t) {
-    dma_barrier();   // vmcnt(0): tile t resident; every wave is done with the buffer refilled below
-    if (t + 1 < ntiles) {
-      bf16_t* nb = smem + ((t + 1) & 1) * 2 * TE;
-      dma_tile<D>(Kp, p.k_ss, (t + 1) * TILE, p.Sk, nb, w, lane);
-      dma_tile<D>(Vp, p.v_ss, (t + 1) * TILE, p.Sk, nb + TE, w, lane);
-    }
-    const bf16_t* Ks = smem + (t & 1) * 2 * TE;
-    const bf16_t* Vs = Ks + TE;
-    const int k0 = t * TILE;
-    if (CAUSAL && k0 > qw + 31 + off) continue;
-
-    f32x16 s[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = zero16();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[kt] = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s[kt]);
-    }
-    const bool need_mask = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[kt][r] * sl2;
-        if (need_mask) {
-          const int key = k0 + kt * 32 + acc_row(r, h);
-          if (key >= p.Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
-        }
-        s[kt][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float msub = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = fast_exp2(m - msub);
-    float ls = 0.f;
-    u16x8 pf[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = fast_exp2(s[kt][r] - msub);
-        s[kt][r] = pv;
-        ls += pv;
-      }
-      pf[kt][0] = pack8(s[kt], 0);
-      pf[kt][1] = pack8(s[kt], 1);
-    }
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-          o[dt] = mfma32(IO::tr_frag(Vs, dt, kt * 32 + 16 * ss, lane), pf[kt][ss], o[dt]);
-    }
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < p.Sq) {
-    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
-        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
-      }
-    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// forward v4 = v3's LDS-DMA ring + a VALU-lean tile body.  Per 64-key tile a wave issues 32 MFMAs
-// (1024 MFMA cycles); v3 spent ~3x that on VALU (address math, zero-fills, scale, rescale, masks).
-// v4: (1) every LDS fragment address is a per-lane base computed ONCE (the swizzle depends only on
+// Forward tile body (the recipe of v5 below): per 64-key tile a wave issues 32 MFMAs (1024 MFMA cycles);
+// the first LDS-DMA generation spent ~3x that on VALU (address math, zero-fills, scale, rescale, masks).
+// (1) every LDS fragment address is a per-lane base computed ONCE (the swizzle depends only on
 // row & 15, which tile/k-block steps never change) plus a compile-time immediate -- the loop is
 // unrolled by the 2-deep ring so the buffer offset is an immediate too; (2) the softmax scale is
 // folded into one FMA feeding v_exp (max taken on raw scores); (3) the O rescale is skipped when no
@@ -606,173 +298,6 @@ __device__ __forceinline__ BlockCoord block_order(bool heavy_is_high, int order,
   if (!grouped_ok(order, gridDim.y, gridDim.z, grp)) return heavy_first(heavy_is_high);
   return grouped_coord(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y, grp,
                        heavy_is_high);
-}
-
-template <int D, bool CAUSAL>
-struct FwdV4 {
-  static constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
-
-  __device__ __forceinline__ static void tile(const bf16_t* __restrict__ lds, const int (&koff)[KS],
-                                              const int (&voff)[DT][2], const u16x8 (&qf)[KS], f32x16 (&o)[DT],
-                                              float& m, float& l, float sl2, int k0, bool diag, int lim) {
-    f32x16 s0, s1;
-    {
-      const f32x16 z = zero16();
-      s0 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[0]), qf[0], z);
-      s1 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[0] + 32 * D), qf[0], z);
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) {
-        s0 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[ks]), qf[ks], s0);
-        s1 = mfma32(*reinterpret_cast<const u16x8*>(lds + koff[ks] + 32 * D), qf[ks], s1);
-      }
-    }
-    if (diag) {   // keys k0 + kt*32 + acc_row(r, h) > lim are masked (future / past Sk)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = (r & 3) + 8 * (r >> 2);
-        s0[r] = (k0 + rr > lim) ? -INFINITY : s0[r];
-        s1[r] = (k0 + 32 + rr > lim) ? -INFINITY : s1[r];
-      }
-    }
-    float mx = fmaxf(s0[0], s1[0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-    const float mn = fmaxf(m, mx);
-    const float msub = (mn == -INFINITY) ? 0.f : mn;
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = fast_exp2(fmaf(s0[r], sl2, -msub));
-      s1[r] = fast_exp2(fmaf(s1[r], sl2, -msub));
-      ls += s0[r] + s1[r];
-    }
-    u16x8 pf[2][2];
-    pf[0][0] = pack8(s0, 0); pf[0][1] = pack8(s0, 1);
-    pf[1][0] = pack8(s1, 0); pf[1][1] = pack8(s1, 1);
-    if (!__all(mn == m)) {
-      const float alpha = fast_exp2(m - msub);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-      l *= alpha;
-      m = mn;
-    }
-    l += ls;
-    const bf16_t* vs = lds + TE;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const int kb = kt * 32 + 16 * ss;
-          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][0] + kb * D));
-          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vs + voff[dt][1] + kb * D));
-          const u16x8 fr = __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-          o[dt] = mfma32(fr, pf[kt][ss], o[dt]);
-        }
-    }
-  }
-};
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT, 2) void fa_fwd_v4_kernel(AttnParams p) {
-  using K = FwdV4<D, CAUSAL>;
-  constexpr int KS = K::KS, DT = K::DT, TE = K::TE;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf 0/1][K | V]
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = heavy_first(true);
-  const int b = CAUSAL ? bc.b : (int)blockIdx.z, hq = CAUSAL ? bc.h : (int)blockIdx.y;
-  const int qb = CAUSAL ? bc.t : (int)blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
-  const int off = p.Sk - p.Sq;
-  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
-  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  int kend = p.Sk;
-  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
-  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  DmaLane<D> lk, lv;
-  lk.init(p.k_ss, w, lane);
-  lv.init(p.v_ss, w, lane);
-  if (ntiles > 0) {
-    lk.issue(Kp, p.k_ss, 0, p.Sk, smem, w);
-    lv.issue(Vp, p.v_ss, 0, p.Sk, smem + TE, w);
-  }
-
-  // per-lane LDS element offsets (swizzle depends on row & 15 only)
-  int koff[KS];
-  const int F = swz_f<D>(c32);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) koff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
-  int voff[DT][2];
-  {
-    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    const int r1 = 4 * (g >> 1) + q;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
-      voff[dt][0] = r1 * D + (((col >> 3) ^ swz_f<D>(r1)) << 3) + (col & 7);
-      voff[dt][1] = (r1 + 8) * D + (((col >> 3) ^ swz_f<D>(r1 + 8)) << 3) + (col & 7);
-    }
-  }
-
-  u16x8 qf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-    else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) qf[ks][k] = 0;
-    }
-  }
-  f32x16 o[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
-  float m = -INFINITY, l = 0.f;
-  // keys > lim are masked for this lane's query row; a tile needs masking if its last key > qw + off
-  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
-
-  for (int t = 0; t < ntiles; t += 2) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int tt = t + u;
-      if (tt < ntiles) {
-        dma_barrier();
-        if (tt + 1 < ntiles) {
-          bf16_t* nb = smem + (1 - u) * 2 * TE;
-          lk.issue(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w);
-          lv.issue(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w);
-        }
-        const int k0 = tt * TILE;
-        if (!(CAUSAL && k0 > qw + 31 + off)) {
-          const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
-          K::tile(smem + u * 2 * TE, koff, voff, qf, o, m, l, sl2, k0, diag, lim);
-        }
-      }
-    }
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < p.Sq) {
-    bf16_t* Op = p.o + b * p.o_sb + hq * p.o_sh + (int64_t)qrow * p.o_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv);
-        *reinterpret_cast<u16x4*>(Op + dt * 32 + 8 * g + 4 * h) = v;
-      }
-    if (h == 0) p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] = lt > 0.f ? (m + __log2f(lt)) * LN2 : INFINITY;
-  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -890,7 +415,7 @@ __device__ __forceinline__ void wg_colsum_store(float (&v)[D / 2], float* lds, f
 }
 
 // ------------------------------------------------------------------------------------------------
-// forward v5 = v4 + (1) deferred rescale (T13): the running max m used in exp2 moves only when some
+// forward v5 (default) = the VALU-lean tile body above + (1) deferred rescale (T13): the running max m used in exp2 moves only when some
 // row's tile max exceeds it by more than RESCALE_THR (log2 units), so the 64-register O rescale runs on a
 // handful of tiles instead of most of them (probabilities stay <= 2^THR, exact in fp32 / bf16 range);
 // (2) the K row fragments stream two MFMA steps ahead of their use and the V transposed fragments one
@@ -1224,221 +749,9 @@ __global__ __launch_bounds__(NT) void fa_bwd_delta_kernel(AttnParams p) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// backward (b): dK, dV.  Workgroup = 128 keys (4 waves x 32) of kv head hk; sweeps the q heads of
-// the group and the query tiles (64 rows) that can see those keys.
-// ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT) void fa_bwd_dkdv_kernel(AttnParams p) {
-  using IO = TileIO<D>;
-  constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
-  __shared__ float lse_s[TILE], dl_s[TILE];
-  bf16_t* Qs = smem;
-  bf16_t* Gs = smem + TILE * D;        // dO
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hk = blockIdx.y;
-  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;
-  const int group = p.H / p.Hkv;
-  const int off = p.Sk - p.Sq;
-  const int kw = kb * 128 + w * 32, key = kw + c32;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  u16x8 kf[KS], vf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (key < p.Sk) {
-      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
-      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
-    }
-  }
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
-
-  int qstart = 0;
-  if (CAUSAL) qstart = max(0, kb * 128 - off) / TILE * TILE;
-  for (int hi = 0; hi < group; ++hi) {
-    const int hq = hk * group + hi;
-    const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-    const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
-    const float* Lp = p.lse + ((int64_t)b * p.H + hq) * p.Sq;
-    const float* Dp = p.delta + ((int64_t)b * p.H + hq) * p.Sq;
-    u16x8 qr[IO::NCH], gr[IO::NCH];
-    if (qstart < p.Sq) {
-      IO::load(Qp, p.q_ss, qstart, p.Sq, qr);
-      IO::load(Gp, p.do_ss, qstart, p.Sq, gr);
-    }
-    for (int q0 = qstart; q0 < p.Sq; q0 += TILE) {
-      {
-        __syncthreads();
-        IO::store(Qs, qr);
-        IO::store(Gs, gr);
-        if (threadIdx.x < TILE) {
-          const int q = q0 + threadIdx.x;
-          lse_s[threadIdx.x] = q < p.Sq ? Lp[q] * LOG2E : INFINITY;
-          dl_s[threadIdx.x] = q < p.Sq ? Dp[q] : 0.f;
-        }
-        __syncthreads();
-        if (q0 + TILE < p.Sq) {
-          IO::load(Qp, p.q_ss, q0 + TILE, p.Sq, qr);
-          IO::load(Gp, p.do_ss, q0 + TILE, p.Sq, gr);
-        }
-      }
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        const int qb0 = q0 + qs * 32;
-        if (CAUSAL && qb0 + 31 + off < kw) continue;  // all queries of the subtile precede these keys
-        f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s = mfma32(IO::row_frag(Qs, qs * 32 + c32, ks, h), kf[ks], s);
-          dp = mfma32(IO::row_frag(Gs, qs * 32 + c32, ks, h), vf[ks], dp);
-        }
-        // S rows = queries (registers), columns = keys (lanes)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = qs * 32 + acc_row(r, h);
-          const int q = q0 + qi;
-          float pv = fast_exp2(s[r] * sl2 - lse_s[qi]);
-          if (key >= p.Sk || (CAUSAL && key > q + off)) pv = 0.f;
-          s[r] = pv;
-          dp[r] = pv * (dp[r] - dl_s[qi]);
-        }
-        const u16x8 pf0 = pack8(s, 0), pf1 = pack8(s, 1);
-        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dv[dt] = mfma32(IO::tr_frag(Gs, dt, qs * 32, lane), pf0, dv[dt]);
-          dv[dt] = mfma32(IO::tr_frag(Gs, dt, qs * 32 + 16, lane), pf1, dv[dt]);
-          dk[dt] = mfma32(IO::tr_frag(Qs, dt, qs * 32, lane), df0, dk[dt]);
-          dk[dt] = mfma32(IO::tr_frag(Qs, dt, qs * 32 + 16, lane), df1, dk[dt]);
-        }
-      }
-    }
-  }
-  if (key < p.Sk) {
-    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
-    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 a, c;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
-        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
-        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
-      }
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
-// backward (c): dQ.  Workgroup = 128 query rows (4 waves x 32) of head hq; sweeps key tiles.
-// ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT) void fa_bwd_dq_kernel(AttnParams p) {
-  using IO = TileIO<D>;
-  constexpr int KS = D / 16, DT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * TILE * D];
-  bf16_t* Ks = smem;
-  bf16_t* Vs = smem + TILE * D;
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
-  const int off = p.Sk - p.Sq;
-  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
-  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  u16x8 qf[KS], gf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) {
-      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
-    }
-  }
-  const float lse2 = qrow < p.Sq ? p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : INFINITY;
-  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
-  f32x16 dq[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
-
-  int kend = p.Sk;
-  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
-  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  u16x8 kr[IO::NCH], vr[IO::NCH];
-  if (ntiles > 0) {
-    IO::load(Kp, p.k_ss, 0, p.Sk, kr);
-    IO::load(Vp, p.v_ss, 0, p.Sk, vr);
-  }
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    IO::store(Ks, kr);
-    IO::store(Vs, vr);
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      IO::load(Kp, p.k_ss, (t + 1) * TILE, p.Sk, kr);
-      IO::load(Vp, p.v_ss, (t + 1) * TILE, p.Sk, vr);
-    }
-    const int k0 = t * TILE;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int kb0 = k0 + kt * 32;
-      if (CAUSAL && kb0 > qw + 31 + off) continue;
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        s = mfma32(IO::row_frag(Ks, kt * 32 + c32, ks, h), qf[ks], s);
-        dp = mfma32(IO::row_frag(Vs, kt * 32 + c32, ks, h), gf[ks], dp);
-      }
-      // S^T: rows = keys (registers), columns = queries (lanes)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb0 + acc_row(r, h);
-        float pv = fast_exp2(s[r] * sl2 - lse2);
-        if (key >= p.Sk || (CAUSAL && key > qrow + off)) pv = 0.f;
-        dp[r] = pv * (dp[r] - dl);
-      }
-      const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dq[dt] = mfma32(IO::tr_frag(Ks, dt, kt * 32, lane), df0, dq[dt]);
-        dq[dt] = mfma32(IO::tr_frag(Ks, dt, kt * 32 + 16, lane), df1, dq[dt]);
-      }
-    }
-  }
-  if (qrow < p.Sq) {
-    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
-        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// backward v2 (dK/dV and dQ): same recipe as forward v4 -- LDS-DMA double-buffered operand tiles
+// backward operand staging (dK/dV and dQ): same recipe as the forward -- LDS-DMA double-buffered operand tiles
 // (one barrier per tile), per-lane LDS bases + immediates (no per-read address math), scale folded
 // into an FMA ahead of v_exp, and compare/select masks only on boundary sub-tiles.  LSE and delta
 // rows travel by LDS-DMA too (4-byte pieces), so no ordinary global load sits in the loop to force
@@ -1471,246 +784,8 @@ __device__ __forceinline__ u16x8 tr_pair(const bf16_t* p0, const bf16_t* p1) {
   return __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT) void fa_bwd_dkdv_v2_kernel(AttnParams p) {
-  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
-  // [buf][Q | dO] + [buf][lse | delta]
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];
-  __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x;
-  const int group = p.H / p.Hkv;
-  const int off = p.Sk - p.Sq;
-  const int kw = kb * 128 + w * 32, key = kw + c32;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  u16x8 kf[KS], vf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (key < p.Sk) {
-      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
-      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
-    }
-  }
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
-
-  int roff[KS];
-  const int F = swz_f<D>(c32);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
-  int toff[DT][2];
-  tr_offsets<D>(lane, toff);
-
-  const int qstart = CAUSAL ? max(0, kb * 128 - off) / TILE * TILE : 0;
-  const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
-  const int total = qtiles * group;
-
-  auto issue = [&](int it, int buf) {
-    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
-    const int hq = hk * group + hi;
-    const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-    const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
-    bf16_t* base = smem + buf * 2 * TE;
-    dma_tile<D>(Qp, p.q_ss, q0, p.Sq, base, w, lane);
-    dma_tile<D>(Gp, p.do_ss, q0, p.Sq, base + TE, w, lane);
-    if (w == 0) dma_f32_row(p.lse + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][0], lane);
-    if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][1], lane);
-  };
-  if (total > 0) issue(0, 0);
-
-  for (int it = 0; it < total; it += 2) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int cur = it + u;
-      if (cur >= total) break;
-      dma_barrier();
-      if (cur + 1 < total) issue(cur + 1, 1 - u);
-      const int q0 = qstart + (cur % qtiles) * TILE;
-      const bf16_t* Qs = smem + u * 2 * TE;
-      const bf16_t* Gs = Qs + TE;
-      const float* Ls = sstat[u][0];
-      const float* Ds = sstat[u][1];
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        const int qb0 = q0 + qs * 32;
-        if (CAUSAL && qb0 + 31 + off < kw) continue;      // every query precedes these keys
-        f32x16 s, dp;
-        {
-          const f32x16 z = zero16();
-          s = mfma32(*reinterpret_cast<const u16x8*>(Qs + roff[0] + qs * 32 * D), kf[0], z);
-          dp = mfma32(*reinterpret_cast<const u16x8*>(Gs + roff[0] + qs * 32 * D), vf[0], z);
-#pragma unroll
-          for (int ks = 1; ks < KS; ++ks) {
-            s = mfma32(*reinterpret_cast<const u16x8*>(Qs + roff[ks] + qs * 32 * D), kf[ks], s);
-            dp = mfma32(*reinterpret_cast<const u16x8*>(Gs + roff[ks] + qs * 32 * D), vf[ks], dp);
-          }
-        }
-        // rows of S = queries qb0 + rr + 4h (registers), columns = keys (lanes)
-        const int tmask = CAUSAL ? key - off - qb0 - 4 * h : -1;   // masked if rr < tmask
-        const int tsq = p.Sq - qb0 - 4 * h;                          // masked if rr >= tsq
-        const bool edge = (CAUSAL && kw + 31 > qb0 + off) || (qb0 + 32 > p.Sq);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + qs * 32 + 8 * g + 4 * h);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(Ds + qs * 32 + 8 * g + 4 * h);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i, rr = i + 8 * g;
-            float pv = fast_exp2(fmaf(s[r], sl2, -l4[i] * LOG2E));
-            if (edge) pv = (rr < tmask || rr >= tsq) ? 0.f : pv;
-            s[r] = pv;
-            dp[r] = pv * (dp[r] - d4[i]);
-          }
-        }
-        const u16x8 pf0 = pack8(s, 0), pf1 = pack8(s, 1);
-        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dv[dt] = mfma32(tr_pair(Gs + toff[dt][0] + qs * 32 * D, Gs + toff[dt][1] + qs * 32 * D), pf0, dv[dt]);
-          dv[dt] = mfma32(tr_pair(Gs + toff[dt][0] + (qs * 32 + 16) * D, Gs + toff[dt][1] + (qs * 32 + 16) * D),
-                          pf1, dv[dt]);
-          dk[dt] = mfma32(tr_pair(Qs + toff[dt][0] + qs * 32 * D, Qs + toff[dt][1] + qs * 32 * D), df0, dk[dt]);
-          dk[dt] = mfma32(tr_pair(Qs + toff[dt][0] + (qs * 32 + 16) * D, Qs + toff[dt][1] + (qs * 32 + 16) * D),
-                          df1, dk[dt]);
-        }
-      }
-    }
-  }
-  if (key < p.Sk) {
-    bf16_t* DKp = p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss;
-    bf16_t* DVp = p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 a, c;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { a[i] = f2bf(dk[dt][4 * g + i] * p.scale); c[i] = f2bf(dv[dt][4 * g + i]); }
-        *reinterpret_cast<u16x4*>(DKp + dt * 32 + 8 * g + 4 * h) = a;
-        *reinterpret_cast<u16x4*>(DVp + dt * 32 + 8 * g + 4 * h) = c;
-      }
-  }
-}
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT) void fa_bwd_dq_v2_kernel(AttnParams p) {
-  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];   // [buf][K | V]
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const int b = blockIdx.z, hq = blockIdx.y;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
-  const int off = p.Sk - p.Sq;
-  const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
-  const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16_t* Gp = p.dout + b * p.do_sb + hq * p.do_sh;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  int kend = p.Sk;
-  if (CAUSAL) kend = min(p.Sk, q0 + 128 + off);
-  const int ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
-  if (ntiles > 0) {
-    dma_tile<D>(Kp, p.k_ss, 0, p.Sk, smem, w, lane);
-    dma_tile<D>(Vp, p.v_ss, 0, p.Sk, smem + TE, w, lane);
-  }
-  u16x8 qf[KS], gf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) {
-      qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
-      gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
-    }
-  }
-  const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
-  const float dl = qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f;
-  f32x16 dq[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
-  int roff[KS];
-  const int F = swz_f<D>(c32);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
-  int toff[DT][2];
-  tr_offsets<D>(lane, toff);
-  const int lim = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
-
-  for (int t = 0; t < ntiles; t += 2) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int tt = t + u;
-      if (tt >= ntiles) break;
-      dma_barrier();
-      if (tt + 1 < ntiles) {
-        bf16_t* nb = smem + (1 - u) * 2 * TE;
-        dma_tile<D>(Kp, p.k_ss, (tt + 1) * TILE, p.Sk, nb, w, lane);
-        dma_tile<D>(Vp, p.v_ss, (tt + 1) * TILE, p.Sk, nb + TE, w, lane);
-      }
-      const bf16_t* Ks = smem + u * 2 * TE;
-      const bf16_t* Vs = Ks + TE;
-      const int k0 = tt * TILE;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const int kb0 = k0 + kt * 32;
-        if (CAUSAL && kb0 > qw + 31 + off) continue;
-        f32x16 s, dp;
-        {
-          const f32x16 z = zero16();
-          s = mfma32(*reinterpret_cast<const u16x8*>(Ks + roff[0] + kt * 32 * D), qf[0], z);
-          dp = mfma32(*reinterpret_cast<const u16x8*>(Vs + roff[0] + kt * 32 * D), gf[0], z);
-#pragma unroll
-          for (int ks = 1; ks < KS; ++ks) {
-            s = mfma32(*reinterpret_cast<const u16x8*>(Ks + roff[ks] + kt * 32 * D), qf[ks], s);
-            dp = mfma32(*reinterpret_cast<const u16x8*>(Vs + roff[ks] + kt * 32 * D), gf[ks], dp);
-          }
-        }
-        const bool edge = (kb0 + 32 > p.Sk) || (CAUSAL && kb0 + 31 > qw + off);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = (r & 3) + 8 * (r >> 2);
-          float pv = fast_exp2(fmaf(s[r], sl2, nlse2));
-          if (edge) pv = (kb0 + rr > lim) ? 0.f : pv;
-          dp[r] = pv * (dp[r] - dl);
-        }
-        const u16x8 df0 = pack8(dp, 0), df1 = pack8(dp, 1);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dq[dt] = mfma32(tr_pair(Ks + toff[dt][0] + kt * 32 * D, Ks + toff[dt][1] + kt * 32 * D), df0, dq[dt]);
-          dq[dt] = mfma32(tr_pair(Ks + toff[dt][0] + (kt * 32 + 16) * D, Ks + toff[dt][1] + (kt * 32 + 16) * D),
-                          df1, dq[dt]);
-        }
-      }
-    }
-  }
-  if (qrow < p.Sq) {
-    bf16_t* DQp = p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(dq[dt][4 * g + i] * p.scale);
-        *reinterpret_cast<u16x4*>(DQp + dt * 32 + 8 * g + 4 * h) = v;
-      }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// backward v3: same data flow as v2, re-shaped for intra-wave MFMA/VALU overlap.  Each 64-row tile is
+// backward v3: the staging above, re-shaped for intra-wave MFMA/VALU overlap.  Each 64-row tile is
 // one straight-line region: BOTH 32-row subtiles' S / dP chains are issued first, then the softmax-
 // gradient VALU work of subtile 0 runs under the MFMAs of subtile 1's chains and subtile 0's dK/dV
 // (dQ) updates, and so on -- independent work the scheduler can interleave even at one wave per SIMD.
@@ -2083,89 +1158,6 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   }
 }
 
-// dK/dV v5: dK/dV v3 (4 waves x 32 keys, one wave per SIMD: its 312 registers rule out a second wave) with
-// the NBUF-deep counted-vmcnt ring of forward v7, so the next Q / dO tile's DMA has two tiles of cover.
-template <int D, bool CAUSAL, int NBUF>
-__global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_v5_kernel(AttnParams p) {
-  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D;
-  using Dma = DmaLane<D, true, 4>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NBUF * 2 * TE];        // [stage][Q | dO]
-  __shared__ __attribute__((aligned(16))) float sstat[NBUF][2][TILE];        // [stage][-lse log2e | delta]
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
-  const BlockCoord bc = block_order(false, p.order, 1);
-  const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
-  const int kb = remap ? bc.t : (int)blockIdx.x;
-  const int group = p.H / p.Hkv;
-  const int off = p.Sk - p.Sq;
-  const int kw = kb * 128 + w * 32, key = kw + c32;
-  const bf16_t* Kp = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vp = p.v + b * p.v_sb + hk * p.v_sh;
-  const float sl2 = p.scale * LOG2E;
-
-  const int qstart = CAUSAL ? max(0, kb * 128 - off) / TILE * TILE : 0;
-  const int qtiles = p.Sq > qstart ? (p.Sq - qstart + TILE - 1) / TILE : 0;
-  const int total = qtiles * group;
-  Dma lq, lg;
-  lq.init(p.q_ss, w, lane);
-  lg.init(p.do_ss, w, lane);
-  auto issue = [&](int it, int st) {
-    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
-    const int hq = hk * group + hi;
-    bf16_t* base = smem + st * 2 * TE;
-    lq.issue(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w);
-    lg.issue(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w);
-    if (w == 0) dma_f32_row(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[st][0], lane);
-    if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[st][1], lane);
-  };
-#pragma unroll
-  for (int t = 0; t < NBUF - 1; ++t)
-    if (t < total) issue(t, t);
-
-  u16x8 kf[KS], vf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (key < p.Sk) {
-      kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
-      vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { kf[ks][k] = 0; vf[ks][k] = 0; }
-    }
-  }
-  retire(kf);
-  retire(vf);
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
-  int roff[KS];
-  const int F = swz_f<D>(c32);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
-  int toff[DT][2];
-  tr_offsets<D>(lane, toff);
-
-  // waves 0 / 1 also carry the lse / delta row DMA: one more instruction per tile in their count
-  int stage = 0;
-  for (int it = 0; it < total; ++it) {
-    if (w < 2) ring_wait<2 * Dma::NI + 1, NBUF>(it + 1 < total);
-    else ring_wait<2 * Dma::NI, NBUF>(it + 1 < total);
-    if (it + NBUF - 1 < total) issue(it + NBUF - 1, stage == 0 ? NBUF - 1 : stage - 1);
-    const int q0 = qstart + (it % qtiles) * TILE;
-    if (!(CAUSAL && q0 + TILE - 1 + off < kw)) {
-      const bf16_t* Qs = smem + stage * 2 * TE;
-      const float* Ls = sstat[stage][0];
-      const int tmask = CAUSAL ? key - off - q0 - 4 * h : -1;
-      const int tsq = p.Sq - q0 - 4 * h;
-      BwdKVTile<D, CAUSAL>::run(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask, tsq, h);
-    }
-    stage = stage + 1 == NBUF ? 0 : stage + 1;
-  }
-  acc_fence();
-  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
-  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
-}
 
 // dQ v4: dQ v3's per-wave tile on a 512-thread workgroup (8 waves x 32 query rows = 256 rows per staged
 // K/V tile, 384 instead of 192 FLOP per staged byte) with the NBUF-deep counted-vmcnt ring of forward v7.
@@ -2291,17 +1283,7 @@ template <int D>
 int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
   AttnParams p = p0;                       // p.order bit 0: forward block order
   p.order = p0.order & 1;
-  dim3 grid((p.Sq + 127) / 128, p.H, p.B);
-  if (variant == 2) {
-    if (causal) fa_fwd_kernel<D, true><<<grid, NT, 0, st>>>(p);
-    else fa_fwd_kernel<D, false><<<grid, NT, 0, st>>>(p);
-  } else if (variant == 4) {
-    if (causal) fa_fwd_v4_kernel<D, true><<<grid, NT, 0, st>>>(p);
-    else fa_fwd_v4_kernel<D, false><<<grid, NT, 0, st>>>(p);
-  } else if (variant == 5) {
-    if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
-    else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
-  } else if (variant == 7 || variant == 8) {   // 8 waves x 32 rows; 7: 3-deep ring, 8: 2-deep
+  if (variant == 7 || variant == 8) {      // alternative: v5's tile on 8 waves x 32 rows; 7: 3-deep ring, 8: 2-deep
     dim3 g8((p.Sq + 255) / 256, p.H, p.B);
     if (variant == 7) {
       if (causal) fa_fwd_v7_kernel<D, true, 3><<<g8, NT8, 0, st>>>(p);
@@ -2310,117 +1292,41 @@ int launch_fwd(const AttnParams& p0, int causal, int variant, hipStream_t st) {
       if (causal) fa_fwd_v7_kernel<D, true, 2><<<g8, NT8, 0, st>>>(p);
       else fa_fwd_v7_kernel<D, false, 2><<<g8, NT8, 0, st>>>(p);
     }
-  } else {
-    if (causal) fa_fwd_v3_kernel<D, true><<<grid, NT, 0, st>>>(p);
-    else fa_fwd_v3_kernel<D, false><<<grid, NT, 0, st>>>(p);
+  } else {                                 // default (5): 4 waves x 32 rows, LDS-DMA ring
+    dim3 grid((p.Sq + 127) / 128, p.H, p.B);
+    if (causal) fa_fwd_v5_kernel<D, true><<<grid, NT, 0, st>>>(p);
+    else fa_fwd_v5_kernel<D, false><<<grid, NT, 0, st>>>(p);
   }
   return (int)hipGetLastError();
 }
 
+// Backward: dQ first (it computes delta = rowsum(dO * O) itself unless PDT_FA_FUSE_DELTA=0), then dK/dV v3
+// (one wave per SIMD).  dQ kernel: 9 (default at head dim 128) dQ v4, 8 waves x 32 rows, 2-deep ring;
+// 8 the same with a 3-deep ring; 3 (default at head dim 64) dQ v3, 4 waves x 32 rows.
 template <int D>
 int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.Sq;
   dim3 gkv((p.Sk + 127) / 128, p.Hkv, p.B);
   dim3 gq((p.Sq + 127) / 128, p.H, p.B);
+  dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
   const int variant = bwd_variant(D);
   AttnParams kv = p, qp = p;               // per-kernel block order (p.order bit 1: dK/dV, bit 2: dQ)
   kv.order = (p.order >> 1) & 1;
   qp.order = (p.order >> 2) & 1;
-  kv.fuse_delta = qp.fuse_delta = 0;
-  // dQ v3 / v4 + dK/dV v3 (variants 3, 7, 8, 9 -- the defaults): dQ first, computing delta itself
+  kv.fuse_delta = 0;
   static const bool fuse = [] { const char* e = getenv("PDT_FA_FUSE_DELTA"); return !e || atoi(e) != 0; }();
-  if (fuse && (variant == 3 || variant == 7 || variant == 8 || variant == 9)) {
-    qp.fuse_delta = 1;
-    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
-    if (causal) {
-      if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-      else if (variant == 7) fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(qp);
-      else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
-      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
-    } else {
-      if (variant == 3) fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-      else if (variant == 7) fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(qp);
-      else if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
-      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
-    }
-    return (int)hipGetLastError();
-  }
-  fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
-  if (variant == 1) {
-    if (causal) {
-      fa_bwd_dkdv_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-    }
-  } else if (variant == 2) {
-    if (causal) {
-      fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-    }
-  } else if (variant == 5 || variant == 6) {   // mixed generations (kernel bisection in tests)
-    if (causal) {
-      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
-      else fa_bwd_dkdv_v2_kernel<D, true><<<gkv, NT, 0, st>>>(kv);
-      if (variant == 5) fa_bwd_dq_v2_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-      else fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-    } else {
-      if (variant == 5) fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
-      else fa_bwd_dkdv_v2_kernel<D, false><<<gkv, NT, 0, st>>>(kv);
-      if (variant == 5) fa_bwd_dq_v2_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-      else fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-    }
-  } else if (variant == 7) {   // v3 with the dQ kernel at one wave per SIMD (inline-asm DMA, no spills):
-                               // 4-8 % slower than variant 3's two waves per SIMD (profiles/r2_attn_experiments.txt)
-    if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, true, 1><<<gq, NT, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, false, 1><<<gq, NT, 0, st>>>(qp);
-    }
-  } else if (variant == 8 || variant == 9) {   // dK/dV v3 (one wave per SIMD) + dQ v4 (8 waves; 8: 3-deep ring)
-    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
-    if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
-      if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
-      else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
-      if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
-      else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
-    }
-  } else if (variant == 10) {   // dK/dV v5 (3-deep ring) + dQ v4 (8 waves, 2-deep ring)
-    dim3 gq8((p.Sq + 255) / 256, p.H, p.B);
-    if (causal) {
-      fa_bwd_dkdv_v5_kernel<D, true, 3><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v5_kernel<D, false, 3><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
-    }
-  } else if (variant == 3) {   // v3, one wave per SIMD for dK/dV (no spills)
-    if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-    }
-  } else {                     // v3, two waves per SIMD for dK/dV
-    if (causal) {
-      fa_bwd_dkdv_v3_kernel<D, true, 2><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
-    } else {
-      fa_bwd_dkdv_v3_kernel<D, false, 2><<<gkv, NT, 0, st>>>(kv);
-      fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
-    }
+  qp.fuse_delta = fuse ? 1 : 0;
+  if (!fuse) fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
+  if (causal) {
+    if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
+    else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
+    else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
+    fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+  } else {
+    if (variant == 3) fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
+    else if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
+    else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
+    fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
   }
   return (int)hipGetLastError();
 }
@@ -2449,9 +1355,8 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
 static void colsum_rows(int B, int Sq, int Sk, int D, int& rq, int& rkv) {
   const int v = bwd_variant(D);
   rq = rkv = 0;
-  if (v == 8 || v == 9) rq = B * ((Sq + 255) / 256);
-  else if (v == 3 || v == 4 || v == 7) rq = B * ((Sq + 127) / 128);
-  else return;
+  if (v == 3) rq = B * ((Sq + 127) / 128);
+  else rq = B * ((Sq + 255) / 256);
   rkv = B * ((Sk + 127) / 128);
 }
 

@@ -230,6 +230,17 @@ class Gen:
             for s in tail:
                 self.emit(s)
 
+    def first_step(self, vm):
+        """Barrier on tile 0, its substep-0 fragments, then K-step 0 (or the whole of a <= 2-step item)."""
+        e = self.emit
+        e("s_barrier")
+        for r in self.read_ops(0, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
+                               [(0, i, F0A) for i in range(1, 8)]):
+            e(r)
+        e(f"s_cmp_le_u32 s{S_CNT}, 2")
+        e("s_cbranch_scc1 pdtk%=_first_tail")
+        self.step(0, True, True, vm, first=True)
+
     def program(self):
         L = self.layout
         e = self.emit
@@ -269,24 +280,21 @@ class Gen:
         # prologue: tiles 0 and 1 in flight, tile 0 landed, its substep-0 fragments read.  A persistent
         # workgroup's later items (%[first] = 0) find tiles 0 / 1 already issued by the previous item's last two
         # K-steps (next_tail): then only the wait, counted past the previous epilogue's global stores (%[wnx])
+        # K-step 0 is peeled (its substep-0 MFMAs start every accumulator from C = 0) and emitted twice: for a
+        # later item its end-of-step wait for tile 1 also counts the previous epilogue's stores as older than
+        # tile 2's DMA (vmcnt(%[wnx]) = 16 + stores), so they drain under the K-step instead of stalling it
         e("s_cmp_eq_u32 %[first], 0")
         e("s_cbranch_scc1 pdtk%=_issued")
         self.tile_dma(0)
         self.tile_dma(1)
         e("s_waitcnt vmcnt(16)")
-        e("s_branch pdtk%=_landed")
+        self.first_step(16)
+        e("s_branch pdtk%=_stepped")
         e("pdtk%=_issued:")
         e("s_waitcnt vmcnt(%[wnx])")
-        e("pdtk%=_landed:")
-        e("s_barrier")
-        for r in self.read_ops(0, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
-                               [(0, i, F0A) for i in range(1, 8)]):
-            e(r)
-        # K-step 0 peeled (its substep-0 MFMAs start every accumulator from C = 0), then two K-steps per
-        # iteration (stage 1, stage 0); s88 = K-steps left including the current one
-        e(f"s_cmp_le_u32 s{S_CNT}, 2")
-        e("s_cbranch_scc1 pdtk%=_first_tail")
-        self.step(0, True, True, 16, first=True)
+        self.first_step("%[wnx]")
+        e("pdtk%=_stepped:")
+        # then two K-steps per iteration (stage 1, stage 0); s88 = K-steps left including the current one
         e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
         e(f"s_cmp_le_u32 s{S_CNT}, 2")
         e("s_cbranch_scc1 pdtk%=_tail1")

@@ -8,15 +8,19 @@
 //
 // Protocol per call (epoch e = host call counter, identical on every rank, never 0):
 //   K1 copy-in   : the local input is stored into this rank's staging slot (e & 1), write-through at
-//                  system scope (sc0 sc1), so no peer can read a stale line from any L2.
-//   K2.. phases  : every block signals barrier b to every peer (system-scope atomic store into the PEER's
-//                  signal block) and waits until every peer signalled b for epoch e in its own block; then
-//                  it reads peers' slots with system-scope (cache-bypassing) loads, reduces in fp32 and
-//                  writes the result.  Signals are idempotent stores of the epoch, so any number of blocks
-//                  may send them and no block depends on another block of its grid (no residency
-//                  assumption).  Waits are bounded: on timeout the block records an error word and leaves.
-//   Slot reuse   : slot (e & 1) is rewritten at call e+2, whose copy-in runs after this rank passed the
-//                  first barrier of call e+1, which every peer signals only after finishing call e.
+//                  system scope (sc0 sc1), so no peer can read a stale line from any L2.  Every block then
+//                  counts itself in (system-scope acq_rel counter); the LAST block alone signals barrier 0 to
+//                  every peer (system-scope atomic store into the PEER's signal block), waits until every peer
+//                  signalled it for epoch e, and publishes stat[0] = e in its own signal block.
+//   K2.. phases  : every block reads stat[b] once (no spinning), then reads peers' slots with system-scope
+//                  (cache-bypassing) loads, reduces in fp32 (fp64 for fp64) and writes the result; a phase that
+//                  produces slot data for a later phase (two-shot) ends with the same last-block barrier.  At
+//                  most ONE wave per rank spins on the mesh, so the collectives never hold CUs that the
+//                  compute stream's GEMMs (one 512-register wave per SIMD) need.  Waits are bounded: on
+//                  timeout the waiter records an error word, stat[b] stays stale and the payload is poisoned.
+//   Slot reuse   : slot (e & 1) is rewritten at call e+2, whose copy-in runs after this rank's payload kernels
+//                  of call e+1, which ran after barrier 0 of e+1 completed -- signalled by every peer only
+//                  after its own call-e kernels (the last readers of our slot e & 1) finished.
 //
 // one-shot all-reduce (latency class: scalars, grad-norm, SyncBN stats): 2 kernels, every rank reads W
 // slots.  two-shot all-reduce (bandwidth class): reduce-scatter phase (rank r reduces chunk r from all
@@ -45,6 +49,8 @@ constexpr int MAXW = 8;
 constexpr int NBAR = 4;
 constexpr int64_t SIG_BYTES = 4096;
 constexpr int ERR_OFF = 1024;         // byte offset of the error word in the signal block
+constexpr int CNT_OFF = 2048;         // uint32 [NBAR]: blocks of the current kernel that arrived (arrive())
+constexpr int STAT_OFF = 3072;        // uint32 [NBAR]: epoch of the last call whose barrier b completed
 constexpr int NT = 256;
 constexpr int SYS = 1 | 16;           // buffer-op cache policy: sc0 | sc1 = system-scope coherent
 
@@ -68,9 +74,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
-// Every block: signal barrier `b` of epoch a.epoch to all peers, then wait for all peers' signals.
-// Returns false (for the whole block) if any wait ran out of budget.
-__device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
+// Signal barrier `b` of epoch a.epoch to every peer, then wait for every peer's signal -- ONE workgroup (lanes
+// t < world) per call: the last block of the kernel that produced this rank's slot data (arrive()), or the
+// barrier kernel.  Success is published as stat[b] = epoch in the own signal block; the payload kernel that
+// follows on the stream reads that word once per block (passed()) instead of spinning, so at most one wave
+// per rank ever spins on the mesh and the rest of the GPU stays with the compute stream.
+__device__ __forceinline__ void mesh_wait(const XArgs& a, int b) {
   __shared__ int timed_out;
   const int t = threadIdx.x;
   if (t == 0) timed_out = 0;
@@ -106,35 +115,67 @@ __device__ __forceinline__ bool mesh_barrier(const XArgs& a, int b) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system-scope acquire (one lane per peer)
   }
   __syncthreads();
-  return timed_out == 0;
+  if (t == 0)
+    __hip_atomic_store((gu32*)(a.buf[a.rank] + STAT_OFF) + b, timed_out ? 0u : a.epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// End of a kernel whose blocks stored this rank's slot data: every block releases its stores and counts itself
+// in; the last one to arrive runs the mesh wait for barrier `b` (and re-arms the counter for the next call).
+__device__ __forceinline__ void arrive(const XArgs& a, int b) {
+  __shared__ unsigned last;
+  // every wave's slot stores acknowledged (a workgroup barrier alone does not wait for other waves' stores)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gu32* cnt = (gu32*)(a.buf[a.rank] + CNT_OFF) + b;
+    const unsigned n = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = n + 1 == gridDim.x;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (last) mesh_wait(a, b);
+}
+
+// did barrier `b` of this call complete (published by the previous kernel on this stream)?
+__device__ __forceinline__ bool passed(const XArgs& a, int b) {
+  __shared__ int ok;
+  if (threadIdx.x == 0)
+    ok = __hip_atomic_load((gu32*)(a.buf[a.rank] + STAT_OFF) + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) ==
+         a.epoch;
+  __syncthreads();
+  return ok != 0;
 }
 
 __device__ __forceinline__ u32x4 poison() { return u32x4{~0u, ~0u, ~0u, ~0u}; }
 
+// 16-B vectors of T, accumulated in A (fp32 for fp32 / bf16, fp64 for fp64)
 template <typename T> struct Acc;
-template <> struct Acc<float> {   // 16 B = 4 fp32
+template <> struct Acc<float> {   // 4 fp32
   static constexpr int N = 4;
-  __device__ static void add(float* acc, const u32x4& v) {
+  typedef float A;
+  __device__ static void add(A* acc, const u32x4& v) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] += __uint_as_float(v[i]);
   }
-  __device__ static u32x4 pack(const float* acc, float s) {
+  __device__ static u32x4 pack(const A* acc, float s) {
     u32x4 r;
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(acc[i] * s);
     return r;
   }
 };
-template <> struct Acc<bf16_t> {  // 16 B = 8 bf16
+template <> struct Acc<bf16_t> {  // 8 bf16
   static constexpr int N = 8;
-  __device__ static void add(float* acc, const u32x4& v) {
+  typedef float A;
+  __device__ static void add(A* acc, const u32x4& v) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       acc[2 * i] += __uint_as_float(v[i] << 16);
       acc[2 * i + 1] += __uint_as_float(v[i] & 0xffff0000u);
     }
   }
-  __device__ static u32x4 pack(const float* acc, float s) {
+  __device__ static u32x4 pack(const A* acc, float s) {
     u32x4 r;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -142,23 +183,62 @@ template <> struct Acc<bf16_t> {  // 16 B = 8 bf16
     return r;
   }
 };
+template <> struct Acc<double> {  // 2 fp64 (SyncBN statistics)
+  static constexpr int N = 2;
+  typedef double A;
+  __device__ static void add(A* acc, const u32x4& v) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[i] += __hiloint2double((int)v[2 * i + 1], (int)v[2 * i]);
+  }
+  __device__ static u32x4 pack(const A* acc, float s) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const double d = acc[i] * (double)s;
+      r[2 * i] = (uint32_t)__double2loint(d);
+      r[2 * i + 1] = (uint32_t)__double2hiint(d);
+    }
+    return r;
+  }
+};
 
-// K1: local input -> own staging slot (write-through, system scope).  `pieces` windows of `pvec` vectors,
-// window p read at src + p * pitch (reduce-scatter chunk), stored back to back in the slot.
-__global__ __launch_bounds__(NT) void xgmi_copy_in_kernel(const u32x4* __restrict__ src, XArgs a, int64_t pvec,
+// 16-B vector i of a payload of `bytes` bytes (the last vector may be partial: latency-class scalars)
+__device__ __forceinline__ u32x4 load_vec(const u32x4* src, int64_t i, int64_t bytes) {
+  if ((i + 1) * 16 <= bytes) return src[i];
+  u32x4 v = u32x4{0u, 0u, 0u, 0u};
+  const unsigned char* b = (const unsigned char*)(src + i);
+  for (int k = 0; k < (int)(bytes - i * 16); ++k) v[k >> 2] |= (unsigned)b[k] << (8 * (k & 3));
+  return v;
+}
+__device__ __forceinline__ void store_vec(u32x4* dst, int64_t i, int64_t bytes, const u32x4& v) {
+  if ((i + 1) * 16 <= bytes) {
+    dst[i] = v;
+    return;
+  }
+  unsigned char* b = (unsigned char*)(dst + i);
+  for (int k = 0; k < (int)(bytes - i * 16); ++k) b[k] = (unsigned char)(v[k >> 2] >> (8 * (k & 3)));
+}
+
+// K1: local input -> own staging slot (write-through, system scope), then barrier 0.  `pieces` windows of
+// `pbytes` bytes, window p read at src + p * pitch (reduce-scatter chunk), stored back to back in the slot
+// (a partial last vector of a single piece is zero-padded).
+__global__ __launch_bounds__(NT) void xgmi_copy_in_kernel(const u32x4* __restrict__ src, XArgs a, int64_t pbytes,
                                                           int pieces, int64_t pitch) {
+  const int64_t pvec = (pbytes + 15) / 16;
   const __amdgpu_buffer_rsrc_t dst = rsrc_of(slot_of(a, a.rank), pvec * pieces * 16);
   for (int p = 0; p < pieces; ++p)
     for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < pvec; i += (int64_t)gridDim.x * NT)
-      __builtin_amdgcn_raw_buffer_store_b128(src[p * pitch + i], dst, (int)((p * pvec + i) * 16), 0, SYS);
+      __builtin_amdgcn_raw_buffer_store_b128(load_vec(src + p * pitch, i, pbytes), dst, (int)((p * pvec + i) * 16),
+                                             0, SYS);
+  arrive(a, 0);
 }
 
 // sum over ranks of vector i of every peer slot, starting at byte offset `off`
 template <typename T>
 __device__ __forceinline__ u32x4 reduce_vec(const __amdgpu_buffer_rsrc_t* src, int world, int64_t byte, float s) {
-  float acc[Acc<T>::N];
+  typename Acc<T>::A acc[Acc<T>::N];
 #pragma unroll
-  for (int k = 0; k < Acc<T>::N; ++k) acc[k] = 0.f;
+  for (int k = 0; k < Acc<T>::N; ++k) acc[k] = 0;
   u32x4 v[MAXW];
 #pragma unroll
   for (int p = 0; p < MAXW; ++p)   // all W loads in flight before the first add (one xGMI round trip)
@@ -174,25 +254,26 @@ __device__ __forceinline__ void peer_rsrcs(const XArgs& a, int64_t bytes, __amdg
   for (int p = 0; p < MAXW; ++p) r[p] = rsrc_of(slot_of(a, p < a.world ? p : 0), bytes);
 }
 
-// one-shot all-reduce: out[i] = s * sum_p slot_p[i]
-template <typename T>
+// one-shot all-reduce: out = s * sum_p slot_p (payload of `bytes` bytes, any size)
 // root >= 0: reduce to one rank (ZeRO-2 reduce-to-owner): the others only take part in the barrier.
-__global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __restrict__ out, int64_t nvec, float s,
+template <typename T>
+__global__ __launch_bounds__(NT) void xgmi_allreduce_kernel(XArgs a, u32x4* __restrict__ out, int64_t bytes, float s,
                                                             int root) {
-  const bool ok = mesh_barrier(a, 0);
+  const bool ok = passed(a, 0);
   if (root >= 0 && a.rank != root) return;
+  const int64_t nvec = (bytes + 15) / 16;
   __amdgpu_buffer_rsrc_t src[MAXW];
   peer_rsrcs(a, nvec * 16, src);
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT)
-    out[i] = ok ? reduce_vec<T>(src, a.world, i * 16, s) : poison();
+    store_vec(out, i, bytes, ok ? reduce_vec<T>(src, a.world, i * 16, s) : poison());
 }
 
 // two-shot phase 1 / reduce_scatter: chunk `rank` (cvec vectors) reduced from every peer.
-//   to_slot: write into own staging chunk (phase 1 of two-shot) instead of `out`.
+//   to_slot: write into own staging chunk (phase 1 of two-shot, then barrier 1) instead of `out`.
 template <typename T>
 __global__ __launch_bounds__(NT) void xgmi_reduce_chunk_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, float s,
                                                               int to_slot) {
-  const bool ok = mesh_barrier(a, 0);
+  const bool ok = passed(a, 0);
   const int64_t total = cvec * a.world;
   __amdgpu_buffer_rsrc_t src[MAXW];
   peer_rsrcs(a, total * 16, src);
@@ -203,14 +284,17 @@ __global__ __launch_bounds__(NT) void xgmi_reduce_chunk_kernel(XArgs a, u32x4* _
     if (to_slot) __builtin_amdgcn_raw_buffer_store_b128(v, mine, (int)((base + i) * 16), 0, SYS);
     else out[i] = v;
   }
+  if (to_slot) arrive(a, 1);
 }
 
 // all-gather: out[p * pitch + i] = chunk p of peer p's slot (chunk_in_slot: peer p keeps its piece at
-// chunk p of its slot (two-shot phase 2) or at offset 0 (all_gather of a shard))
+// chunk p of its slot (two-shot phase 2) or at offset 0 (all_gather of a shard)).  Block g starts at peer
+// rank + g: concurrent blocks pull from different peers, so all links carry traffic at once.
 __global__ __launch_bounds__(NT) void xgmi_gather_kernel(XArgs a, u32x4* __restrict__ out, int64_t cvec, int64_t pitch,
                                                          int bar, int chunk_in_slot) {
-  const bool ok = mesh_barrier(a, bar);
-  for (int p = 0; p < a.world; ++p) {
+  const bool ok = passed(a, bar);
+  for (int j = 0; j < a.world; ++j) {
+    const int p = (a.rank + (int)blockIdx.x + j) % a.world;
     const int64_t off = chunk_in_slot ? (int64_t)p * cvec : 0;
     const __amdgpu_buffer_rsrc_t src = rsrc_of(slot_of(a, p), (off + cvec) * 16);
     for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < cvec; i += (int64_t)gridDim.x * NT)
@@ -219,7 +303,7 @@ __global__ __launch_bounds__(NT) void xgmi_gather_kernel(XArgs a, u32x4* __restr
   }
 }
 
-__global__ void xgmi_barrier_kernel(XArgs a) { (void)mesh_barrier(a, 3); }
+__global__ void xgmi_barrier_kernel(XArgs a) { mesh_wait(a, 3); }
 
 // Communication kernels share the GPU with the compute stream: a modest grid (<= 128 blocks of 256
 // lanes, half a block per CU) keeps enough 16-B loads in flight to saturate the links while leaving most
@@ -304,18 +388,22 @@ PDT_API int pdt_xgmi_wallclock_khz() { return wallclock_khz(); }
 
 // kind: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter, 4 barrier,
 //       5 reduce to root (root rank passed as pitch_bytes / 16).
-//   bytes: all-reduce: the whole payload (two-shot: multiple of 16 * world); all-gather / reduce-scatter:
-//          ONE rank's piece (a multiple of 16).
+//   bytes: all-reduce: the whole payload (one-shot / reduce: any size; two-shot: multiple of 16 * world);
+//          all-gather / reduce-scatter: ONE rank's piece (a multiple of 16).
 //   pitch_bytes: all-gather: distance between consecutive peers' pieces in `out`; reduce-scatter: distance
 //          between consecutive pieces in `in` (both = bytes for a contiguous tensor).
+//   dtype: fp32 / bf16 (fp32 accumulation) or fp64 (one-shot / reduce only: SyncBN statistics).
 //   scale multiplies reduced values (1/world = AVG).
 PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t bytes, int64_t pitch_bytes, int dtype,
                                 float scale, const void* const* bufs, int rank, int world, unsigned epoch,
                                 int64_t slot_bytes, unsigned timeout_us, unsigned* host_err, hipStream_t s) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || epoch == 0) return (int)hipErrorInvalidValue;
-  if (bytes % 16 != 0 || pitch_bytes % 16 != 0 || (dtype != kF32 && dtype != kBF16)) return (int)hipErrorInvalidValue;
+  const bool any_size = kind == 0 || kind == 5;
+  if ((!any_size && bytes % 16 != 0) || pitch_bytes % 16 != 0 || bytes < 0) return (int)hipErrorInvalidValue;
+  if (kind != 4 && dtype != kF32 && dtype != kBF16 && !(dtype == kF64 && any_size)) return (int)hipErrorInvalidValue;
   if (slot_bytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;   // 32-bit buffer offsets
-  const int64_t staged = kind == 3 ? bytes * world : bytes;
+  const int64_t padded = (bytes + 15) / 16 * 16;
+  const int64_t staged = kind == 3 ? bytes * world : padded;
   if (staged > slot_bytes) return (int)hipErrorInvalidValue;
   XArgs a{};
   for (int p = 0; p < world; ++p) a.buf[p] = (char*)bufs[p];
@@ -329,20 +417,22 @@ PDT_API int pdt_xgmi_collective(int kind, const void* in, void* out, int64_t byt
     hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, s, a);
     return (int)hipGetLastError();
   }
-  const int64_t nvec = bytes / 16, pitch = pitch_bytes / 16;
+  const int64_t nvec = padded / 16, pitch = pitch_bytes / 16;
+  // copy-in; its last block runs barrier 0
   if (kind == 3)
-    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec * world)), dim3(NT), 0, s, (const u32x4*)in, a, nvec,
+    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec * world)), dim3(NT), 0, s, (const u32x4*)in, a, bytes,
                        world, pitch);
   else
-    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, (const u32x4*)in, a, nvec, 1,
+    hipLaunchKernelGGL(xgmi_copy_in_kernel, dim3(grid_of(nvec)), dim3(NT), 0, s, (const u32x4*)in, a, bytes, 1,
                        (int64_t)0);
-  const bool bf = dtype == kBF16;
+  const bool bf = dtype == kBF16, f64 = dtype == kF64;
   switch (kind) {
     case 0:
     case 5: {
       const int root = kind == 5 ? (int)(pitch_bytes / 16) : -1;   // reduce: pitch carries the root rank
-      if (bf) hipLaunchKernelGGL(xgmi_allreduce_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, root);
-      else hipLaunchKernelGGL(xgmi_allreduce_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, nvec, scale, root);
+      if (bf) hipLaunchKernelGGL(xgmi_allreduce_kernel<bf16_t>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, bytes, scale, root);
+      else if (f64) hipLaunchKernelGGL(xgmi_allreduce_kernel<double>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, bytes, scale, root);
+      else hipLaunchKernelGGL(xgmi_allreduce_kernel<float>, dim3(grid_of(nvec)), dim3(NT), 0, s, a, (u32x4*)out, bytes, scale, root);
       break;
     }
     case 1: {

@@ -217,11 +217,11 @@ def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None, b
 
 
 def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:
-    """Select the flash-attention kernel generation (0 keeps the current choice, -1 restores the default).
-    fwd: 2 register-staged, 3 LDS-DMA ring, 4 VALU-lean LDS-DMA, 5 (default) v4 + deferred rescale + read
-    prefetch + 16-B epilogue, 7 / 8 v5's tile on 8-wave 256-row workgroups (3- / 2-deep ring).  bwd: 1 baseline, 2 LDS-DMA, 3 hand-pipelined dK/dV + dQ (v3; default at head dim
-    64), 8 / 9 dK/dV v3 + dQ v4 (8-wave 256-row workgroups, 3- / 2-deep ring; 9 is the default at head dim
-    128), 10 dK/dV v5 (3-deep ring) + dQ v4.  Returns the pinned (fwd, bwd) pair (0 = default)."""
+    """Select the flash-attention kernels (0 keeps the current choice, -1 restores the default).
+    fwd: 5 (default) 4 waves x 32 query rows per workgroup; 7 / 8 the same tile on 8-wave 256-row workgroups
+    (3- / 2-deep LDS ring).  bwd (dQ kernel; dK/dV is always v3): 9 dQ v4 on 8-wave 256-row workgroups with a
+    2-deep ring (default at head dim 128), 8 the same with a 3-deep ring, 3 dQ v3 on 4-wave 128-row workgroups
+    (default at head dim 64).  Returns the pinned (fwd, bwd) pair (0 = default)."""
     r = _lib.require().pdt_flash_attn_set_variant(int(fwd), int(bwd))
     return r // 32, r % 32
 

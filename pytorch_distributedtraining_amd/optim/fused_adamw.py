@@ -60,14 +60,40 @@ class FusedAdamW(Optimizer):
         return ds
 
     def zero_grad(self, set_to_none: bool = True):
-        """torch semantics for ``.grad``; engine-owned flat gradients (``_pdt_zero_grad``: DDP's
-        compute-dtype mode, where autograd accumulates into the bucket views) are zeroed in place."""
-        super().zero_grad(set_to_none)
+        """torch semantics for ``.grad``, except for engine-owned flat gradients: DDP's compute-dtype masters
+        (``_pdt_zero_grad``) and parameters whose ``.grad`` is still a view of a DDP bucket flat
+        (``_pdt_grad_flat``) get their flat zeroed in place -- ONE fill per flat instead of a None per
+        parameter that the next forward would re-attach view by view (ResNet-50: 161 views, a host gap at
+        every step start), so those gradients read as zeros rather than None."""
+        flats, rest = {}, []
         for group in self.param_groups:
             for p in group["params"]:
                 zero = getattr(p, "_pdt_zero_grad", None)
                 if zero is not None:
-                    zero()
+                    flats[id(zero)] = zero
+                    continue
+                g = p.grad
+                if g is None:
+                    continue
+                f = getattr(p, "_pdt_grad_flat", None)
+                if f is not None and g._base is f:
+                    flats[id(f)] = f.zero_
+                    continue
+                rest.append(p)
+        for zero in flats.values():
+            zero()
+        if set_to_none:
+            for p in rest:
+                p.grad = None
+        elif rest:
+            grads = []
+            for p in rest:
+                if p.grad.grad_fn is not None:
+                    p.grad.detach_()
+                else:
+                    p.grad.requires_grad_(False)
+                grads.append(p.grad)
+            torch._foreach_zero_(grads)
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -99,7 +125,11 @@ class FusedAdamW(Optimizer):
             # torch.amp.GradScaler skips optimizer.step() entirely.  With a device flag the count lives on the
             # device and advances conditionally (pdt_step_inc), so no host sync is needed; once a group has a
             # device count it keeps it (mixing the two counters would double-count).
-            dev_step = cap or gi in self._dsteps or (found_inf is not None and found_inf.device.type == "cuda")
+            # GPU parameters always count on the device: one step_inc launch per group instead of a host tensor
+            # add + .item() per parameter (161 of them for ResNet-50: ~1 ms of host time per step, a GPU-idle gap
+            # in front of the AdamW launch -- profiles/r3_s4h_resnet50-ddp_kernel_table.txt)
+            on_gpu = bool(group["params"]) and group["params"][0].device.type == "cuda"
+            dev_step = cap or on_gpu or gi in self._dsteps or (found_inf is not None and found_inf.device.type == "cuda")
             if found_inf is not None and found_inf.device.type != "cuda" and int(found_inf.reshape(-1)[0]) != 0:
                 continue
             dstep = None

@@ -130,8 +130,8 @@ class Comm:
 
     def _xgmi_ok(self, t, kind="all_reduce") -> bool:
         x = self.xgmi
-        return (x is not None and t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
-                and x.eligible(t.numel() * t.element_size(), kind))
+        return (x is not None and t.is_cuda and t.is_contiguous()
+                and x.eligible(t.numel() * t.element_size(), kind, t.dtype))
 
     # ------------------------------------------------------------------ helpers
     @property

@@ -127,6 +127,7 @@ class _FlatGroup:
             o = self.offset_of[li]
             # same strides as the parameter (channels_last convs): autograd accumulates in place
             p.grad = _pview(self.flat_grad, p, o)
+            p._pdt_grad_flat = self.flat_grad   # FusedAdamW.zero_grad zeroes the flat once, views stay attached
 
 
 def _cast_except_batchnorm(module: nn.Module, dtype: torch.dtype) -> None:

@@ -99,7 +99,7 @@ def _sync_bn_reference(x, weight, bias, running_mean, running_var, eps, momentum
         return torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, False, 0.0, eps)
     xf = x.float()
     local = torch.cat([xf.sum(dims).double(), (xf * xf).sum(dims).double(),
-                       torch.tensor([x.numel() / C], dtype=torch.float64)])
+                       torch.tensor([x.numel() / C], dtype=torch.float64, device=x.device)])
     stats = local.clone()
     if comm.world_size > 1:
         stats = _AllReduceSum.apply(local, comm)

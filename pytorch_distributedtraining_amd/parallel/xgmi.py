@@ -4,7 +4,8 @@ Every rank allocates ONE symmetric HBM buffer ([4 KB signals][staging slot 0][st
 it with ``hipIpcGetMemHandle`` and maps every peer's buffer with ``hipIpcOpenMemHandle`` -- the handles
 are exchanged once through the existing c10d process group (TCPStore bootstrap).  The
 collectives are HIP kernels in ``csrc/kernels/xgmi_comm.hip`` that read peers' staging slots directly
-(system-scope, cache-bypassing loads) after a bounded mesh barrier:
+(system-scope, cache-bypassing loads) after a bounded mesh barrier that ONE workgroup per rank waits in (the
+last block of the copy-in kernel; the payload kernels read its published result and never spin):
 
   * ``all_reduce``   one-shot (<= ``oneshot_max_bytes``: grad-norm / found_inf scalars, loss sync,
                      SyncBN statistics -- latency class) or two-shot (reduce-scatter + all-gather phases:
@@ -23,8 +24,8 @@ Failure is loud: a mesh wait longer than ``timeout_us`` (wall clock, s_memrealti
 kernel poison its output with NaN and set a host-mapped error word; ``raise_if_failed()`` (called by every engine at its end-of-backward and
 optimizer sync points through ``Comm.check_errors``) reads that word without synchronising and raises.
 
-``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes every eligible CUDA collective here (fp32/bf16, sizes a
-multiple of 16 B, world <= 8); ``PDT_XGMI=auto`` routes by SIZE CLASS: payloads in
+``Comm(xgmi=True)`` (or ``PDT_XGMI=1``) routes every eligible CUDA collective here (all_reduce / reduce: fp32,
+bf16 or fp64 of any size; all_gather / reduce_scatter: fp32 / bf16 pieces of a multiple of 16 B; world <= 8); ``PDT_XGMI=auto`` routes by SIZE CLASS: payloads in
 [``min_bytes``, ``max_bytes``] -- by default the latency class up to 1 MiB (grad-norm / found_inf scalars,
 SyncBN statistics, loss sync, small first buckets), where the one-shot mesh kernel is one barrier and one
 read of every peer -- go to the mesh, everything else stays on RCCL's pipelined rings
@@ -46,8 +47,8 @@ MAX_WORLD = 8
 
 
 class SizeClass:
-    """Which payloads the mesh takes: [min_bytes, max_bytes] (None = unbounded), sizes a multiple of 16 B.
-    Pure function of the size, so every rank of a collective routes it the same way."""
+    """Which payloads the mesh takes: [min_bytes, max_bytes] (None = unbounded).  Pure function of the size, so
+    every rank of a collective routes it the same way."""
 
     def __init__(self, min_bytes: int = 0, max_bytes: int | None = None):
         if min_bytes < 0 or (max_bytes is not None and max_bytes < min_bytes):
@@ -55,8 +56,7 @@ class SizeClass:
         self.min_bytes, self.max_bytes = int(min_bytes), max_bytes
 
     def __call__(self, nbytes: int) -> bool:
-        return (nbytes > 0 and nbytes % 16 == 0 and nbytes >= self.min_bytes
-                and (self.max_bytes is None or nbytes <= self.max_bytes))
+        return nbytes > 0 and nbytes >= self.min_bytes and (self.max_bytes is None or nbytes <= self.max_bytes)
 
     def __repr__(self):
         return f"SizeClass({self.min_bytes}, {self.max_bytes})"
@@ -111,8 +111,14 @@ class XGMIComm:
         comm.barrier()
 
     # ------------------------------------------------------------------ eligibility
-    def eligible(self, nbytes: int, kind: str = "all_reduce") -> bool:
-        """fp32/bf16 payloads that are a multiple of 16 B inside the size class (larger ones are chunked)."""
+    def eligible(self, nbytes: int, kind: str = "all_reduce", dtype=None) -> bool:
+        """Payloads inside the size class (larger than a slot: chunked).  all_reduce / reduce: fp32, bf16 or fp64,
+        any size (a 4-byte grad-norm scalar, fp64 SyncBN statistics); all_gather / reduce_scatter: fp32 / bf16
+        pieces that are a multiple of 16 B."""
+        if dtype is not None and dtype not in (torch.float32, torch.bfloat16, torch.float64):
+            return False
+        if kind in ("all_gather", "reduce_scatter") and (nbytes % 16 or dtype == torch.float64):
+            return False
         return self.size_class(nbytes)
 
     # ------------------------------------------------------------------ launch
@@ -157,14 +163,15 @@ class XGMIComm:
             raise ValueError(f"xGMI all_reduce supports sum/avg, got {op}")
         t = self._flat(t)
         nbytes = t.numel() * t.element_size()
-        if not self.eligible(nbytes):
-            raise ValueError(f"xGMI all_reduce: {nbytes} B not eligible")
+        if not self.eligible(nbytes, "all_reduce", t.dtype):
+            raise ValueError(f"xGMI all_reduce: {nbytes} B of {t.dtype} not eligible")
         scale = 1.0 / self.world if op == "avg" else 1.0
         base = t.data_ptr()
 
         def launch():
-            if nbytes <= self.oneshot_max_bytes:
-                self._run("allreduce1", base, base, nbytes, 0, t.dtype, scale)
+            if nbytes <= self.oneshot_max_bytes or t.dtype == torch.float64:
+                for o in range(0, nbytes, self.slot_bytes):     # fp64: one-shot windows (no two-shot kernels)
+                    self._run("allreduce1", base + o, base + o, min(self.slot_bytes, nbytes - o), 0, t.dtype, scale)
                 return
             q = 16 * self.world
             main = (nbytes // q) * q
@@ -172,7 +179,7 @@ class XGMIComm:
             for o in range(0, main, step):
                 c = min(step, main - o)
                 self._run("allreduce2", base + o, base + o, c, 0, t.dtype, scale)
-            if main < nbytes:    # < 16 * world bytes left: latency-class one-shot
+            if main < nbytes:    # < 16 * world bytes left: latency-class one-shot (any size)
                 self._run("allreduce1", base + main, base + main, nbytes - main, 0, t.dtype, scale)
         return self._issue([t], launch, async_op)
 
@@ -183,7 +190,7 @@ class XGMIComm:
             raise ValueError(f"xGMI reduce supports sum/avg, got {op}")
         t = self._flat(t)
         nbytes = t.numel() * t.element_size()
-        if not self.eligible(nbytes) or not 0 <= dst < self.world:
+        if not self.eligible(nbytes, "reduce", t.dtype) or not 0 <= dst < self.world:
             raise ValueError(f"xGMI reduce: {nbytes} B / dst {dst} not eligible")
         scale = 1.0 / self.world if op == "avg" else 1.0
         base = t.data_ptr()
@@ -197,7 +204,8 @@ class XGMIComm:
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> torch.cuda.Event:
         inp, out = self._flat(inp), self._flat(out)
         nbytes = inp.numel() * inp.element_size()
-        if out.numel() != inp.numel() * self.world or out.dtype != inp.dtype or not self.eligible(nbytes):
+        if (out.numel() != inp.numel() * self.world or out.dtype != inp.dtype
+                or not self.eligible(nbytes, "all_gather", inp.dtype)):
             raise ValueError("xGMI all_gather: bad sizes")
         src, dst = inp.data_ptr(), out.data_ptr()
 
@@ -211,7 +219,8 @@ class XGMIComm:
                        async_op: bool = False) -> torch.cuda.Event:
         inp, out = self._flat(inp), self._flat(out)
         nbytes = out.numel() * out.element_size()          # one rank's piece
-        if inp.numel() != out.numel() * self.world or out.dtype != inp.dtype or not self.eligible(nbytes):
+        if (inp.numel() != out.numel() * self.world or out.dtype != inp.dtype
+                or not self.eligible(nbytes, "reduce_scatter", inp.dtype)):
             raise ValueError("xGMI reduce_scatter: bad sizes")
         scale = 1.0 / self.world if op == "avg" else 1.0
         src, dst = inp.data_ptr(), out.data_ptr()

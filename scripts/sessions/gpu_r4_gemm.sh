@@ -11,4 +11,8 @@ rc=$?; echo "check rc=$rc"; cat $OUT/check.jsonl; tail -5 $OUT/check.err
 echo "=== bench"; date
 MODE=bench ROUNDS=${ROUNDS:-5} timeout -k 10 500 python -u scripts/bench_gemm_asm.py > $OUT/bench.jsonl 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.jsonl; tail -5 $OUT/bench.err
+[ $rc -eq 0 ] || exit $rc
+echo "=== stamps"; date
+timeout -k 10 200 python -u scripts/gemm_stamps.py > $OUT/stamps.jsonl 2> $OUT/stamps.err
+rc=$?; echo "stamps rc=$rc"; cat $OUT/stamps.jsonl; tail -3 $OUT/stamps.err
 exit $rc

@@ -217,8 +217,18 @@ def test_xgmi_size_class_routing_policy():
     kw = xgmi_kwargs({"PDT_XGMI": "auto", "PDT_XGMI_MIN_KB": "4", "PDT_XGMI_MAX_KB": "256"})
     sc = SizeClass(kw["min_bytes"], kw["max_bytes"])
     assert not sc(1024) and sc(4096) and sc(256 << 10) and not sc((256 << 10) + 16)
-    assert not sc(4096 + 8)                       # the mesh kernels move 16-byte vectors
+    assert sc(4096 + 8) and SizeClass()(4)        # any size: the kernels zero-pad a partial last 16-B vector
     assert SizeClass()(16) and SizeClass()(1 << 30) and not SizeClass()(0)
+    # the latency-class payloads the reference issues every step reach the mesh: the 4-byte grad-norm /
+    # found_inf / loss scalars (fp32) and fp64 SyncBN statistics; gathers / scatters keep 16-byte pieces
+    from types import SimpleNamespace
+    from pytorch_distributedtraining_amd.parallel.xgmi import XGMIComm
+    x = SimpleNamespace(size_class=SizeClass(0, 1 << 20))
+    el = XGMIComm.eligible
+    assert el(x, 4, "all_reduce", torch.float32) and el(x, 2 * 8 * 64, "all_reduce", torch.float64)
+    assert el(x, 6, "reduce", torch.bfloat16)
+    assert not el(x, 8, "all_gather", torch.float32) and not el(x, 16, "all_gather", torch.float64)
+    assert not el(x, 16, "all_reduce", torch.int64) and not el(x, 2 << 20, "all_reduce", torch.float32)
     with pytest.raises(ValueError):
         SizeClass(100, 10)
 

@@ -173,3 +173,57 @@ def test_xgmi_size_class_routes_small_to_mesh_and_bulk_to_backend():
     for mesh_small, mesh_big, s, b0, b1 in run_workers(_size_class_worker, 2):
         assert mesh_small == 1 and mesh_big == 0
         assert s == exp and b0 == exp and b1 == exp
+
+
+def _trainer_latency_worker(rank, world):
+    """One Stoke-facade step with the reference's per-step small collectives (Stoke-DDP.py:76,86 loss / EMA
+    sync, :192 SyncBN statistics, :253 grad-norm clip with AMP's found_inf) under the PDT_XGMI=auto policy
+    (1 MiB latency class): each must be carried by the mesh, not fall back to the c10d backend."""
+    import torch.nn as nn
+    from pytorch_distributedtraining_amd.parallel import Comm
+    from pytorch_distributedtraining_amd.trainer import ClipGradNormConfig, DDPConfig, StokeOptimizer, Trainer
+    torch.cuda.set_device(0)
+    comm = Comm(xgmi=False)
+    x = comm.enable_xgmi(slot_bytes=1 << 20, max_bytes=1 << 20)
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1, bias=False), nn.BatchNorm2d(8), nn.ReLU(),
+                          nn.Conv2d(8, 3, 3, padding=1))
+    opt = StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs={"lr": 1e-3})
+    # the reference's combination (Stoke-DDP.py:246-252): DDP + OSS + ShardedDDP, so the clip norm is a sum over
+    # the ranks' optimizer shards (a plain DDP replica's norm needs no collective)
+    t = Trainer(model, opt, nn.MSELoss(), batch_size_per_device=2, grad_clip=ClipGradNormConfig(0.1, 2.0),
+                gpu=True, fp16="amp", distributed="ddp", fairscale_oss=True, fairscale_sddp=True, comm=comm,
+                configs=[DDPConfig(local_rank=rank, convert_to_sync_batch_norm=True)], verbose=False)
+    g = torch.Generator().manual_seed(rank)
+    xb, yb = torch.randn(2, 3, 8, 8, generator=g).cuda(), torch.randn(2, 3, 8, 8, generator=g).cuda()
+    calls = {}
+    c = x.calls
+    out = t.model(xb)
+    calls["syncbn_fwd"], c = x.calls - c, x.calls
+    loss = t.loss(out, yb)
+    t.backward(loss)
+    calls["backward"], c = x.calls - c, x.calls
+    t.step()
+    calls["clip_found_inf"], c = x.calls - c, x.calls
+    synced = t.detach_and_sync_loss(loss)
+    calls["loss_lazy"], c = x.calls - c, x.calls
+    v = float(synced)
+    calls["loss_read"] = x.calls - c
+    torch.cuda.synchronize()
+    comm.check_errors()
+    params = torch.cat([p.detach().float().flatten().cpu() for p in t.model_access.parameters()])
+    local = float(loss.detach())
+    comm.barrier()
+    x.close()
+    return calls, v, local, params
+
+
+def test_xgmi_carries_the_per_step_latency_collectives():
+    outs = run_workers(_trainer_latency_worker, 2)
+    for calls, v, _, _ in outs:
+        assert calls["syncbn_fwd"] >= 1, calls          # fp64 statistics (2C+1 doubles: not a 16-B multiple)
+        assert calls["backward"] >= 1, calls            # SyncBN backward sums (fp64)
+        assert calls["clip_found_inf"] >= 1, calls      # 4-byte norm / found_inf scalars
+        assert calls["loss_lazy"] == 0 and calls["loss_read"] == 1, calls
+        assert abs(v - (outs[0][2] + outs[1][2]) / 2) < 1e-5 * max(1.0, abs(v))
+    assert torch.equal(outs[0][3], outs[1][3])          # replicas agree after the step
