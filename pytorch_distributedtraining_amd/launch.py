@@ -79,8 +79,11 @@ def visible_gpu_count() -> int | None:
 
 def _shared_gpu_queues(nproc: int) -> str | None:
     """GPU_MAX_HW_QUEUES for ranks that must share GPUs (more ranks than devices: one-GPU rehearsals), keeping
-    <= 8 HIP hardware queues per GPU (each rank's compute, comm and copy streams).  One rank per GPU keeps
-    HIP's default.  Counted by ``visible_gpu_count`` (no HIP initialisation in the launcher)."""
+    <= 8 HIP hardware queues per GPU (each rank's compute, comm and copy streams) -- less queue contention,
+    not a correctness requirement: since the xGMI collectives wait in ONE wave per rank, the world-4 one-GPU
+    GPT-2 1.3B rehearsal passes with HIP's default 4 queues per rank
+    (profiles/r4/r4_rehearsal_gpt2_fsdp_w4_q4_one_waiter.log).  One rank per GPU keeps HIP's default.  Counted
+    by ``visible_gpu_count`` (no HIP initialisation in the launcher)."""
     ndev = visible_gpu_count()
     if ndev is None or not 0 < ndev < nproc:
         return None
