@@ -90,6 +90,14 @@ __device__ __forceinline__ u16x8 pack8(const f32x16& x, int s) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): the softmax math of two accumulator registers per
+// instruction -- an f32x16 tile's registers r, r + 1 (r even) are an aligned VGPR pair, so no moves are needed.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 pair(const f32x16& t, int r) { return f32x2{t[r], t[r + 1]}; }
+__device__ __forceinline__ f32x2 bcast(float x) { return f32x2{x, x}; }
+__device__ __forceinline__ f32x2 exp2_2(f32x2 x) { return f32x2{fast_exp2(x[0]), fast_exp2(x[1])}; }
+
 struct AttnParams {
   const bf16_t* q; const bf16_t* k; const bf16_t* v;
   bf16_t* o; float* lse;
@@ -114,6 +122,8 @@ struct AttnParams {
   // the dO fragments it holds anyway) and writes them for the dK/dV kernel, which then runs after it -- no
   // separate delta pass re-reading O and dO
   int fuse_delta;
+  // A/B switch (PDT_FA_MASK_ALL=1): every backward tile takes the masked path (the pre-dispatch code)
+  int mask_all;
 };
 
 // delta of this lane's query row from its dO fragments (gf, already in registers) and the O row; written with
@@ -474,7 +484,7 @@ struct FwdV5 {
     }
     float mx = fmaxf(s[0][0], s[1][0]);
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));   // v_max3_f32 chain
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
     if (!__all(mx <= m + RESCALE_THR)) {   // some row's max ran past the deferred reference: move it
       const float mn = fmaxf(m, mx);
@@ -487,19 +497,23 @@ struct FwdV5 {
       m = mn;
     }
     const float msub = (m == -INFINITY) ? 0.f : m;
-    float ls = 0.f;
+    // p = exp2(s * scale * log2e - m), two registers per packed FMA / add (row sums in two partial lanes)
+    f32x2 ls2 = bcast(0.f);
+    const f32x2 sc2 = bcast(sl2), ms2 = bcast(-msub);
     u16x8 pf[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s[t][r] = fast_exp2(fmaf(s[t][r], sl2, -msub));
-        ls += s[t][r];
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 pv = exp2_2(pk_fma(pair(s[t], r), sc2, ms2));
+        s[t][r] = pv[0];
+        s[t][r + 1] = pv[1];
+        ls2 += pv;
       }
       pf[t][0] = pack8(s[t], 0);
       pf[t][1] = pack8(s[t], 1);
     }
-    l += ls;
+    l += ls2[0] + ls2[1];
     constexpr int NV = 4 * DT;   // PV steps: (dt, kt, ss)
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -799,7 +813,7 @@ struct BwdKVTile {
   static constexpr int KS = D / 16, DT = D / 32;
   static constexpr int EA = 16 / KS;        // softmax elements finished per stage-A step
   static constexpr int EB = 16 / (2 * DT);  // ... per stage-B step (== EA since KS == 2 DT)
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  static_assert(EA % 2 == 0, "packed softmax pairs");
 
   // Q / dO row fragment of step i (subtile i / KS, k-step i % KS)
   __device__ __forceinline__ static u16x8 rowf(const bf16_t* base, const int (&roff)[KS], int i) {
@@ -810,18 +824,20 @@ struct BwdKVTile {
     const int o = (qs * 32 + 16 * (j & 1)) * D;
     return tr_pair(base + toff[j >> 1][0] + o, base + toff[j >> 1][1] + o);
   }
-  // softmax-gradient of accumulator registers [e0, e0 + N) of one 32-row subtile:
+  // softmax-gradient of accumulator registers [e0, e0 + N) of one 32-row subtile (scalar: the packed form
+  // produced wrong dK / dV at one wave per SIMD -- an MFMA-result hazard on v_pk_* reads, not chased further):
   //   p = exp2(s * scale*log2e - lse*log2e),  dS = p * (dP - delta)
-  template <int N>
+  // MASK (wave-uniform: the tile crosses the causal diagonal) selects the masked rows; query rows past Sq
+  // arrive as zero Q / dO rows (buffer range check), which contribute exactly 0 to dK (dS * q) and dV (p * dO)
+  // without masking
+  template <int N, bool MASK>
   __device__ __forceinline__ static void smx(f32x16& sv, f32x16& dpv, int e0, const float* nl, const float* dl, float sl2,
                                              int qs, int tmask, int tsq) {
 #pragma unroll
     for (int e = 0; e < N; ++e) {
       const int r = e0 + e, rr = (r & 3) + 8 * (r >> 2) + 32 * qs;
       float pv = fast_exp2(fmaf(sv[r], sl2, nl[e]));
-      // causal mask only: query rows past Sq arrive as zero Q / dO rows (buffer range check), which
-      // contribute exactly 0 to dK (dS * q) and dV (p * dO) without masking
-      if constexpr (CAUSAL) pv = rr < tmask ? 0.f : pv;
+      if constexpr (MASK) pv = rr < tmask ? 0.f : pv;
       sv[r] = pv;
       dpv[r] = pv * (dpv[r] - dl[e]);
     }
@@ -841,7 +857,8 @@ struct BwdKVTile {
   //   stage A (2*KS steps): S / dP chains of subtiles 0 and 1; subtile 0's softmax under subtile 1's chain
   //   stage B (2*DT steps): dV/dK += subtile 0;                   subtile 1's softmax under it
   //   stage C (2*DT steps): dV/dK += subtile 1
-  // Ls holds -lse*log2(e) rows, Ds delta rows.  Masking is branch-free (select) on every tile.
+  // Ls holds -lse*log2(e) rows, Ds delta rows.  MASK: the tile crosses the causal diagonal (selects on its rows).
+  template <bool MASK>
   __device__ __forceinline__ static void run(const bf16_t* Qs, const bf16_t* Gs, const float* Ls, const float* Ds,
                                              const u16x8 (&kf)[KS], const u16x8 (&vf)[KS], const int (&roff)[KS],
                                              const int (&toff)[DT][2], f32x16 (&dk)[DT], f32x16 (&dv)[DT], float sl2,
@@ -867,7 +884,7 @@ struct BwdKVTile {
         float nn[EA], dd[EA];
         if (ks + 1 < KS) ldstat<EA>(Ls, Ds, (ks + 1) * EA, 0, h, nn, dd);
         else ldstat<EA>(Ls, Ds, 0, 1, h, nn, dd);   // EA == EB: first stage-B slice
-        smx<EA>(s[0], dp[0], ks * EA, nl, dl, sl2, 0, tmask, tsq);
+        smx<EA, MASK>(s[0], dp[0], ks * EA, nl, dl, sl2, 0, tmask, tsq);
 #pragma unroll
         for (int e = 0; e < EA; ++e) { nl[e] = nn[e]; dl[e] = dd[e]; }
       }
@@ -886,7 +903,7 @@ struct BwdKVTile {
       mfma32_acc(dk[j >> 1], tb, df[0][j & 1]);
       float nn[EB], dd[EB];
       if (j + 1 < 2 * DT) ldstat<EB>(Ls, Ds, (j + 1) * EB, 1, h, nn, dd);
-      smx<EB>(s[1], dp[1], j * EB, nl, dl, sl2, 1, tmask, tsq);
+      smx<EB, MASK>(s[1], dp[1], j * EB, nl, dl, sl2, 1, tmask, tsq);
       if (j + 1 < 2 * DT) {
 #pragma unroll
         for (int e = 0; e < EB; ++e) { nl[e] = nn[e]; dl[e] = dd[e]; }
@@ -984,7 +1001,12 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
       // rows of S = queries q0 + rr (+4h) with rr in [0, 64); masked if rr < tmask or rr >= tsq
       const int tmask = CAUSAL ? key - off - q0 - 4 * h : -1;
       const int tsq = p.Sq - q0 - 4 * h;
-      BwdKVTile<D, CAUSAL>::run(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask, tsq, h);
+      if (CAUSAL && (p.mask_all || kw + 31 - off - q0 > 0))   // some query of the tile precedes some key of this wave
+        BwdKVTile<D, CAUSAL>::template run<true>(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask,
+                                                 tsq, h);
+      else
+        BwdKVTile<D, CAUSAL>::template run<false>(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask,
+                                                  tsq, h);
     }
   }
   acc_fence();
@@ -1016,20 +1038,23 @@ struct BwdQTile {
     const int o = (kt * 32 + 16 * (j & 1)) * D;
     return tr_pair(base + toff[j >> 1][0] + o, base + toff[j >> 1][1] + o);
   }
-  // dS^T registers [e0, e0 + EA) of key subtile kt (rows = keys, lanes = queries)
+  // dS^T registers [e0, e0 + EA) of key subtile kt (rows = keys, lanes = queries);
+  // MASK (wave-uniform): the tile holds keys past some lane's last valid key (causal diagonal / ragged Sk)
+  template <bool MASK>
   __device__ __forceinline__ static void smx(const f32x16& sv, f32x16& dpv, int e0, int kt, float sl2, float nlse2,
                                              float dl, int lim) {
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int r = e0 + e, rr = (r & 3) + 8 * (r >> 2) + 32 * kt;
       float pv = fast_exp2(fmaf(sv[r], sl2, nlse2));
-      pv = rr > lim ? 0.f : pv;
+      if constexpr (MASK) pv = rr > lim ? 0.f : pv;
       dpv[r] = pv * (dpv[r] - dl);
     }
   }
   // One 64-key tile, hand-pipelined like BwdKVTile: stage A = S/dP chains of both key subtiles (subtile
   // 0's softmax-gradient under subtile 1's chain), stage B = dQ += dS0 K0 (subtile 1's softmax under it),
-  // stage C = dQ += dS1 K1.  Masking is branch-free (lim = last valid key row of this lane's query).
+  // stage C = dQ += dS1 K1.  MASK: selects against lim (= last valid key row of this lane's query) on edge tiles.
+  template <bool MASK>
   __device__ __forceinline__ static void run(const bf16_t* Ks, const bf16_t* Vs, const u16x8 (&qf)[KS],
                                              const u16x8 (&gf)[KS], const int (&roff)[KS], const int (&toff)[DT][2],
                                              f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim) {
@@ -1045,7 +1070,7 @@ struct BwdQTile {
       else ta = trf(Ks, toff, 0, 0);
       s[kt] = mfma32(ka, qf[ks], ks == 0 ? z : s[kt]);
       dp[kt] = mfma32(va, gf[ks], ks == 0 ? z : dp[kt]);
-      if (kt == 1) smx(s[0], dp[0], ks * EA, 0, sl2, nlse2, dl, lim);
+      if (kt == 1) smx<MASK>(s[0], dp[0], ks * EA, 0, sl2, nlse2, dl, lim);
       ka = kn; va = vn;
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1054,7 +1079,7 @@ struct BwdQTile {
     for (int j = 0; j < 2 * DT; ++j) {
       const u16x8 tn = j + 1 < 2 * DT ? trf(Ks, toff, 0, j + 1) : trf(Ks, toff, 1, 0);
       dq[j >> 1] = mfma32(ta, df[0][j & 1], dq[j >> 1]);
-      smx(s[1], dp[1], j * EA, 1, sl2, nlse2, dl, lim);
+      smx<MASK>(s[1], dp[1], j * EA, 1, sl2, nlse2, dl, lim);
       if ((j + 1) * EA == 8) df[1][0] = pack8(dp[1], 0);
       ta = tn;
       __builtin_amdgcn_sched_barrier(0);
@@ -1129,6 +1154,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int toff[DT][2];
   tr_offsets<D>(lane, toff);
   const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+  const int wlim = min(p.Sk - 1, CAUSAL ? qw + off : p.Sk - 1) - 4;   // min of lim0 over the wave's lanes
 
   for (int t = 0; t < ntiles; t += 2) {
 #pragma unroll
@@ -1144,7 +1170,10 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
       const int k0 = tt * TILE;
       if (CAUSAL && k0 > qw + 31 + off) continue;               // every key of the tile follows these queries
       const bf16_t* Ks = smem + u * 2 * TE;
-      BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      if (p.mask_all || k0 + TILE - 1 > wlim)   // some lane's last valid key falls inside this tile
+        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      else
+        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
   }
   if (p.cs_q == nullptr) {
@@ -1220,6 +1249,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   int toff[DT][2];
   tr_offsets<D>(lane, toff);
   const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+  const int wlim = min(p.Sk - 1, CAUSAL ? qw + off : p.Sk - 1) - 4;   // min of lim0 over the wave's lanes
 
   int stage = 0;
   for (int t = 0; t < ntiles; ++t) {
@@ -1233,7 +1263,10 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     const int k0 = t * TILE;
     if (!(CAUSAL && k0 > qw + 31 + off)) {
       const bf16_t* Ks = smem + stage * 2 * TE;
-      BwdQTile<D, CAUSAL>::run(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      if (p.mask_all || k0 + TILE - 1 > wlim)   // some lane's last valid key falls inside this tile
+        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      else
+        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
     stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
@@ -1314,6 +1347,8 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   kv.order = (p.order >> 1) & 1;
   qp.order = (p.order >> 2) & 1;
   kv.fuse_delta = 0;
+  static const int mask_all = [] { const char* e = getenv("PDT_FA_MASK_ALL"); return e && atoi(e) != 0 ? 1 : 0; }();
+  kv.mask_all = qp.mask_all = mask_all;
   static const bool fuse = [] { const char* e = getenv("PDT_FA_FUSE_DELTA"); return !e || atoi(e) != 0; }();
   qp.fuse_delta = fuse ? 1 : 0;
   if (!fuse) fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);

@@ -166,6 +166,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldc;
   int k_per_split;
   int xpr;                // XCD block cut (see tile_of)
+  int grp;                // tile rows per group inside an XCD block (see tile_of)
 };
 
 __device__ __forceinline__ void tile_of(const GemmArgs& p, int id, int ntiles, int& tm, int& tn) {
@@ -176,9 +177,12 @@ __device__ __forceinline__ void tile_of(const GemmArgs& p, int id, int ntiles, i
   const int mt = p.M / TM, nt = p.N / TN;
   const int xcd = id & 7, loc = id >> 3;
   if (p.xpr > 0) {
-    const int xpc = 8 / p.xpr, rb = mt / p.xpr, cb = nt / xpc;
-    tm = (xcd / xpc) * rb + loc / cb;
-    tn = (xcd % xpc) * cb + loc % cb;
+    // inside the block, groups of grp tile rows walked column-major within the group: the ~32 tiles an XCD's
+    // CUs hold at once form a grp x (32 / grp) rectangle (4 x 8 for GPT-2's c_fc: 4 A panels + 8 B panels per
+    // K-step in its L2) instead of one row of tiles that streams every B panel (1 A + 32 B at c_fc)
+    const int xpc = 8 / p.xpr, rb = mt / p.xpr, cb = nt / xpc, g = p.grp, per = g * cb;
+    tm = (xcd / xpc) * rb + (loc / per) * g + loc % g;
+    tn = (xcd % xpc) * cb + (loc % per) / g;
   } else {
     const int q8 = ntiles >> 3, r8 = ntiles & 7;
     const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
@@ -542,7 +546,8 @@ struct ItemOps {
 // results through the 32 KiB of LDS past the ring (4 rounds of 64 rows, full-row 16-byte stores) and the stores
 // drain under the next item's first K-steps (its first wait counts them: vmcnt(16 + stores)).
 // DIAG = 1 (diagnostic builds only, pdt_gemm_stamps_bf16): wave 0 stamps s_memtime at each item's start, after
-// its main loop and after its epilogue into p.aux_out (uint64 [item][4], the 4th = s_memrealtime at item start)
+// its main loop and after its epilogue into p.aux_out (uint64 [item][8]: [3] = s_memrealtime at item start, [4..7] =
+// the stamped loop's own phase stamps: start, prologue wait done, first K-step done, tail entry)
 // -- for the phase shares of an item, never for timing the production kernel.
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;
@@ -633,6 +638,17 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
 #define PDT_KLOOP_TT_ASM(MAC)                                                                                     \
   asm volatile(MAC : : PDT_ITEM_OPS, [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),    \
                [rd0] "v"(rd0), [rdx] "v"(rd1) : PDT_KLOOP_CLOBBERS)
+// DIAG: the stamped loop (gen_gemm_kloop.py *_STAMPS) hands its 4 phase stamps out as 8 SGPR halves
+#define PDT_STAMP_OUTS                                                                                            \
+  [st0] "=s"(ph[0]), [st1] "=s"(ph[1]), [st2] "=s"(ph[2]), [st3] "=s"(ph[3]), [st4] "=s"(ph[4]),               \
+      [st5] "=s"(ph[5]), [st6] "=s"(ph[6]), [st7] "=s"(ph[7])
+#define PDT_KLOOP_NT_ASM_ST(MAC)                                                                                  \
+  asm volatile(MAC : PDT_STAMP_OUTS : PDT_ITEM_OPS, [voa] "v"(voa0), [vob] "v"(vob0), [rd0] "v"(rd0),            \
+               [rd1] "v"(rd1) : PDT_KLOOP_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99")
+#define PDT_KLOOP_TT_ASM_ST(MAC)                                                                                  \
+  asm volatile(MAC : PDT_STAMP_OUTS : PDT_ITEM_OPS, [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0),         \
+               [vob1] "v"(vob1), [rd0] "v"(rd0), [rdx] "v"(rd1)                                                  \
+               : PDT_KLOOP_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99")
 
   ItemOps<LAYOUT> cur;
   int item = blockIdx.x;
@@ -656,8 +672,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     uint64_t st0 = 0, st1 = 0, rt0 = 0;
     if (DIAG) { st0 = stamp(); rt0 = __builtin_amdgcn_s_memrealtime(); }
     // ---------------------------------------------------------------- main loop
-    if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM(PDT_GEMM_KLOOP_NT);
-    else PDT_KLOOP_TT_ASM(PDT_GEMM_KLOOP_TT);
+    uint32_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (DIAG) {
+      if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM_ST(PDT_GEMM_KLOOP_NT_STAMPS);
+      else PDT_KLOOP_TT_ASM_ST(PDT_GEMM_KLOOP_TT_STAMPS);
+    } else {
+      if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM(PDT_GEMM_KLOOP_NT);
+      else PDT_KLOOP_TT_ASM(PDT_GEMM_KLOOP_TT);
+    }
     if (DIAG) st1 = stamp();
     const int m0 = cur.m0, n0 = cur.n0, tm = cur.tm;
 
@@ -763,8 +785,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     if (DIAG) {
       const uint64_t st2 = stamp();
       if (tid == 0) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(p.aux_out) + 4 * (int64_t)item;
+        uint64_t* d = reinterpret_cast<uint64_t*>(p.aux_out) + 8 * (int64_t)item;
         d[0] = st0; d[1] = st1; d[2] = st2; d[3] = rt0;
+        for (int i = 0; i < 4; ++i) d[4 + i] = ((uint64_t)ph[2 * i + 1] << 32) | ph[2 * i];
       }
     }
     if (!has_next) break;
@@ -774,6 +797,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
   }
 #undef PDT_KLOOP_CLOBBERS
 #undef PDT_ITEM_OPS
+#undef PDT_KLOOP_NT_ASM_ST
+#undef PDT_KLOOP_TT_ASM_ST
+#undef PDT_STAMP_OUTS
 #undef PDT_KLOOP_NT_ASM
 #undef PDT_KLOOP_TT_ASM
 }
@@ -827,6 +853,21 @@ __global__ __launch_bounds__(256) void colpart_reduce_kernel(const float* __rest
   float s = 0.f;
   for (int r = 0; r < R; ++r) s += part[(int64_t)r * N + n];
   out[n] = f2bf(s);
+}
+
+// rows per group of tile_of's walk, dividing the block's rows.  Measured on the flagship's NT shapes
+// (profiles/r4/r4_gemm_grp_ab.log, PDT_GEMM_GRP forces one): short K (<= 4096: the A panels of an item are
+// small) runs best on 8-row groups -- c_fc 1,228 -> 1,446 TFLOP/s, qkv 1,307 -> 1,427, attention projection
+// 1,302 -> 1,367 -- long K on 4-row ones (4 x 8 tiles in flight per XCD; 8-row groups lose 2-8 % there)
+int xcd_grp(int mt, int nt, int K, int xpr) {
+  if (xpr <= 0) return 1;
+  const int rb = mt / xpr, cb = nt / (8 / xpr);
+  static const int forced = [] { const char* e = getenv("PDT_GEMM_GRP"); return e ? atoi(e) : 0; }();
+  if (forced > 0 && rb % forced == 0) return forced;
+  const int pref[3] = {K <= 4096 ? 8 : 4, K <= 4096 ? 4 : 8, 2};
+  for (int g : pref)
+    if (rb % g == 0 && g * cb >= 16) return g;
+  return 1;
 }
 
 int xcd_cut(int mt, int nt) {
@@ -889,6 +930,7 @@ PDT_API int pdt_gemm_bf16(int layout, int epi, const void* A, const void* B, voi
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.k_per_split = (int)(K / splits);
   a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  a.grp = xcd_grp((int)(M / TM), (int)(N / TN), (int)(K / splits), a.xpr);
   const int run_epi = splits > 1 ? E_F32 : epi;
   if (splits > 1) a.ldc = N;
   int err = layout == L_NT ? launch_layout<L_NT>(run_epi, a, splits, s) : launch_layout<L_TT>(run_epi, a, splits, s);
@@ -922,6 +964,7 @@ PDT_API int pdt_gemm2_bf16(int layout, int epi, const void* A, const void* B, vo
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.k_per_split = (int)(K / splits);
   a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  a.grp = xcd_grp((int)(M / TM), (int)(N / TN), (int)(K / splits), a.xpr);
   const int run_epi = splits > 1 ? E_F32 : epi;
   if (splits > 1) a.ldc = N;
   int err = layout == L_NT ? launch_asm_layout<L_NT>(run_epi, a, splits, s)
@@ -947,6 +990,7 @@ PDT_API int pdt_gemm_stamps_bf16(int layout, const void* A, const void* B, void*
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux_out = (bf16_t*)stamps;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = N; a.k_per_split = (int)K;
   a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
+  a.grp = xcd_grp((int)(M / TM), (int)(N / TN), (int)K, a.xpr);
   const dim3 grid(persist_grid((int)((M / TM) * (N / TN))), 1);
   if (layout == L_NT) gemm_asm_kernel<L_NT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
   else gemm_asm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);

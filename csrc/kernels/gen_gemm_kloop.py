@@ -67,8 +67,9 @@ VARIANTS = [
 
 
 class Gen:
-    def __init__(self, layout, sched=None):
+    def __init__(self, layout, sched=None, stamps=False):
         self.layout = layout
+        self.stamps = stamps      # diagnostic build: s_memtime at the phase boundaries into s[92:99]
         self.lines = []
         self.sc = dict(VARIANTS[0] if sched is None else sched)
 
@@ -230,6 +231,12 @@ class Gen:
             for s in tail:
                 self.emit(s)
 
+    def stamp(self, i):
+        """Diagnostic builds: s_memtime into s[92 + 2i : 93 + 2i] (i = 0 start, 1 prologue wait done, 2 first
+        K-step done, 3 tail entry); read back after the loop's final lgkmcnt(0)."""
+        if self.stamps:
+            self.emit(f"s_memtime s[{92 + 2 * i}:{93 + 2 * i}]")
+
     def first_step(self, vm):
         """Barrier on tile 0, its substep-0 fragments, then K-step 0 (or the whole of a <= 2-step item)."""
         e = self.emit
@@ -283,17 +290,21 @@ class Gen:
         # K-step 0 is peeled (its substep-0 MFMAs start every accumulator from C = 0) and emitted twice: for a
         # later item its end-of-step wait for tile 1 also counts the previous epilogue's stores as older than
         # tile 2's DMA (vmcnt(%[wnx]) = 16 + stores), so they drain under the K-step instead of stalling it
+        self.stamp(0)
         e("s_cmp_eq_u32 %[first], 0")
         e("s_cbranch_scc1 pdtk%=_issued")
         self.tile_dma(0)
         self.tile_dma(1)
         e("s_waitcnt vmcnt(16)")
+        self.stamp(1)
         self.first_step(16)
         e("s_branch pdtk%=_stepped")
         e("pdtk%=_issued:")
         e("s_waitcnt vmcnt(%[wnx])")
+        self.stamp(1)
         self.first_step("%[wnx]")
         e("pdtk%=_stepped:")
+        self.stamp(2)
         # then two K-steps per iteration (stage 1, stage 0); s88 = K-steps left including the current one
         e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
         e(f"s_cmp_le_u32 s{S_CNT}, 2")
@@ -309,14 +320,20 @@ class Gen:
         e("s_cbranch_scc0 pdtk%=_loop")
         e("s_branch pdtk%=_tail1")
         e("pdtk%=_tail0:")                      # 2 K-steps left, stage 0 (T even)
+        self.stamp(3)
         self.next_tail(False)
         e("pdtk%=_tail1:")                      # 2 K-steps left, stage 1 (T odd: the next item loads itself)
+        self.stamp(3)
         self.step(1, False, True, 0)
         self.step(0, False, False, 0)
         e("s_branch pdtk%=_done")
         e("pdtk%=_first_tail:")                 # K = 128: both K-steps, the first from C = 0
         self.next_tail(True)
         e("pdtk%=_done:")
+        if self.stamps:
+            e("s_waitcnt lgkmcnt(0)")
+            for i in range(8):
+                e(f"s_mov_b32 %[st{i}], s{92 + i}")
         e("s_nop 15")
         e("s_nop 15")
         return self.lines
@@ -336,6 +353,8 @@ def main():
         n_mfma = sum(1 for ln in lines if ln.startswith("v_mfma"))
         out.append(f"// {name} {sched}: {len(lines)} lines, {n_mfma} MFMAs")
         out.append(render(name, lines))
+        out.append(f"// {name}_STAMPS: the same loop with s_memtime phase stamps (gemm.hip DIAG builds)")
+        out.append(render(name + "_STAMPS", Gen(L, sched, stamps=True).program()))
     out.append("#define PDT_AGPR_CLOBBERS " + ", ".join(f'"a{i}"' for i in range(256)))
     out.append("")
     with open(os.path.join(here, "gemm_kloop.inc"), "w") as f:

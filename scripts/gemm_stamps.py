@@ -26,7 +26,7 @@ def run(name, layout, M, N, K):
         lda, ldb = M, N
     c = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     items = (M // 256) * (N // 256)
-    st = torch.zeros(items, 4, dtype=torch.int64, device=dev)
+    st = torch.zeros(items, 8, dtype=torch.int64, device=dev)
     for _ in range(3):
         _lib.call("pdt_gemm_stamps_bf16", layout, a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda, ldb,
                   st.data_ptr(), _lib.stream_handle(dev))
@@ -46,7 +46,20 @@ def run(name, layout, M, N, K):
     # clock: cycles per realtime tick over the whole run of one workgroup
     ids = list(range(0, items, grid))
     clk = float((s[ids[-1], 0] - s[ids[0], 0]) / max(1.0, float(s[ids[-1], 3] - s[ids[0], 3])) * 100e6) if len(ids) > 1 else 0.0
-    out = {"case": name, "shape": [M, N, K], "items": items, "k_steps": T,
+    # inside the main loop: T0 asm start, T1 prologue wait done, T2 first K-step done, T3 tail entry
+    pre = s[:, 4] - s[:, 0]
+    pro = s[:, 5] - s[:, 4]
+    k0 = s[:, 6] - s[:, 5]
+    mid = (s[:, 7] - s[:, 6]) / max(1, T - 3)
+    tail = (s[:, 1] - s[:, 7]) / 2
+    later = torch.arange(items) >= grid          # items whose tiles 0 / 1 the previous item issued
+    def med(x, sel=None):
+        x = x if sel is None else x[sel]
+        return float(x.median()) if x.numel() else None
+    out_ph = {"pre_asm_cyc": med(pre), "prologue_wait_cyc_first_item": med(pro, ~later),
+              "prologue_wait_cyc_later_items": med(pro, later), "kstep0_cyc": med(k0),
+              "kstep0_cyc_later_items": med(k0, later), "steady_kstep_cyc": med(mid), "tail_kstep_cyc": med(tail)}
+    out = {"case": name, "shape": [M, N, K], "items": items, "k_steps": T, **out_ph,
            "loop_cyc_median": float(loop.median()), "loop_cyc_per_kstep": float(loop.median()) / T,
            "epi_cyc_median": float(epi.median()), "epi_cyc_p90": float(epi.quantile(0.9)),
            "gap_cyc_median": float(torch.tensor(gaps).median()) if gaps else None, "clock_hz": clk}
