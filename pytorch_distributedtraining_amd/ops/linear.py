@@ -250,6 +250,74 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+FUSED_GELU = os.environ.get("PDT_FUSED_GELU", "1") == "1"
+_ZERO_BIAS: dict = {}
+
+
+def linear_bias_gelu_ok(x, weight, bias) -> bool:
+    """gelu_tanh(x W^T + b) in ONE hand-GEMM pass (``ops.gemm.gemm_nt_gelu``: bias + GELU in the epilogue, the
+    pre-activation kept for the backward) -- bf16, the hand kernel's tile grid, K >= 128."""
+    from . import gemm as G
+    if not (FUSED_GELU and G.KERNEL["name"] == "asm" and x.is_cuda and bias is not None):
+        return False
+    if torch.is_autocast_enabled("cuda") or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 \
+            or bias.dtype != torch.bfloat16 or not weight.is_contiguous():
+        return False
+    m = x.numel() // x.shape[-1]
+    n, k = weight.shape
+    return (m % 256 == 0 and n % 256 == 0 and k % 64 == 0 and k >= 128 and x.shape[-1] == k
+            and G.gemm_ok(G.L_NT, m, n, k, k, k) and weight.data_ptr() % 16 == 0)
+
+
+class _LinearBiasGeluFn(torch.autograd.Function):
+    """y = gelu_tanh(x W^T + b): forward on the hand NT GEMM with the bias + GELU epilogue (replaces hipBLASLt +
+    the separate bias-GELU pass over the [tokens, 4d] hidden); backward = the fused GELU-backward + bias-gradient
+    sweep over the kept pre-activation, then the Linear's weight / data gradients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from . import gemm as G
+        x2 = x.reshape(-1, x.shape[-1])
+        x2 = x2 if x2.is_contiguous() and x2.data_ptr() % 16 == 0 else x2.contiguous()
+        y, pre = G.gemm_nt_gelu(x2, weight, bias)
+        ctx.save_for_backward(x2, weight, pre)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, pre = ctx.saved_tensors
+        dy2 = dy.reshape(pre.shape)
+        dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
+        rows, n = pre.shape
+        key = (n, pre.device)
+        zb = _ZERO_BIAS.get(key)
+        if zb is None:
+            zb = _ZERO_BIAS[key] = torch.zeros(n, dtype=torch.bfloat16, device=pre.device)
+        lib = _lib.require()
+        dpre = torch.empty_like(pre)
+        db = torch.empty(n, dtype=w.dtype, device=pre.device)
+        ws = torch.empty(lib.pdt_colsum_ws_floats(rows, n), dtype=torch.float32, device=pre.device)
+        # pre already holds the bias: the sweep runs with a zero bias
+        _lib.call("pdt_bias_gelu_bwd_db", dy2.data_ptr(), pre.data_ptr(), zb.data_ptr(), dpre.data_ptr(),
+                  db.data_ptr(), ws.data_ptr(), rows, n, _lib.dtype_code(pre.dtype), _lib.dtype_code(db.dtype), 1, 0,
+                  _lib.stream_handle(pre.device))
+        dw = wgrad(dpre, x2, w.dtype) if ctx.needs_input_grad[1] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _dgrad_via_transpose(rows, w.shape[0], w.shape[1], w):
+                dx = F.linear(dpre, transpose16(w))
+            else:
+                dx = torch.mm(dpre, w)
+            dx = dx.view(*ctx.xshape)
+        return dx, dw, (db if ctx.needs_input_grad[2] else None)
+
+
+def linear_bias_gelu(x, weight, bias):
+    """gelu_tanh(x W^T + b) (GPT-2's c_fc + GELU): one fused pass where ``linear_bias_gelu_ok``."""
+    return _LinearBiasGeluFn.apply(x, weight, bias)
+
+
 def linear(x, weight, bias=None):
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
