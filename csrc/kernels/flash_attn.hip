@@ -1154,7 +1154,6 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   int toff[DT][2];
   tr_offsets<D>(lane, toff);
   const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
-  const int wlim = min(p.Sk - 1, CAUSAL ? qw + off : p.Sk - 1) - 4;   // min of lim0 over the wave's lanes
 
   for (int t = 0; t < ntiles; t += 2) {
 #pragma unroll
@@ -1170,10 +1169,9 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
       const int k0 = tt * TILE;
       if (CAUSAL && k0 > qw + 31 + off) continue;               // every key of the tile follows these queries
       const bf16_t* Ks = smem + u * 2 * TE;
-      if (p.mask_all || k0 + TILE - 1 > wlim)   // some lane's last valid key falls inside this tile
-        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
-      else
-        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      // one tile body with select masks on every tile: a second (unmasked) copy of the unrolled body made the dQ
+      // kernel 20 % slower in the flagship step (instruction-cache footprint), unlike dK/dV
+      BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
   }
   if (p.cs_q == nullptr) {
@@ -1249,7 +1247,6 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   int toff[DT][2];
   tr_offsets<D>(lane, toff);
   const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
-  const int wlim = min(p.Sk - 1, CAUSAL ? qw + off : p.Sk - 1) - 4;   // min of lim0 over the wave's lanes
 
   int stage = 0;
   for (int t = 0; t < ntiles; ++t) {
@@ -1263,10 +1260,9 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     const int k0 = t * TILE;
     if (!(CAUSAL && k0 > qw + 31 + off)) {
       const bf16_t* Ks = smem + stage * 2 * TE;
-      if (p.mask_all || k0 + TILE - 1 > wlim)   // some lane's last valid key falls inside this tile
-        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
-      else
-        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      // one tile body with select masks on every tile: a second (unmasked) copy of the unrolled body made the dQ
+      // kernel 20 % slower in the flagship step (instruction-cache footprint), unlike dK/dV
+      BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
     }
     stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
