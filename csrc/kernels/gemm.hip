@@ -491,15 +491,17 @@ __device__ __forceinline__ void stg_write_out(const u16x8 (&buf)[8], bf16_t* dst
     *reinterpret_cast<u16x8*>(dst + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31)) = buf[it];
   }
 }
-// DGELU: the aux rows of round r into the image (the same mapping as the write-out, reversed)
-__device__ __forceinline__ void stg_load(char* img, const bf16_t* src, int64_t ldc, int m0, int n0, int r, int w,
-                                         int lane) {
-  u16x8 t[8];
+// DGELU: the aux rows of round r (the same mapping as the write-out, reversed): fetched into registers a round
+// ahead (stg_fetch), put into the image when the round starts (stg_put)
+__device__ __forceinline__ void stg_fetch(u16x8 (&t)[8], const bf16_t* src, int64_t ldc, int m0, int n0, int r, int w,
+                                          int lane) {
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int q = 16 * w + 2 * it + (lane >> 5);
     t[it] = *reinterpret_cast<const u16x8*>(src + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31));
   }
+}
+__device__ __forceinline__ void stg_put(char* img, const u16x8 (&t)[8], int w, int lane) {
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int q = 16 * w + 2 * it + (lane >> 5), c16 = lane & 31;
@@ -712,11 +714,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
       // round r: this wave's accumulator tiles i = 2 r, 2 r + 1 -> image rows q = 32 wr + 16 (i & 1) + (lane & 15)
+      u16x8 aux[2][8];                       // DGELU: the pre-activation rows of rounds r (in use) and r + 1 (in flight)
+      if constexpr (EPI == E_DGELU) stg_fetch(aux[0], p.aux, p.ldc, m0, n0, 0, w, lane);
       sfor<0, 4>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
         if constexpr (EPI == E_DGELU) {
           __syncthreads();                   // the previous round's image is read
-          stg_load(img, p.aux, p.ldc, m0, n0, r, w, lane);
+          stg_put(img, aux[r & 1], w, lane);
+          if constexpr (r < 3) stg_fetch(aux[(r + 1) & 1], p.aux, p.ldc, m0, n0, r + 1, w, lane);
         }
         __syncthreads();
         sfor<0, 16>([&](auto kc) {

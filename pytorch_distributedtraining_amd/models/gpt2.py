@@ -22,7 +22,7 @@ import torch.nn as nn
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
 from ..ops.embedding import Embedding
 from ..ops.fp8 import fp8_enabled, fp8_gelu_mlp, fp8_gelu_mlp_ok, fp8_recompute_safe
-from ..ops.linear import Linear, linear, linear_bias_gelu, linear_bias_gelu_ok
+from ..ops.linear import Linear, gelu_mlp, gelu_mlp_ok, linear, linear_bias_gelu, linear_bias_gelu_ok
 from ..ops.norms import LayerNorm
 
 
@@ -100,6 +100,9 @@ class MLP(nn.Module):
                                                                     self.c_proj.weight, self.c_proj.bias):
                 # fp8 GEMMs with bias + GELU fused into the casts (the bf16 hidden never reaches HBM)
                 return fp8_gelu_mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, m1, m2)
+        if gelu_mlp_ok(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias):
+            # c_fc + bias + GELU fused forward, c_proj dgrad + GELU backward + c_fc bias gradient fused backward
+            return gelu_mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
         if linear_bias_gelu_ok(x, self.c_fc.weight, self.c_fc.bias):
             # bias + GELU in the hand GEMM's epilogue (ops.linear.linear_bias_gelu)
             return self.c_proj(linear_bias_gelu(x, self.c_fc.weight, self.c_fc.bias))

@@ -318,6 +318,63 @@ def linear_bias_gelu(x, weight, bias):
     return _LinearBiasGeluFn.apply(x, weight, bias)
 
 
+# opt-in: measured 144.1k vs 145.0k tokens/s without it (the DGELU epilogue: 1,045 TFLOP/s vs the plain 1,466 --
+# its pre-activation read and GELU-derivative math cost more than the separate sweep; profiles/r4/r4_dgelu_ab.log)
+FUSED_DGELU = os.environ.get("PDT_FUSED_DGELU", "0") == "1"
+
+
+def gelu_mlp_ok(x, w1, b1, w2, b2) -> bool:
+    """The whole MLP (c_fc + GELU + c_proj) as ``gelu_mlp``: c_fc as ``linear_bias_gelu`` and c_proj's data
+    gradient on the hand NT GEMM with the GELU-backward + c_fc bias-gradient epilogue."""
+    return (FUSED_DGELU and linear_bias_gelu_ok(x, w1, b1) and w2.dtype == torch.bfloat16 and w2.is_contiguous()
+            and b2 is not None and b2.dtype == torch.bfloat16 and w2.shape[1] == w1.shape[0]
+            and w2.shape[0] % 64 == 0 and w2.shape[0] >= 128)
+
+
+class _GeluMlpFn(torch.autograd.Function):
+    """out = gelu_tanh(x W1^T + b1) W2^T + b2 (GPT-2's MLP).  Forward: c_fc + bias + GELU in one hand-GEMM pass,
+    c_proj on hipBLASLt.  Backward: c_proj's data gradient, the GELU backward and c_fc's bias gradient in ONE hand-GEMM
+    pass (DGELU epilogue over the kept pre-activation) -- no separate sweep over the [tokens, 4d] hidden."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        from . import gemm as G
+        x2 = x.reshape(-1, x.shape[-1])
+        x2 = x2 if x2.is_contiguous() and x2.data_ptr() % 16 == 0 else x2.contiguous()
+        y1, pre = G.gemm_nt_gelu(x2, w1, b1)
+        out = F.linear(y1, w2, b2)
+        ctx.save_for_backward(x2, w1, pre, y1, w2)
+        ctx.xshape = x.shape
+        return out.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import gemm as G
+        x2, w1, pre, y1, w2 = ctx.saved_tensors
+        d2 = dout.reshape(-1, dout.shape[-1])
+        d2 = d2 if d2.is_contiguous() and d2.data_ptr() % 16 == 0 else d2.contiguous()
+        dw2 = wgrad(d2, y1, w2.dtype) if ctx.needs_input_grad[3] else None
+        db2 = None
+        if ctx.needs_input_grad[4]:
+            db2 = take_bias_grad(d2)      # summed by the kernel that produced dY (the next LayerNorm's backward)
+            db2 = db2.to(w2.dtype) if db2 is not None else _colsum(d2, w2.dtype)
+        # c_proj dgrad (d2 W2) x GELU'(pre), and c_fc's bias gradient, in one pass
+        dpre, db1 = G.gemm_nt_dgelu(d2, transpose16(w2), pre, bias_dtype=w1.dtype)
+        dw1 = wgrad(dpre, x2, w1.dtype) if ctx.needs_input_grad[1] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _dgrad_via_transpose(dpre.shape[0], w1.shape[0], w1.shape[1], w1):
+                dx = F.linear(dpre, transpose16(w1))
+            else:
+                dx = torch.mm(dpre, w1)
+            dx = dx.view(*ctx.xshape)
+        return dx, dw1, (db1 if ctx.needs_input_grad[2] else None), dw2, db2
+
+
+def gelu_mlp(x, w1, b1, w2, b2):
+    return _GeluMlpFn.apply(x, w1, b1, w2, b2)
+
+
 def linear(x, weight, bias=None):
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")

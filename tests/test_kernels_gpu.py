@@ -1454,3 +1454,31 @@ def test_fused_linear_bias_gelu_matches_unfused(M, C):
     assert rel_err(y, y2) < 1e-2
     for a, b in zip(g, (x.grad, lin.weight.grad, lin.bias.grad)):
         assert rel_err(a, b) < 2e-2, rel_err(a, b)
+
+
+@pytest.mark.parametrize("M,C", [(1024, 256), (8 * 1024, 2048)])
+def test_fused_gelu_mlp_matches_unfused(M, C):
+    """GPT-2's MLP as ops.linear.gelu_mlp (c_fc + bias + GELU epilogue forward; c_proj data gradient x GELU' + c_fc
+    bias gradient in one DGELU-epilogue GEMM backward) against the unfused modules: output and all five gradients."""
+    from pytorch_distributedtraining_amd.ops import linear as L
+    from pytorch_distributedtraining_amd.ops.activations import bias_gelu
+    torch.manual_seed(M + C)
+    fc, proj = L.Linear(C, 4 * C).to(DEV).bfloat16(), L.Linear(4 * C, C).to(DEV).bfloat16()
+    x = torch.randn(M, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    L.FUSED_DGELU, old = True, L.FUSED_DGELU       # opt-in path: force it on for the test
+    try:
+        assert L.gelu_mlp_ok(x, fc.weight, fc.bias, proj.weight, proj.bias)
+    finally:
+        L.FUSED_DGELU = old
+    y = L.gelu_mlp(x, fc.weight, fc.bias, proj.weight, proj.bias)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    params = (x, fc.weight, fc.bias, proj.weight, proj.bias)
+    g = [t.grad.clone() for t in params]
+    for t in params:
+        t.grad = None
+    y2 = proj(bias_gelu(fc.matmul(x), fc.bias, approximate="tanh"))
+    y2.backward(dy)
+    assert rel_err(y, y2) < 1e-2
+    for a, t in zip(g, params):
+        assert rel_err(a, t.grad) < 2e-2, (t.shape, rel_err(a, t.grad))
