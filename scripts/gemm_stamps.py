@@ -73,3 +73,7 @@ if __name__ == "__main__":
     run("nt_attn_proj", 0, TOK, d, d)
     run("nt_sq8k", 0, 8192, 8192, 8192)
     run("tt_fc", 1, 4 * d, d, TOK)
+    # the same products with operands small enough to stay in the 256 MB Infinity Cache across the repeated
+    # launches: is the long-K steady K-step bound by HBM latency (A streamed once) or by the loop itself?
+    run("tt_fc_k8k_cached", 1, 4 * d, d, 8192)
+    run("nt_fc_proj_m8k_cached", 0, 8192, d, 4 * d)
