@@ -443,6 +443,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #include "gemm_kloop.inc"
 namespace {
 
+// tanh-form GELU of two values per packed instruction (v_pk_mul / v_pk_fma / v_pk_add; exp2 / rcp stay scalar):
+// u * sigmoid(2z), the gelu.h identity
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_tanh2(f32x2 u) {
+  const f32x2 t = __builtin_elementwise_fma(f32x2{kGeluB, kGeluB}, u * u, f32x2{kGeluA, kGeluA});
+  const f32x2 a = u * t;
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])} + f32x2{1.f, 1.f};
+  return u * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+
 constexpr int RING = 2 * STB;                // the two ring stages (128 KiB)
 constexpr int STAGE_BYTES = 32768;          // epilogue staging: LDS past the ring, 64 rows x 512 B per round
 constexpr int SMEM3 = RING + STAGE_BYTES;   // 160 KiB: all of the CU's LDS
@@ -748,13 +758,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
         stg_write_out(buf, EPI == E_GELU ? p.aux_out : C, p.ldc, m0, n0, r, w, lane);
         if constexpr (EPI == E_GELU) {       // then GELU of the stored (rounded) pre-activation, same rows
           __syncthreads();
+          // the image still holds this thread's pre-activation values as stored (bf16): GELU of those, two per
+          // packed instruction (gelu_tanh2) -- no second accumulator read / bias add / rounding
           sfor<0, 16>([&](auto kc) {
             constexpr int k = 16 * r + decltype(kc)::value, i = k >> 3, j = k & 7;
-            const f32x4 v = acc_tile<k>();
             const uint32_t at = stg_off(32 * wr + 16 * (i & 1) + (lane & 15), lcol + 16 * j);
+            const u16x4 hh = *reinterpret_cast<const u16x4*>(img + at);
+            const f32x2 y0 = gelu_tanh2(f32x2{bf2f(hh[0]), bf2f(hh[1])});
+            const f32x2 y1 = gelu_tanh2(f32x2{bf2f(hh[2]), bf2f(hh[3])});
             u16x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = f2bf(gelu_f<true>(bf2f(f2bf(v[e] + bj[j][e]))));
+            o[0] = f2bf(y0[0]); o[1] = f2bf(y0[1]); o[2] = f2bf(y1[0]); o[3] = f2bf(y1[1]);
             *reinterpret_cast<u16x4*>(img + at) = o;
           });
           __syncthreads();
