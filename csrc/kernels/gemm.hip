@@ -567,7 +567,7 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 
-template <int LAYOUT, int EPI, int DIAG = 0>
+template <int LAYOUT, int EPI, int DIAG = 0, bool P3 = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM3];
   const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;
@@ -650,6 +650,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
 #define PDT_KLOOP_TT_ASM(MAC)                                                                                     \
   asm volatile(MAC : : PDT_ITEM_OPS, [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),    \
                [rd0] "v"(rd0), [rdx] "v"(rd1) : PDT_KLOOP_CLOBBERS)
+// P3: the 3-stage A-ring program (gen_gemm_kloop.py Gen3) also uses v96.. for its third A buffer's read addresses
+#define PDT_KLOOP_NT_ASM3(MAC)                                                                                    \
+  asm volatile(MAC : : PDT_ITEM_OPS, [voa] "v"(voa0), [vob] "v"(vob0), [rd0] "v"(rd0), [rd1] "v"(rd1)           \
+               : PDT_KLOOP_CLOBBERS, "v96", "v97")
+#define PDT_KLOOP_TT_ASM3(MAC)                                                                                    \
+  asm volatile(MAC : : PDT_ITEM_OPS, [voa0] "v"(voa0), [voa1] "v"(voa1), [vob0] "v"(vob0), [vob1] "v"(vob1),    \
+               [rd0] "v"(rd0), [rdx] "v"(rd1)                                                                    \
+               : PDT_KLOOP_CLOBBERS, "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103")
 // DIAG: the stamped loop (gen_gemm_kloop.py *_STAMPS) hands its 4 phase stamps out as 8 SGPR halves
 #define PDT_STAMP_OUTS                                                                                            \
   [st0] "=s"(ph[0]), [st1] "=s"(ph[1]), [st2] "=s"(ph[2]), [st3] "=s"(ph[3]), [st4] "=s"(ph[4]),               \
@@ -673,7 +681,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     if (has_next) nxt.init(p, next_item, ntiles);
     // the last two K-steps load the next item's first two K-tiles (even K-step counts only: stage parity)
     // integer arithmetic, not a select: a bool-derived operand can be rematerialised as a VGPR v_cndmask
-    const int hnx = __builtin_amdgcn_readfirstlane((((nall - 1 - next_item) >> 31) + 1) & ~cur.T & 1);
+    // (P3, the 3-stage program: no next-item prefetch -- every item runs its own prologue)
+    const int hnx = P3 ? 0 : __builtin_amdgcn_readfirstlane((((nall - 1 - next_item) >> 31) + 1) & ~cur.T & 1);
     const int cnt = __builtin_amdgcn_readfirstlane(cur.T);
     first = __builtin_amdgcn_readfirstlane(first);
     // the main loop's own DMA starts at K-tile 2 when the previous item's last K-steps issued tiles 0 and 1
@@ -688,6 +697,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     if constexpr (DIAG) {
       if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM_ST(PDT_GEMM_KLOOP_NT_STAMPS);
       else PDT_KLOOP_TT_ASM_ST(PDT_GEMM_KLOOP_TT_STAMPS);
+    } else if constexpr (P3) {
+      if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM3(PDT_GEMM_KLOOP_NT3);
+      else PDT_KLOOP_TT_ASM3(PDT_GEMM_KLOOP_TT3);
     } else {
       if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM(PDT_GEMM_KLOOP_NT);
       else PDT_KLOOP_TT_ASM(PDT_GEMM_KLOOP_TT);
@@ -815,6 +827,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
   }
 #undef PDT_KLOOP_CLOBBERS
 #undef PDT_ITEM_OPS
+#undef PDT_KLOOP_NT_ASM3
+#undef PDT_KLOOP_TT_ASM3
 #undef PDT_KLOOP_NT_ASM_ST
 #undef PDT_KLOOP_TT_ASM_ST
 #undef PDT_STAMP_OUTS
@@ -835,9 +849,31 @@ static int persist_grid(int nitems) {
   return g >= 8 ? g & ~7 : g;
 }
 
+// The 3-stage program (two K-steps of DMA lead for A) where it measured faster (profiles/r4/r4_gemm_p3_ab.log, one
+// process, interleaved rounds): NT with K >= 8192 per item (c_proj forward shape 1,467 -> 1,589 TFLOP/s, 8192^3
+// 1,549 -> 1,619: hipBLASLt parity) and TT with more items than workgroups (qkv weight gradient 1,361 -> 1,422);
+// the one-item-per-workgroup TT shapes ran 3-7 % slower with it.  Needs >= 6 K-steps per item; gives up the
+// next-item prefetch.  PDT_GEMM_P3=0 / 1 forces it off / on (A/B runs).
+bool use_p3(int layout, const GemmArgs& a, int items, int grid) {
+  static const int forced = [] { const char* e = getenv("PDT_GEMM_P3"); return e ? atoi(e) : -1; }();
+  const int T = a.k_per_split / KB;
+  if (T < 6 || forced == 0) return false;
+  if (forced == 1) return true;
+  return layout == L_TT ? items > grid : a.k_per_split >= 8192;
+}
+
 template <int LAYOUT>
 int launch_asm_layout(int epi, const GemmArgs& a, int splits, hipStream_t s) {
-  const dim3 grid(persist_grid((a.M / TM) * (a.N / TN) * splits), 1);
+  const int items = (a.M / TM) * (a.N / TN) * splits;
+  const dim3 grid(persist_grid(items), 1);
+  if (use_p3(LAYOUT, a, items, (int)grid.x) && (epi == E_PLAIN || epi == E_BIAS || epi == E_F32)) {
+    switch (epi) {   // (GELU / DGELU epilogues keep the 2-stage program)
+      case E_PLAIN: gemm_asm_kernel<LAYOUT, E_PLAIN, 0, true><<<grid, NTH, 0, s>>>(a); break;
+      case E_BIAS: gemm_asm_kernel<LAYOUT, E_BIAS, 0, true><<<grid, NTH, 0, s>>>(a); break;
+      default: gemm_asm_kernel<LAYOUT, E_F32, 0, true><<<grid, NTH, 0, s>>>(a); break;
+    }
+    return (int)hipGetLastError();
+  }
   switch (epi) {
     case E_PLAIN: gemm_asm_kernel<LAYOUT, E_PLAIN><<<grid, NTH, 0, s>>>(a); break;
     case E_BIAS: gemm_asm_kernel<LAYOUT, E_BIAS><<<grid, NTH, 0, s>>>(a); break;

@@ -78,10 +78,21 @@ class Gen:
 
     # ---------------------------------------------------------------- pieces of work
     def rd_reg(self, stage, op, sub_or_blk):
-        """NT: one address register per (stage, operand, substep); TT: one per (stage, operand, block)."""
+        """NT: one address register per (stage, operand, substep); TT: one per (stage, operand, block).  Stage 2
+        (the 3-stage program's third A buffer, in the epilogue staging area) uses v96.. (A only)."""
+        if stage == 2:
+            assert op == 0
+            return f"v{96 + sub_or_blk}"
         if self.layout == NT:
             return f"v{RD + stage * 4 + op * 2 + sub_or_blk}"
         return f"v{RD + stage * 16 + op * 8 + sub_or_blk}"
+
+    def read_ops2(self, sa, sb, sub, which):
+        """read_ops with separate A / B stages (3-stage program)."""
+        out = []
+        for op, blk, dst in which:
+            out += self.read_ops(sa if op == 0 else sb, sub, [(op, blk, dst)])
+        return out
 
     def read_ops(self, stage, sub, which):
         """LDS reads of one fragment set: list of instruction strings.  which = [(op, blk, dst_base)]."""
@@ -95,6 +106,13 @@ class Gen:
                 out.append(f"ds_read_b64_tr_b16 v[{dst + 4 * blk}:{dst + 4 * blk + 1}], {r} offset:{o}")
                 out.append(f"ds_read_b64_tr_b16 v[{dst + 4 * blk + 2}:{dst + 4 * blk + 3}], {r} offset:{o + 2048}")
         return out
+
+    def dma_ops_at(self, off, op):
+        """dma_ops into the LDS byte offset `off` (3-stage program: A buffers 0 / STB / 2 STB, B buffers OPB / STB + OPB)."""
+        ops, tail = self.dma_ops(0, op)
+        ops = [([x.replace(f"%[m0b], {op * OPB + i * 4096}", f"%[m0b], {off + i * 4096}") if x.startswith("s_add_u32 m0")
+                 else x for x in setup], load) for i, (setup, load) in enumerate(ops)]
+        return ops, tail
 
     def dma_ops(self, stage, op):
         """8 LDS-DMA pieces of one operand of one tile into `stage` (each piece: SALU set-up, then the load
@@ -339,6 +357,136 @@ class Gen:
         return self.lines
 
 
+class Gen3(Gen):
+    """3-stage program for long-K items: the A operand gets a third LDS buffer (the epilogue's 32 KiB staging area,
+    idle during the loop), so A's K-tile t+3 is DMA'd in K-step t -- two K-steps of lead instead of one: an A
+    operand streamed from HBM (every weight-gradient shape) no longer waits on HBM latency at the step boundary
+    (2,350 vs 2,240 cycles per K-step, profiles/r4/r4_gemm_stamps_cached_vs_streamed.jsonl).  B keeps 2 buffers
+    (DMA'd one K-step ahead, in Q2, before A's pieces in Q3, so a wait for B never forces a younger A tile).  No
+    next-item prefetch; items need T >= 6 K-steps (the host's choice).  Unrolled by 6 = lcm(3, 2)."""
+
+    A_OFF = (0, STB, 2 * STB)
+    B_OFF = (OPB, STB + OPB)
+
+    def step3(self, p, dma_a, dma_b, has_next, vm, first=False):
+        sa, sb = p % 3, p % 2
+        nxa, nxb = (p + 1) % 3, (p + 1) % 2
+        e = self.emit
+        e(f"; ---- K-step (3-stage): A {sa} B {sb} dma A {dma_a} B {dma_b} next {has_next} first {first}")
+        e("s_waitcnt lgkmcnt(0)")
+        f1 = self.read_ops2(sa, sb, 1, [(0, i, F1A) for i in range(4)] + [(1, j, F1B) for j in range(8)] +
+                            [(0, i, F1A) for i in range(4, 8)])
+        sc = self.sc
+        self.interleave_reads(self.mfmas(F0A, F0B, range(0, 4), first), f1, sc["rd1"])
+        q2 = self.mfmas(F0A, F0B, range(4, 8), first)
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_barrier")
+        q3 = self.mfmas(F1A, F1B, range(0, 4))
+        if dma_b:
+            pb, tb = self.dma_ops_at(self.B_OFF[sb], 1)
+            self.interleave_dma(q2, pb, tb, sc["dma"])
+        else:
+            for m in q2:
+                e(m)
+        if dma_a:
+            pa, ta = self.dma_ops_at(self.A_OFF[sa], 0)
+            self.interleave_dma(q3, pa, ta, sc["dma"])
+        else:
+            for m in q3:
+                e(m)
+        if has_next:
+            e(f"s_waitcnt vmcnt({vm})")
+            e("s_barrier")
+        q4 = self.mfmas(F1A, F1B, range(4, 8))
+        if has_next:
+            f0 = self.read_ops2(nxa, nxb, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
+                                [(0, i, F0A) for i in range(1, 8)])
+            self.interleave_reads(q4, f0, sc["rd0"])
+        else:
+            for m in q4:
+                e(m)
+
+    def tile_dma_at(self, off, op):
+        pieces, tail = self.dma_ops_at(off, op)
+        for setup, load in pieces:
+            for x in setup:
+                self.emit(x)
+            self.emit("s_nop 0")
+            self.emit(load)
+        for x in tail:
+            self.emit(x)
+
+    def program(self):
+        L = self.layout
+        e = self.emit
+        e("; pdt gemm main loop, 3-stage A (generated by gen_gemm_kloop.py)")
+        for base, x in ((S_RA, "a"), (S_RB, "b")):
+            e(f"s_mov_b32 s{base}, %[{x}lo]")
+            e(f"s_mov_b32 s{base + 1}, %[{x}hi]")
+            e(f"s_mov_b32 s{base + 2}, %[{x}nr]")
+            e(f"s_mov_b32 s{base + 3}, 0x20000")
+        e(f"s_mov_b32 s{S_CNT}, %[cnt]")
+        e(f"s_mov_b32 s{S_OA}, 0")
+        e(f"s_mov_b32 s{S_OB}, 0")
+        if L == NT:
+            for stage in (0, 1):
+                for op in (0, 1):
+                    for sub in (0, 1):
+                        dst = self.rd_reg(stage, op, sub)
+                        src = "%[rd0]" if sub == 0 else "%[rd1]"
+                        if op == 0:
+                            e(f"v_add_u32 {dst}, {stage * STB}, {src}")
+                        else:
+                            e(f"v_add_u32 {dst}, %[db], {src}")
+                            if stage:
+                                e(f"v_add_u32 {dst}, {STB}, {dst}")
+            for sub in (0, 1):
+                e(f"v_add_u32 {self.rd_reg(2, 0, sub)}, {2 * STB}, {'%[rd0]' if sub == 0 else '%[rd1]'}")
+        else:
+            for i in range(8):
+                a0 = self.rd_reg(0, 0, i)
+                e(f"v_xor_b32 {a0}, {2 * i}, %[rdx]")
+                e(f"v_lshl_add_u32 {a0}, {a0}, 4, %[rd0]")
+                e(f"v_add_u32 {self.rd_reg(0, 1, i)}, %[db], {a0}")
+                e(f"v_add_u32 {self.rd_reg(1, 0, i)}, {STB}, {a0}")
+                e(f"v_add_u32 {self.rd_reg(1, 1, i)}, {STB}, {self.rd_reg(0, 1, i)}")
+                e(f"v_add_u32 {self.rd_reg(2, 0, i)}, {2 * STB}, {a0}")
+        # prologue: A0 B0 A1 B1 A2 in flight; tile 0 (A0, B0) landed: A1 B1 A2 (24 pieces) may still fly
+        self.tile_dma_at(self.A_OFF[0], 0)
+        self.tile_dma_at(self.B_OFF[0], 1)
+        self.tile_dma_at(self.A_OFF[1], 0)
+        self.tile_dma_at(self.B_OFF[1], 1)
+        self.tile_dma_at(self.A_OFF[2], 0)
+        e("s_waitcnt vmcnt(24)")
+        e("s_barrier")
+        for r in self.read_ops2(0, 0, 0, [(0, 0, F0A)] + [(1, j, F0B) for j in range(8)] +
+                                [(0, i, F0A) for i in range(1, 8)]):
+            e(r)
+        # K-step 0 (accumulators from C = 0); then steady steps while t + 3 < T (s88 = T - t > 3): B tile t + 2 and
+        # A tile t + 3 in flight, the wait for tile t + 1 leaves A(t+2), B(t+2), A(t+3) (24 pieces) flying
+        self.step3(0, True, True, True, 24, first=True)
+        e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+        e("pdtk%=_loop3:")
+        for p in (1, 2, 3, 4, 5, 0):
+            e(f"s_cmp_le_u32 s{S_CNT}, 3")
+            e(f"s_cbranch_scc1 pdtk%=_t3_{p}")
+            self.step3(p, True, True, True, 24)
+            e(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+        e("s_branch pdtk%=_loop3")
+        # the last three K-steps, entered at phase p: t = T-3 issues B(T-1) only (its wait for tile T-2 leaves A(T-1)
+        # and B(T-1) flying), t = T-2 drains, t = T-1 has no next tile
+        for p in range(6):
+            e(f"pdtk%=_t3_{p}:")
+            self.step3(p, False, True, True, 16)
+            self.step3((p + 1) % 6, False, False, True, 0)
+            self.step3((p + 2) % 6, False, False, False, 0)
+            e("s_branch pdtk%=_done3")
+        e("pdtk%=_done3:")
+        e("s_nop 15")
+        e("s_nop 15")
+        return self.lines
+
+
 def render(name, lines):
     return f"#define {name} \\\n" + " \\\n".join(f'  "{ln}\\n"' for ln in lines) + "\n"
 
@@ -355,6 +503,9 @@ def main():
         out.append(render(name, lines))
         out.append(f"// {name}_STAMPS: the same loop with s_memtime phase stamps (gemm.hip DIAG builds)")
         out.append(render(name + "_STAMPS", Gen(L, sched, stamps=True).program()))
+        lines3 = Gen3(L, sched).program()
+        out.append(f"// {name}3: 3-stage A ring for long-K items, {len(lines3)} lines")
+        out.append(render(name + "3", lines3))
     out.append("#define PDT_AGPR_CLOBBERS " + ", ".join(f'"a{i}"' for i in range(256)))
     out.append("")
     with open(os.path.join(here, "gemm_kloop.inc"), "w") as f:

@@ -50,7 +50,7 @@ def timeit(fn, iters=10):
 
 def check():
     torch.manual_seed(0)
-    for (M, N, K) in ((512, 512, 128), (2048, 1024, 1536), (1024, 768, 4096), (1024, 768, 4160)):
+    for (M, N, K) in ((512, 512, 128), (2048, 1024, 1536), (1024, 768, 4096), (1024, 768, 4160), (1024, 768, 8192)):
         a = torch.randn(M, K, device=dev).bfloat16()
         b = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
         bias = torch.randn(N, device=dev).bfloat16()
@@ -78,6 +78,20 @@ def check():
             t_asm = with_kernel("asm", lambda: G.gemm_tt(at, bt, splits=s))
             t_hip = with_kernel("hip", lambda: G.gemm_tt(at, bt, splits=s))
             out(case=f"tt_s{s}", shape=[M, N, 2 * K], rel=rel(t_asm, reft), bitwise_eq_hip=bool(torch.equal(t_asm, t_hip)))
+    # K-step counts 6..11: every tail phase of the 3-stage program (T - 3 mod 6) and of the 2-stage one, both
+    # layouts, bitwise against the compiler-scheduled kernel (run with PDT_GEMM_P3=1 to force the 3-stage program)
+    for T in range(6, 12):
+        K = 64 * T
+        a = torch.randn(512, K, device=dev).bfloat16()
+        b = (torch.randn(768, K, device=dev) * K ** -0.5).bfloat16()
+        c_asm = with_kernel("asm", lambda: G.gemm_nt(a, b))
+        c_hip = with_kernel("hip", lambda: G.gemm_nt(a, b))
+        at = torch.randn(K, 512, device=dev).bfloat16()
+        bt = torch.randn(K, 768, device=dev).bfloat16()
+        t_asm = with_kernel("asm", lambda: G.gemm_tt(at, bt, splits=1))
+        t_hip = with_kernel("hip", lambda: G.gemm_tt(at, bt, splits=1))
+        out(case="tails", k_steps=T, nt_bitwise_eq_hip=bool(torch.equal(c_asm, c_hip)),
+            tt_bitwise_eq_hip=bool(torch.equal(t_asm, t_hip)))
     # full grid at a flagship shape: every element against the compiler-scheduled kernel
     M, N, K = TOK, 2048, 2048
     a = torch.randn(M, K, device=dev).bfloat16()
