@@ -859,7 +859,11 @@ bool use_p3(int layout, const GemmArgs& a, int items, int grid) {
   const int T = a.k_per_split / KB;
   if (T < 6 || forced == 0) return false;
   if (forced == 1) return true;
-  return layout == L_TT ? items > grid : a.k_per_split >= 8192;
+  // NT: also every product whose XCD block is <= 8 tiles wide (A panels barely reused, i.e. streamed): attention
+  // projection 1,338 -> 1,382, the qkv data gradient (K = 6144) 1,298 -> 1,492 (r4_gemm_p3_nt_shapes_ab.log); wide
+  // blocks (c_fc, qkv forward: A re-read from L2) keep the 2-stage program and its next-item prefetch
+  const int cb = a.xpr > 0 ? (a.N / TN) / (8 / a.xpr) : a.N / TN;
+  return layout == L_TT ? items > grid : (a.k_per_split >= 8192 || cb <= 8);
 }
 
 template <int LAYOUT>

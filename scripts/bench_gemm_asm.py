@@ -112,7 +112,7 @@ def bench():
     torch.manual_seed(1)
     d = 2048
     nt = {"qkv": (TOK, 3 * d, d), "attn_proj": (TOK, d, d), "fc": (TOK, 4 * d, d), "fc_proj": (TOK, d, 4 * d),
-          "sq8k": (8192, 8192, 8192)}
+          "qkv_dgrad": (TOK, d, 3 * d), "sq8k": (8192, 8192, 8192)}
     for name, (M, N, K) in nt.items():
         if ONLY and ONLY not in name:
             continue
