@@ -36,6 +36,37 @@ from .gemm import gemm_tt, tt_ok, tt_splits
 _WGRAD_CHUNK = 4096
 
 
+# PDT_NT_HIP: "auto" (default: per shape, the hand NT GEMM where it timed >= 1 % faster than hipBLASLt on the shape's
+# first uncaptured call -- since round 4 they trade places by shape and box: the 3-stage program wins the long-K /
+# narrow products, hipBLASLt the attention projection), "1" (always where it applies), "0" (never)
+HIP_NT = os.environ.get("PDT_NT_HIP", "auto")
+_NT_CHOICE: dict = {}
+
+
+def _nt_hip_ok(a2: torch.Tensor, w: torch.Tensor, bias) -> bool:
+    from . import gemm as G
+    return (HIP_NT != "0" and G.KERNEL["name"] == "asm" and a2.is_cuda and a2.dim() == 2 and a2.shape[0] >= 4096
+            and a2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())) and G.nt_ok(a2, w)
+            and a2.shape[1] // 64 >= 2 and w.shape[0] % 8 == 0)
+
+
+def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
+    """a2 [M, K] @ w[N, K]^T (+ bias): the hand NT GEMM (ops.gemm.gemm_nt) or hipBLASLt, per shape as timed."""
+    if _nt_hip_ok(a2, w, bias):
+        from . import gemm as G
+        if HIP_NT == "1":
+            return G.gemm_nt(a2, w, bias)
+        key = (tuple(a2.shape), tuple(w.shape), bias is not None, a2.device)
+        c = _NT_CHOICE.get(key)
+        if c is None and not torch.cuda.is_current_stream_capturing():
+            c = _NT_CHOICE[key] = _timed_ms(lambda: G.gemm_nt(a2, w, bias)) < \
+                0.99 * _timed_ms(lambda: F.linear(a2, w, bias))
+        if c:
+            return G.gemm_nt(a2, w, bias)
+    return F.linear(a2, w, bias)
+
+
 def _tall_skinny(m: int, n: int, k: int) -> bool:
     return m >= 16 * _WGRAD_CHUNK and max(n, k) <= 1024
 
@@ -208,6 +239,9 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
+            return nt_matmul(x2, weight, bias).view(*x.shape[:-1], weight.shape[0])
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -237,7 +271,7 @@ class _LinearFn(torch.autograd.Function):
             dw = wgrad(dy2, x2, w.dtype)
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
-                dx = F.linear(dy2, transpose16(w))
+                dx = nt_matmul(dy2, transpose16(w))
             else:
                 dx = torch.mm(dy2, w)
             dx = dx.view(*dy.shape[:-1], w.shape[1])
@@ -306,7 +340,7 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(rows, w.shape[0], w.shape[1], w):
-                dx = F.linear(dpre, transpose16(w))
+                dx = nt_matmul(dpre, transpose16(w))
             else:
                 dx = torch.mm(dpre, w)
             dx = dx.view(*ctx.xshape)
@@ -364,7 +398,7 @@ class _GeluMlpFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dpre.shape[0], w1.shape[0], w1.shape[1], w1):
-                dx = F.linear(dpre, transpose16(w1))
+                dx = nt_matmul(dpre, transpose16(w1))
             else:
                 dx = torch.mm(dpre, w1)
             dx = dx.view(*ctx.xshape)
