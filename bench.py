@@ -57,8 +57,9 @@ def parse():
     ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"], help="swinir-stoke precision")
     ap.add_argument("--graph", type=int, default=0,
-                    help="gpt2-ddp / swinir-stoke at one rank: capture the whole training step (fwd, bwd, clip, fused "
-                         "AdamW) in a HIP graph and replay it (utils.graphs.GraphedStep / Trainer.graph)")
+                    help="gpt2-ddp / swinir-stoke: capture the whole training step (fwd, bwd, clip, fused AdamW; at "
+                         "N > 1 over RCCL also the gradient collectives) in a HIP graph and replay it "
+                         "(utils.graphs.GraphedStep / Trainer.graph)")
     ap.add_argument("--fp8", type=int, default=0,
                     help="gpt2/llama: run the transformer linears' GEMMs in fp8 (ops.fp8.fp8_autocast, delayed "
                          "scaling); reported with dtype 'fp8-linears' -- never the bf16 headline")
@@ -364,7 +365,8 @@ def bench_gpt2(args, comm, dev, world, rank):
         params = model.optimizer_parameters()
         sharded = False
         par = f"dp{world}"
-    graph = bool(args.graph) and not fsdp and world == 1 and dev.type == "cuda"
+    # world > 1: the bucket all-reduces are captured with the step (RCCL; DDP.prepare_capture)
+    graph = bool(args.graph) and not fsdp and dev.type == "cuda" and (world == 1 or comm.backend == "nccl")
     opt = FusedAdamW(params, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, capturable=graph)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
@@ -417,6 +419,8 @@ def bench_gpt2(args, comm, dev, world, rank):
             _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
             opt.step(grad_scale=coef)
             return loss.detach()
+        if world > 1:
+            model.prepare_capture()
         graphed = GraphedStep(graph_body, static, warmup=2)
 
         def step():                                   # noqa: F811 - the graphed replacement
@@ -567,7 +571,7 @@ def bench_swinir(args, comm, dev, world, rank):
             tr.backward(loss)
             tr.step()
 
-    graph = bool(args.graph) and world == 1 and args.precision == "bf16"
+    graph = bool(args.graph) and args.precision == "bf16" and (world == 1 or comm.backend == "nccl")
     if graph:
         # the whole optimizer step (2 micro-batches + fused AdamW) replayed as one HIP graph (Trainer.graph)
         eager_step = step

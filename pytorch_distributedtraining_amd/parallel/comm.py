@@ -63,7 +63,7 @@ class Handle:
         if self._done:
             return
         timed = _WAIT_EVENTS is not None and (self._work is not None or self._event is not None) \
-            and torch.cuda.is_available()
+            and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -130,8 +130,11 @@ class Comm:
 
     def _xgmi_ok(self, t, kind="all_reduce") -> bool:
         x = self.xgmi
+        # not under HIP-graph capture: the mesh's epochs are host-issued kernel arguments, and a replayed
+        # epoch would match the flags of the previous replay -- captured steps take RCCL, which captures
         return (x is not None and t.is_cuda and t.is_contiguous()
-                and x.eligible(t.numel() * t.element_size(), kind, t.dtype))
+                and x.eligible(t.numel() * t.element_size(), kind, t.dtype)
+                and not torch.cuda.is_current_stream_capturing())
 
     # ------------------------------------------------------------------ helpers
     @property

@@ -193,6 +193,7 @@ class DistributedDataParallel(nn.Module):
         self._observed = []
         self._warned_unused = False
         self._ready = None
+        self._graph_safe = False
 
         module.to(self.device)
         if compute_dtype is not None:
@@ -253,8 +254,20 @@ class DistributedDataParallel(nn.Module):
         self._ready = Readiness(
             self.params, [list(b.params) for b in self.plan],
             on_first=lambda: ref()._queue_finalize(), on_ready=lambda b: ref()._launch(b),
-            observe=(lambda i: ref()._observed.append(i)) if self._rebuild_pending else None)
+            observe=(lambda i: ref()._observed.append(i)) if self._rebuild_pending else None,
+            native=not self._graph_safe)
         self._ready.set_enabled(not self._no_sync)
+
+    def prepare_capture(self):
+        """Switch bucket readiness to per-parameter Python hooks before a HIP-graph capture (Trainer.graph at
+        world > 1).  The native hooks hold the parameters' AccumulateGrad nodes, which remember the stream
+        they were created on (see _readiness.NullReadiness); Python post-accumulate hooks hold no node.  The
+        hooks run once, while the step is captured, and the bucket all-reduces they launch (RCCL: the mesh
+        is bypassed under capture, parallel/comm.py) are recorded into the graph with the backward."""
+        if not self._graph_safe:
+            self._graph_safe = True
+            if getattr(self._ready, "kind", "none") == "native":
+                self._arm_readiness()
 
     def _rebuild(self):
         """Re-plan buckets in the observed gradient-ready order (first iteration), keeping values."""

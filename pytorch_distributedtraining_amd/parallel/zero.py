@@ -452,11 +452,24 @@ class ShardedDataParallel(nn.Module):
                 self._bank_li[gi] = (bank, li)
         # bucket readiness on C++ AccumulateGrad post hooks (parallel/_readiness.py): Python runs once per ready
         # bucket; frozen parameters get no hook and their buckets are released at the end of backward
+        self._readiness_plan = readiness
+        self._ready = None
+        self._arm_readiness(native=True)
+
+    def _arm_readiness(self, native: bool):
+        if self._ready is not None:
+            self._ready.remove()
         ref = weakref.ref(self)
         self._ready = NullReadiness() if self.comm.world_size == 1 else \
-            Readiness(self.params, readiness, on_first=lambda: ref()._queue_finalize(),
-                      on_ready=lambda b: ref()._launch(b))
-        self._ready.set_enabled(self.comm.world_size > 1)
+            Readiness(self.params, self._readiness_plan, on_first=lambda: ref()._queue_finalize(),
+                      on_ready=lambda b: ref()._launch(b), native=native)
+        self._ready.set_enabled(self.comm.world_size > 1 and not self._no_sync)
+
+    def prepare_capture(self):
+        """Per-parameter Python readiness hooks before a HIP-graph capture (Trainer.graph at world > 1; see
+        DistributedDataParallel.prepare_capture)."""
+        if getattr(self._ready, "kind", "none") == "native":
+            self._arm_readiness(native=False)
 
     def _wire_dtype(self, bank):
         if self.reduce_fp16 and bank.dtype == torch.float32:

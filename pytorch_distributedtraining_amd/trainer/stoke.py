@@ -406,14 +406,25 @@ class Trainer:
         buffers and replays the graph, advancing the Trainer's step counters exactly as the eager call does.
         Removes the per-launch host cost of many-small-kernel steps (SwinIR: ~3,500 launches per step).
 
-        Needs one rank (collectives are not captured), the fused optimizer (switched to its capturable device
-        step count here) and no fp16 GradScaler (its scale update is host logic)."""
+        Needs the fused optimizer (switched to its capturable device step count here; under OSS the wrapped
+        one) and no fp16 GradScaler (its scale update is host logic).  At world > 1 the collectives are
+        captured with the step: RCCL (``nccl``) process group, DDP or ShardedDDP engine (their bucket
+        readiness is switched to capture-safe hooks: ``prepare_capture``), and the xGMI mesh is bypassed
+        while capturing (its epochs are host arguments).  FSDP's unit hooks are not capture-safe."""
         from ..utils.graphs import GraphedStep
-        fused = isinstance(self._optimizer, FusedAdamW)
-        if not (self.gpu and self.world_size_ == 1 and fused and self.scaler is None):
-            raise RuntimeError("Trainer.graph needs one GPU rank, FusedAdamW and no fp16 GradScaler")
-        for g in self._optimizer.param_groups:
-            g["capturable"] = True
+        opt = self._optimizer
+        inner = opt.optim if isinstance(getattr(opt, "optim", None), FusedAdamW) else opt
+        fused = isinstance(inner, FusedAdamW)
+        if not (self.gpu and fused and self.scaler is None):
+            raise RuntimeError("Trainer.graph needs a GPU, FusedAdamW and no fp16 GradScaler")
+        if self.world_size_ > 1:
+            if self.comm.backend != "nccl" or not hasattr(self._engine, "prepare_capture"):
+                raise RuntimeError("Trainer.graph at world > 1 needs the RCCL (nccl) backend and a DDP or "
+                                   f"ShardedDDP engine (backend {self.comm.backend}, engine "
+                                   f"{type(self._engine).__name__})")
+            self._engine.prepare_capture()
+        for g in list(inner.param_groups) + (list(opt.param_groups) if inner is not opt else []):
+            g["capturable"] = True      # OSS copies its groups' hyper-parameters into the wrapped optimizer
         gs = GraphedStep(step_fn, *static_inputs, warmup=warmup)
         tr = self
         state = {"delta": None}

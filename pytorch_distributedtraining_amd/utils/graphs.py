@@ -18,6 +18,14 @@ instead.  The benchmarked steps are GPU-bound (kernel time ~= step time in the r
 ``bench.py --workload gpt2-ddp --graph 1`` replays the whole GPT-2 124M step as one graph at 23.26 ms/step vs
 23.39 eager (+0.6 %, profiles/r2_gpt2_124m_ddp_graph_ab.log), so the bench default stays eager.
 
+World > 1 (Trainer.graph, ``bench.py --graph 1`` over RCCL): the DDP / ShardedDDP bucket collectives are
+captured with the step.  The engines switch to Python post-accumulate readiness hooks first
+(``prepare_capture``: the native hooks hold AccumulateGrad nodes bound to the eager stream), the hooks run once
+while capturing and the RCCL launches they make are recorded; the xGMI mesh is bypassed while capturing (its
+epochs are host-issued kernel arguments).  Pinned on one GPU by
+tests/test_kernels_gpu.py::test_graphed_ddp_step_captures_hook_driven_rccl_collectives (a one-rank RCCL group
+with the engine's hooks armed as at world 2) and on CPU by the ``capture_safe_hooks`` engine tests.
+
     step = GraphedStep(train_step, x_static, y_static, warmup=3)
     for x, y in loader:
         loss = step(x, y)        # copies into the static buffers, replays the graph

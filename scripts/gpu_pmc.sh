@@ -3,7 +3,7 @@
 set -u
 PROBE=${PROBE:-scripts/pmc_kernels.py}
 export PYTHONPATH=.
-OUT=gpurun_out
+OUT=${OUT:-gpurun_out}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 200 python $PROBE > $OUT/probe_plain.log 2>&1 || exit $?

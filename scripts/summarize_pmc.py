@@ -25,7 +25,7 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             full = r.get("Kernel_Name", "?")
-            m = re.search(r"((?:fa_|win_attn|bn_|norm_|adamw|swin_mlp|fp8_cast|wgrad_kernel|gemm_kernel|Custom_Cijk|Cijk)\w*)(<[^()]*>)?", full)
+            m = re.search(r"((?:fa_|win_attn|bn_|norm_|adamw|swin_mlp|fp8_cast|wgrad_kernel|gemm_kernel|gemm_asm|Custom_Cijk|Cijk)\w*)(<[^()]*>)?", full)
             if m:
                 acc[(m.group(1) + (m.group(2) or ""))[:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
@@ -38,6 +38,10 @@ def derived(c):
     out = []
     if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
         out.append(f"MFMA_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (SIMD_CYCLES_PER_GRBM * c['GRBM_GUI_ACTIVE']):.3f}")
+    if c.get("SQ_INSTS_MFMA") and c.get("SQ_INSTS_VALU") is not None:
+        out.append(f"VALU_per_MFMA={(c['SQ_INSTS_VALU'] - c['SQ_INSTS_MFMA']) / c['SQ_INSTS_MFMA']:.2f}")
+    if c.get("SQ_INSTS_MFMA") and c.get("SQ_INSTS_LDS") is not None:
+        out.append(f"LDS_per_MFMA={c['SQ_INSTS_LDS'] / c['SQ_INSTS_MFMA']:.2f}")
     return out
 
 

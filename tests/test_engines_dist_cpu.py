@@ -79,6 +79,38 @@ def test_ddp_matches_single_process(world, accum):
         assert torch.allclose(outs[0][k], ref[k], atol=2e-5), k
 
 
+def _w_ddp_capture_hooks(rank, world, accum):
+    """DDP after ``prepare_capture`` (Trainer.graph at world > 1): Python post-accumulate hooks instead of the
+    native AccumulateGrad hooks, including across the first-iteration bucket rebuild."""
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    m = _model()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.001, first_bucket_mb=0.0005)
+    ddp.prepare_capture()
+    opt = FusedAdamW(m.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    for s in range(STEPS):
+        for a in range(accum):
+            x, y = _data(s * accum + a, world)
+            ctx = ddp.no_sync() if a < accum - 1 else torch.enable_grad()
+            with ctx:
+                loss = nn.functional.mse_loss(ddp(_shard(x, rank, world)), _shard(y, rank, world)) / accum
+                loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        assert ddp._ready.kind == "python"
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+@pytest.mark.parametrize("world,accum", [(2, 2), (4, 1)])
+def test_ddp_capture_safe_hooks_match_single_process(world, accum):
+    ref = _reference(world, accum=accum)
+    outs = run_workers(_w_ddp_capture_hooks, world, accum)
+    for k in ref:
+        for r in range(1, world):
+            assert torch.allclose(outs[0][k], outs[r][k], atol=0)
+        assert torch.allclose(outs[0][k], ref[k], atol=2e-5), k
+
+
 def _w_ddp_master(rank, world):
     """DDP compute-dtype mode (flat compute copies + fp32 master per group): only FusedAdamW.zero_grad()
     clears the accumulated flat gradient between steps."""
@@ -330,7 +362,7 @@ def test_ddp_broadcasts_only_changed_buffers():
     assert not torch.equal(rm0, rm1)   # each rank's last forward updated with its own batch
 
 
-def _w_zero2(rank, world, mode, accum, compute_bf16):
+def _w_zero2(rank, world, mode, accum, compute_bf16, capture_hooks=False):
     from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
     from pytorch_distributedtraining_amd.parallel.zero import OSS, ShardedDataParallel
     m = _model()
@@ -338,6 +370,9 @@ def _w_zero2(rank, world, mode, accum, compute_bf16):
     opt = OSS(m.parameters(), optim=FusedAdamW, lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4,
               compute_dtype=torch.bfloat16 if compute_bf16 else None)
     model = ShardedDataParallel(m, opt, reduce_buffer_size=512, reduce_mode=mode)
+    if capture_hooks:                    # Trainer.graph at world > 1: Python readiness hooks
+        model.prepare_capture()
+        assert model._ready.kind == "python"
     gbytes = []
     for s in range(STEPS):
         for a in range(accum):
@@ -382,6 +417,15 @@ def test_zero2_reduce_to_owner_matches_and_shards_gradients(world, mode, accum):
             assert min(o[2]) >= mbytes        # ZeRO-1 keeps full gradients
     assert sorted(osd["state"].keys()) == list(range(6))
     assert all(float(e["step"]) == STEPS for e in osd["state"].values())
+
+
+@pytest.mark.parametrize("mode", ["reduce", "all_reduce"])
+def test_zero2_capture_safe_hooks_match_single_process(mode):
+    ref = _reference(2, accum=2)
+    outs = run_workers(_w_zero2, 2, mode, 2, False, True)
+    for k in ref:
+        assert torch.equal(outs[0][0][k], outs[1][0][k])
+        assert torch.allclose(outs[0][0][k], ref[k], atol=2e-5), k
 
 
 def test_zero2_bf16_compute_copy_masters_are_sharded():

@@ -1216,6 +1216,71 @@ def test_graphed_ddp_gpt2_step_with_large_vocab():
             assert d.mean().item() < 5e-5, (k, d.mean().item())
 
 
+def test_graphed_ddp_step_captures_hook_driven_rccl_collectives(tmp_path):
+    """The world > 1 DDP path under HIP-graph capture (Trainer.graph / bench --graph at N > 1): bucket readiness
+    on capture-safe Python hooks (``prepare_capture``), bucket all-reduces launched from those hooks during the
+    capture over RCCL.  One GPU: a one-rank ``nccl`` group with the engine's Comm told world 2, so DDP arms its
+    multi-rank hooks and every bucket goes through ``dist.all_reduce(AVG)`` (identity over one rank) -- the
+    replayed step must match the eager one."""
+    import copy
+    import torch.distributed as dist
+    from pytorch_distributedtraining_amd.models.gpt2 import build_gpt2
+    from pytorch_distributedtraining_amd.optim import FusedAdamW, clip_grad_norm_
+    from pytorch_distributedtraining_amd.parallel.comm import Comm
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributedtraining_amd.utils.graphs import GraphedStep
+    if dist.is_initialized():
+        pytest.skip("a default process group already exists in this process")
+    dist.init_process_group("nccl", init_method="file://" + str(tmp_path / "rdzv"), rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        torch.manual_seed(0)
+        base = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=2, vocab_size=4096).to(DEV)
+
+        def make(capturable):
+            comm = Comm(xgmi=False)
+            comm.world_size = 2                    # arm the multi-rank hooks; the group itself has one rank
+            ddp = DistributedDataParallel(copy.deepcopy(base), comm=comm, compute_dtype=torch.bfloat16,
+                                          bucket_cap_mb=1.0, first_bucket_mb=0.25)
+            params = ddp.optimizer_parameters()
+            opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, capturable=capturable)
+
+            def step(x):
+                opt.zero_grad(set_to_none=False)
+                loss = ddp(x[:, :-1], labels=x[:, 1:])
+                loss.backward()
+                _, coef, _ = clip_grad_norm_(params, 1.0, apply=False)
+                opt.step(grad_scale=coef)
+                return loss.detach()
+            return ddp, comm, step
+
+        g = torch.Generator(device=DEV).manual_seed(1)
+        batches = [torch.randint(0, 4096, (4, 257), device=DEV, generator=g) for _ in range(4)]
+        ddp_e, _, eager = make(False)
+        losses_e = [eager(batches[0]).item() for _ in range(4)] + [eager(b).item() for b in batches[1:]]
+        ddp_g, comm_g, stepg = make(True)
+        assert len(ddp_g.plan) > 2
+        ddp_g.prepare_capture()
+        static = batches[0].clone()
+        graphed = GraphedStep(stepg, static, warmup=3)
+        losses_g = [graphed(batches[0]).item()]
+        assert ddp_g._ready.kind == "python"
+        calls_after_capture = comm_g.stats["calls"]
+        assert calls_after_capture >= 4 * len(ddp_g.plan)       # every bucket, in 3 warm-ups + the capture
+        losses_g += [graphed(b).item() for b in batches[1:]]
+        assert comm_g.stats["calls"] == calls_after_capture     # replays run no Python
+        torch.cuda.synchronize()
+        for a, b in zip(losses_e[3:], losses_g):
+            assert abs(a - b) < 2e-3 * max(1.0, abs(a)), (losses_e, losses_g)
+        se, sg = ddp_e.full_state_dict(), ddp_g.full_state_dict()
+        for k in se:
+            if se[k].dim() >= 2:
+                d = (se[k].float() - sg[k].float()).abs()
+                assert d.mean().item() < 5e-5, (k, d.mean().item())
+    finally:
+        dist.destroy_process_group()
+
+
 def test_llama_packed_rope_gqa_attention_matches_unfused():
     """Llama attention: in-place RoPE on the packed qkv projection + packed GQA flash attention (one packed
     gradient) vs the unfused path (separate rotated q / k tensors, flash_attn on views), fwd and bwd."""
