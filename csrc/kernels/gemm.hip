@@ -863,7 +863,10 @@ bool use_p3(int layout, const GemmArgs& a, int items, int grid) {
   // projection 1,338 -> 1,382, the qkv data gradient (K = 6144) 1,298 -> 1,492 (r4_gemm_p3_nt_shapes_ab.log); wide
   // blocks (c_fc, qkv forward: A re-read from L2) keep the 2-stage program and its next-item prefetch
   const int cb = a.xpr > 0 ? (a.N / TN) / (8 / a.xpr) : a.N / TN;
-  return layout == L_TT ? items > grid : (a.k_per_split >= 8192 || cb <= 8);
+  // TT: only where the token split made the extra items (output below one wave of tiles: the qkv weight
+  // gradient); a many-tile output -- the tied LM head's 1,568 tiles x 2 splits -- ran 7 % slower with it
+  // (15.3 vs 16.4 ms, profiles/r4/r4_lm_head_wgrad_ab.jsonl)
+  return layout == L_TT ? (items > grid && (a.M / TM) * (a.N / TN) < grid) : (a.k_per_split >= 8192 || cb <= 8);
 }
 
 template <int LAYOUT>

@@ -98,13 +98,18 @@ def tt_splits(m: int, n: int, k: int, cus: int = 256) -> int:
         return 1
     if tiles >= cus:
         # a full wave already; split only to rescue a badly quantised last wave (GPT-2's LM-head weight gradient:
-        # 1,568 tiles = 6.125 waves of 256 CUs run as 7; 2 slices = 12.25 -> 13, 94 % vs 87.5 % of the rounds busy)
+        # 1,568 tiles = 6.125 waves of 256 CUs run as 7; 2 slices = 12.25 -> 13 rounds, 4 slices 24.5 -> 25:
+        # 87.5 / 94 / 98 % of the rounds busy, measured 16.2 / 15.3 / 14.8 ms, r4_lm_head_wgrad_ab.jsonl)
         eff1 = tiles / (-(-tiles // cus) * cus)
-        if eff1 < 0.9 and k % (32 * 2) == 0 and k // 2 >= 4096:
-            eff2 = 2 * tiles / (-(-(2 * tiles) // cus) * cus)
-            if eff2 > eff1 + 0.05:
-                return 2
-        return 1
+        best, best_eff = 1, eff1
+        if eff1 < 0.9:
+            for s in (2, 4):
+                if k % (32 * s) or k // s < 4096:
+                    break
+                eff = s * tiles / (-(-(s * tiles) // cus) * cus)
+                if eff > best_eff + 0.03:
+                    best, best_eff = s, eff
+        return best if best_eff > eff1 + 0.05 else 1
     best, best_eff = 1, 0.0
     for s in (1, 2, 4, 8, 16):
         if s > 1 and (k % (32 * s) or k // s < 4096):
