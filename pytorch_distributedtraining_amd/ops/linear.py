@@ -242,6 +242,12 @@ def _bgrad_in_gemm(dy2: torch.Tensor, w: torch.Tensor) -> bool:
             and not _tall_skinny(m, n, k) and _split_k(m, n, k) == 1 and n % 8 == 0 and k % 8 == 0 and colsum_ok(n))
 
 
+def _as_output(t: torch.Tensor, shape) -> torch.Tensor:
+    """A Function's forward output in its final shape WITHOUT being a view: autograd forbids in-place updates of
+    view outputs created inside a custom Function (Llama's RoPE rotates the qkv projection in place)."""
+    return torch.ops.aten._unsafe_view(t, shape)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -249,7 +255,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_bias = bias is not None
         x2 = x.reshape(-1, x.shape[-1])
         if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
-            return nt_matmul(x2, weight, bias).view(*x.shape[:-1], weight.shape[0])
+            return _as_output(nt_matmul(x2, weight, bias), (*x.shape[:-1], weight.shape[0]))
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -324,7 +330,7 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         y, pre = G.gemm_nt_gelu(x2, weight, bias)
         ctx.save_for_backward(x2, weight, pre)
         ctx.xshape = x.shape
-        return y.view(*x.shape[:-1], weight.shape[0])
+        return _as_output(y, (*x.shape[:-1], weight.shape[0]))
 
     @staticmethod
     def backward(ctx, dy):
@@ -387,7 +393,7 @@ class _GeluMlpFn(torch.autograd.Function):
         out = F.linear(y1, w2, b2)
         ctx.save_for_backward(x2, w1, pre, y1, w2)
         ctx.xshape = x.shape
-        return out.view(*x.shape[:-1], w2.shape[0])
+        return _as_output(out, (*x.shape[:-1], w2.shape[0]))
 
     @staticmethod
     def backward(ctx, dout):

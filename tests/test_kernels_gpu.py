@@ -1281,6 +1281,25 @@ def test_graphed_ddp_step_captures_hook_driven_rccl_collectives(tmp_path):
         dist.destroy_process_group()
 
 
+def test_linear_output_accepts_inplace_updates_on_hand_gemm_path(monkeypatch):
+    """The framework Linear's forward output on the hand NT GEMM path is a plain tensor, not a view created inside
+    the autograd Function: Llama's RoPE rotates the qkv projection in place (a view output would raise), and the
+    gradients through the in-place update match fp32."""
+    from pytorch_distributedtraining_amd.ops import linear as L
+    monkeypatch.setattr(L, "HIP_NT", "1")
+    torch.manual_seed(0)
+    x = torch.randn(2, 2048, 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(768, 512, device=DEV) / 23).bfloat16().requires_grad_()
+    y = L.linear(x, w)
+    assert not y._is_view()
+    y.mul_(2.0)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr, wr = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    ((xr @ wr.t()) * 2.0 * g.float()).sum().backward()
+    assert rel_err(x.grad, xr.grad) < 1e-2 and rel_err(w.grad, wr.grad) < 1e-2
+
+
 def test_llama_packed_rope_gqa_attention_matches_unfused():
     """Llama attention: in-place RoPE on the packed qkv projection + packed GQA flash attention (one packed
     gradient) vs the unfused path (separate rotated q / k tensors, flash_attn on views), fwd and bwd."""
