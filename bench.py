@@ -428,6 +428,12 @@ def bench_gpt2(args, comm, dev, world, rank):
             state["i"] += 1
             state["loss"] = graphed(b)
     if ckpt_on and args.act_ckpt_layers == "auto":
+        # two fully checkpointed steps, the peak taken over the second: the first one also runs the once-per-shape
+        # kernel timings (ops.linear / ops.blaslt choices), whose transient buffers would inflate the peak and
+        # make the sizing recompute every layer
+        step()
+        torch.cuda.synchronize(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
         step()
         torch.cuda.synchronize(dev)
         size_checkpointing()
