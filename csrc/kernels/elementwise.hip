@@ -60,10 +60,18 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_kernel(const T* __restrict__
   }
 }
 
+// ACT 0: erf GELU, 1: tanh GELU of (h + bias); 2: h already holds the GELU derivative (gemm.hip E_GELU's kept
+// output): the backward is a multiply, no transcendental, no bias
+template <int ACT>
+__device__ __forceinline__ float act_grad(float v, float b) {
+  if constexpr (ACT == 2) return v;
+  else return gelu_grad<ACT == 1>(v + b);
+}
+
 // GELU backward fused with the bias gradient: workgroups sweep (2048-column group) x (row chunk) as in
 // reduce.h; each thread keeps its 8 columns' dbias partial sums in registers while it writes dh, so the
 // bias gradient costs no second pass over the [rows, N] activation gradient.
-template <typename T, typename B, bool TANH>
+template <typename T, typename B, int ACT>
 __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restrict__ dy, const T* __restrict__ h,
                                                               const B* __restrict__ bias, T* __restrict__ dh,
                                                               int rows, int N, int rows_per,
@@ -73,9 +81,9 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restric
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(rows, r0 + rows_per);
   float b[8], acc[8];
-  Vec8<B>::load(bias + col, b);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int k = 0; k < 8; ++k) { acc[k] = 0.f; b[k] = 0.f; }
+  if (ACT != 2) Vec8<B>::load(bias + col, b);
   int r = r0;
   for (; r + 4 <= r1; r += 4) {   // 8 loads in flight per thread (2 rows held it at ~5.2 TB/s)
     float v[4][8], g[4][8];
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restric
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        g[u][k] *= gelu_grad<TANH>(v[u][k] + b[k]);
+        g[u][k] *= act_grad<ACT>(v[u][k], b[k]);
         acc[k] += g[u][k];
       }
       Vec8<T>::store(dh + (int64_t)(r + u) * N + col, g[u]);
@@ -100,7 +108,7 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restric
     Vec8<T>::load(dy + (int64_t)r * N + col, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      g[k] *= gelu_grad<TANH>(v[k] + b[k]);
+      g[k] *= act_grad<ACT>(v[k], b[k]);
       acc[k] += g[k];
     }
     Vec8<T>::store(dh + (int64_t)r * N + col, g);
@@ -111,7 +119,7 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_kernel(const T* __restric
 // Narrow rows (N < 2048, e.g. the SwinIR-S MLP's 120): the column-group mapping above would leave all but
 // N/8 threads of a workgroup idle; here the workgroup covers NT / (N/8) rows per pass (coalesced: adjacent
 // rows are adjacent in memory) and folds its row groups through LDS into ONE partial row.
-template <typename T, typename B, bool TANH>
+template <typename T, typename B, int ACT>
 __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_narrow(const T* __restrict__ dy, const T* __restrict__ h,
                                                               const B* __restrict__ bias, T* __restrict__ dh,
                                                               int rows, int N, int rows_per,
@@ -123,7 +131,7 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_narrow(const T* __restric
   float b[8], acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { acc[k] = 0.f; b[k] = 0.f; }
-  if (act) Vec8<B>::load(bias + col, b);
+  if (act && ACT != 2) Vec8<B>::load(bias + col, b);
   const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
   if (act) {
     for (int r = r0 + rg; r < r1; r += rpb) {
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_narrow(const T* __restric
       Vec8<T>::load(dy + (int64_t)r * N + col, g);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        g[k] *= gelu_grad<TANH>(v[k] + b[k]);
+        g[k] *= act_grad<ACT>(v[k], b[k]);
         acc[k] += g[k];
       }
       Vec8<T>::store(dh + (int64_t)r * N + col, g);
@@ -357,23 +365,30 @@ PDT_API int pdt_bias_gelu_bwd(const void* dy, const void* h, const void* bias, v
   return (int)hipGetLastError();
 }
 
-// dh = dy * gelu'(h + bias) and dbias[N] (+= if accumulate) in one sweep; ws: pdt_colsum_ws_floats(rows, N)
+// dh = dy * gelu'(h + bias) and dbias[N] (+= if accumulate) in one sweep; ws: pdt_colsum_ws_floats(rows, N).
+// tanh_approx: 0 erf, 1 tanh, 2 "h is gelu'(pre-activation)" (dh = dy * h; bias unused, may be null)
 PDT_API int pdt_bias_gelu_bwd_db(const void* dy, const void* h, const void* bias, void* dh, void* dbias, float* ws,
                                  int rows, int N, int dt, int bdt, int tanh_approx, int accumulate, hipStream_t st) {
-  if (N % 8 != 0 || bias == nullptr) return (int)hipErrorInvalidValue;
+  if (N % 8 != 0 || (bias == nullptr && tanh_approx != 2) || tanh_approx < 0 || tanh_approx > 2)
+    return (int)hipErrorInvalidValue;
   const red::ColPlan pl = red::col_plan(rows, N);
   dim3 grid(pl.col_groups, pl.R);
   const bool narrow = N < 8 * NT;   // one column group: use the row-packed kernel (same partial layout)
-#define PDT_L(T, B, TH)                                                                                          \
-  if (narrow) bias_gelu_bwd_db_narrow<T, B, TH><<<pl.R, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias,  \
-                                                                      (T*)dh, rows, N, pl.rows_per, ws);         \
-  else bias_gelu_bwd_db_kernel<T, B, TH><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh, \
-                                                              rows, N, pl.rows_per, ws)
-  if (dt == kBF16 && bdt == kBF16) { if (tanh_approx) PDT_L(bf16_t, bf16_t, true); else PDT_L(bf16_t, bf16_t, false); }
-  else if (dt == kBF16 && bdt == kF32) { if (tanh_approx) PDT_L(bf16_t, float, true); else PDT_L(bf16_t, float, false); }
-  else if (dt == kF32 && bdt == kF32) { if (tanh_approx) PDT_L(float, float, true); else PDT_L(float, float, false); }
-  else if (dt == kF32 && bdt == kBF16) { if (tanh_approx) PDT_L(float, bf16_t, true); else PDT_L(float, bf16_t, false); }
+#define PDT_L(T, B, A)                                                                                           \
+  if (narrow) bias_gelu_bwd_db_narrow<T, B, A><<<pl.R, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias,   \
+                                                                     (T*)dh, rows, N, pl.rows_per, ws);          \
+  else bias_gelu_bwd_db_kernel<T, B, A><<<grid, NT, 0, st>>>((const T*)dy, (const T*)h, (const B*)bias, (T*)dh,  \
+                                                             rows, N, pl.rows_per, ws)
+#define PDT_ACT(T, B)                            \
+  if (tanh_approx == 2) { PDT_L(T, B, 2); }      \
+  else if (tanh_approx == 1) { PDT_L(T, B, 1); } \
+  else { PDT_L(T, B, 0); }
+  if (dt == kBF16 && bdt == kBF16) { PDT_ACT(bf16_t, bf16_t); }
+  else if (dt == kBF16 && bdt == kF32) { PDT_ACT(bf16_t, float); }
+  else if (dt == kF32 && bdt == kF32) { PDT_ACT(float, float); }
+  else if (dt == kF32 && bdt == kBF16) { PDT_ACT(float, bf16_t); }
   else return (int)hipErrorInvalidValue;
+#undef PDT_ACT
 #undef PDT_L
   float* ws2 = ws + (int64_t)pl.R * N;
   if (bdt == kBF16) red::col_reduce<bf16_t>(ws, pl.R, N, (bf16_t*)dbias, ws2, accumulate, st);

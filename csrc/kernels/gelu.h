@@ -20,6 +20,25 @@ __device__ __forceinline__ float sigmoid2z(float u) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a));
 }
 
+// GELU value AND derivative of two pre-activations per packed instruction (v_pk_fma / v_pk_mul; exp2 / rcp stay
+// scalar), sharing the one sigmoid: y = u s, d = s + u s (1 - s) 2 sqrt(2/pi) (1 + 3 c u^2).  The GEMM epilogue of
+// GPT-2's c_fc stores d instead of the pre-activation, so the backward's GELU step is one multiply (no
+// transcendentals where the matrix pipe idles, gemm.hip E_DGELU) -- both GEMM kernels call this one function,
+// so their results stay bitwise equal.
+typedef float gelu_f32x2 __attribute__((ext_vector_type(2)));
+constexpr float kGeluD1 = 2.f * 0.7978845608028654f;
+constexpr float kGeluD3 = kGeluD1 * 3.f * 0.044715f;
+__device__ __forceinline__ void gelu_fwd_grad2(gelu_f32x2 u, gelu_f32x2& y, gelu_f32x2& d) {
+  const gelu_f32x2 u2 = u * u;
+  const gelu_f32x2 a = u * __builtin_elementwise_fma(gelu_f32x2{kGeluB, kGeluB}, u2, gelu_f32x2{kGeluA, kGeluA});
+  const gelu_f32x2 e = gelu_f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])} + gelu_f32x2{1.f, 1.f};
+  const gelu_f32x2 s = gelu_f32x2{__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
+  y = u * s;
+  const gelu_f32x2 t = __builtin_elementwise_fma(-s, s, s);                                   // s (1 - s)
+  const gelu_f32x2 q = __builtin_elementwise_fma(gelu_f32x2{kGeluD3, kGeluD3}, u2, gelu_f32x2{kGeluD1, kGeluD1});
+  d = __builtin_elementwise_fma(u * t, q, s);
+}
+
 template <bool TANH>
 __device__ __forceinline__ float gelu_f(float u) {
   if (TANH) {

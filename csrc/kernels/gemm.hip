@@ -7,9 +7,11 @@
 // Epilogues (the reason this kernel exists next to hipBLASLt, whose GELU_AUX_BIAS / DGELU_BGRAD epilogues
 // are unsupported on gfx950, profiles/r2_hipblaslt_epilogue_probe.txt):
 //   PLAIN   C = bf16(acc)                         BIAS   C = bf16(acc + bias[n])
-//   GELU    pre = acc + bias[n] -> aux_out (bf16), C = gelu_tanh(pre)   (GPT-2 c_fc: one pass, no bias_gelu)
-//   DGELU   g = acc * gelu_tanh'(aux[m, n]) -> C, per-tile column sums of g -> ws (fp32) -> dbias
-//           (GPT-2 c_proj dgrad + GELU backward + bias gradient of c_fc: no bias_gelu_bwd_db pass)
+//   GELU    h = bf16(acc + bias[n]); C = gelu_tanh(h), aux_out = gelu_tanh'(h) (bf16)   (GPT-2 c_fc: one pass,
+//           the derivative -- not the pre-activation -- is what the backward keeps)
+//   DGELU   g = acc * aux[m, n] (the stored derivative) -> C, per-tile column sums of g -> ws (fp32) -> dbias
+//           (GPT-2 c_proj dgrad + GELU backward + bias gradient of c_fc: no bias_gelu_bwd_db pass, and no
+//           transcendental in an epilogue that runs while the matrix pipe idles)
 //   F32     fp32 split-K partial slab (reduced by splitk_reduce_kernel)
 //
 // Main loop (cdna_hip_programming.md §5): 256 x 256 output tile per 512-thread workgroup, 8 waves as
@@ -159,8 +161,8 @@ struct GemmArgs {
   const bf16_t* B;
   void* C;
   const bf16_t* bias;     // E_BIAS / E_GELU: [N]
-  const bf16_t* aux;      // E_DGELU: pre-activation [M, ldc]
-  bf16_t* aux_out;        // E_GELU: pre-activation out [M, ldc]
+  const bf16_t* aux;      // E_DGELU: gelu'(pre-activation) [M, ldc], as E_GELU wrote it
+  bf16_t* aux_out;        // E_GELU: gelu'(pre-activation) out [M, ldc]
   float* ws;              // E_F32: slabs [splits][M][N]; E_DGELU: column partials [M / 256][N]
   int M, N, K;
   int64_t lda, ldb, ldc;
@@ -381,19 +383,23 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][j][r] + bj[j][r]);
         } else if constexpr (EPI == E_GELU) {
-          u16x4 pre;
+          // GELU and its derivative of the ROUNDED (bf16) pre-activation, as an unfused bf16 Linear + GELU
+          // computes them; the derivative is kept for the backward (aux_out)
+          u16x4 dd;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const bf16_t h = f2bf(acc[i][j][r] + bj[j][r]);
-            pre[r] = h;
-            o[r] = f2bf(gelu_f<true>(bf2f(h)));   // GELU of the stored (rounded) pre-activation
+          for (int r = 0; r < 4; r += 2) {
+            gelu_f32x2 y2, d2;
+            gelu_fwd_grad2(gelu_f32x2{bf2f(f2bf(acc[i][j][r] + bj[j][r])), bf2f(f2bf(acc[i][j][r + 1] + bj[j][r + 1]))},
+                           y2, d2);
+            o[r] = f2bf(y2[0]); o[r + 1] = f2bf(y2[1]);
+            dd[r] = f2bf(d2[0]); dd[r + 1] = f2bf(d2[1]);
           }
-          *reinterpret_cast<u16x4*>(p.aux_out + e) = pre;
-        } else {   // E_DGELU
+          *reinterpret_cast<u16x4*>(p.aux_out + e) = dd;
+        } else {   // E_DGELU: aux holds gelu'(pre) as E_GELU stored it
           const u16x4 h = *reinterpret_cast<const u16x4*>(p.aux + e);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float g = acc[i][j][r] * gelu_grad<true>(bf2f(h[r]));
+            const float g = acc[i][j][r] * bf2f(h[r]);
             const bf16_t gb = f2bf(g);
             o[r] = gb;
             cs[j][r] += bf2f(gb);   // the bias gradient sums the gradient as stored
@@ -443,16 +449,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_kernel(GemmArgs p) {
 #include "gemm_kloop.inc"
 namespace {
 
-// tanh-form GELU of two values per packed instruction (v_pk_mul / v_pk_fma / v_pk_add; exp2 / rcp stay scalar):
-// u * sigmoid(2z), the gelu.h identity
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 gelu_tanh2(f32x2 u) {
-  const f32x2 t = __builtin_elementwise_fma(f32x2{kGeluB, kGeluB}, u * u, f32x2{kGeluA, kGeluA});
-  const f32x2 a = u * t;
-  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])} + f32x2{1.f, 1.f};
-  return u * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-}
-
 constexpr int RING = 2 * STB;                // the two ring stages (128 KiB)
 constexpr int STAGE_BYTES = 32768;          // epilogue staging: LDS past the ring, 64 rows x 512 B per round
 constexpr int SMEM3 = RING + STAGE_BYTES;   // 160 KiB: all of the CU's LDS
@@ -493,23 +489,41 @@ __device__ __forceinline__ void stg_read(const char* img, u16x8 (&buf)[8], int w
     buf[it] = *reinterpret_cast<const u16x8*>(img + q * 512 + ((c16 ^ (q & 15)) & 15 | (c16 & 16)) * 16);
   }
 }
-__device__ __forceinline__ void stg_write_out(const u16x8 (&buf)[8], bf16_t* dst, int64_t ldc, int m0, int n0, int r,
-                                              int w, int lane) {
+// Global side of the staging rounds through buffer instructions: ONE per-lane byte offset (lane term + the wave's
+// rows) and a scalar per-(round, row pair) offset, instead of a 64-bit address per row and round that the compiler
+// precomputes and keeps live (the DGELU epilogue spilled those).  Resource = the 256 x 256 tile at (m0, n0).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const bf16_t* base, int64_t ldc, int m0, int n0) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)m0 * ldc + n0), (short)0,
+                                           (int)((255 * ldc + 256) * 2), 0x00020000);
+}
+// lane offset of image row q = 16 w + 2 it + (lane >> 5), chunk lane & 31 (it = 0); global row stg_row(r, q)
+__device__ __forceinline__ uint32_t stg_voff(int64_t ldc, int w, int lane) {
+  return (uint32_t)(128 * (w >> 1) + 16 * (w & 1) + (lane >> 5)) * ((uint32_t)ldc * 2u) + (uint32_t)(lane & 31) * 16u;
+}
+// sum over the 16 lanes of a DPP row (quad swaps, then half-row and row mirrors): no lane-index registers, unlike
+// __shfl_xor's ds_bpermute (whose hoisted index VGPRs spilled in the DGELU kernel)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));    // quad (1,0,3,2)
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));    // quad (2,3,0,1)
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));   // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));   // row_mirror
+  return v;
+}
+__device__ __forceinline__ void stg_write_out(const u16x8 (&buf)[8], __amdgpu_buffer_rsrc_t rs, uint32_t vo,
+                                              uint32_t ldc2, int r) {
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int q = 16 * w + 2 * it + (lane >> 5);
-    *reinterpret_cast<u16x8*>(dst + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31)) = buf[it];
-  }
+  for (int it = 0; it < 8; ++it)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, buf[it]), rs, (int)vo,
+                                           (int)((32 * r + 2 * it) * ldc2), 0);
 }
 // DGELU: the aux rows of round r (the same mapping as the write-out, reversed): fetched into registers a round
 // ahead (stg_fetch), put into the image when the round starts (stg_put)
-__device__ __forceinline__ void stg_fetch(u16x8 (&t)[8], const bf16_t* src, int64_t ldc, int m0, int n0, int r, int w,
-                                          int lane) {
+__device__ __forceinline__ void stg_fetch(u16x8 (&t)[8], __amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t ldc2, int r) {
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int q = 16 * w + 2 * it + (lane >> 5);
-    t[it] = *reinterpret_cast<const u16x8*>(src + (int64_t)(m0 + stg_row(r, q)) * ldc + n0 + 8 * (lane & 31));
-  }
+  for (int it = 0; it < 8; ++it)
+    t[it] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo,
+                                                                            (int)((32 * r + 2 * it) * ldc2), 0));
 }
 __device__ __forceinline__ void stg_put(char* img, const u16x8 (&t)[8], int w, int lane) {
 #pragma unroll
@@ -517,6 +531,114 @@ __device__ __forceinline__ void stg_put(char* img, const u16x8 (&t)[8], int w, i
     const int q = 16 * w + 2 * it + (lane >> 5), c16 = lane & 31;
     *reinterpret_cast<u16x8*>(img + q * 512 + ((c16 ^ (q & 15)) & 15 | (c16 & 16)) * 16) = t[it];
   }
+}
+// DGELU round 0 by LDS-DMA, issued BEFORE the item's main loop: the aux rows of round 0 land straight in the
+// staging image (idle during the loop) under the first K-step, so the epilogue's first round waits on nothing.
+// Piece i of wave w fills image rows q = 16 w + 2 i + (lane >> 5), lane-linear 16-byte positions p = lane & 31;
+// position p of row q holds the image's swizzled chunk, i.e. logical chunk ((p ^ q) & 15) | (p & 16) (the XOR is
+// an involution), whose global row is stg_row(0, q): the swizzle rides on the per-lane source offset (rule 21).
+// Every wave waits for these 8 pieces (vmcnt, in order) and passes a barrier inside the main loop before the
+// epilogue reads the image.
+__device__ __forceinline__ void stg_dma_round0(const bf16_t* src, int64_t ldc, int m0, int n0, uint32_t img_lds,
+                                               int w, int lane) {
+  const uint64_t base = (uint64_t)(uintptr_t)(src + (int64_t)m0 * ldc + n0);
+  v4i rsrc;                                       // (kernel arguments and item coordinates: already scalar)
+  rsrc[0] = (int)(uint32_t)base;
+  rsrc[1] = (int)((base >> 32) & 0xffff);
+  rsrc[2] = (int)(uint32_t)((255 * ldc + 256) * 2);
+  rsrc[3] = 0x00020000;
+  const int hi = lane >> 5, p = lane & 31;
+  const uint32_t row0 = (uint32_t)(128 * (w >> 1) + 16 * (w & 1));
+  const uint32_t ldc2 = (uint32_t)ldc * 2u;       // 32-bit lane math (a 64-bit product wants a VGPR copy of ldc)
+  uint32_t vo[8], so[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t c16 = (uint32_t)(((p ^ (2 * i + hi)) & 15) | (p & 16));
+    vo[i] = (uint32_t)hi * ldc2 + c16 * 16u;
+    so[i] = __builtin_amdgcn_readfirstlane((row0 + 2 * i) * ldc2);
+  }
+  const uint32_t m = __builtin_amdgcn_readfirstlane(img_lds + 16 * w * 512);
+  asm volatile(
+      "s_mov_b32 m0, %[m]\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v0], %[rs], %[s0] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v1], %[rs], %[s1] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v2], %[rs], %[s2] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v3], %[rs], %[s3] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v4], %[rs], %[s4] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v5], %[rs], %[s5] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v6], %[rs], %[s6] offen lds\n\t"
+      "s_add_u32 m0, m0, 1024\n\ts_nop 0\n\tbuffer_load_dwordx4 %[v7], %[rs], %[s7] offen lds"
+      :
+      : [m] "s"(m), [rs] "s"(rsrc), [v0] "v"(vo[0]), [v1] "v"(vo[1]), [v2] "v"(vo[2]), [v3] "v"(vo[3]),
+        [v4] "v"(vo[4]), [v5] "v"(vo[5]), [v6] "v"(vo[6]), [v7] "v"(vo[7]), [s0] "s"(so[0]), [s1] "s"(so[1]),
+        [s2] "s"(so[2]), [s3] "s"(so[3]), [s4] "s"(so[4]), [s5] "s"(so[5]), [s6] "s"(so[6]), [s7] "s"(so[7])
+      : "memory", "scc");
+}
+
+// The thread id for one item's per-lane terms, rebuilt from the wave index (SGPR) and the lane id (v_mbcnt) behind an
+// opaque asm: no VGPR -- not even threadIdx.x -- has to stay live across the persistent loop's main-loop statements
+// (a spilled one is reloaded from scratch with a vmcnt(0) that drains the prefetched K-tiles and epilogue stores).
+__device__ __forceinline__ int item_tid(int wv) {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return wv * 64 + l;
+}
+// A scalar the compiler must treat as unknown at this point: integer divisions by it are expanded here, per item,
+// instead of hoisting their (VGPR) float reciprocals out of the persistent loop.
+__device__ __forceinline__ int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+// Epilogue operands loaded BEFORE an item's main loop by inline-asm buffer loads, i.e. invisible to the compiler's
+// waitcnt pass: a compiler-issued load pending across the main-loop statement is waited for with vmcnt(0) after it,
+// which drains the next item's prefetched K-tiles (gen_gemm_kloop.py next_tail).  Every path through the main loop
+// waits (in order) for all vector-memory ops older than its last DMA, so these have landed when it ends; `settle`
+// (an empty volatile asm after the main loop, ordered after it like every volatile asm) makes each use depend on
+// that point.  Bias: the lane's 8 x 4 columns (immediate offsets 32 B apart); DGELU: round 1 of the derivative rows.
+__device__ __forceinline__ v4i scalar_rsrc(const void* base, uint32_t nbytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  v4i r;
+  r[0] = (int)(uint32_t)a; r[1] = (int)((a >> 32) & 0xffff); r[2] = (int)nbytes; r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void preload_bias(u16x4 (&b)[8], const bf16_t* bias, int n0, int lcol) {
+  const v4i rs = scalar_rsrc(bias + n0, 512);
+  const uint32_t vo = (uint32_t)lcol * 2u;
+  asm volatile("buffer_load_dwordx2 %0, %8, %9, 0 offen offset:0\n\t"
+               "buffer_load_dwordx2 %1, %8, %9, 0 offen offset:32\n\t"
+               "buffer_load_dwordx2 %2, %8, %9, 0 offen offset:64\n\t"
+               "buffer_load_dwordx2 %3, %8, %9, 0 offen offset:96\n\t"
+               "buffer_load_dwordx2 %4, %8, %9, 0 offen offset:128\n\t"
+               "buffer_load_dwordx2 %5, %8, %9, 0 offen offset:160\n\t"
+               "buffer_load_dwordx2 %6, %8, %9, 0 offen offset:192\n\t"
+               "buffer_load_dwordx2 %7, %8, %9, 0 offen offset:224"
+               : "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6]),
+                 "=&v"(b[7])
+               : "v"(vo), "s"(rs)
+               : "memory");
+}
+__device__ __forceinline__ void preload_round1(u16x8 (&t)[8], const bf16_t* src, int64_t ldc, int m0, int n0,
+                                               uint32_t vo) {
+  const v4i rs = scalar_rsrc(src + (int64_t)m0 * ldc + n0, (uint32_t)((255 * ldc + 256) * 2));
+  const uint32_t l2 = (uint32_t)ldc * 2u;
+  asm volatile("buffer_load_dwordx4 %0, %8, %9, %10 offen\n\t"
+               "buffer_load_dwordx4 %1, %8, %9, %11 offen\n\t"
+               "buffer_load_dwordx4 %2, %8, %9, %12 offen\n\t"
+               "buffer_load_dwordx4 %3, %8, %9, %13 offen\n\t"
+               "buffer_load_dwordx4 %4, %8, %9, %14 offen\n\t"
+               "buffer_load_dwordx4 %5, %8, %9, %15 offen\n\t"
+               "buffer_load_dwordx4 %6, %8, %9, %16 offen\n\t"
+               "buffer_load_dwordx4 %7, %8, %9, %17 offen"
+               : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]),
+                 "=&v"(t[7])
+               : "v"(vo), "s"(rs), "s"(32 * l2), "s"(34 * l2), "s"(36 * l2), "s"(38 * l2), "s"(40 * l2),
+                 "s"(42 * l2), "s"(44 * l2), "s"(46 * l2)
+               : "memory");
+}
+template <class V, int N>
+__device__ __forceinline__ void settle(V (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i]));
 }
 
 // Per-item operands of the main-loop / next-item statements (gen_gemm_kloop.py): buffer resources of the item's
@@ -573,14 +695,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
   const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void*)smem;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 1, wc = w & 1;
+  const int wv = __builtin_amdgcn_readfirstlane(w);   // the wave index in an SGPR (see item_tid)
   const int ntiles = (p.M / TM) * (p.N / TN);
   const int splits = (p.K + p.k_per_split - 1) / p.k_per_split;
   const int nall = ntiles * splits;
 
-  // ---- item-independent operands
+  // ---- item-independent operands (scalar)
   uint64_t astep, bstep;
   uint32_t abytes, bbytes, rsa, rsb;
-  uint32_t voa0, voa1, vob0, vob1, rd0, rd1;
   int32_t db;
   if (LAYOUT == L_NT) {
     astep = bstep = KB * 2;
@@ -588,13 +710,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     bbytes = (uint32_t)((TN - 1) * p.ldb * 2 + KB * 2);
     rsa = (uint32_t)(32 * p.lda * 2);
     rsb = (uint32_t)(32 * p.ldb * 2);
-    const int row = 8 * w + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
-    voa0 = voa1 = (uint32_t)(row * p.lda * 2 + c * 16);
-    vob0 = vob1 = (uint32_t)(row * p.ldb * 2 + c * 16);
-    const int x = lane & 15, g = lane >> 4, h = (x >> 1) & 7;
-    rd0 = lds_addr + 16384 * wr + (uint32_t)(x * 128 + 16 * (g ^ h));
-    rd1 = lds_addr + 16384 * wr + (uint32_t)(x * 128 + 16 * ((4 + g) ^ h));
     db = OPB + 16384 * (wc - wr);
   } else {
     astep = (uint64_t)KB * p.lda * 2;
@@ -603,25 +718,43 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     bbytes = (uint32_t)((KB - 1) * p.ldb * 2 + TN * 2);
     rsa = (uint32_t)(8 * p.lda * 2);
     rsb = (uint32_t)(8 * p.ldb * 2);
-    const int r0 = 2 * w + (lane >> 5);
-    voa0 = (uint32_t)(r0 * p.lda * 2 + ((lane & 31) ^ tt_f(r0)) * 16);
-    voa1 = (uint32_t)(r0 * p.lda * 2 + ((lane & 31) ^ tt_f(r0 + 8)) * 16);
-    vob0 = (uint32_t)(r0 * p.ldb * 2 + ((lane & 31) ^ tt_f(r0)) * 16);
-    vob1 = (uint32_t)(r0 * p.ldb * 2 + ((lane & 31) ^ tt_f(r0 + 8)) * 16);
-    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    rd0 = lds_addr + 256 * wr + (uint32_t)((8 * g + q) * 512 + 16 * (pp >> 1) + 8 * (pp & 1));
-    rd1 = (uint32_t)tt_f(8 * g + q);     // the block XOR term
     db = OPB + 256 * (wc - wr);
   }
+  // per-lane operands of the main-loop statement (DMA source offsets, LDS read addresses) from thread id t --
+  // evaluated every item from an opaque copy of the thread id, so nothing per-lane stays live across the epilogue
+  // (where it would be spilled, and its reload's vmcnt(0) would drain the next item's prefetched K-tiles and the
+  // epilogue's stores in front of every main loop)
+  auto lane_ops = [&](int t, uint32_t& voa0, uint32_t& voa1, uint32_t& vob0, uint32_t& vob1, uint32_t& rd0,
+                      uint32_t& rd1) {
+    const int lw = t >> 6, ll = t & 63, lwr = lw >> 1;
+    if (LAYOUT == L_NT) {
+      const int row = 8 * lw + (ll >> 3);
+      const int c = (ll & 7) ^ ((row >> 1) & 7);
+      voa0 = voa1 = (uint32_t)(row * p.lda * 2 + c * 16);
+      vob0 = vob1 = (uint32_t)(row * p.ldb * 2 + c * 16);
+      const int x = ll & 15, g = ll >> 4, h = (x >> 1) & 7;
+      rd0 = lds_addr + 16384 * lwr + (uint32_t)(x * 128 + 16 * (g ^ h));
+      rd1 = lds_addr + 16384 * lwr + (uint32_t)(x * 128 + 16 * ((4 + g) ^ h));
+    } else {
+      const int r0 = 2 * lw + (ll >> 5);
+      voa0 = (uint32_t)(r0 * p.lda * 2 + ((ll & 31) ^ tt_f(r0)) * 16);
+      voa1 = (uint32_t)(r0 * p.lda * 2 + ((ll & 31) ^ tt_f(r0 + 8)) * 16);
+      vob0 = (uint32_t)(r0 * p.ldb * 2 + ((ll & 31) ^ tt_f(r0)) * 16);
+      vob1 = (uint32_t)(r0 * p.ldb * 2 + ((ll & 31) ^ tt_f(r0 + 8)) * 16);
+      const int g = ll >> 4, q = (ll >> 2) & 3, pp = ll & 3;
+      rd0 = lds_addr + 256 * lwr + (uint32_t)((8 * g + q) * 512 + 16 * (pp >> 1) + 8 * (pp & 1));
+      rd1 = (uint32_t)tt_f(8 * g + q);     // the block XOR term
+    }
+  };
   const uint32_t m0b = __builtin_amdgcn_readfirstlane(lds_addr + w * 1024);
   const int dbs = __builtin_amdgcn_readfirstlane(db);
   const uint32_t asl = (uint32_t)astep, ash = (uint32_t)(astep >> 32);
   const uint32_t bsl = (uint32_t)bstep, bsh = (uint32_t)(bstep >> 32);
-  // global stores an epilogue issues after the next item's first DMA (the next main loop's first wait skips them)
-  constexpr int NST = EPI == E_F32 ? 64 : EPI == E_GELU ? 64 : 32;
+  // vector-memory ops an epilogue (and the next item's pre-loop loads: round-0 aux DMA + round-1 rows, bias) issues
+  // after the next item's first DMA: the next main loop's first wait skips them (vmcnt counts in issue order; a
+  // smaller count only waits more)
+  constexpr int NST = EPI == E_F32 ? 64 : EPI == E_GELU ? 64 + 8 : EPI == E_DGELU ? 32 + 1 + 8 + 8 : EPI == E_BIAS ? 40 : 32;
   constexpr int WNX = 16 + NST < 63 ? 16 + NST : 63;
-  const int lrow = 128 * wr + (lane & 15);
-  const int lcol = 128 * wc + 4 * (lane >> 4);
   char* const img = smem + RING;
 
 #define PDT_KLOOP_CLOBBERS                                                                                      \
@@ -678,7 +811,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     const int next_item = item + (int)gridDim.x;
     const bool has_next = next_item < nall;
     ItemOps<LAYOUT> nxt = cur;
-    if (has_next) nxt.init(p, next_item, ntiles);
+    if (has_next) {
+      GemmArgs q = p;                    // tile-walk divisors opaque per item (opaque_s)
+      q.M = opaque_s(p.M); q.N = opaque_s(p.N); q.xpr = opaque_s(p.xpr); q.grp = opaque_s(p.grp);
+      q.K = opaque_s(p.K); q.k_per_split = opaque_s(p.k_per_split);
+      nxt.init(q, next_item, opaque_s(ntiles));
+    }
     // the last two K-steps load the next item's first two K-tiles (even K-step counts only: stage parity)
     // integer arithmetic, not a select: a bool-derived operand can be rematerialised as a VGPR v_cndmask
     // (P3, the 3-stage program: no next-item prefetch -- every item runs its own prologue)
@@ -692,6 +830,18 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     lo.blo = __builtin_amdgcn_readfirstlane(lo.blo); lo.bhi = __builtin_amdgcn_readfirstlane(lo.bhi);
     uint64_t st0 = 0, st1 = 0, rt0 = 0;
     if (DIAG) { st0 = stamp(); rt0 = __builtin_amdgcn_s_memrealtime(); }
+    const int ltid = item_tid(wv);     // per-item lane terms (lane_ops)
+    uint32_t voa0, voa1, vob0, vob1, rd0, rd1;
+    lane_ops(ltid, voa0, voa1, vob0, vob1, rd0, rd1);
+    // DGELU: this item's round-0 derivative rows into the (idle) staging image under the main loop, round 1 into
+    // registers; bias epilogues: the bias columns (preload_*)
+    u16x4 pb[8];
+    u16x8 pa[8];
+    if constexpr (EPI == E_DGELU) {
+      stg_dma_round0(p.aux, p.ldc, cur.m0, cur.n0, lds_addr + RING, ltid >> 6, ltid & 63);
+      preload_round1(pa, p.aux, p.ldc, cur.m0, cur.n0, stg_voff(p.ldc, ltid >> 6, ltid & 63));
+    }
+    if constexpr (EPI == E_BIAS || EPI == E_GELU) preload_bias(pb, p.bias, cur.n0, 128 * ((ltid >> 6) & 1) + 4 * ((ltid & 63) >> 4));
     // ---------------------------------------------------------------- main loop
     uint32_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if constexpr (DIAG) {
@@ -704,9 +854,19 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
       if constexpr (LAYOUT == L_NT) PDT_KLOOP_NT_ASM(PDT_GEMM_KLOOP_NT);
       else PDT_KLOOP_TT_ASM(PDT_GEMM_KLOOP_TT);
     }
+    if constexpr (EPI == E_DGELU) settle(pa);
+    if constexpr (EPI == E_BIAS || EPI == E_GELU) settle(pb);
     if (DIAG) st1 = stamp();
     const int m0 = cur.m0, n0 = cur.n0, tm = cur.tm;
 
+    // The epilogue's lane terms are recomputed every item from an opaque copy of the thread id: hoisted out of the
+    // persistent loop they stay live across the main-loop statement (which leaves the compiler 96 VGPRs) and spill
+    // to scratch -- the DGELU kernel spilled 46 VGPRs that way, reloaded from scratch in every epilogue.
+    const int etid = item_tid(wv);
+    {
+    const int tid = etid, w = etid >> 6, lane = etid & 63, wr = w >> 1, wc = w & 1;
+    const int lrow = 128 * wr + (lane & 15);
+    const int lcol = 128 * wc + 4 * (lane >> 4);
     // ---------------------------------------------------------------- epilogue
     // acc tile (i, j): C[m0 + 128 wr + 16 i + (lane & 15)][n0 + 128 wc + 16 j + 4 (lane >> 4) + r]
     if constexpr (EPI == E_F32) {
@@ -720,15 +880,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
       bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
       u16x8 buf[8];
       float bj[8][4];
-      if constexpr (EPI == E_BIAS || EPI == E_GELU) {
-        // (the wait for these loads also drains the next item's first DMA that the main loop left in flight:
-        // a bias epilogue gives up that overlap)
+      if constexpr (EPI == E_BIAS || EPI == E_GELU) {   // loaded before the main loop (preload_bias)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const u16x4 b = *reinterpret_cast<const u16x4*>(p.bias + n0 + lcol + 16 * j);
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(b[r]);
-        }
+          for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(pb[j][r]);
       }
       float cs[8][4];
 #pragma unroll
@@ -736,69 +892,81 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
       // round r: this wave's accumulator tiles i = 2 r, 2 r + 1 -> image rows q = 32 wr + 16 (i & 1) + (lane & 15)
-      u16x8 aux[2][8];                       // DGELU: the pre-activation rows of rounds r (in use) and r + 1 (in flight)
-      if constexpr (EPI == E_DGELU) stg_fetch(aux[0], p.aux, p.ldc, m0, n0, 0, w, lane);
+      // DGELU: the derivative rows of round 0 are already in the image (stg_dma_round0 under the main loop); rounds
+      // 1-3 are fetched into registers a round ahead of their use
+      u16x8 aux[2][8];                       // round r in aux[r & 1]: round 1 loaded before the main loop, 2 and 3
+      const uint32_t svo = stg_voff(p.ldc, w, lane), ldc2 = (uint32_t)(p.ldc * 2);   // a round ahead
+      const __amdgpu_buffer_rsrc_t rsc = tile_rsrc(C, p.ldc, m0, n0);
+      if constexpr (EPI == E_DGELU) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) aux[1][it] = pa[it];
+      }
       sfor<0, 4>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
-        if constexpr (EPI == E_DGELU) {
+        if constexpr (EPI == E_DGELU && r > 0) {
           __syncthreads();                   // the previous round's image is read
           stg_put(img, aux[r & 1], w, lane);
-          if constexpr (r < 3) stg_fetch(aux[(r + 1) & 1], p.aux, p.ldc, m0, n0, r + 1, w, lane);
+          if constexpr (r < 3) stg_fetch(aux[(r + 1) & 1], tile_rsrc(p.aux, p.ldc, m0, n0), svo, ldc2, r + 1);
         }
         __syncthreads();
+        u16x4 dk[16];                        // GELU: this round's derivatives, written out after the values
+        u16x4 hk[8];                         // DGELU: 8 tiles' derivatives read before their first write (a
+                                             // read-after-write order would serialise 16 LDS round trips)
         sfor<0, 16>([&](auto kc) {
-          constexpr int k = 16 * r + decltype(kc)::value, i = k >> 3, j = k & 7;
+          constexpr int kk = decltype(kc)::value, k = 16 * r + kk, i = k >> 3, j = k & 7;
+          if constexpr (EPI == E_DGELU && (kk & 7) == 0) {
+            sfor<0, 8>([&](auto hc) {
+              constexpr int k2 = k + decltype(hc)::value, i2 = k2 >> 3, j2 = k2 & 7;
+              hk[decltype(hc)::value] = *reinterpret_cast<const u16x4*>(
+                  img + stg_off(32 * wr + 16 * (i2 & 1) + (lane & 15), lcol + 16 * j2));
+            });
+          }
           const f32x4 v = acc_tile<k>();
           const uint32_t at = stg_off(32 * wr + 16 * (i & 1) + (lane & 15), lcol + 16 * j);
           u16x4 o;
           if constexpr (EPI == E_DGELU) {
-            const u16x4 hh = *reinterpret_cast<const u16x4*>(img + at);
+            const u16x4 hh = hk[kk & 7];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const bf16_t gb = f2bf(v[e] * gelu_grad<true>(bf2f(hh[e])));
+              const bf16_t gb = f2bf(v[e] * bf2f(hh[e]));
               o[e] = gb;
               cs[j][e] += bf2f(gb);          // the bias gradient sums the gradient as stored
             }
+          } else if constexpr (EPI == E_GELU) {
+            // value and derivative of the rounded pre-activation, two per packed instruction (gelu.h)
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+              gelu_f32x2 y2, d2;
+              gelu_fwd_grad2(gelu_f32x2{bf2f(f2bf(v[e] + bj[j][e])), bf2f(f2bf(v[e + 1] + bj[j][e + 1]))}, y2, d2);
+              o[e] = f2bf(y2[0]); o[e + 1] = f2bf(y2[1]);
+              dk[kk][e] = f2bf(d2[0]); dk[kk][e + 1] = f2bf(d2[1]);
+            }
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = f2bf((EPI == E_BIAS || EPI == E_GELU) ? v[e] + bj[j][e] : v[e]);
+            for (int e = 0; e < 4; ++e) o[e] = f2bf(EPI == E_BIAS ? v[e] + bj[j][e] : v[e]);
           }
           *reinterpret_cast<u16x4*>(img + at) = o;
         });
         __syncthreads();
         stg_read(img, buf, w, lane);
-        stg_write_out(buf, EPI == E_GELU ? p.aux_out : C, p.ldc, m0, n0, r, w, lane);
-        if constexpr (EPI == E_GELU) {       // then GELU of the stored (rounded) pre-activation, same rows
+        stg_write_out(buf, rsc, svo, ldc2, r);
+        if constexpr (EPI == E_GELU) {       // then the derivatives, same rows
           __syncthreads();
-          // the image still holds this thread's pre-activation values as stored (bf16): GELU of those, two per
-          // packed instruction (gelu_tanh2) -- no second accumulator read / bias add / rounding
           sfor<0, 16>([&](auto kc) {
-            constexpr int k = 16 * r + decltype(kc)::value, i = k >> 3, j = k & 7;
+            constexpr int kk = decltype(kc)::value, k = 16 * r + kk, i = k >> 3, j = k & 7;
             const uint32_t at = stg_off(32 * wr + 16 * (i & 1) + (lane & 15), lcol + 16 * j);
-            const u16x4 hh = *reinterpret_cast<const u16x4*>(img + at);
-            const f32x2 y0 = gelu_tanh2(f32x2{bf2f(hh[0]), bf2f(hh[1])});
-            const f32x2 y1 = gelu_tanh2(f32x2{bf2f(hh[2]), bf2f(hh[3])});
-            u16x4 o;
-            o[0] = f2bf(y0[0]); o[1] = f2bf(y0[1]); o[2] = f2bf(y1[0]); o[3] = f2bf(y1[1]);
-            *reinterpret_cast<u16x4*>(img + at) = o;
+            *reinterpret_cast<u16x4*>(img + at) = dk[kk];
           });
           __syncthreads();
           stg_read(img, buf, w, lane);
-          stg_write_out(buf, C, p.ldc, m0, n0, r, w, lane);
+          stg_write_out(buf, tile_rsrc(p.aux_out, p.ldc, m0, n0), svo, ldc2, r);
         }
       });
       if constexpr (EPI == E_DGELU) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = cs[j][e];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            cs[j][e] = v;
-          }
+          for (int e = 0; e < 4; ++e) cs[j][e] = row16_sum(cs[j][e]);
         __syncthreads();                                   // the last round's image is read
         float* red = reinterpret_cast<float*>(img);        // [2 wave rows][256 columns]
         if ((lane & 15) == 0) {
@@ -812,6 +980,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
       }
       __syncthreads();                       // the staging image is free for the next item's epilogue
     }
+    }   // epilogue lane terms
     if (DIAG) {
       const uint64_t st2 = stamp();
       if (tid == 0) {

@@ -2,9 +2,11 @@
 
 * ``gemm_nt(a, b)``            a [M, K] @ b [N, K]^T  (Linear forward; dgrad against a transposed weight)
 * ``gemm_nt(..., bias=)``      + bias
-* ``gemm_nt_gelu(a, b, bias)`` -> (gelu_tanh(a b^T + bias), pre-activation): GPT-2's c_fc in ONE pass
-* ``gemm_nt_dgelu(a, b, pre)`` -> (g = (a b^T) * gelu_tanh'(pre), colsum(g)): c_proj's dgrad, the GELU
-  backward and c_fc's bias gradient in ONE pass
+* ``gemm_nt_gelu(a, b, bias)`` -> (gelu_tanh(h), gelu_tanh'(h)) with h = a b^T + bias: GPT-2's c_fc in ONE
+  pass; the backward keeps the derivative, not the pre-activation
+* ``gemm_nt_dgelu(a, b, d)`` -> (g = (a b^T) * d, colsum(g)): c_proj's dgrad, the GELU backward (d is the
+  derivative ``gemm_nt_gelu`` kept: a multiply, no transcendental in the epilogue) and c_fc's bias gradient in
+  ONE pass
 * ``gemm_tt(a, b)``            a [K, M]^T @ b [K, N]  (weight gradient dY^T X), optional token split
 
 hipBLASLt has no gfx950 kernel for the GELU_AUX_BIAS / DGELU_BGRAD epilogues
@@ -68,25 +70,26 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) 
 
 
 def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor):
-    """(gelu_tanh(a b^T + bias), a b^T + bias) -- both bf16 [M, N]; the GELU reads the stored (rounded)
-    pre-activation, which is what the backward differentiates."""
+    """(gelu_tanh(h), gelu_tanh'(h)) with h = bf16(a b^T + bias) -- both bf16 [M, N].  Value and derivative are
+    taken of the ROUNDED pre-activation (what an unfused bf16 Linear + GELU differentiates); the derivative is
+    what the backward needs (``gemm_nt_dgelu`` / the ``pdt_bias_gelu_bwd_db`` sweep in mode 2)."""
     m, k = a.shape
     n = b.shape[0]
     y = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
-    pre = torch.empty_like(y)
-    _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=pre)
-    return y, pre
+    d = torch.empty_like(y)
+    _launch(L_NT, E_GELU, a, b, y, m, n, k, bias=bias, aux_out=d)
+    return y, d
 
 
-def gemm_nt_dgelu(a: torch.Tensor, b: torch.Tensor, pre: torch.Tensor, bias_dtype=torch.bfloat16):
-    """(g, db): g = (a b^T) * gelu_tanh'(pre) bf16 [M, N], db = g.sum(0) (fp32 partial per 256-row tile,
-    reduced in a fixed order)."""
+def gemm_nt_dgelu(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor, bias_dtype=torch.bfloat16):
+    """(g, db): g = (a b^T) * d bf16 [M, N] (d = the GELU derivative ``gemm_nt_gelu`` returned), db = g.sum(0)
+    (fp32 partial per 256-row tile, reduced in a fixed order)."""
     m, k = a.shape
     n = b.shape[0]
     g = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     db = torch.empty(n, dtype=torch.bfloat16, device=a.device)
     ws = torch.empty((m // 256) * n, dtype=torch.float32, device=a.device)
-    _launch(L_NT, E_DGELU, a, b, g, m, n, k, aux=pre, dbias=db, ws=ws)
+    _launch(L_NT, E_DGELU, a, b, g, m, n, k, aux=d, dbias=db, ws=ws)
     return g, db.to(bias_dtype)
 
 

@@ -299,12 +299,11 @@ class _LinearFn(torch.autograd.Function):
 
 
 FUSED_GELU = os.environ.get("PDT_FUSED_GELU", "1") == "1"
-_ZERO_BIAS: dict = {}
 
 
 def linear_bias_gelu_ok(x, weight, bias) -> bool:
     """gelu_tanh(x W^T + b) in ONE hand-GEMM pass (``ops.gemm.gemm_nt_gelu``: bias + GELU in the epilogue, the
-    pre-activation kept for the backward) -- bf16, the hand kernel's tile grid, K >= 128."""
+    GELU derivative kept for the backward) -- bf16, the hand kernel's tile grid, K >= 128."""
     from . import gemm as G
     if not (FUSED_GELU and G.KERNEL["name"] == "asm" and x.is_cuda and bias is not None):
         return False
@@ -319,37 +318,34 @@ def linear_bias_gelu_ok(x, weight, bias) -> bool:
 
 class _LinearBiasGeluFn(torch.autograd.Function):
     """y = gelu_tanh(x W^T + b): forward on the hand NT GEMM with the bias + GELU epilogue (replaces hipBLASLt +
-    the separate bias-GELU pass over the [tokens, 4d] hidden); backward = the fused GELU-backward + bias-gradient
-    sweep over the kept pre-activation, then the Linear's weight / data gradients."""
+    the separate bias-GELU pass over the [tokens, 4d] hidden), which keeps gelu'(h) rather than h; backward = one
+    multiply + bias-gradient sweep over that derivative (no transcendental), then the Linear's weight / data
+    gradients."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         from . import gemm as G
         x2 = x.reshape(-1, x.shape[-1])
         x2 = x2 if x2.is_contiguous() and x2.data_ptr() % 16 == 0 else x2.contiguous()
-        y, pre = G.gemm_nt_gelu(x2, weight, bias)
-        ctx.save_for_backward(x2, weight, pre)
+        y, d = G.gemm_nt_gelu(x2, weight, bias)
+        ctx.save_for_backward(x2, weight, d)
         ctx.xshape = x.shape
         return _as_output(y, (*x.shape[:-1], weight.shape[0]))
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, pre = ctx.saved_tensors
-        dy2 = dy.reshape(pre.shape)
+        x2, w, d = ctx.saved_tensors
+        dy2 = dy.reshape(d.shape)
         dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
-        rows, n = pre.shape
-        key = (n, pre.device)
-        zb = _ZERO_BIAS.get(key)
-        if zb is None:
-            zb = _ZERO_BIAS[key] = torch.zeros(n, dtype=torch.bfloat16, device=pre.device)
+        rows, n = d.shape
         lib = _lib.require()
-        dpre = torch.empty_like(pre)
-        db = torch.empty(n, dtype=w.dtype, device=pre.device)
-        ws = torch.empty(lib.pdt_colsum_ws_floats(rows, n), dtype=torch.float32, device=pre.device)
-        # pre already holds the bias: the sweep runs with a zero bias
-        _lib.call("pdt_bias_gelu_bwd_db", dy2.data_ptr(), pre.data_ptr(), zb.data_ptr(), dpre.data_ptr(),
-                  db.data_ptr(), ws.data_ptr(), rows, n, _lib.dtype_code(pre.dtype), _lib.dtype_code(db.dtype), 1, 0,
-                  _lib.stream_handle(pre.device))
+        dpre = torch.empty_like(d)
+        db = torch.empty(n, dtype=w.dtype, device=d.device)
+        ws = torch.empty(lib.pdt_colsum_ws_floats(rows, n), dtype=torch.float32, device=d.device)
+        # mode 2: d already is gelu'(pre-activation) -> dpre = dy * d and its column sums
+        _lib.call("pdt_bias_gelu_bwd_db", dy2.data_ptr(), d.data_ptr(), None, dpre.data_ptr(),
+                  db.data_ptr(), ws.data_ptr(), rows, n, _lib.dtype_code(d.dtype), _lib.dtype_code(db.dtype), 2, 0,
+                  _lib.stream_handle(d.device))
         dw = wgrad(dpre, x2, w.dtype) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:
@@ -366,9 +362,11 @@ def linear_bias_gelu(x, weight, bias):
     return _LinearBiasGeluFn.apply(x, weight, bias)
 
 
-# opt-in: measured 144.1k vs 145.0k tokens/s without it (the DGELU epilogue: 1,045 TFLOP/s vs the plain 1,466 --
-# its pre-activation read and GELU-derivative math cost more than the separate sweep; profiles/r4/r4_dgelu_ab.log)
-FUSED_DGELU = os.environ.get("PDT_FUSED_DGELU", "0") == "1"
+# default since round 5: the forward keeps gelu'(h) (the DGELU epilogue is a multiply), the epilogue no longer spills
+# (spill reloads had put a vmcnt(0) in front of every main loop) and its round-0 / round-1 rows load under the main loop:
+# DGELU 1,246 TFLOP/s vs 1,035 for the plain GEMM + sweep it replaces; flagship 147.3k vs 144.0k tokens/s
+# (profiles/r5/r5_dgelu_gemm.jsonl, r5_dgelu_bench.log).  PDT_FUSED_DGELU=0 restores the sweep.
+FUSED_DGELU = os.environ.get("PDT_FUSED_DGELU", "1") == "1"
 
 
 def gelu_mlp_ok(x, w1, b1, w2, b2) -> bool:
@@ -382,23 +380,23 @@ def gelu_mlp_ok(x, w1, b1, w2, b2) -> bool:
 class _GeluMlpFn(torch.autograd.Function):
     """out = gelu_tanh(x W1^T + b1) W2^T + b2 (GPT-2's MLP).  Forward: c_fc + bias + GELU in one hand-GEMM pass,
     c_proj on hipBLASLt.  Backward: c_proj's data gradient, the GELU backward and c_fc's bias gradient in ONE hand-GEMM
-    pass (DGELU epilogue over the kept pre-activation) -- no separate sweep over the [tokens, 4d] hidden."""
+    pass (DGELU epilogue: a multiply by the kept derivative) -- no separate sweep over the [tokens, 4d] hidden."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
         from . import gemm as G
         x2 = x.reshape(-1, x.shape[-1])
         x2 = x2 if x2.is_contiguous() and x2.data_ptr() % 16 == 0 else x2.contiguous()
-        y1, pre = G.gemm_nt_gelu(x2, w1, b1)
+        y1, d1 = G.gemm_nt_gelu(x2, w1, b1)
         out = F.linear(y1, w2, b2)
-        ctx.save_for_backward(x2, w1, pre, y1, w2)
+        ctx.save_for_backward(x2, w1, d1, y1, w2)
         ctx.xshape = x.shape
         return _as_output(out, (*x.shape[:-1], w2.shape[0]))
 
     @staticmethod
     def backward(ctx, dout):
         from . import gemm as G
-        x2, w1, pre, y1, w2 = ctx.saved_tensors
+        x2, w1, d1, y1, w2 = ctx.saved_tensors
         d2 = dout.reshape(-1, dout.shape[-1])
         d2 = d2 if d2.is_contiguous() and d2.data_ptr() % 16 == 0 else d2.contiguous()
         dw2 = wgrad(d2, y1, w2.dtype) if ctx.needs_input_grad[3] else None
@@ -406,8 +404,8 @@ class _GeluMlpFn(torch.autograd.Function):
         if ctx.needs_input_grad[4]:
             db2 = take_bias_grad(d2)      # summed by the kernel that produced dY (the next LayerNorm's backward)
             db2 = db2.to(w2.dtype) if db2 is not None else _colsum(d2, w2.dtype)
-        # c_proj dgrad (d2 W2) x GELU'(pre), and c_fc's bias gradient, in one pass
-        dpre, db1 = G.gemm_nt_dgelu(d2, transpose16(w2), pre, bias_dtype=w1.dtype)
+        # c_proj dgrad (d2 W2) x GELU'(pre) (= d1, kept by the forward), and c_fc's bias gradient, in one pass
+        dpre, db1 = G.gemm_nt_dgelu(d2, transpose16(w2), d1, bias_dtype=w1.dtype)
         dw1 = wgrad(dpre, x2, w1.dtype) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:

@@ -61,14 +61,18 @@ def check():
         out(case="nt_plain", shape=[M, N, K], rel=rel(c_asm, ref), bitwise_eq_hip=bool(torch.equal(c_asm, c_hip)))
         out(case="nt_bias", shape=[M, N, K],
             rel=rel(with_kernel("asm", lambda: G.gemm_nt(a, b, bias)), ref + bias.float()))
-        y, pre = with_kernel("asm", lambda: G.gemm_nt_gelu(a, b, bias))
-        out(case="nt_gelu", shape=[M, N, K], rel_pre=rel(pre, ref + bias.float()),
-            rel_y=rel(y, torch.nn.functional.gelu(ref + bias.float(), approximate="tanh")))
+        y, dd = with_kernel("asm", lambda: G.gemm_nt_gelu(a, b, bias))
+        hr = (ref + bias.float()).requires_grad_()
+        yr = torch.nn.functional.gelu(hr, approximate="tanh")
+        yr.sum().backward()
+        out(case="nt_gelu", shape=[M, N, K], rel_dgelu=rel(dd, hr.grad), rel_y=rel(y, yr.detach()))
         h = torch.randn(M, N, device=dev).bfloat16()
-        g, db = with_kernel("asm", lambda: G.gemm_nt_dgelu(a, b, h))
         hr = h.float().requires_grad_()
-        torch.nn.functional.gelu(hr, approximate="tanh").backward(ref)
-        out(case="nt_dgelu", shape=[M, N, K], rel_g=rel(g, hr.grad), rel_db=rel(db, hr.grad.sum(0)))
+        torch.nn.functional.gelu(hr, approximate="tanh").sum().backward()
+        dh = hr.grad.bfloat16()
+        g, db = with_kernel("asm", lambda: G.gemm_nt_dgelu(a, b, dh))
+        want = ref * dh.float()
+        out(case="nt_dgelu", shape=[M, N, K], rel_g=rel(g, want), rel_db=rel(db, want.sum(0)))
         at = torch.randn(K * 2, M, device=dev).bfloat16()
         bt = torch.randn(K * 2, N, device=dev).bfloat16()
         reft = at.float().t() @ bt.float()
@@ -123,10 +127,25 @@ def bench():
         arms = {"asm": lambda: with_kernel("asm", lambda: G.gemm_nt(a, b)),
                 "hip": lambda: with_kernel("hip", lambda: G.gemm_nt(a, b)),
                 "lt": lambda: a @ b.t()}
+        if name != "sq8k":
+            arms["asm_bias"] = lambda: with_kernel("asm", lambda: G.gemm_nt(a, b, bias))
+            arms["lt_bias"] = lambda: torch.nn.functional.linear(a, b, bias)
         if name == "fc":
             arms["asm_gelu"] = lambda: with_kernel("asm", lambda: G.gemm_nt_gelu(a, b, bias))
-            h = torch.randn(M, N, device=dev).bfloat16()
+            h = torch.rand(M, N, device=dev).bfloat16()
             arms["asm_dgelu"] = lambda: with_kernel("asm", lambda: G.gemm_nt_dgelu(a, b, h))
+            # the unfused alternative of the DGELU epilogue: plain GEMM, then the derivative-mode sweep (dy * d and
+            # its column sums) that _LinearBiasGeluFn.backward runs
+            from pytorch_distributedtraining_amd.ops import _lib
+            lib = _lib.require()
+            dpre, dbias = torch.empty_like(h), torch.empty(N, device=dev, dtype=torch.bfloat16)
+            ws = torch.empty(lib.pdt_colsum_ws_floats(M, N), dtype=torch.float32, device=dev)
+
+            def plain_sweep():
+                c = with_kernel("asm", lambda: G.gemm_nt(a, b))
+                _lib.call("pdt_bias_gelu_bwd_db", c.data_ptr(), h.data_ptr(), None, dpre.data_ptr(), dbias.data_ptr(),
+                          ws.data_ptr(), M, N, 1, 1, 2, 0, _lib.stream_handle(dev))
+            arms["asm_plain+sweep"] = plain_sweep
         res = {k: [] for k in arms}
         for _ in range(ROUNDS):
             for k, fn in arms.items():

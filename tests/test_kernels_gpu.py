@@ -778,8 +778,9 @@ def _gelu_tanh(x):
 @pytest.mark.parametrize("M,N,K", [(2048, 1024, 1536), (4096, 768, 256), (512, 2048, 4096), (1024, 768, 4096),
                                    (1024, 768, 4160)])
 def test_hand_gemm_nt_epilogues(M, N, K):
-    """Hand MFMA GEMM, NT layout (y = a b^T, a [M, K], b [N, K]): plain, bias, bias+GELU (pre-activation kept)
-    and the backward dGELU epilogue (g = dy b * GELU'(h) with the bias gradient sum_rows g) vs fp32 torch."""
+    """Hand MFMA GEMM, NT layout (y = a b^T, a [M, K], b [N, K]): plain, bias, bias+GELU (the GELU derivative of the
+    rounded pre-activation kept) and the backward dGELU epilogue (g = dy b * d with the bias gradient sum_rows g)
+    vs fp32 torch."""
     from pytorch_distributedtraining_amd.ops import gemm as G
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).bfloat16()
@@ -788,24 +789,36 @@ def test_hand_gemm_nt_epilogues(M, N, K):
     ref = a.float() @ b.float().t()
     assert rel_err(G.gemm_nt(a, b), ref) < 4e-3
     assert rel_err(G.gemm_nt(a, b, bias), ref + bias.float()) < 4e-3
-    y, pre = G.gemm_nt_gelu(a, b, bias)
-    assert rel_err(pre, ref + bias.float()) < 4e-3
+    y, d = G.gemm_nt_gelu(a, b, bias)
     assert rel_err(y, _gelu_tanh(ref + bias.float())) < 6e-3
+    assert rel_err(d, _gelu_tanh_grad(ref + bias.float())) < 6e-3
     # the compiler-scheduled kernel (PDT_GEMM_KERNEL=hip) runs the same MFMA order per accumulator: bitwise equal
     old = G.KERNEL["name"]
     try:
         G.KERNEL["name"] = "hip"
         assert torch.equal(G.gemm_nt(a, b, bias), _with_asm(G, lambda: G.gemm_nt(a, b, bias)))
-        y2, pre2 = G.gemm_nt_gelu(a, b, bias)
+        y2, d2 = G.gemm_nt_gelu(a, b, bias)
+        h = torch.randn(M, N, device=DEV).bfloat16()
+        dh = _gelu_tanh_grad(h.float()).bfloat16()
+        g2, db2 = G.gemm_nt_dgelu(a, b, dh)
     finally:
         G.KERNEL["name"] = old
-    assert torch.equal(y2, y) and torch.equal(pre2, pre)
-    h = torch.randn(M, N, device=DEV).bfloat16()
-    g, db = G.gemm_nt_dgelu(a, b, h)
+    assert torch.equal(y2, y) and torch.equal(d2, d)
+    g, db = G.gemm_nt_dgelu(a, b, dh)
+    assert torch.equal(g, g2)
     hr = h.float().requires_grad_()
     _gelu_tanh(hr).backward(ref)
     assert rel_err(g, hr.grad) < 6e-3
     assert rel_err(db, hr.grad.sum(0)) < 6e-3
+    assert rel_err(db2, hr.grad.sum(0)) < 6e-3
+
+
+def _gelu_tanh_grad(x):
+    """d/dx gelu_tanh(x) in fp32 (autograd of torch's own GELU)."""
+    with torch.enable_grad():
+        xr = x.detach().float().requires_grad_()
+        _gelu_tanh(xr).sum().backward()
+    return xr.grad
 
 
 def _with_asm(G, fn):
@@ -821,7 +834,7 @@ def _with_asm(G, fn):
 def test_hand_gemm_nt_gelu_full_grid_production_shape(kernel):
     """GPT-2 1.3B c_fc at 96 x 1024 tokens (98,304 x 8,192 x 2,048, the full grid of 256 x 256 tiles; asm: 256
     persistent workgroups x 48 tiles each, the next tile's first K-tiles loading under the current epilogue):
-    every element of the GELU output and the kept pre-activation against fp32."""
+    every element of the GELU output and of the kept derivative against fp32."""
     from pytorch_distributedtraining_amd.ops import gemm as G
     M, N, K = 96 * 1024, 8192, 2048
     torch.manual_seed(7)
@@ -831,15 +844,45 @@ def test_hand_gemm_nt_gelu_full_grid_production_shape(kernel):
     old = G.KERNEL["name"]
     G.KERNEL["name"] = kernel
     try:
-        y, pre = G.gemm_nt_gelu(a, b, bias)
+        y, d = G.gemm_nt_gelu(a, b, bias)
     finally:
         G.KERNEL["name"] = old
     ref = torch.addmm(bias.float(), a.float(), b.float().t())
-    for got, want in ((pre, ref), (y, _gelu_tanh(ref))):
+    # value and derivative of the ROUNDED pre-activation (what the kernel differentiates)
+    hb = ref.bfloat16().float()
+    del ref
+    for got, want in ((y, _gelu_tanh(hb)), (d, _gelu_tanh_grad(hb))):
         rms = float(want.square().mean().sqrt())
         bad = (got.float() - want).abs() > 0.008 * want.abs() + 0.01 * rms
         assert int(bad.sum()) == 0, int(bad.sum())
         del want
+
+
+@pytest.mark.parametrize("kernel", ["asm", "hip"])
+def test_hand_gemm_nt_dgelu_full_grid_production_shape(kernel):
+    """GPT-2 1.3B c_proj's data gradient with the GELU backward + c_fc bias gradient epilogue at 96 x 1024 tokens
+    (98,304 x 8,192 x 2,048 against the transposed weight; asm: the round-0 derivative rows LDS-DMA'd under each
+    item's main loop, rounds 1-3 fetched a round ahead): every element of g and of the column sums vs fp32."""
+    from pytorch_distributedtraining_amd.ops import gemm as G
+    M, N, K = 96 * 1024, 8192, 2048
+    torch.manual_seed(11)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    d = (torch.rand(M, N, device=DEV) * 1.3 - 0.15).bfloat16()      # the range of gelu_tanh'
+    old = G.KERNEL["name"]
+    G.KERNEL["name"] = kernel
+    try:
+        g, db = G.gemm_nt_dgelu(a, b, d)
+    finally:
+        G.KERNEL["name"] = old
+    want = (a.float() @ b.float().t()).mul_(d.float())
+    rms = float(want.square().mean().sqrt())
+    bad = (g.float() - want).abs() > 0.008 * want.abs() + 0.01 * rms
+    assert int(bad.sum()) == 0, int(bad.sum())
+    dbw = want.sum(0)
+    del want
+    scale = float(dbw.abs().mean())
+    assert float((db.float() - dbw).abs().max()) < 0.02 * scale + 0.01 * float(dbw.abs().max())
 
 
 @pytest.mark.parametrize("M,K,N", [(70000, 60, 180), (65536 + 123, 120, 60), (16384, 768, 768), (16384, 768, 3072),
