@@ -47,25 +47,61 @@ class FusedAdamW(Optimizer):
         self._tables = mt.TableCache()
         self._dsteps: dict = {}
 
-    def _device_step(self, gi, group, dev):
-        """The group's shared device step tensor (created eagerly, before any capture, from the state)."""
-        ds = self._dsteps.get(gi)
-        if ds is None or ds.device != dev:
-            start = 0.0
-            for p in group["params"]:
-                st = self.state.get(p)
-                if st and "step" in st:
-                    start = max(start, float(st["step"]))
-            ds = self._dsteps[gi] = torch.full((), start, dtype=torch.float32, device=dev)
-        return ds
+    def _counters(self, present):
+        """Device step counters for this step's parameters (those with a gradient), as [(counter, params)].
+
+        torch counts steps per parameter.  Parameters whose step histories are identical share ONE device counter
+        (one ``step_inc`` launch, one AdamW launch); a counter whose parameters did not all get a gradient this
+        step is split (the ones stepping get a clone), so a parameter that skips steps -- an unused branch, a late
+        unfreeze -- keeps its own count and bias correction.  Parameters without a counter (new state, or a host
+        step loaded from a checkpoint) are grouped by their step value.  ``_dsteps``: id(counter) -> (counter,
+        set of ids of the parameters sharing it)."""
+        members = self._dsteps
+        shared, fresh = {}, {}
+        for p in present:
+            c = self._init_state(p)["step"]
+            ent = members.get(id(c))
+            if ent is not None and ent[0] is c:
+                shared.setdefault(id(c), []).append(p)
+            else:
+                fresh.setdefault((float(c), p.device), []).append(p)
+        out = []
+        for (v, dev), ps in fresh.items():
+            c = torch.full((), v, dtype=torch.float32, device=dev)
+            for p in ps:
+                old = self.state[p]["step"]
+                ent = members.get(id(old))
+                if ent is not None and ent[0] is old:
+                    ent[1].discard(id(p))
+                    if not ent[1]:
+                        del members[id(old)]
+                self.state[p]["step"] = c
+            members[id(c)] = (c, {id(p) for p in ps})
+            out.append((c, ps))
+        for cid, ps in shared.items():
+            c, mem = members[cid]
+            if len(ps) != len(mem):
+                ids = {id(p) for p in ps}
+                mem -= ids
+                c = c.clone()
+                members[id(c)] = (c, ids)
+                for p in ps:
+                    self.state[p]["step"] = c
+            out.append((c, ps))
+        return out
 
     def zero_grad(self, set_to_none: bool = True):
         """torch semantics for ``.grad``, except for engine-owned flat gradients: DDP's compute-dtype masters
         (``_pdt_zero_grad``) and parameters whose ``.grad`` is still a view of a DDP bucket flat
         (``_pdt_grad_flat``) get their flat zeroed in place -- ONE fill per flat instead of a None per
         parameter that the next forward would re-attach view by view (ResNet-50: 161 views, a host gap at
-        every step start), so those gradients read as zeros rather than None."""
-        flats, rest = {}, []
+        every step start).  Those gradients therefore read as zeros, not None, after ``set_to_none=True`` (as
+        with torch DDP's ``gradient_as_bucket_view``, whose views stay attached to the bucket).  A flat is filled
+        whole only when every parameter viewing it (``_pdt_grad_members``) belongs to THIS optimizer; otherwise
+        only this optimizer's own views are zeroed, so another optimizer stepping the same bucket later still
+        sees its gradients."""
+        mine = {id(p) for group in self.param_groups for p in group["params"]}
+        flats, views, rest, owned = {}, [], [], {}
         for group in self.param_groups:
             for p in group["params"]:
                 zero = getattr(p, "_pdt_zero_grad", None)
@@ -77,11 +113,20 @@ class FusedAdamW(Optimizer):
                     continue
                 f = getattr(p, "_pdt_grad_flat", None)
                 if f is not None and g._base is f:
-                    flats[id(f)] = f.zero_
+                    ok = owned.get(id(f))
+                    if ok is None:
+                        members = getattr(p, "_pdt_grad_members", None)
+                        ok = owned[id(f)] = members is not None and all(id(q) in mine for q in members)
+                    if ok:
+                        flats[id(f)] = f.zero_
+                    else:
+                        views.append(g)      # keep the view attached: the bucket reduction reads it in place
                     continue
                 rest.append(p)
         for zero in flats.values():
             zero()
+        if views:
+            torch._foreach_zero_(views)
         if set_to_none:
             for p in rest:
                 p.grad = None
@@ -97,7 +142,7 @@ class FusedAdamW(Optimizer):
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
-        self._dsteps.clear()     # device step counters are rebuilt from the loaded per-param steps
+        self._dsteps.clear()     # device step counters are rebuilt from the loaded per-parameter steps
         for p in self.state:
             p._pdt_opt_state = True   # engines must not re-lay-out this parameter any more (DDP rebuild)
 
@@ -123,16 +168,17 @@ class FusedAdamW(Optimizer):
             cap = bool(group.get("capturable", False))
             # An overflowed fp16 step (found_inf != 0) must leave params, moments AND the step count alone:
             # torch.amp.GradScaler skips optimizer.step() entirely.  With a device flag the count lives on the
-            # device and advances conditionally (pdt_step_inc), so no host sync is needed; once a group has a
+            # device and advances conditionally (pdt_step_inc), so no host sync is needed; once a parameter has a
             # device count it keeps it (mixing the two counters would double-count).
-            # GPU parameters always count on the device: one step_inc launch per group instead of a host tensor
+            # GPU parameters always count on the device: one step_inc launch per counter instead of a host tensor
             # add + .item() per parameter (161 of them for ResNet-50: ~1 ms of host time per step, a GPU-idle gap
             # in front of the AdamW launch -- profiles/r3_s4h_resnet50-ddp_kernel_table.txt)
             on_gpu = bool(group["params"]) and group["params"][0].device.type == "cuda"
-            dev_step = cap or on_gpu or gi in self._dsteps or (found_inf is not None and found_inf.device.type == "cuda")
+            dev_step = cap or on_gpu or (found_inf is not None and found_inf.device.type == "cuda") or any(
+                id(self.state[p].get("step")) in self._dsteps for p in group["params"] if p in self.state)
             if found_inf is not None and found_inf.device.type != "cuda" and int(found_inf.reshape(-1)[0]) != 0:
                 continue
-            dstep = None
+            present = []
             for p in group["params"]:
                 g = grad_of(p)
                 if g is None:
@@ -142,18 +188,22 @@ class FusedAdamW(Optimizer):
                 if p.dtype != torch.float32:
                     raise TypeError("FusedAdamW keeps fp32 master params; wrap low-precision models with an "
                                     "engine (FSDP/ZeRO) or keep params fp32 and use autocast")
-                st = self._init_state(p)
-                if dev_step and p.device.type == "cuda":
-                    if dstep is None:
-                        dstep = self._device_step(gi, group, p.device)
-                        mt.step_inc_(dstep, found_inf)   # one device increment per group (graph-capturable)
-                    st["step"] = dstep
-                    key = (g.dtype, -1, p.device)
-                else:
+                present.append(p)
+            counters = {}
+            if dev_step:
+                for c, ps in self._counters(present):
+                    mt.step_inc_(c, found_inf)    # one device increment per counter (graph-capturable)
+                    counters[id(c)] = c
+                    for p in ps:
+                        buckets.setdefault((grad_of(p).dtype, id(c), p.device), []).append(p)
+            else:
+                for p in present:
+                    st = self._init_state(p)
                     st["step"] += 1
-                    key = (g.dtype, int(st["step"].item()), p.device)
-                buckets.setdefault(key, []).append(p)
-            for (gdt, step, dev), ps in buckets.items():
+                    buckets.setdefault((grad_of(p).dtype, -int(st["step"].item()), p.device), []).append(p)
+            for (gdt, ckey, dev), ps in buckets.items():
+                dstep = counters.get(ckey)
+                step = -ckey if dstep is None else 1
                 grads = [_like(grad_of(p), p) for p in ps]
                 ms = [self.state[p]["exp_avg"] for p in ps]
                 vs = [self.state[p]["exp_avg_sq"] for p in ps]
@@ -166,11 +216,11 @@ class FusedAdamW(Optimizer):
                 table = None
                 if dev.type == "cuda":
                     cols = [ps, grads, ms, vs, lps if has_lp else [None] * len(ps)]
-                    table = self._tables.get((gi, gdt, step > 0), cols)
+                    table = self._tables.get((gi, gdt, ckey if dstep is not None else 0), cols)
                 mt.adamw_step(ps, grads, ms, vs, lr=lr, beta1=beta1, beta2=beta2, eps=group["eps"],
                               weight_decay=group["weight_decay"], step=max(step, 1),
                               decoupled=group.get("decoupled", True), grad_scale=grad_scale, found_inf=found_inf,
-                              out_bf16=lps if has_lp else None, table=table, dstep=dstep if step < 0 else None)
+                              out_bf16=lps if has_lp else None, table=table, dstep=dstep)
                 with torch.no_grad():
                     for p, x in lp_other:
                         x.copy_(p)

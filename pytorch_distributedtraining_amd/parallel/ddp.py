@@ -128,6 +128,7 @@ class _FlatGroup:
             # same strides as the parameter (channels_last convs): autograd accumulates in place
             p.grad = _pview(self.flat_grad, p, o)
             p._pdt_grad_flat = self.flat_grad   # FusedAdamW.zero_grad zeroes the flat once, views stay attached
+            p._pdt_grad_members = self.params   # ... when one optimizer owns every parameter viewing it
 
 
 def _cast_except_batchnorm(module: nn.Module, dtype: torch.dtype) -> None:
