@@ -75,12 +75,13 @@ def train(loader, t: Trainer, sched1, epoch, sink):
             sched1.step()
         if (idx + 1) % 10 == 0:
             t.print_ema_loss(prepend_msg=f"Step {idx + 1} -- EMA Loss")
-        # a SyncedLoss: the running sum stays on the device; the cross-rank mean and the host read happen only
-        # when a log line reads it (Stoke-DDP.py:86 synced on every micro-batch)
-        sum_loss += t.detach_and_sync_loss(loss=loss) * t.grad_accum
+        # lazy=True: a SyncedLoss -- the running sum stays on the device; the cross-rank mean and the host read
+        # happen only when a log line reads it (Stoke-DDP.py:86 synced on every micro-batch; every rank reads it)
+        sum_loss += t.detach_and_sync_loss(loss=loss, lazy=True) * t.grad_accum
         n += 1
         if (n + 1) % 50 == 0:
             sink.log({"train_loss": float(sum_loss / n), "epoch": epoch}, step=t.optimizer_steps)
+    t.flush_prints()
     return float(sum_loss / max(n, 1))
 
 

@@ -5,7 +5,9 @@ GQA 32q/8kv heads of 128, SwiGLU FFN 14336, vocab 128256), random init.
 MI355X-first layout: one fused q|k|v projection (``attention.wqkv``) and one fused gate|up projection
 (``feed_forward.w13``) so each block issues 4 large GEMMs instead of 7; RMSNorm / RoPE / SwiGLU /
 GQA flash attention / cross-entropy run on the HIP kernels.  ``convert_meta_state_dict`` maps Meta-style
-checkpoints (wq/wk/wv, w1/w3) onto the fused layout.
+checkpoints (wq/wk/wv, w1/w3) onto the fused layout and ``export_meta_state_dict`` maps back (bitwise: the fused
+weights are row concatenations), so a checkpoint saved here loads into a standard Meta-layout Llama
+(``Trainer(portable_checkpoint=True)`` writes that layout into the envelope).
 """
 from __future__ import annotations
 
@@ -138,6 +140,14 @@ class Llama(nn.Module):
         n = self.num_params() - self.tok_embeddings.weight.numel()
         return 6 * n + 12 * c.n_layers * seq_len * c.dim
 
+    def to_portable_state_dict(self, sd: dict) -> dict:
+        """This module's (fused) state dict -> the Meta layout (``export_meta_state_dict``)."""
+        return export_meta_state_dict(sd, self.config)
+
+    def from_portable_state_dict(self, sd: dict) -> dict:
+        """A Meta-layout state dict -> this module's fused layout; a fused one passes through."""
+        return convert_meta_state_dict(sd, self.config) if any(".attention.wq." in k for k in sd) else sd
+
     def forward(self, tokens, labels=None):
         S = tokens.shape[1]
         x = self.tok_embeddings(tokens)
@@ -173,6 +183,31 @@ def convert_meta_state_dict(sd: dict, cfg: LlamaConfig) -> dict:
             continue
         elif ".feed_forward.w1." in k:
             out[k.replace(".w1.", ".w13.")] = torch.cat([v, sd[k.replace(".w1.", ".w3.")]], 0)
+        else:
+            out[k] = v
+    return out
+
+
+def export_meta_state_dict(sd: dict, cfg: LlamaConfig) -> dict:
+    """Inverse of ``convert_meta_state_dict``: attention.wqkv -> wq | wk | wv (rows H*d | Hkv*d | Hkv*d) and
+    feed_forward.w13 -> w1 | w3 (rows ffn_dim each), every other key unchanged; views are cloned so the result
+    owns its storage."""
+    nq, nkv = cfg.n_heads * cfg.head_dim, cfg.n_kv_heads * cfg.head_dim
+    out = {}
+    for k, v in sd.items():
+        if ".attention.wqkv." in k:
+            q, kk, vv = torch.split(v, [nq, nkv, nkv], 0)
+            for name, t in ((".wq.", q), (".wk.", kk), (".wv.", vv)):
+                out[k.replace(".wqkv.", name)] = t.clone()
+        elif ".feed_forward.w13." in k:
+            w1, w3 = torch.split(v, [cfg.ffn_dim, cfg.ffn_dim], 0)
+            out[k.replace(".w13.", ".w1.")] = w1.clone()
+            w2k = k.replace(".w13.", ".w2.")
+            if w2k in sd:
+                out[w2k] = sd[w2k]
+            out[k.replace(".w13.", ".w3.")] = w3.clone()
+        elif ".feed_forward.w2." in k and k.replace(".w2.", ".w13.") in sd:
+            continue                          # emitted next to w1 / w3 above
         else:
             out[k] = v
     return out

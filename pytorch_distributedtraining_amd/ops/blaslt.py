@@ -65,14 +65,6 @@ def prefer_bgradb(dy2: torch.Tensor, x2: torch.Tensor, separate) -> bool:
         _CHOICE[key] = False
         return False
 
-    def t(fn):
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(3):
-            fn()
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1)
-    c = _CHOICE[key] = t(lambda: wgrad_bgrad(dy2, x2)) < t(separate)
+    from .linear import timed_choice
+    c = _CHOICE[key] = timed_choice(lambda: wgrad_bgrad(dy2, x2), separate)
     return c

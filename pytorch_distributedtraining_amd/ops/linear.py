@@ -45,10 +45,11 @@ _NT_CHOICE: dict = {}
 
 def _nt_hip_ok(a2: torch.Tensor, w: torch.Tensor, bias) -> bool:
     from . import gemm as G
+    # (G.nt_ok also requires 16-byte aligned operand pointers)
     return (HIP_NT != "0" and G.KERNEL["name"] == "asm" and a2.is_cuda and a2.dim() == 2 and a2.shape[0] >= 4096
             and a2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
-            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())) and G.nt_ok(a2, w)
-            and a2.shape[1] // 64 >= 2 and w.shape[0] % 8 == 0)
+            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
+            and G.nt_ok(a2, w) and a2.shape[1] // 64 >= 2 and w.shape[0] % 8 == 0)
 
 
 def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
@@ -60,8 +61,7 @@ def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
         key = (tuple(a2.shape), tuple(w.shape), bias is not None, a2.device)
         c = _NT_CHOICE.get(key)
         if c is None and not torch.cuda.is_current_stream_capturing():
-            c = _NT_CHOICE[key] = _timed_ms(lambda: G.gemm_nt(a2, w, bias)) < \
-                0.99 * _timed_ms(lambda: F.linear(a2, w, bias))
+            c = _NT_CHOICE[key] = timed_choice(lambda: G.gemm_nt(a2, w, bias), lambda: F.linear(a2, w, bias), 0.99)
         if c:
             return G.gemm_nt(a2, w, bias)
     return F.linear(a2, w, bias)
@@ -102,6 +102,24 @@ def _timed_ms(fn, iters: int = 3) -> float:
     return e0.elapsed_time(e1)
 
 
+def timed_choice(fa, fb, margin: float = 1.0) -> bool:
+    """Whether ``fa`` runs faster than ``margin`` x ``fb`` -- the per-shape kernel picks (hand GEMM vs hipBLASLt,
+    1x1 conv as GEMM vs MIOpen, BGRADB).  Decided IDENTICALLY on every rank: each rank times both arms (a timing
+    can overlap in-flight bucket collectives and differ between ranks), then the times are summed over the default
+    process group -- one 2-float all-reduce, issued in the same order by every rank since every rank meets the
+    same shapes in the same order -- so all ranks run the same kernels and reduce bitwise-comparable gradients.
+    The env switches of each pick (PDT_NT_HIP, PDT_WGRAD_HIP, PDT_CONV1X1) pin the choice outright."""
+    ta, tb = _timed_ms(fa), _timed_ms(fb)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else \
+            torch.device("cpu")
+        t = torch.tensor([ta, tb], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        ta, tb = (float(v) for v in t.tolist())
+    return ta < margin * tb
+
+
 def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, ragged: bool = False) -> bool:
     """Hand kernel vs hipBLASLt for this weight-gradient shape.  Measured, not assumed: the two trade places
     by shape and by box (GPT-2 1.3B attention projection +12 %, fc1 +3 %, Llama-3 8B qkv -14 % on one box;
@@ -115,8 +133,7 @@ def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, ragged: bool = False)
             return True
         # against the path wgrad() would otherwise take (split-K batched GEMM for small outputs, else one GEMM)
         hip = hip_wgrad_ragged if ragged else hip_wgrad
-        c = _WGRAD_CHOICE[key] = _timed_ms(lambda: hip(dy2, x2)) < \
-            _timed_ms(lambda: _library_wgrad(dy2, x2, torch.bfloat16))
+        c = _WGRAD_CHOICE[key] = timed_choice(lambda: hip(dy2, x2), lambda: _library_wgrad(dy2, x2, torch.bfloat16))
     return c
 
 

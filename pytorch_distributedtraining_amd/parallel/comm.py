@@ -12,7 +12,9 @@ debug mode (``PDT_COMM_DEBUG=1`` or ``TORCH_DISTRIBUTED_DEBUG=DETAIL``) ``verify
 compares the rolling hash across ranks -- the mismatch detector of SURVEY.md §5.2.
 
 Reference: the collectives the reference triggers through torch/Fairscale,
-re-issued here as few, large, bucketed operations sized for 7 xGMI links per GPU.
+re-issued here as few, large, bucketed operations.  The bucket / window sizes are chosen from link arithmetic
+for 7 xGMI links per GPU and are defaults UNMEASURED on a multi-GPU node: no sweep against RCCL
+has run yet (every run so far had one GPU).
 """
 from __future__ import annotations
 

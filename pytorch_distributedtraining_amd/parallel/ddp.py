@@ -7,8 +7,8 @@ rebuild, :1442-1468 no_sync, :1558 buffer broadcast; reducer.hpp:30-31 bucket ca
 MI355X-first design:
   * ONE flat layout for everything: the native ``BucketPlanner`` orders parameters into buckets
     (reverse registration order, first bucket small so communication starts early, later buckets
-    large -- 64 MiB default, sized so a ring step per xGMI link stays bandwidth- rather than
-    latency-bound), and the model parameters, their gradients (``gradient_as_bucket_view``: autograd
+    large -- 64 MiB default, chosen by arithmetic so a ring step per xGMI link would stay bandwidth- rather
+    than latency-bound; a default, unmeasured on a multi-GPU node), and the model parameters, their gradients (``gradient_as_bucket_view``: autograd
     accumulates straight into the bucket, no copy-in) and -- with ``compute_dtype`` -- the fp32 master
     copy all share that layout.  The optimizer then updates the whole model with ONE fused AdamW
     launch reading bf16 grads and writing the bf16 compute params in its epilogue.
@@ -150,7 +150,8 @@ class DistributedDataParallel(nn.Module):
     Args:
         module: the model (its parameters are re-pointed into flat buffers on ``device``).
         comm: collective layer (default process group).
-        bucket_cap_mb / first_bucket_mb: bucket sizes (defaults 64 / 8 MiB for xGMI; torch uses 25 / 1).
+        bucket_cap_mb / first_bucket_mb: bucket sizes (defaults 64 / 8 MiB, picked from xGMI link arithmetic and
+            unmeasured on a multi-GPU node; torch uses 25 / 1).
         broadcast_buffers: broadcast buffers from rank 0 every forward.
         buffer_sync: "changed" (default) sends only buffers written since the last sync; "all" sends every
             buffer every forward like torch DDP.

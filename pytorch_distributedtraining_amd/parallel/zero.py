@@ -382,6 +382,21 @@ class _Window:
         self.drop = []      # non-owned local param idx whose LAST window this is (gradient freed after packing)
 
 
+def _merge_in_order(seqs):
+    """Merge sequences of (key, ...) tuples by key, keeping each sequence's own order (ties: earlier sequence)."""
+    heads = [0] * len(seqs)
+    out = []
+    while True:
+        best = None
+        for i, sq in enumerate(seqs):
+            if heads[i] < len(sq) and (best is None or sq[heads[i]][0] < seqs[best][heads[best]][0]):
+                best = i
+        if best is None:
+            return out
+        out.append(seqs[best][heads[best]])
+        heads[best] += 1
+
+
 class ShardedDataParallel(nn.Module):
     """ZeRO-2: gradients are reduce-scattered (averaged) onto the ranks that own their optimizer shard, and
     non-owners drop them.  ``reduce_mode="all_reduce"``: ZeRO-1 (full gradients all-reduced, DDP + OSS).
@@ -431,11 +446,18 @@ class ShardedDataParallel(nn.Module):
             n = bank.seg if reduce_mode == "reduce" else bank.total
             self._grad[id(bank)] = torch.zeros(n, dtype=bank.dtype, device=bank.device)
         if reduce_mode == "reduce":
+            # every bank's windows in release order, merged across banks by when backward completes them -- the
+            # smallest parameter index a window touches arrives last (backward runs in reverse registration
+            # order) -- so with several banks (dtypes / devices) bank 1's first window is not queued behind bank
+            # 0's last one; each bank keeps its own order (a k-way merge, never a sort)
+            seqs = []
             for bank in sharded_optimizer.banks():
                 wins, first = self._plan_windows(bank, reduce_buffer_size)
-                for k, w in enumerate(wins):
-                    self._buckets.append(w)
-                    readiness.append([bank.idxs[li] for li in first.get(k, [])])
+                seqs.append([(-min((bank.idxs[m[1]] for m in w.members), default=0), w,
+                              [bank.idxs[li] for li in first.get(k, [])]) for k, w in enumerate(wins)])
+            for _key, w, ready in _merge_in_order(seqs):
+                self._buckets.append(w)
+                readiness.append(ready)
         else:
             tmp = []
             for bank in sharded_optimizer.banks():

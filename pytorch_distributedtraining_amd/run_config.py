@@ -92,7 +92,10 @@ def apply_env_overrides(cfg: RunConfig, env=None) -> RunConfig:
     return dataclasses.replace(cfg, **upd) if upd else cfg
 
 
-XGMI_AUTO_MAX_KB = 1024     # PDT_XGMI=auto: the mesh takes the latency class up to this size, RCCL the rest
+# PDT_XGMI=auto: the mesh takes the latency class up to this size, RCCL the rest.  A default from the size-class
+# arithmetic of SURVEY.md §5.8, unmeasured on a multi-GPU node (the mesh has only run as ranks sharing one GPU),
+# which is also why PDT_XGMI defaults to off
+XGMI_AUTO_MAX_KB = 1024
 
 
 def xgmi_mode(env=None) -> str:

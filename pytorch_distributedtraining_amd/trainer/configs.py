@@ -5,7 +5,8 @@ convert_to_sync_batch_norm=True) :190-193; FairscaleOSSConfig(broadcast_fp16=Tru
 ClipGradNormConfig(max_norm, norm_type=2.0) :253; StokeOptimizer(optimizer, optimizer_kwargs)
 :226-235; DistributedOptions.ddp / FP16Options.amp :247-248; DeepspeedConfig / DeepspeedZeROConfig
 imported :18 (here they map onto the framework's own ZeRO engines).  Defaults follow SURVEY.md B1.cfg
-except where MI355X tuning differs (DDP bucket caps sized for 7 xGMI links -- documented per field).
+except where the MI355X defaults differ (DDP bucket caps picked from 7-xGMI-link arithmetic -- documented per
+field; defaults, unmeasured on a multi-GPU node).
 """
 from __future__ import annotations
 
@@ -43,7 +44,8 @@ class DDPConfig:
     local_rank: Optional[int] = None
     backend: str = "nccl"                 # RCCL on ROCm; 'gloo' for CPU runs
     init_method: str = "env://"
-    bucket_cap_mb: float = 64.0           # torch default 25; larger buckets keep xGMI ring steps bandwidth-bound
+    bucket_cap_mb: float = 64.0           # torch default 25; larger buckets should keep xGMI ring steps
+                                          # bandwidth-bound (arithmetic; unmeasured on a multi-GPU node)
     first_bucket_mb: float = 8.0          # torch default 1
     broadcast_buffers: bool = True
     find_unused_parameters: bool = False

@@ -43,12 +43,18 @@ def _val(x):
 
 
 class SyncedLoss:
-    """A rank-local device scalar whose cross-rank mean is taken lazily (``Trainer.detach_and_sync_loss``).
+    """A rank-local device scalar whose cross-rank mean is taken lazily (``Trainer.detach_and_sync_loss(loss,
+    lazy=True)`` or ``Trainer(lazy_loss_sync=True)``).
 
     Linear arithmetic keeps it on the device and unsynchronised: ``+``/``-`` with another SyncedLoss or a number,
-    ``*``/``/`` by a number (the mean over ranks commutes with these).  Reading it -- ``float()``, ``item()``,
-    formatting, comparisons -- runs ONE all-reduce (AVG) and one host read, then caches the value.  A number
-    added to it is treated as already rank-uniform (e.g. the ``0.0`` a running sum starts from)."""
+    ``*``/``/`` by a number (the mean over ranks commutes with these).  Reading it -- ``float()``, ``int()``,
+    ``item()``, ``bool()``, formatting, comparisons, ``==`` -- runs ONE all-reduce (AVG) and one host read, then
+    caches the value.  READING IS A COLLECTIVE: every rank must read the value at the same point (a read on one rank
+    only, e.g. under ``if rank == 0``, waits forever for the others); ``float(x)`` on every rank first, then use the
+    float.  Not hashable and not JSON-serialisable (log ``float(x)``).  A number added to it is treated as already
+    rank-uniform (e.g. the ``0.0`` a running sum starts from)."""
+
+    __hash__ = None
 
     __slots__ = ("t", "comm", "_value")
 
@@ -121,15 +127,34 @@ class SyncedLoss:
     def __ge__(self, o):
         return self.item() >= float(o)
 
+    def __eq__(self, o):
+        return self.item() == float(o)
+
+    def __ne__(self, o):
+        return self.item() != float(o)
+
+    def __bool__(self):
+        return bool(self.item())
+
+    def __int__(self):
+        return int(self.item())
+
 
 class Trainer:
     def __init__(self, model: nn.Module, optimizer, loss, batch_size_per_device: int, grad_accum_steps: int = 1,
                  grad_clip=None, gpu: bool = False, fp16=None, distributed=None, fairscale_oss: bool = False,
                  fairscale_sddp: bool = False, fairscale_fsdp: bool = False, configs=None, info_rank=0,
-                 verbose: bool = True, ema_weight: float = 0.1, comm: Comm | None = None, fp8: bool = False):
+                 verbose: bool = True, ema_weight: float = 0.1, comm: Comm | None = None, fp8: bool = False,
+                 lazy_loss_sync: bool = False, ema_print_every: int = 1, portable_checkpoint: bool = False):
         """``fp8=True`` (with bf16 precision on GPU): every framework ``Linear`` of the model runs its forward,
         data- and weight-gradient GEMMs in fp8 with delayed scaling (``ops.fp8.fp8_autocast``); norms,
-        attention, the loss and the optimizer stay bf16 / fp32."""
+        attention, the loss and the optimizer stay bf16 / fp32.
+        ``lazy_loss_sync``: ``detach_and_sync_loss`` returns a ``SyncedLoss`` (synchronised when read) instead of
+        Stoke's float (an all-reduce and a host read per call).  ``ema_print_every``: ``print_ema_loss`` acts on
+        every N-th call only (Stoke prints on every call; the others then issue nothing at all).
+        ``portable_checkpoint``: ``save`` writes the model in its standard layout where the model defines one
+        (``to_portable_state_dict``: Llama's fused wqkv / w13 split back into Meta's wq, wk, wv / w1, w3); ``load``
+        accepts either layout (``from_portable_state_dict``)."""
         self.verbose = verbose
         self.logger = RankLogger(info_rank, verbose)
         self._loss_fn = loss
@@ -253,6 +278,11 @@ class Trainer:
         self._optimizer_steps = 0
         self._ema_weight = ema_weight
         self._ema = None           # device tensor
+        self._lazy_loss = bool(lazy_loss_sync)
+        self._portable = bool(portable_checkpoint)
+        self._ema_every = max(1, int(ema_print_every))
+        self._ema_calls = 0
+        self._ema_pending = []     # (event, pinned host scalar, message parts): EMA prints waiting for their copy
         self._last_loss = None
         self._training = True
         # PDT_COMM_DEBUG=1: cross-rank collective-sequence check every K optimizer steps
@@ -449,23 +479,55 @@ class Trainer:
         self._optimizer.zero_grad(set_to_none=True)
 
     # ------------------------------------------------------------------ loss sync / printing
-    def detach_and_sync_loss(self, loss, device=None):
-        """The loss averaged over ranks, as a ``SyncedLoss``: a device scalar that is NOT synchronised yet.
-        Stoke returns a float (an all-reduce plus a host read on every micro-batch, Stoke-DDP.py:86); here
-        ``sum_loss += t.detach_and_sync_loss(loss)`` stays on the device (sums of rank-local values), and the
-        one all-reduce + host read happen when the value is read (``float()``, formatting, comparisons) --
-        on log steps only.  Every rank must read it at the same point (it is a collective)."""
-        return SyncedLoss(loss.detach().float().reshape(1).clone(), self.comm)
+    def detach_and_sync_loss(self, loss, device=None, lazy: bool | None = None):
+        """The loss averaged over ranks (Stoke-DDP.py:86).  Default: a float, as Stoke returns -- one all-reduce
+        and one host read per call, a collective every rank makes.  ``lazy=True`` (or ``Trainer(lazy_loss_sync=
+        True)``): a ``SyncedLoss`` device scalar that is NOT synchronised yet -- ``sum_loss += t.detach_and_sync_loss(
+        loss, lazy=True)`` stays on the device, and the one all-reduce + host read happen when the sum is read (on
+        log steps only); reading it is then the collective."""
+        s = SyncedLoss(loss.detach().float().reshape(1).clone(), self.comm)
+        if lazy if lazy is not None else self._lazy_loss:
+            return s
+        return s.item()
 
     def print_ema_loss(self, prepend_msg: str = "Current EMA Loss", postpend_msg: str = ""):
-        """Collective (every rank calls it): one device all-reduce of the EMA; only the printing rank reads the
-        value back to the host."""
-        if self._ema is None:
+        """Print the EMA of the loss averaged over ranks (Stoke-DDP.py:76).  Every rank calls it (on a print call
+        the ranks reduce their EMAs to the printing rank -- a device-side collective, no host wait on any rank).  The
+        printing rank copies the value to pinned host memory asynchronously and prints it once the copy has
+        landed (usually at its next call; ``flush_prints`` waits for the rest), so no call blocks the host on the
+        device.  With ``ema_print_every=N`` only every N-th call does anything."""
+        self._ema_calls += 1
+        if self._ema is None or (self._ema_calls - 1) % self._ema_every:
             return
         t = self._ema.reshape(1).clone()
-        self.comm.all_reduce(t, "avg")
-        if self.logger.will_print():
-            self.logger.print(f"{prepend_msg}: {float(t.item()):.5f} {postpend_msg}".rstrip())
+        if self.world_size_ > 1:
+            self.comm.reduce(t, dst=int(self.logger.info_rank if not isinstance(self.logger.info_rank, (list, tuple))
+                                        else self.logger.info_rank[0]), op="avg")
+        if not self.logger.will_print():
+            return
+        parts = (prepend_msg, postpend_msg)
+        if t.is_cuda:
+            host = torch.empty(1, dtype=torch.float32, pin_memory=True)
+            host.copy_(t, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._ema_pending.append((ev, host, parts))
+            self._flush_ema(block=False)
+        else:
+            self._print_ema(float(t), parts)
+
+    def _print_ema(self, v, parts):
+        self.logger.print(f"{parts[0]}: {v:.5f} {parts[1]}".rstrip())
+
+    def _flush_ema(self, block: bool):
+        while self._ema_pending and (block or self._ema_pending[0][0].query()):
+            ev, host, parts = self._ema_pending.pop(0)
+            ev.synchronize()
+            self._print_ema(float(host), parts)
+
+    def flush_prints(self):
+        """Print every EMA line still waiting for its device-to-host copy (waits for those copies)."""
+        self._flush_ema(block=True)
 
     def print_on_devices(self, msg, rank=None):
         self.logger.print(msg, ranks=None if rank is None else (rank if isinstance(rank, (list, tuple)) else [rank]))
@@ -492,6 +554,13 @@ class Trainer:
 
     # ------------------------------------------------------------------ checkpointing
     def _model_state(self):
+        sd = self._model_state_native()
+        fn = getattr(self._module, "to_portable_state_dict", None)
+        if self._portable and fn is not None and sd:
+            sd = fn(sd)
+        return sd
+
+    def _model_state_native(self):
         eng = self._engine
         if hasattr(eng, "sharding_strategy"):           # FSDP: full unflattened fp32 state dict, unit by
             return eng.state_dict(rank0_only=True, offload_to_cpu=True)   # unit to rank 0's host memory
@@ -513,6 +582,7 @@ class Trainer:
     def save(self, path: str, name: str | None = None, extension: str = "pt", create_directory: bool = True,
              extras: dict | None = None):
         name = name or uuid.uuid4().hex[:8]
+        self.flush_prints()
         model_state = self._model_state()
         opt_state = self._optimizer_state()
         return ckpt.save_checkpoint(
@@ -525,6 +595,9 @@ class Trainer:
     def load(self, path: str, tag: str, strict: bool = True, extension: str = "pt"):
         payload = ckpt.load_checkpoint(path, tag, extension=extension,
                                        map_location=self.device if self.device.type == "cpu" else "cpu")
+        fn = getattr(self._module, "from_portable_state_dict", None)
+        if fn is not None:
+            payload["model_state_dict"] = fn(payload["model_state_dict"])
         eng = self._engine
         if hasattr(eng, "sharding_strategy"):
             eng.load_state_dict(payload["model_state_dict"], strict=strict)

@@ -1,0 +1,84 @@
+"""Llama checkpoint layout (north star: "the same state_dict/checkpoint layout"): the fused wqkv / w13 weights of
+models/llama.py convert to Meta's wq / wk / wv / w1 / w3 and back bitwise, a Meta-layout Llama module loads the
+exported dict strictly, and Trainer(portable_checkpoint=True) writes that layout into the Stoke envelope
+(Stoke-DDP.py:142-145) and loads it back."""
+import os
+
+import torch
+import torch.nn as nn
+
+from pytorch_distributedtraining_amd.models.llama import (build_llama, convert_meta_state_dict,
+                                                          export_meta_state_dict, llama_config)
+
+
+class _MetaRMSNorm(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+
+
+class _MetaBlock(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        d, hd = c.dim, c.head_dim
+        self.attention = nn.Module()
+        self.attention.wq = nn.Linear(d, c.n_heads * hd, bias=False)
+        self.attention.wk = nn.Linear(d, c.n_kv_heads * hd, bias=False)
+        self.attention.wv = nn.Linear(d, c.n_kv_heads * hd, bias=False)
+        self.attention.wo = nn.Linear(c.n_heads * hd, d, bias=False)
+        self.feed_forward = nn.Module()
+        self.feed_forward.w1 = nn.Linear(d, c.ffn_dim, bias=False)
+        self.feed_forward.w2 = nn.Linear(c.ffn_dim, d, bias=False)
+        self.feed_forward.w3 = nn.Linear(d, c.ffn_dim, bias=False)
+        self.attention_norm = _MetaRMSNorm(d)
+        self.ffn_norm = _MetaRMSNorm(d)
+
+
+class _MetaLlama(nn.Module):
+    """The Meta reference checkpoint layout (parameters only)."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.tok_embeddings = nn.Embedding(c.vocab_size, c.dim)
+        self.layers = nn.ModuleList([_MetaBlock(c) for _ in range(c.n_layers)])
+        self.norm = _MetaRMSNorm(c.dim)
+        self.output = nn.Linear(c.dim, c.vocab_size, bias=False)
+
+
+def test_meta_round_trip_is_bitwise_and_loads_strictly():
+    torch.manual_seed(0)
+    cfg = llama_config("llama3-tiny", n_heads=4, n_kv_heads=2)
+    ref = _MetaLlama(cfg)
+    meta = ref.state_dict()
+    fused = convert_meta_state_dict(meta, cfg)
+    m = build_llama("llama3-tiny", n_heads=4, n_kv_heads=2)
+    m.load_state_dict(fused, strict=True)
+    back = export_meta_state_dict(m.state_dict(), cfg)
+    assert set(back) == set(meta)
+    for k in meta:
+        assert torch.equal(back[k], meta[k]), k
+    _MetaLlama(cfg).load_state_dict(back, strict=True)
+
+
+def test_trainer_portable_checkpoint(tmp_path):
+    from pytorch_distributedtraining_amd.trainer import StokeOptimizer, Trainer
+    torch.manual_seed(1)
+    cfg = llama_config("llama3-tiny")
+    model = build_llama("llama3-tiny")
+    opt = StokeOptimizer(optimizer=torch.optim.AdamW, optimizer_kwargs={"lr": 1e-3})
+    t = Trainer(model, opt, lambda loss: loss, batch_size_per_device=2, verbose=False, portable_checkpoint=True)
+    x = torch.randint(0, cfg.vocab_size, (2, 17))
+    t.backward(t.loss(t.model(x[:, :-1], labels=x[:, 1:])))
+    t.step()
+    path, tag = t.save(str(tmp_path), name="llama")
+    payload = torch.load(os.path.join(path, tag + ".pt"), weights_only=True)
+    sd = payload["model_state_dict"]
+    assert "layers.0.attention.wq.weight" in sd and "layers.0.attention.wqkv.weight" not in sd
+    _MetaLlama(cfg).load_state_dict(sd, strict=True)
+    before = {k: v.clone() for k, v in t.model_access.state_dict().items()}
+    with torch.no_grad():
+        for p in t.model_access.parameters():
+            p.zero_()
+    t.load(path, tag)                                       # the Meta layout loads back into the fused module
+    for k, v in t.model_access.state_dict().items():
+        assert torch.equal(v, before[k]), k

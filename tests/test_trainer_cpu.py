@@ -217,7 +217,7 @@ def _w_lazy_loss(rank, world):
         t.backward(loss)
         t.step()
         c0 = t.comm.stats["calls"]
-        lazy = lazy + t.detach_and_sync_loss(loss) * 2
+        lazy = lazy + t.detach_and_sync_loss(loss, lazy=True) * 2
         calls.append(t.comm.stats["calls"] - c0)                  # no collective while summing
         d = loss.detach().reshape(1).clone()
         torch.distributed.all_reduce(d)
@@ -235,3 +235,48 @@ def test_lazy_synced_loss_matches_eager(world):
         assert abs(v - e) < 1e-5 * max(1.0, abs(e)), (v, e)
         assert n == 1                                               # one all-reduce for the whole sum
     assert outs[0][0] == outs[1][0]
+
+
+def _w_ema_print(rank, world):
+    """print_ema_loss (Stoke-DDP.py:76): the printed value is the EMA of the rank-averaged loss; with
+    ema_print_every=3 only every third call issues a collective; detach_and_sync_loss returns Stoke's float by
+    default and the lazy SyncedLoss compares / converts like a number."""
+    import io
+    from pytorch_distributedtraining_amd.trainer import SyncedLoss
+    torch.manual_seed(0)
+    t = Trainer(_model(), _opt(), nn.MSELoss(), batch_size_per_device=2, distributed="ddp", verbose=False,
+                ema_print_every=3)
+    out = io.StringIO()
+    t.logger.stream = out
+    ema, calls = None, []
+    for step in range(6):
+        g = torch.Generator().manual_seed(10 * step + rank)
+        x, y = torch.randn(2, 3, 8, 8, generator=g), torch.randn(2, 3, 8, 8, generator=g)
+        loss = t.loss(t.model(x), y)
+        d = loss.detach().reshape(1).clone()
+        torch.distributed.all_reduce(d)
+        m = float(d) / world
+        ema = m if ema is None else 0.1 * m + 0.9 * ema
+        c0 = t.comm.stats["calls"]
+        t.print_ema_loss(prepend_msg=f"s{step}")
+        calls.append(t.comm.stats["calls"] - c0)
+        t.backward(loss)
+        t.step()
+        if step == 3:
+            expect = ema
+    t.flush_prints()
+    f = t.detach_and_sync_loss(loss)
+    lz = t.detach_and_sync_loss(loss, lazy=True)
+    ok = isinstance(f, float) and isinstance(lz, SyncedLoss) and lz == f and int(lz) == int(f) and bool(lz)
+    return out.getvalue(), expect, calls, ok
+
+
+def test_ema_print_every_and_loss_sync_api():
+    outs = run_workers(_w_ema_print, 2)
+    text0, expect, calls, ok = outs[0]
+    lines = [ln for ln in text0.splitlines() if ln.startswith("s")]
+    assert [ln.split(":")[0] for ln in lines] == ["s0", "s3"]            # calls 1 and 4 of 6
+    assert abs(float(lines[1].split(":")[1]) - expect) < 1e-4 * max(1.0, abs(expect))
+    assert outs[1][0] == ""                                             # rank 1 prints nothing
+    for _, _, c, o in outs:
+        assert c == [1, 0, 0, 1, 0, 0] and o                            # a collective on print calls only

@@ -205,7 +205,7 @@ def _trainer_latency_worker(rank, world):
     calls["backward"], c = x.calls - c, x.calls
     t.step()
     calls["clip_found_inf"], c = x.calls - c, x.calls
-    synced = t.detach_and_sync_loss(loss)
+    synced = t.detach_and_sync_loss(loss, lazy=True)
     calls["loss_lazy"], c = x.calls - c, x.calls
     v = float(synced)
     calls["loss_read"] = x.calls - c
