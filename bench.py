@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--grad-clip", type=float, default=1.0)
     ap.add_argument("--reshard", type=int, default=1, help="FSDP reshard after forward (FULL_SHARD)")
     ap.add_argument("--act-ckpt", type=int, default=0)
+    ap.add_argument("--act-ckpt-policy", default=None, choices=["full", "selective"],
+                    help="what a checkpointed layer recomputes: the whole block forward (full), or only norms / "
+                         "attention forward / SwiGLU with the GEMM outputs kept (selective; Llama default)")
     ap.add_argument("--act-ckpt-layers", default="all",
                     help="with activation checkpointing: 'all', a layer count, or 'auto' = recompute only as many "
                          "layers as the HBM needs (sized after the first warm-up step)")
@@ -347,7 +350,8 @@ def bench_gpt2(args, comm, dev, world, rank):
     with torch.device(dev):
         if llama:
             from pytorch_distributedtraining_amd.models.llama import build_llama
-            model = build_llama(name, max_seq_len=max(S, 2048), activation_checkpointing=bool(args.act_ckpt or 1))
+            model = build_llama(name, max_seq_len=max(S, 2048), activation_checkpointing=bool(args.act_ckpt or 1),
+                                checkpoint_policy=args.act_ckpt_policy or "selective")
         else:
             model = build_gpt2(name, n_positions=max(1024, S), activation_checkpointing=bool(args.act_ckpt))
     nparams = model.num_params()
@@ -454,6 +458,7 @@ def bench_gpt2(args, comm, dev, world, rank):
             "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
                        "micro_batch_per_gpu": mb, "params": nparams, "hip_graph": graph, "sharding": "full_shard" if args.reshard else
                        "shard_grad_op", "optimizer": "fused AdamW + global-norm clip",
+                       **({"act_ckpt_policy": getattr(inner.config, "checkpoint_policy", "full")} if ckpt_on else {}),
                        **({"act_ckpt_layers": inner.config.checkpoint_layers
                            if inner.config.checkpoint_layers is not None else
                            getattr(inner.config, "n_layers", getattr(inner.config, "n_layer", None))}

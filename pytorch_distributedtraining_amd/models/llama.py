@@ -24,7 +24,8 @@ from ..ops.rope import apply_rope_qk_
 from ..ops.embedding import Embedding
 from ..ops.fp8 import fp8_recompute_safe
 from ..ops.linear import Linear
-from ..ops.norms import RMSNorm
+from ..ops.norms import RMSNorm, rms_norm
+from ..utils import recompute
 
 
 @dataclass
@@ -39,10 +40,13 @@ class LlamaConfig:
     rope_theta: float = 500000.0
     max_seq_len: int = 8192
     activation_checkpointing: bool = False
-    # selective checkpointing: how many of the layers (the first ones) recompute their forward in backward;
-    # None = all of them when activation_checkpointing is on.  With 288 GB of HBM most of the recompute can be
-    # bought back (bench.py --act-ckpt-layers auto sizes it to the memory)
+    # how many of the layers (the first ones) are checkpointed; None = all of them when activation_checkpointing is
+    # on.  With 288 GB of HBM most of the recompute can be bought back (bench.py --act-ckpt-layers auto sizes it)
     checkpoint_layers: int | None = None
+    # "full": a checkpointed layer re-runs its whole forward in backward (torch.utils.checkpoint); "selective": it
+    # keeps its GEMM outputs (qkv, gate/up) and residual stream and recomputes only the norms, the attention
+    # forward and SwiGLU when backward needs their outputs (utils.recompute) -- no GEMM runs twice
+    checkpoint_policy: str = "full"
 
     @property
     def head_dim(self):
@@ -77,7 +81,11 @@ class Attention(nn.Module):
         # reads q / k / v as head ranges of it (and writes ONE packed gradient): no separate rotated q / k
         # tensors and no gradient scatter into the packed layout
         o = flash_attn_gqa_packed(qkv, self.h, self.hkv, causal=True)
-        return self.wo(o.reshape(B, S, self.h * self.d))
+        o2 = o.reshape(B, S, self.h * self.d)
+        r = getattr(o, "_pdt_recipe", None)          # selective recompute: wo's saved input is the same forward
+        if r is not None:
+            recompute.tag(o2, r[0], r[1], view=lambda t: t.reshape(B, S, self.h * self.d))
+        return self.wo(o2)
 
 
 class FeedForward(nn.Module):
@@ -87,7 +95,10 @@ class FeedForward(nn.Module):
         self.w2 = Linear(cfg.ffn_dim, cfg.dim, bias=False)
 
     def forward(self, x):
-        return self.w2(swiglu(self.w13(x)))
+        g = self.w13(x)
+        a = swiglu(g)
+        recompute.tag(a, recompute.Recipe(lambda: swiglu(g)))   # (only inside selective_recompute)
+        return self.w2(a)
 
 
 class LlamaBlock(nn.Module):
@@ -99,13 +110,23 @@ class LlamaBlock(nn.Module):
         self.feed_forward = FeedForward(cfg)
 
     def forward(self, x, cos, sin, pending=None):
-        """(x, pending) -> (x', ffn_out); residual adds fused into the next RMSNorm kernel."""
+        """(x, pending) -> (x', ffn_out); residual adds fused into the next RMSNorm kernel.  Inside
+        ``utils.recompute.selective_recompute()`` the norm outputs are saved as recipes over the residual stream."""
         if pending is None:
             h = self.attention_norm(x)
         else:
             h, x = self.attention_norm.forward_add(x, pending)
+        _tag_norm(h, x, self.attention_norm)
         y, x = self.ffn_norm.forward_add(x, self.attention(h, cos, sin))
+        _tag_norm(y, x, self.ffn_norm)
         return x, self.feed_forward(y)
+
+
+def _tag_norm(out, s, norm):
+    """norm(s) is exactly ``out`` (the fused add-norm normalises the rounded sum it stores): saved as that recipe."""
+    if recompute.active():
+        w, eps = norm.weight, norm.eps
+        recompute.tag(out, recompute.Recipe(lambda: rms_norm(s, w, eps)))
 
 
 class Llama(nn.Module):
@@ -154,8 +175,13 @@ class Llama(nn.Module):
         cos, sin = self.rope_cos[:S], self.rope_sin[:S]
         pending = None
         n_ckpt = self.config.checkpoint_layers if self.config.checkpoint_layers is not None else len(self.layers)
+        selective = self.config.checkpoint_policy == "selective"
         for i, layer in enumerate(self.layers):
-            if self.config.activation_checkpointing and self.training and i < n_ckpt:
+            ckpt = self.config.activation_checkpointing and self.training and i < n_ckpt
+            if ckpt and selective:
+                with recompute.selective_recompute():
+                    x, pending = layer(x, cos, sin, pending)
+            elif ckpt:
                 x, pending = torch.utils.checkpoint.checkpoint(fp8_recompute_safe(layer), x, cos, sin, pending,
                                                                use_reentrant=False)
             else:

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from ..utils import recompute as _rc
 
 
 def _strides(t):
@@ -159,6 +160,10 @@ class _FlashAttnGQAPackedFn(torch.autograd.Function):
         _check(qkv, "qkv")
         q, k, v = qkv[:, :, :hq], qkv[:, :, hq:hq + hkv], qkv[:, :, hq + hkv:]
         o, lse = _fwd(q, k, v, causal, scale)
+        if _rc.active():     # selective recompute: o / lse saved as "run this forward again" (utils.recompute)
+            recipe = _rc.Recipe(lambda: _fwd(q, k, v, causal, scale))
+            _rc.tag(o, recipe, 0)
+            _rc.tag(lse, recipe, 1)
         ctx.save_for_backward(qkv, o, lse)
         ctx.hq, ctx.hkv, ctx.causal, ctx.scale = hq, hkv, causal, scale
         return o

@@ -32,6 +32,7 @@ from .attention import take_bias_grad
 from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 from .gemm import gemm_tt, tt_ok, tt_splits
+from .grad_slots import claim, is_sharded_param
 
 _WGRAD_CHUNK = 4096
 
@@ -151,12 +152,12 @@ def hip_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) ->
             and tt_ok(dy2, x2, hip_wgrad_splits(m, n, k)))
 
 
-def hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+def hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int | None = None, out: torch.Tensor | None = None):
     """dW [N, K] = dy2^T x2 on the hand MFMA GEMM (csrc/kernels/gemm.hip, TT layout: both operands token-major,
-    fragments read transposed from LDS), bf16 out."""
+    fragments read transposed from LDS), bf16 out (into ``out`` when given)."""
     m, n = dy2.shape
     k = x2.shape[1]
-    return gemm_tt(dy2, x2, splits or hip_wgrad_splits(m, n, k))
+    return gemm_tt(dy2, x2, splits or hip_wgrad_splits(m, n, k), out=out)
 
 
 def _ragged_rows(n: int) -> int:
@@ -174,11 +175,12 @@ def hip_wgrad_ragged_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dt
             and nm < n and tt_ok(dy2[:, :nm], x2, hip_wgrad_splits(m, nm, k)))
 
 
-def hip_wgrad_ragged(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+def hip_wgrad_ragged(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     m, n = dy2.shape
     k = x2.shape[1]
     nm = _ragged_rows(n)
-    out = torch.empty(n, k, dtype=torch.bfloat16, device=dy2.device)
+    if out is None:
+        out = torch.empty(n, k, dtype=torch.bfloat16, device=dy2.device)
     gemm_tt(dy2[:, :nm], x2, hip_wgrad_splits(m, nm, k), out=out[:nm])
     if m % 16 == 0 and x2.is_contiguous():
         # the < 256-row remainder is a K = tokens, tiny-output product: 16 token slices as one batched GEMM
@@ -192,27 +194,50 @@ def hip_wgrad_ragged(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None):
     """dW = dy2^T @ x2 ([M, N]^T [M, K] -> [N, K]) in ``out_dtype``; the hand MFMA kernel for large bf16
-    shapes (a ragged row count split between it and hipBLASLt), row-split batched GEMM for tall-skinny M."""
+    shapes (a ragged row count split between it and hipBLASLt), row-split batched GEMM for tall-skinny M.
+    ``out``: a contiguous [N, K] ``out_dtype`` tensor the result is written into (the GEMM's own output where
+    the path allows, e.g. an FSDP unit's flat-gradient slot -- ops.grad_slots)."""
     m, n = dy2.shape
     k = x2.shape[1]
     if not dy2.is_cuda:
-        return torch.mm(dy2.t(), x2).to(out_dtype)
-    if hip_wgrad_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2):
-        return hip_wgrad(dy2, x2)
-    if hip_wgrad_ragged_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2, ragged=True):
-        return hip_wgrad_ragged(dy2, x2)
-    return _library_wgrad(dy2, x2, out_dtype)
+        r = torch.mm(dy2.t(), x2).to(out_dtype)
+    elif hip_wgrad_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2):
+        r = hip_wgrad(dy2, x2, out=out)
+    elif hip_wgrad_ragged_ok(dy2, x2, out_dtype) and _prefer_hip_wgrad(dy2, x2, ragged=True):
+        r = hip_wgrad_ragged(dy2, x2, out=out)
+    else:
+        r = _library_wgrad(dy2, x2, out_dtype, out=out)
+    if out is not None and r.data_ptr() != out.data_ptr():
+        out.copy_(r)
+        r = out
+    return r
 
 
-def _library_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+def _wgrad_result(w: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
+    """A Linear backward's weight gradient: written into the parameter's FSDP flat-gradient slot when it has one
+    (ops.grad_slots; returns None, autograd then carries no gradient for the weight), else returned."""
+    slot = claim(w)
+    if slot is None:
+        return wgrad(dy2, x2, w.dtype)
+    dst, acc = slot
+    if acc:
+        dst.add_(wgrad(dy2, x2, w.dtype))
+    else:
+        wgrad(dy2, x2, w.dtype, out=dst)
+    return None
+
+
+def _library_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None):
     """dW on hipBLASLt: one GEMM, a token-split batched GEMM (small outputs) or the row-split tall-skinny form."""
     m, n = dy2.shape
     k = x2.shape[1]
     if not _tall_skinny(m, n, k):
         sk = _split_k(m, n, k)
         if sk == 1:
+            if out is not None and out.dtype == dy2.dtype == x2.dtype:
+                return torch.mm(dy2.t(), x2, out=out)
             return torch.mm(dy2.t(), x2).to(out_dtype)
         c = m // sk
         g = torch.bmm(dy2.view(sk, c, n).transpose(1, 2), x2.view(sk, c, k), out_dtype=torch.float32).sum(0)
@@ -241,7 +266,7 @@ def _dgrad_via_transpose(m: int, n: int, k: int, w: torch.Tensor) -> bool:
     tied LM head 4.97 -> 4.36 ms at 32 x 1024 tokens, profiles/r1_v11_gemm_dgrad_layout.jsonl); the weight
     transpose costs ~1 % of the GEMM.  GPT-2 124M's 0.6-2.4M-element weights gain too (901k -> 930-936k tokens/s,
     profiles/r2_gpt2_124m_dgrad_nt_threshold.log); SwinIR's (< 11k elements) keep the single mm."""
-    return (w.dtype in (torch.bfloat16, torch.float16) and w.is_contiguous() and m >= 4096
+    return (w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and w.is_contiguous() and m >= 4096
             and n % 64 == 0 and k % 64 == 0 and n * k >= _DGRAD_T_MIN and n // 64 <= 65535 and w.data_ptr() % 16 == 0)
 
 
@@ -299,7 +324,7 @@ class _LinearFn(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             if not x2.is_contiguous():
                 x2 = x2.contiguous()
-            dw = wgrad(dy2, x2, w.dtype)
+            dw = _wgrad_result(w, dy2, x2)
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
                 dx = nt_matmul(dy2, transpose16(w))
@@ -311,7 +336,7 @@ class _LinearFn(torch.autograd.Function):
             if db is not None:
                 db = db.to(w.dtype)
             else:
-                db = _colsum(dy2, w.dtype) if colsum_ok(dy2.shape[1]) else dy2.sum(0).to(w.dtype)
+                db = _colsum(dy2, w.dtype) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.sum(0).to(w.dtype)
         return dx, dw, db
 
 
@@ -363,7 +388,7 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         _lib.call("pdt_bias_gelu_bwd_db", dy2.data_ptr(), d.data_ptr(), None, dpre.data_ptr(),
                   db.data_ptr(), ws.data_ptr(), rows, n, _lib.dtype_code(d.dtype), _lib.dtype_code(db.dtype), 2, 0,
                   _lib.stream_handle(d.device))
-        dw = wgrad(dpre, x2, w.dtype) if ctx.needs_input_grad[1] else None
+        dw = _wgrad_result(w, dpre, x2) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(rows, w.shape[0], w.shape[1], w):
@@ -416,14 +441,14 @@ class _GeluMlpFn(torch.autograd.Function):
         x2, w1, d1, y1, w2 = ctx.saved_tensors
         d2 = dout.reshape(-1, dout.shape[-1])
         d2 = d2 if d2.is_contiguous() and d2.data_ptr() % 16 == 0 else d2.contiguous()
-        dw2 = wgrad(d2, y1, w2.dtype) if ctx.needs_input_grad[3] else None
+        dw2 = _wgrad_result(w2, d2, y1) if ctx.needs_input_grad[3] else None
         db2 = None
         if ctx.needs_input_grad[4]:
             db2 = take_bias_grad(d2)      # summed by the kernel that produced dY (the next LayerNorm's backward)
             db2 = db2.to(w2.dtype) if db2 is not None else _colsum(d2, w2.dtype)
         # c_proj dgrad (d2 W2) x GELU'(pre) (= d1, kept by the forward), and c_fc's bias gradient, in one pass
         dpre, db1 = G.gemm_nt_dgelu(d2, transpose16(w2), d1, bias_dtype=w1.dtype)
-        dw1 = wgrad(dpre, x2, w1.dtype) if ctx.needs_input_grad[1] else None
+        dw1 = _wgrad_result(w1, dpre, x2) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dpre.shape[0], w1.shape[0], w1.shape[1], w1):
@@ -443,8 +468,10 @@ def linear(x, weight, bias=None):
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
             return linear(x.to(dt), weight.to(dt), None if bias is None else bias.to(dt))
-    if x.is_cuda and x.dtype == weight.dtype and x.dtype in (torch.bfloat16, torch.float32) and \
-            (bias is None or bias.dtype == x.dtype):
+    if (x.is_cuda or is_sharded_param(weight) or hasattr(x, "_pdt_recipe")) and x.dtype == weight.dtype and \
+            x.dtype in (torch.bfloat16, torch.float32) and (bias is None or bias.dtype == x.dtype):
+        # (an FSDP parameter takes this path on the CPU too: its backward writes dW into the unit's flat slot; so does
+        # an input saved as a recompute recipe (utils.recompute): this Function saves x itself, not a view of it)
         return _LinearFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
 

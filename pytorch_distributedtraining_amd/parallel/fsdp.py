@@ -8,14 +8,21 @@ Design (MI355X-first, not a port of torch FSDP):
                         AdamW epilogue, so no separate cast pass),
       - ``full``:       the bf16 gathered buffer; its storage is released after forward
                         (FULL_SHARD) and re-gathered before backward.
-    The original parameters are replaced by views into ``full`` (one ``split`` => one ``cat`` in
-    backward), so module code and state_dict keys are unchanged.
+    The original parameters are replaced by views into ``full`` -- the outputs of ONE autograd node per unit
+    (``_UnitViewsFn``) -- so module code and state_dict keys are unchanged.
+  * Gradients land in ONE flat buffer per unit, allocated when the unit's backward starts: each parameter gets a
+    slot in it (``ops.grad_slots``), the framework Linears write their weight gradients straight into their slots
+    (the GEMM output), and whatever else produces a parameter gradient is copied / added in by the unit's node.
+    No per-parameter gradient is concatenated (the ``split`` -> ``cat`` of the first design).
   * Forward: the unit's all-gather is issued asynchronously and the NEXT unit (recorded forward order)
     is prefetched, so RCCL all-gathers overlap the current block's GEMMs.  Backward: pre-backward
     hooks on the unit outputs re-gather and prefetch the previous unit.
   * The unit's gradient arrives as one flat bf16 tensor; it is reduce-scattered (AVG) asynchronously
     on c10d's RCCL stream while backward continues; the fp32 shard gradient is produced at the end of
-    backward (``flat_param.grad``).  ``no_sync()`` accumulates locally (grad accumulation).
+    backward (``flat_param.grad``).  Gradient accumulation (``no_sync()`` micro-steps): ``accumulate="sharded"``
+    (default) reduce-scatters every micro-step and accumulates the fp32 SHARD (gradient memory stays 1/world);
+    ``accumulate="local"`` keeps an unsharded fp32 gradient per unit and communicates on the last micro-step
+    only (torch FSDP's no_sync: fewer collectives, world x the gradient memory).
   * world_size == 1: ``full`` IS ``lp_shard`` and no collective is issued.
   * ``state_dict()`` returns the FULL, unflattened fp32 state dict under the original keys
     (FULL_STATE_DICT semantics), as the Stoke checkpoint envelope expects.
@@ -32,6 +39,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 
+from ..ops import grad_slots
 from ..utils import profiling as prof
 from ..utils.native import require_runtime
 from .comm import Comm, default_comm
@@ -64,25 +72,19 @@ class _Unit:
         self.layout = rt.FlatLayout(numels, ws, ALIGN)
         self.total, self.shard_numel = int(self.layout.total), int(self.layout.shard_numel)
         self.offsets = list(self.layout.offsets)
-        # split sizes covering the whole flat buffer (params + padding pieces)
-        self.split_sizes, self.piece_of_param = [], []
-        cur = 0
-        for off, n in zip(self.offsets, numels):
-            if off > cur:
-                self.split_sizes.append(off - cur)
-            self.piece_of_param.append(len(self.split_sizes))
-            self.split_sizes.append(n)
-            cur = off + n
-        if self.total > cur:
-            self.split_sizes.append(self.total - cur)
         self.numels = numels
         self.state = self.SHARDED
         self.handle = None
         self.pending = []          # (Handle, rs_out) waiting for finalize
-        self.accum_full = None     # fp32 full grad accumulated under no_sync
+        self.accum_full = None     # accumulate="local": fp32 full grad accumulated under no_sync
+        self.accum_shard = None    # accumulate="sharded": fp32 reduced shard accumulated under no_sync
+        self.pending_acc = []      # accumulate="sharded": (Handle, rs_out) of a no_sync micro-step
         self.in_backward = False
         self.bwd_hooked = False
         self.order_idx = -1
+        self.grad_flat = None      # this backward's flat gradient (slots of ops.grad_slots), see begin_backward
+        self.slot_keys = []
+        self.written = []
 
     # -------------------------------------------------------------- construction
     def materialize(self, tensors):
@@ -155,18 +157,61 @@ class _Unit:
         if self.comm.world_size > 1 and self.state == self.GATHERED:
             self._free_full()
 
-    def install_views(self, full_tensor):
-        pieces = torch.split(full_tensor, self.split_sizes)
-        for (mod, attr, _fqn, shape), pi in zip(self.params, self.piece_of_param):
-            setattr(mod, attr, pieces[pi].view(shape))
+    def views_of(self, full_tensor):
+        """The parameter views of a flat [total] tensor (one per unique parameter, in ``params`` order)."""
+        return [full_tensor[off:off + n].view(shape) for (_m, _a, _f, shape), off, n in
+                zip(self.params, self.offsets, self.numels)]
+
+    def install_views(self, views):
+        for (mod, attr, _fqn, _shape), v in zip(self.params, views):
+            setattr(mod, attr, v)
 
     # -------------------------------------------------------------- gradients
+    def begin_backward(self):
+        """Allocate this backward's flat gradient and register one slot per parameter (ops.grad_slots), keyed by
+        the gathered storage the saved parameter views point at (so call after the unit is gathered)."""
+        if self.grad_flat is not None:
+            return
+        self.grad_flat = torch.empty(self.total, dtype=self.mp.param_dtype, device=self.device)
+        self.written = [False] * len(self.params)
+        full = self.full.view(-1)
+        self.slot_keys = [grad_slots.register(v, d, self, i) for i, (v, d) in
+                          enumerate(zip(self.views_of(full), self.views_of(self.grad_flat)))]
+
+    def slot_written(self, i):
+        self.written[i] = True
+
+    def post_backward_views(self, grads):
+        """Called once per backward by the unit's node with the gradients autograd carried for each parameter view
+        (None where no consumer produced one, or where a framework op wrote its slot instead)."""
+        if self.grad_flat is None:      # backward entered without the pre-backward hook (e.g. the root unit
+            self.begin_backward()       # through a path that skipped the loss-side hook)
+        flat = self.grad_flat
+        grad_slots.release(self.slot_keys)
+        cur = 0
+        for i, (g, off, n) in enumerate(zip(grads, self.offsets, self.numels)):
+            if off > cur:
+                flat[cur:off].zero_()                   # alignment padding
+            cur = off + n
+            slot = flat[off:off + n]
+            if g is None:
+                if not self.written[i]:
+                    slot.zero_()
+            elif self.written[i]:
+                slot.add_(g.reshape(-1))
+            else:
+                slot.copy_(g.reshape(-1))
+        if self.total > cur:
+            flat[cur:].zero_()
+        self.grad_flat, self.slot_keys, self.written = None, [], []
+        self.post_backward(flat)
+
     def post_backward(self, grad_full):
-        """Called once per backward with the unit's flat gradient (param dtype, length total)."""
+        """The unit's flat gradient (param dtype, length total) of one backward."""
         self.in_backward = False
         grad = grad_full.detach()
         owner = self.owner
-        if owner._no_sync:
+        if owner._no_sync and owner.accumulate == "local":
             if self.accum_full is None:
                 self.accum_full = grad.to(torch.float32)
             else:
@@ -178,21 +223,45 @@ class _Unit:
             elif grad.dtype != self.mp.reduce_dtype:
                 grad = grad.to(self.mp.reduce_dtype)
             if self.comm.world_size == 1:
-                self.pending.append((None, grad))
+                out, h = grad, None
             else:
                 out = torch.empty(self.shard_numel, dtype=self.mp.reduce_dtype, device=grad.device)
                 with prof.range(f"fsdp.reduce_scatter[{self.name or 'root'}]"):
                     h = self.comm.reduce_scatter(out, grad, op="avg", async_op=True)
+            if owner._no_sync:          # accumulate="sharded": fold the reduced shard into the fp32 accumulator
+                self.pending_acc.append((h, out))
+            else:
                 self.pending.append((h, out))
         # params are not needed again until the next forward (which re-gathers the updated shard)
         self.reshard()
 
+    def fold_accumulation(self):
+        """accumulate="sharded": wait for this micro-step's reduce-scatters and add them to the fp32 shard."""
+        for h, out in self.pending_acc:
+            if h is not None:
+                h.wait()
+            if self.accum_shard is None:
+                self.accum_shard = out.to(torch.float32) if out.dtype != torch.float32 else out.clone()
+            else:
+                self.accum_shard.add_(out)
+        self.pending_acc = []
+
     def finalize(self):
+        self.fold_accumulation()
         for h, out in self.pending:
             if h is not None:
                 h.wait()
             fp = self.flat_param
-            if fp.grad is not None:
+            if self.accum_shard is not None:
+                # the micro-steps' reduced shards (fp32) plus this one: an fp32 .grad for the optimizer
+                out = self.accum_shard.add_(out)
+                self.accum_shard = None
+                if fp.grad is not None:
+                    fp.grad.add_(out)
+                else:
+                    fp.grad = out
+                fp._pdt_grad = None
+            elif fp.grad is not None:
                 fp.grad.add_(out)
             elif self.owner.keep_low_precision_grads and out.dtype != torch.float32:
                 # the reduced bf16 shard gradient is handed to the fused optimizer as is (no fp32 cast
@@ -203,17 +272,20 @@ class _Unit:
         self.pending.clear()
 
 
-class _UnitFn(torch.autograd.Function):
-    """Identity-like node: forward hands out the gathered flat buffer, backward receives its gradient."""
+class _UnitViewsFn(torch.autograd.Function):
+    """One node per unit: forward hands out the parameter views of the gathered flat buffer, backward receives
+    each parameter's gradient (None where a framework op wrote the unit's slot itself) and builds the unit's flat
+    gradient (``_Unit.post_backward_views``)."""
 
     @staticmethod
     def forward(ctx, flat_param, unit):
         ctx.unit = unit
-        return unit.full.view(-1)
+        ctx.set_materialize_grads(False)
+        return tuple(unit.views_of(unit.full.view(-1)))
 
     @staticmethod
-    def backward(ctx, grad_full):
-        ctx.unit.post_backward(grad_full)
+    def backward(ctx, *grads):
+        ctx.unit.post_backward_views(grads)
         return None, None
 
 
@@ -231,13 +303,17 @@ class FullyShardedDataParallel(nn.Module):
         keep_low_precision_grads: leave the reduced shard gradient in ``reduce_dtype`` as
             ``flat_param._pdt_grad`` (read by FusedAdamW / clip_grad_norm_) instead of materialising an
             fp32 ``.grad`` -- use with the framework's fused optimizer.
+        accumulate: "sharded" (default) or "local" -- gradient accumulation under ``no_sync`` (module docstring).
     """
 
     def __init__(self, module: nn.Module, wrap_classes=None, sharding_strategy=ShardingStrategy.FULL_SHARD,
                  mixed_precision: MixedPrecision | None = None, comm: Comm | None = None, device=None,
                  forward_prefetch: bool = True, backward_prefetch: bool = True, sync_module_states: bool = True,
-                 keep_low_precision_grads: bool = False):
+                 keep_low_precision_grads: bool = False, accumulate: str = "sharded"):
         super().__init__()
+        if accumulate not in ("sharded", "local"):
+            raise ValueError(f"accumulate must be 'sharded' or 'local', got {accumulate!r}")
+        self.accumulate = accumulate
         self.keep_low_precision_grads = keep_low_precision_grads
         self.module = module
         self.comm = comm or default_comm()
@@ -324,11 +400,13 @@ class FullyShardedDataParallel(nn.Module):
                 del m._parameters[pn]
         # start with views installed (no-grad) so attribute access works outside forward
         if unit.state == unit.GATHERED:
-            self._install(unit, unit.full.view(-1))
+            self._install(unit, unit.views_of(unit.full.view(-1)))
         return unit
 
-    def _install(self, unit, full_tensor):
-        unit.install_views(full_tensor)
+    def _install(self, unit, views):
+        for v in views:
+            v._pdt_fsdp_unit = unit       # framework ops route these through their own backward (ops.grad_slots)
+        unit.install_views(views)
         for (m, pn, _fqn, src) in getattr(unit, "ties", []):
             sm, sattr = unit.params[src][0], unit.params[src][1]
             setattr(m, pn, getattr(sm, sattr))
@@ -342,10 +420,10 @@ class FullyShardedDataParallel(nn.Module):
         unit.refresh_lp()
         unit.wait()
         if torch.is_grad_enabled():
-            full = _UnitFn.apply(unit.flat_param, unit)
+            views = _UnitViewsFn.apply(unit.flat_param, unit)
         else:
-            full = unit.full.view(-1)
-        self._install(unit, full)
+            views = unit.views_of(unit.full.view(-1))
+        self._install(unit, views)
 
     def _make_pre_forward(self, unit):
         def hook(_mod, _args):
@@ -381,6 +459,7 @@ class FullyShardedDataParallel(nn.Module):
                 fired["done"] = True
                 unit.in_backward = True
                 unit.wait()
+                unit.begin_backward()
                 if self.backward_prefetch:
                     i = unit.order_idx - 1
                     if 0 <= i < len(self._fwd_order):
@@ -399,6 +478,8 @@ class FullyShardedDataParallel(nn.Module):
             self._order_frozen = True
             self.comm.check_errors()
             if self._no_sync:
+                for u in self.all_units():
+                    u.fold_accumulation()
                 return
             for u in self.all_units():
                 u.finalize()
@@ -423,7 +504,14 @@ class FullyShardedDataParallel(nn.Module):
 
     def _loss_side_hook(self, grad):
         self._queue_finalize()
+        if self.root_unit is not None:        # the root's parameters (head, embeddings) get their slots first
+            self.root_unit.begin_backward()
         return grad
+
+    def accumulator_bytes(self) -> int:
+        """Bytes of gradient-accumulation state held between no_sync micro-steps (fp32 full / shard buffers)."""
+        return sum(t.numel() * t.element_size() for u in self.all_units()
+                   for t in (u.accum_full, u.accum_shard) if t is not None)
 
     @contextmanager
     def no_sync(self):

@@ -79,14 +79,21 @@ def run_workers(fn, world=2, *args, timeout=240):
         return out
 
 
-def assert_adam_close(sd1, sd2, lr=1e-3, steps=3, frac=0.995):
+def assert_adam_close(sd1, sd2, lr=1e-3, steps=3, frac=0.995, zero_grad_slices=None):
     """States trained with Adam(W) at world 1 vs world N: bf16 gradients reduced in a different order can flip
     the sign of near-zero components, and Adam then moves them ~lr the other way each step.  The bulk must agree
-    tightly; every element must stay within the 2 * lr * steps displacement (+ lr of slack)."""
+    tightly; every element must stay within the 2 * lr * steps displacement (+ lr of slack).
+    ``zero_grad_slices``: {key suffix: slice} of elements whose exact gradient is 0 (e.g. an attention key bias:
+    softmax is invariant to a per-query shift, so sum_j dK_j = 0) -- their Adam updates are pure rounding noise
+    and only the displacement bound applies to them."""
     import torch
     for k in sd1:
         a, b = sd1[k].float(), sd2[k].float()
         close = torch.isclose(a, b, atol=3e-3, rtol=3e-2)
+        for suffix, sl in (zero_grad_slices or {}).items():
+            if k.endswith(suffix):
+                close = close.clone()
+                close.view(-1)[sl] = True
         assert close.float().mean() > frac, (k, float(close.float().mean()))
         assert float((a - b).abs().max()) <= 2 * steps * lr + lr, (k, float((a - b).abs().max()))
 

@@ -716,3 +716,76 @@ def test_zero2_windows_interleave_banks_and_match_single_process():
     # the fp64 layer's windows (params 2, 3) are released before the fp32 windows that wait for layer a (0, 1)
     first_a = min(i for i, (_, lo) in enumerate(order) if lo <= 1)
     assert all(i < first_a for i, (dt, _) in enumerate(order) if dt == "torch.float64")
+
+
+class _FwBlock(nn.Module):
+    """A block on the framework's own Linear (its backward writes dW into FSDP's flat-gradient slots)."""
+
+    def __init__(self):
+        super().__init__()
+        from pytorch_distributedtraining_amd.ops.linear import Linear
+        self.fc = Linear(32, 32)
+        self.ln = nn.LayerNorm(32)
+
+    def forward(self, x):
+        return x + torch.tanh(self.fc(self.ln(x)))
+
+
+def _fw_model(seed=0):
+    from pytorch_distributedtraining_amd.ops.linear import Linear
+    torch.manual_seed(seed)
+    return nn.Sequential(Linear(16, 32), _FwBlock(), _FwBlock(), Linear(32, 4))
+
+
+def _graph_names(t):
+    seen, out, todo = set(), set(), [t.grad_fn]
+    while todo:
+        f = todo.pop()
+        if f is None or f in seen:
+            continue
+        seen.add(f)
+        out.add(type(f).__name__)
+        todo.extend(n for n, _ in f.next_functions)
+    return out
+
+
+def _w_fsdp_accum(rank, world, accumulate, accum):
+    from pytorch_distributedtraining_amd.optim import FusedAdamW
+    from pytorch_distributedtraining_amd.parallel.fsdp import FullyShardedDataParallel, MixedPrecision
+    m = _fw_model()
+    f = FullyShardedDataParallel(m, wrap_classes=(_FwBlock,), mixed_precision=MixedPrecision(torch.float32,
+                                 torch.float32), device="cpu", accumulate=accumulate)
+    opt = FusedAdamW(f.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    acc_bytes, names = [], set()
+    for s in range(STEPS):
+        for a in range(accum):
+            x, y = _data(s * accum + a, world)
+            ctx = f.no_sync() if a < accum - 1 else torch.enable_grad()
+            with ctx:
+                loss = nn.functional.mse_loss(f(_shard(x, rank, world)), _shard(y, rank, world)) / accum
+                names |= _graph_names(loss)
+                loss.backward()
+            if a < accum - 1:
+                acc_bytes.append(f.accumulator_bytes())
+        opt.step()
+        opt.zero_grad()
+    return {k: v.clone() for k, v in f.state_dict().items()}, max(acc_bytes or [0]), sorted(names)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fsdp_sharded_accumulation_matches_world1_and_bounds_memory(world):
+    """grad_accum_steps=2 under FSDP (Stoke-DDP.py:251): accumulate="sharded" reduce-scatters every micro-step into
+    an fp32 SHARD accumulator -- same result as world 1 and as accumulate="local", with <= 0.6x its accumulator
+    memory.  The unit gradients are assembled without any Cat / Split node (framework Linears write their slots)."""
+    ref = _reference(world, accum=2, model_fn=_fw_model)
+    sh = run_workers(_w_fsdp_accum, world, "sharded", 2)
+    lo = run_workers(_w_fsdp_accum, world, "local", 2)
+    for k in ref:
+        for r in range(world):
+            assert torch.allclose(sh[r][0][k], ref[k], atol=2e-5), (k, r)
+            assert torch.allclose(lo[r][0][k], ref[k], atol=2e-5), (k, r)
+    for r in range(world):
+        assert sh[r][1] <= 0.6 * lo[r][1], (sh[r][1], lo[r][1])
+        names = sh[r][2]
+        assert "_UnitViewsFnBackward" in names
+        assert not any(n.startswith(("CatBackward", "SplitBackward", "SplitWithSizesBackward")) for n in names), names

@@ -51,7 +51,8 @@ def test_fsdp_two_ranks_on_one_gpu_matches_one_rank(strategy):
     for a, b in zip(l1, l2):
         assert abs(a - b) < 2e-2 * abs(a)
     # (seen: 1 of 196,608 c_attn elements 3.4e-3 apart -- within Adam's sign-flip displacement)
-    assert_adam_close(sd1, sd2)
+    # the k third of the qkv bias has an exactly-zero gradient (softmax shift invariance): noise-driven Adam steps
+    assert_adam_close(sd1, sd2, zero_grad_slices={"attn.c_attn.bias": slice(256, 512)})
 
 
 def _train_ddp(rank, world, steps):

@@ -239,6 +239,66 @@ def test_flash_attn_full_grid_rows(fwd, bwd, order):
         reset_kernel_variant()
 
 
+def test_flash_attn_packed_flagship_b96_full_rows():
+    """The flagship's exact attention call -- GPT-2 1.3B at B96 S1024 H16 D128, causal, the packed [B, S, 3, H, D]
+    projection with the c_attn bias gradient summed by the backward kernels, default kernels and block order --
+    with every row of the first and last batch element checked against fp32 (o, dq, dk, dv), and the bias
+    gradient against the column sums of the whole packed gradient."""
+    from pytorch_distributedtraining_amd.ops import flash_attn_qkvpacked
+    from pytorch_distributedtraining_amd.ops.attention import take_bias_grad
+    B, S, H, D = 96, 1024, 16, 128
+    torch.manual_seed(96)
+    leaf = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    qkv = leaf.view(B, S, 3, H, D) * 1.0       # a non-leaf, as the c_attn output is: its gradient is not copied
+    got = []
+    qkv.register_hook(got.append)
+    o = flash_attn_qkvpacked(qkv, causal=True, bias_grad=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    g = got[0]
+    db = take_bias_grad(g.view(B * S, 3 * H * D))
+    assert db is not None
+    want = g.view(B * S, 3 * H * D).float().sum(0)
+    assert float((db.float() - want).abs().max()) < 2e-3 * float(want.abs().max()) + 1e-2
+    for b in (0, B - 1):
+        x = qkv[b:b + 1].detach().float().requires_grad_()
+        orf = _attn_ref(x[:, :, 0], x[:, :, 1], x[:, :, 2], True, 1 / math.sqrt(D))
+        orf.backward(do[b:b + 1].float())
+        for got, ref, tol in ((o[b:b + 1], orf, 2e-2), (g[b:b + 1, :, 0], x.grad[:, :, 0], 4e-2),
+                              (g[b:b + 1, :, 1], x.grad[:, :, 1], 4e-2), (g[b:b + 1, :, 2], x.grad[:, :, 2], 4e-2)):
+            rn = ref.norm(dim=-1)
+            row_err = (got.float() - ref).norm(dim=-1) / torch.maximum(rn, rn.mean())
+            assert float(row_err.max()) < tol, (b, float(row_err.max()), int(row_err.argmax()))
+
+
+@pytest.mark.parametrize("N,K", [(2048, 8192), (2048, 6144)])
+def test_hand_gemm_nt_3stage_full_grid_production_shapes(N, K):
+    """The asm NT GEMM's 3-stage program (third A buffer in the epilogue staging area; use_p3 picks it for K >= 8192
+    and for narrow products) at the shapes it runs in the flagship: c_proj forward (98,304 x 2,048 x 8,192) and the
+    qkv data gradient (98,304 x 2,048 x 6,144), every element against fp32 torch, with and without the bias
+    epilogue (the bias is loaded before each item's main loop)."""
+    from pytorch_distributedtraining_amd.ops import gemm as G
+    M = 96 * 1024
+    torch.manual_seed(N + K)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    old = G.KERNEL["name"]
+    G.KERNEL["name"] = "asm"
+    try:
+        c = G.gemm_nt(a, b)
+        cb = G.gemm_nt(a, b, bias)
+    finally:
+        G.KERNEL["name"] = old
+    want = a.float() @ b.float().t()
+    for got in (c, cb):
+        if got is cb:
+            want.add_(bias.float())
+        rms = float(want.square().mean().sqrt())
+        bad = (got.float() - want).abs() > 0.008 * want.abs() + 0.01 * rms
+        assert int(bad.sum()) == 0, int(bad.sum())
+
+
 def test_flash_attn_qkvpacked_matches_unpacked():
     from pytorch_distributedtraining_amd.ops import flash_attn, flash_attn_qkvpacked
     qkv = torch.randn(2, 300, 3, 4, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -1615,3 +1675,47 @@ def test_fused_gelu_mlp_matches_unfused(M, C):
     assert rel_err(y, y2) < 1e-2
     for a, t in zip(g, params):
         assert rel_err(a, t.grad) < 2e-2, (t.shape, rel_err(a, t.grad))
+
+
+def test_llama_selective_recompute_gpu_bitwise():
+    """Selective activation recomputation on the GPU path (FSDP bf16 compute, hand kernels): norms, the flash
+    attention forward (o and its log-sum-exp, shared by the wo weight gradient and the attention backward) and
+    SwiGLU are recomputed from the kept GEMM outputs -- 4 recipe runs per layer, gradients bitwise equal to the
+    un-checkpointed step."""
+    from pytorch_distributedtraining_amd.models.llama import build_llama
+    from pytorch_distributedtraining_amd.parallel import FullyShardedDataParallel
+    from pytorch_distributedtraining_amd.utils import recompute
+    torch.manual_seed(0)
+    with torch.device(DEV):
+        m = build_llama("llama3-tiny", n_layers=3)
+    f = FullyShardedDataParallel(m, device=torch.device(DEV))
+    x = torch.randint(0, 1024, (4, 257), device=DEV)
+    runs = []
+    orig = recompute.Recipe.get
+
+    def get(self, i):
+        if self.cache is None:
+            runs.append(self)
+        return orig(self, i)
+
+    def grads(ckpt):
+        m.config.activation_checkpointing, m.config.checkpoint_policy = ckpt, "selective"
+        loss = f(x[:, :-1], labels=x[:, 1:])
+        loss.backward()
+        torch.cuda.synchronize()
+        out = [p.grad.clone() if p.grad is not None else p._pdt_grad.clone() for p in f.flat_parameters()]
+        for p in f.flat_parameters():
+            p.grad = None
+            p._pdt_grad = None
+        return loss.detach(), out
+
+    recompute.Recipe.get = get
+    try:
+        l0, g0 = grads(False)
+        assert not runs
+        l1, g1 = grads(True)
+    finally:
+        recompute.Recipe.get = orig
+    assert torch.equal(l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert len(runs) == 4 * 3

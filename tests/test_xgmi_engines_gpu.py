@@ -78,7 +78,8 @@ def test_fsdp_over_xgmi_matches_one_rank(world, strategy):
     assert all(o[0] == l2 for o in outs)
     for a, b in zip(l1, l2):
         assert abs(a - b) < 2e-2 * abs(a)
-    assert_adam_close(sd1, sd2)
+    # the k third of the qkv bias has an exactly-zero gradient (softmax shift invariance): noise-driven Adam steps
+    assert_adam_close(sd1, sd2, zero_grad_slices={"attn.c_attn.bias": slice(256, 512)})
 
 
 def _ddp_bf16(rank, world):
