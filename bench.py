@@ -344,8 +344,10 @@ def bench_gpt2(args, comm, dev, world, rank):
     # per-GPU micro-batch sized for 288 GB HBM: GPT-2 124M DDP 16 -> 64 sequences 700k -> 886k tokens/s
     # (profiles/r2_gpt2_124m_ddp_microbatch.log); GPT-2 1.3B FSDP 32 -> 64 +2.8 % (module docstring), 64 -> 96
     # +1.3 % at 188 GB peak (128: +2.0 % at 243 GB -- not taken, leaves < 50 GB headroom;
-    # profiles/r2_flagship_microbatch_64_96_128.log)
-    mb = args.micro_batch or (8 if llama else 96 if fsdp else 64)
+    # profiles/r2_flagship_microbatch_64_96_128.log); Llama-3 8B with selective recompute on all 32 layers 8 -> 16
+    # sequences 22.9k -> 24.9k tokens/s at 182 GB peak (AdamW's fixed 39 ms/step amortised;
+    # profiles/r5/r5_llama3_8b_ckpt_policy.jsonl)
+    mb = args.micro_batch or (16 if llama else 96 if fsdp else 64)
     S = args.seq
     with torch.device(dev):
         if llama:
