@@ -6,7 +6,8 @@
 //
 //   forward   stats  : per-channel (sum, sum^2) partials over row chunks (fp32) -> fp64 combine
 //             apply  : y = relu(x * scale[c] + shift[c] (+ res))         ONE pass (reads x (+res), writes y)
-//   backward  reduce : (sum dy', sum dy' * xhat) with dy' = dy * (y > 0)  (ReLU mask from the saved output)
+//   backward  reduce : (sum dy', sum dy' * xhat) with dy' = dy * relu'(.)  (ReLU mask: recomputed from x, or a
+//                      1-bit-per-element mask the forward apply wrote after a residual add)
 //             apply  : dx = (dy' - s1/M - xhat * s2/M) * invstd * w ; dres = dy' (residual branch)
 //
 // x is [R rows, C] contiguous (R = N*H*W), C % 8 == 0.  A thread owns 8 consecutive channels for the
@@ -34,18 +35,23 @@ struct Tile {
 };
 
 // MODE 0: (x, x^2)  MODE 1: (dy', dy' * xhat), dy' = dy * relu'(.) per MASK:
-//   MASK 0: no ReLU;  1: mask = (y > 0) from the saved output (needed after a residual add);
+//   MASK 0: no ReLU;  1: mask = (y > 0) from the saved output;
 //   2: mask = (x * scale + shift > 0) recomputed from x with the forward's own coefficients (BN -> ReLU with
-//      no residual: y is then never read -- one bf16 stream less in both backward passes)
+//      no residual: y is then never read -- one bf16 stream less in both backward passes);
+//   3: mask bits written by the forward apply (after a residual add, where x alone does not determine it): one
+//      byte per (row, 8-channel group), bit k = channel 8g + k -- 1/16 of the bytes of reading y back
 template <int MASK>
 __device__ __forceinline__ void relu_mask(float (&g)[8], const float (&xv)[8], const float* yv, const float (&sc)[8],
-                                          const float (&sh)[8]) {
+                                          const float (&sh)[8], unsigned bits) {
   if constexpr (MASK == 1) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
   } else if constexpr (MASK == 2) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = xv[k] * sc[k] + sh[k] > 0.f ? g[k] : 0.f;
+  } else if constexpr (MASK == 3) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = (bits >> k) & 1u ? g[k] : 0.f;
   }
 }
 
@@ -56,6 +62,7 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ scsh, int64_t R, int C,
                                                        float* __restrict__ part) {
   constexpr bool RELU = MASK == 1;   // y is read
+  const uint8_t* __restrict__ mbits = reinterpret_cast<const uint8_t*>(y);   // MASK 3: y is the bit mask
   __shared__ __attribute__((aligned(16))) float sa[NT * 8];
   __shared__ __attribute__((aligned(16))) float sb[NT * 8];
   const Tile t(C);
@@ -78,8 +85,10 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
       const int64_t off0 = r * C + t.cg * 8, off1 = (r + stride) * C + t.cg * 8;
       typename Vec8<bf16_t>::raw_t x0 = Vec8<bf16_t>::load_raw(x + off0), x1 = Vec8<bf16_t>::load_raw(x + off1);
       typename Vec8<bf16_t>::raw_t g0, g1, y0, y1;
+      unsigned b0 = 0, b1 = 0;
       if (MODE == 1) { g0 = Vec8<bf16_t>::load_raw(dy + off0); g1 = Vec8<bf16_t>::load_raw(dy + off1); }
       if (MODE == 1 && RELU) { y0 = Vec8<bf16_t>::load_raw(y + off0); y1 = Vec8<bf16_t>::load_raw(y + off1); }
+      if (MODE == 1 && MASK == 3) { b0 = mbits[r * t.G + t.cg]; b1 = mbits[(r + stride) * t.G + t.cg]; }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         float xv[8];
@@ -91,7 +100,7 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
           float g[8], yv[8];
           Vec8<bf16_t>::unpack(u ? g1 : g0, g);
           if (RELU) Vec8<bf16_t>::unpack(u ? y1 : y0, yv);
-          relu_mask<MASK>(g, xv, yv, sc, sh);
+          relu_mask<MASK>(g, xv, yv, sc, sh, u ? b1 : b0);
 #pragma unroll
           for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
         }
@@ -108,7 +117,7 @@ __global__ __launch_bounds__(NT) void bn_reduce_kernel(const bf16_t* __restrict_
         float g[8], yv[8];
         Vec8<bf16_t>::load(dy + off, g);
         if (RELU) Vec8<bf16_t>::load(y + off, yv);
-        relu_mask<MASK>(g, xv, yv, sc, sh);
+        relu_mask<MASK>(g, xv, yv, sc, sh, MASK == 3 ? (unsigned)mbits[r * t.G + t.cg] : 0u);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a[k] += g[k]; b[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
       }
@@ -199,10 +208,11 @@ __global__ void bn_eval_coef_kernel(const float* __restrict__ rmean, const float
   shift[c] = bc - rmean[c] * is * wc;
 }
 
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool MOUT = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                      bf16_t* __restrict__ y, int64_t R, int C) {
+                                                      bf16_t* __restrict__ y, int64_t R, int C,
+                                                      uint8_t* __restrict__ mask_out) {
   const Tile t(C);
   if (!t.act) return;
   float sc[8], sh[8];
@@ -226,6 +236,12 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
     }
+    if (MOUT) {   // relu'(pre) = (pre > 0) = (y > 0): the backward's MASK 3 bits
+      unsigned bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bits |= (v[k] > 0.f ? 1u : 0u) << k;
+      mask_out[r * t.G + t.cg] = (uint8_t)bits;
+    }
     Vec8<bf16_t>::store(y + off, v);
   }
 }
@@ -240,6 +256,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t R,
                                                           int C) {
   constexpr bool RELU = MASK == 1;
+  const uint8_t* __restrict__ mbits = reinterpret_cast<const uint8_t*>(y);   // MASK 3: y is the bit mask
   const Tile t(C);
   if (!t.act) return;
   const double inv_m = 1.0 / count[0];
@@ -266,7 +283,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
     Vec8<bf16_t>::load(dy + off, g);
     Vec8<bf16_t>::load(x + off, xv);
     if (RELU) Vec8<bf16_t>::load(y + off, yv);
-    relu_mask<MASK>(g, xv, yv, sc, sh);
+    relu_mask<MASK>(g, xv, yv, sc, sh, MASK == 3 ? (unsigned)mbits[r * t.G + t.cg] : 0u);
     if (DRES) Vec8<bf16_t>::store(dres + off, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = g[k] * k1[k] - k2[k] - (xv[k] - mu[k]) * is[k] * k3[k];
@@ -319,31 +336,35 @@ PDT_API int pdt_bn_eval_coef(const float* rmean, const float* rvar, int C, float
   return (int)hipGetLastError();
 }
 
-// y = act(x * scale + shift (+ res)); act: 0 none, 1 relu
+// y = act(x * scale + shift (+ res)); act: 0 none, 1 relu.  mask_out (nullable, relu only): [R, C / 8] bytes of
+// relu'(.) bits for the backward's relu = 3 mode
 PDT_API int pdt_bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t R,
-                         int C, int relu, hipStream_t st) {
-  if (!pdt_bn_ok(C)) return (int)hipErrorInvalidValue;
+                         int C, int relu, void* mask_out, hipStream_t st) {
+  if (!pdt_bn_ok(C) || (mask_out && !relu)) return (int)hipErrorInvalidValue;
   const int g = apply_grid(R, C);
-#define PDT_L(RS, RL) bn_apply_kernel<RS, RL><<<g, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)res, scale, shift, \
-                                                                (bf16_t*)y, R, C)
-  if (res) { if (relu) PDT_L(true, true); else PDT_L(true, false); }
-  else { if (relu) PDT_L(false, true); else PDT_L(false, false); }
+#define PDT_L(RS, RL, MO) bn_apply_kernel<RS, RL, MO><<<g, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)res, scale, \
+                                                                        shift, (bf16_t*)y, R, C, (uint8_t*)mask_out)
+  if (mask_out) { if (res) PDT_L(true, true, true); else PDT_L(false, true, true); }
+  else if (res) { if (relu) PDT_L(true, true, false); else PDT_L(true, false, false); }
+  else { if (relu) PDT_L(false, true, false); else PDT_L(false, false, false); }
 #undef PDT_L
   return (int)hipGetLastError();
 }
 
 // backward sums: out[0:2C] = (sum dy', sum dy' * xhat) fp64 (local; caller all-reduces for SyncBN);
 // dw / db (fp32, nullable) receive the local parameter gradients.  relu: 0 none, 1 mask from y, 2 mask from
-// x * scale + shift (scsh = [scale C | shift C], the forward's coefficients; y is not read)
+// x * scale + shift (scsh = [scale C | shift C], the forward's coefficients; y is not read), 3 mask bits from
+// pdt_bn_apply's mask_out (passed as y)
 PDT_API int pdt_bn_bwd_reduce(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
                               const float* scsh, int64_t R, int C, int relu, float* ws, double* out, float* dw,
                               float* db, hipStream_t st) {
-  if (!pdt_bn_ok(C) || relu < 0 || relu > 2 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
+  if (!pdt_bn_ok(C) || relu < 0 || relu > 3 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
   const int P = reduce_grid(R, C);
 #define PDT_L(M) bn_reduce_kernel<1, M><<<P, NT, 0, st>>>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)y, mean, \
                                                           invstd, scsh, R, C, ws)
   if (relu == 1) PDT_L(1);
   else if (relu == 2) PDT_L(2);
+  else if (relu == 3) PDT_L(3);
   else PDT_L(0);
 #undef PDT_L
   bn_combine_kernel<<<(2 * C + 63) / 64, 64 * CW, 0, st>>>(ws, P, C, 0.0, out, dw, db);
@@ -354,12 +375,13 @@ PDT_API int pdt_bn_bwd_reduce(const void* dy, const void* y, const void* x, cons
 PDT_API int pdt_bn_bwd_apply(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
                              const float* w, const float* scsh, const double* sums, const double* count, void* dx,
                              void* dres, int64_t R, int C, int relu, hipStream_t st) {
-  if (!pdt_bn_ok(C) || relu < 0 || relu > 2 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
+  if (!pdt_bn_ok(C) || relu < 0 || relu > 3 || (relu == 2 && !scsh)) return (int)hipErrorInvalidValue;
   const int g = apply_grid(R, C);
 #define PDT_L(M, DR) bn_bwd_apply_kernel<M, DR><<<g, NT, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, \
       (const bf16_t*)x, mean, invstd, w, scsh, sums, count, (bf16_t*)dx, (bf16_t*)dres, R, C)
   if (relu == 1) { if (dres) PDT_L(1, true); else PDT_L(1, false); }
   else if (relu == 2) { if (dres) PDT_L(2, true); else PDT_L(2, false); }
+  else if (relu == 3) { if (dres) PDT_L(3, true); else PDT_L(3, false); }
   else { if (dres) PDT_L(0, true); else PDT_L(0, false); }
 #undef PDT_L
   return (int)hipGetLastError();

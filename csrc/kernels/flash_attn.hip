@@ -113,11 +113,11 @@ struct AttnParams {
   int B, H, Hkv, Sq, Sk;
   float scale;   // softmax scale (natural domain)
   int order;     // workgroup -> block order: 0 heavy-first, 1 XCD-grouped (block_order)
-  // backward, nullable: per-workgroup column sums of the stored dQ / dK, dV rows (the bias gradient of the
+  // backward, nullable: per-workgroup column sums of the stored dQ rows (the q part of the bias gradient of the
   // Linear that produced q, k, v -- GPT-2's c_attn -- without a separate column-sum pass over dqkv):
-  // cs_q [B * nqb][H * D] (nqb = query blocks of the dQ kernel), cs_kv [B * nkb][2][Hkv * D] (nkb = Sk / 128)
+  // cs_q [B * nqb][H * D] (nqb = query blocks of the dQ kernel).  The k and v parts need no kernel work
+  // (pdt_flash_attn_bwd).
   float* cs_q;
-  float* cs_kv;
   // backward: the dQ kernel computes delta = rowsum(dO * O) and the log2-domain lse for its rows itself (from
   // the dO fragments it holds anyway) and writes them for the dK/dV kernel, which then runs after it -- no
   // separate delta pass re-reading O and dO
@@ -1010,21 +1010,16 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
     }
   }
   acc_fence();
-  if (p.cs_kv == nullptr) {
-    store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
-    store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
-  } else {   // + this workgroup's column sums of the stored dK / dV rows (the k / v parts of the bias gradient)
-    float vals[DT * 16];
-    float* row = p.cs_kv + ((int64_t)b * gridDim.x + kb) * 2 * p.Hkv * D + hk * D;
-    float* lds = reinterpret_cast<float*>(smem);
-    store_row16_vals<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk,
-                         vals);
-    wg_colsum_store<D, 4>(vals, lds, row, w, lane);
-    store_row16_vals<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk, vals);
-    lds_barrier();     // the k sums' LDS reads are done before the v sums overwrite it
-    wg_colsum_store<D, 4>(vals, lds, row + p.Hkv * D, w, lane);
-  }
+  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
+  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
 }
+
+// dQ kernels: the per-element select inside every tile's softmax steps (1) or the dS post-mask on diagonal tiles
+// only (0, default) -- a compile-time A/B switch (-DPDT_FA_DQ_MASK_EVERY_TILE=1)
+#ifndef PDT_FA_DQ_MASK_EVERY_TILE
+#define PDT_FA_DQ_MASK_EVERY_TILE 0
+#endif
+constexpr bool kMaskEveryTile = PDT_FA_DQ_MASK_EVERY_TILE != 0;
 
 template <int D, bool CAUSAL>
 struct BwdQTile {
@@ -1051,13 +1046,28 @@ struct BwdQTile {
       dpv[r] = pv * (dpv[r] - dl);
     }
   }
+  // dS registers [R0, R1) of key subtile kt -> 0 where the key row is past lim.  Only dS feeds an MFMA in this
+  // kernel, so masking it after the fact equals masking P (the select discards whatever exp2 made of a masked
+  // score, inf / NaN included)
+  template <int R0, int R1>
+  __device__ __forceinline__ static void mask_ds(f32x16& dpv, int kt, int lim) {
+#pragma unroll
+    for (int r = R0; r < R1; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + 32 * kt;
+      dpv[r] = rr > lim ? 0.f : dpv[r];
+    }
+  }
   // One 64-key tile, hand-pipelined like BwdKVTile: stage A = S/dP chains of both key subtiles (subtile
   // 0's softmax-gradient under subtile 1's chain), stage B = dQ += dS0 K0 (subtile 1's softmax under it),
-  // stage C = dQ += dS1 K1.  MASK: selects against lim (= last valid key row of this lane's query) on edge tiles.
+  // stage C = dQ += dS1 K1.  MASK: selects against lim (= last valid key row of this lane's query) inside the
+  // softmax steps of every tile; otherwise ``diag`` (wave-uniform: the tile crosses the causal diagonal or Sk)
+  // masks the finished dS registers in three short branches -- the interior tiles issue no mask VALU at all and
+  // the body stays ONE copy (a second unrolled body cost 20 % in instruction-cache misses)
   template <bool MASK>
   __device__ __forceinline__ static void run(const bf16_t* Ks, const bf16_t* Vs, const u16x8 (&qf)[KS],
                                              const u16x8 (&gf)[KS], const int (&roff)[KS], const int (&toff)[DT][2],
-                                             f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim) {
+                                             f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim,
+                                             bool diag = false) {
     f32x16 s[2], dp[2];
     u16x8 df[2][2];
     const f32x16 z = zero16();
@@ -1074,16 +1084,21 @@ struct BwdQTile {
       ka = kn; va = vn;
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (!MASK && diag) mask_ds<0, 16>(dp[0], 0, lim);
     df[0][0] = pack8(dp[0], 0); df[0][1] = pack8(dp[0], 1);
 #pragma unroll
     for (int j = 0; j < 2 * DT; ++j) {
       const u16x8 tn = j + 1 < 2 * DT ? trf(Ks, toff, 0, j + 1) : trf(Ks, toff, 1, 0);
       dq[j >> 1] = mfma32(ta, df[0][j & 1], dq[j >> 1]);
       smx<MASK>(s[1], dp[1], j * EA, 1, sl2, nlse2, dl, lim);
-      if ((j + 1) * EA == 8) df[1][0] = pack8(dp[1], 0);
+      if ((j + 1) * EA == 8) {
+        if (!MASK && diag) mask_ds<0, 8>(dp[1], 1, lim);
+        df[1][0] = pack8(dp[1], 0);
+      }
       ta = tn;
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (!MASK && diag) mask_ds<8, 16>(dp[1], 1, lim);
     df[1][1] = pack8(dp[1], 1);
 #pragma unroll
     for (int j = 0; j < 2 * DT; ++j) {
@@ -1169,9 +1184,11 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
       const int k0 = tt * TILE;
       if (CAUSAL && k0 > qw + 31 + off) continue;               // every key of the tile follows these queries
       const bf16_t* Ks = smem + u * 2 * TE;
-      // one tile body with select masks on every tile: a second (unmasked) copy of the unrolled body made the dQ
-      // kernel 20 % slower in the flagship step (instruction-cache footprint), unlike dK/dV
-      BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+      if (kMaskEveryTile)
+        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      else
+        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0, diag);
     }
   }
   if (p.cs_q == nullptr) {
@@ -1260,9 +1277,11 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     const int k0 = t * TILE;
     if (!(CAUSAL && k0 > qw + 31 + off)) {
       const bf16_t* Ks = smem + stage * 2 * TE;
-      // one tile body with select masks on every tile: a second (unmasked) copy of the unrolled body made the dQ
-      // kernel 20 % slower in the flagship step (instruction-cache footprint), unlike dK/dV
-      BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+      if (kMaskEveryTile)
+        BwdQTile<D, CAUSAL>::template run<true>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0);
+      else
+        BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0, diag);
     }
     stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
@@ -1381,46 +1400,57 @@ PDT_API int pdt_flash_attn_fwd(const void* q, const void* k, const void* v, void
   return D == 64 ? launch_fwd<64>(p, causal, variant, st) : launch_fwd<128>(p, causal, variant, st);
 }
 
-// rows of the backward's column-sum partials (cs_q, cs_kv) for the current kernel variant; 0 = the variant
-// does not produce them
-static void colsum_rows(int B, int Sq, int Sk, int D, int& rq, int& rkv) {
-  const int v = bwd_variant(D);
-  rq = rkv = 0;
-  if (v == 3) rq = B * ((Sq + 127) / 128);
-  else rq = B * ((Sq + 255) / 256);
-  rkv = B * ((Sk + 127) / 128);
+// rows of the backward's dQ column-sum partials (cs_q) for the current kernel variant
+static int colsum_rows(int B, int Sq, int D) {
+  return bwd_variant(D) == 3 ? B * ((Sq + 127) / 128) : B * ((Sq + 255) / 256);
 }
 
-// fp32 workspace floats pdt_flash_attn_bwd needs for the bias-gradient column sums (0: unsupported by the
-// current backward variant -- the caller sums dqkv itself)
+// fp32 workspace floats pdt_flash_attn_bwd needs for the bias-gradient column sums (0: unsupported -- the caller
+// sums dqkv itself)
 PDT_API int64_t pdt_flash_attn_colsum_ws_floats(int B, int H, int Hkv, int Sq, int Sk, int D) {
+  (void)Hkv; (void)Sk;
   if (D != 64 && D != 128) return 0;
-  int rq, rkv;
-  colsum_rows(B, Sq, Sk, D, rq, rkv);
-  if (rq == 0) return 0;
-  const int64_t hd = (int64_t)H * D, kd = (int64_t)2 * Hkv * D;
-  return (int64_t)rq * hd + (int64_t)rkv * kd + 64 * (hd + kd);
+  const int64_t hd = (int64_t)H * D;
+  return (int64_t)colsum_rows(B, Sq, D) * hd + 64 * hd;
 }
+
+namespace {
+// dbias_k = 0, dbias_v[hk][d] = sum over the group's query heads of cso[h][d] (see pdt_flash_attn_bwd)
+template <typename W>
+__global__ void kv_bias_grad_kernel(const float* __restrict__ cso, int Hkv, int group, int D, W* __restrict__ dk,
+                                    W* __restrict__ dv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Hkv * D) return;
+  const int hk = i / D, d = i - hk * D;
+  float s = 0.f;
+  for (int g = 0; g < group; ++g) s += cso[(hk * group + g) * D + d];
+  dk[i] = from_f<W>(0.f);
+  dv[i] = from_f<W>(s);
+}
+}  // namespace
 
 // strides[0..23]: q k v o dout dq dk dv, each (b, s, h).  delta: fp32 workspace of B*H*Sq.
-// dbias (nullable; dtype code dbias_dt: bf16 or fp32): column sums of the stored dq | dk | dv rows -> [H*D |
-// Hkv*D | Hkv*D] (the bias gradient of a packed qkv projection), from per-workgroup partials the dQ / dK-dV
-// kernels write into cs_ws (pdt_flash_attn_colsum_ws_floats) and a deterministic column reduce.
+// dbias (nullable; dtype code dbias_dt: bf16 or fp32): the bias gradient of a packed qkv projection, i.e. the
+// column sums of the stored dq | dk | dv rows -> [H*D | Hkv*D | Hkv*D]:
+//   q part: per-workgroup partials of the dQ kernel (cs_ws, pdt_flash_attn_colsum_ws_floats) + a deterministic
+//           column reduce;
+//   k part: exactly 0 -- a key bias adds q . b_k to every score of query row q, which the row softmax cancels
+//           (sum_k dS[q, k] = sum_k P (dP - delta) = delta - delta = 0);
+//   v part: sum over rows of dO (each P row sums to 1: sum_q sum_k P[q, k] dO[q] = sum_q dO[q]), folded over the
+//           query heads of each kv head; dout_colsum = the fp32 [H*D] column sums of dO (required with dbias).
+// So the dK/dV kernel carries no column-sum epilogue at all.
 PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
                                const void* dout, void* dq, void* dk, void* dv, float* delta, const int64_t* strides,
                                int B, int H, int Hkv, int Sq, int Sk, int D, float scale, int causal, float* cs_ws,
-                               void* dbias, int dbias_dt, hipStream_t st) {
+                               void* dbias, int dbias_dt, const float* dout_colsum, hipStream_t st) {
   if (H % Hkv != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
-  int rq = 0, rkv = 0;
+  int rq = 0;
   if (dbias) {
-    colsum_rows(B, Sq, Sk, D, rq, rkv);
-    if (rq == 0 || !cs_ws || (dbias_dt != kBF16 && dbias_dt != kF32)) return (int)hipErrorInvalidValue;
+    rq = colsum_rows(B, Sq, D);
+    if (!cs_ws || !dout_colsum || (dbias_dt != kBF16 && dbias_dt != kF32)) return (int)hipErrorInvalidValue;
   }
   AttnParams p{};
-  if (dbias) {
-    p.cs_q = cs_ws;
-    p.cs_kv = cs_ws + (int64_t)rq * H * D;
-  }
+  if (dbias) p.cs_q = cs_ws;
   p.q = (const bf16_t*)q; p.k = (const bf16_t*)k; p.v = (const bf16_t*)v; p.o = (bf16_t*)o;
   p.lse = const_cast<float*>(lse); p.dout = (const bf16_t*)dout;
   p.dq = (bf16_t*)dq; p.dk = (bf16_t*)dk; p.dv = (bf16_t*)dv; p.delta = delta;
@@ -1436,14 +1466,17 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
   p.order = block_order_mode(B, Hkv, Sk, D);
   const int err = D == 64 ? launch_bwd<64>(p, causal, st) : launch_bwd<128>(p, causal, st);
   if (err || !dbias) return err;
-  const int hd = H * D, kd = 2 * Hkv * D;
-  float* ws2 = p.cs_kv + (int64_t)rkv * kd;
+  const int hd = H * D, kvd = Hkv * D, group = H / Hkv;
+  float* ws2 = p.cs_q + (int64_t)rq * hd;
+  const int g = (kvd + 255) / 256;
   if (dbias_dt == kBF16) {
-    red::col_reduce<bf16_t>(p.cs_q, rq, hd, (bf16_t*)dbias, ws2, 0, st);
-    red::col_reduce<bf16_t>(p.cs_kv, rkv, kd, (bf16_t*)dbias + hd, ws2 + (int64_t)64 * hd, 0, st);
+    bf16_t* out = (bf16_t*)dbias;
+    red::col_reduce<bf16_t>(p.cs_q, rq, hd, out, ws2, 0, st);
+    kv_bias_grad_kernel<bf16_t><<<g, 256, 0, st>>>(dout_colsum, Hkv, group, D, out + hd, out + hd + kvd);
   } else {
-    red::col_reduce<float>(p.cs_q, rq, hd, (float*)dbias, ws2, 0, st);
-    red::col_reduce<float>(p.cs_kv, rkv, kd, (float*)dbias + hd, ws2 + (int64_t)64 * hd, 0, st);
+    float* out = (float*)dbias;
+    red::col_reduce<float>(p.cs_q, rq, hd, out, ws2, 0, st);
+    kv_bias_grad_kernel<float><<<g, 256, 0, st>>>(dout_colsum, Hkv, group, D, out + hd, out + hd + kvd);
   }
   return (int)hipGetLastError();
 }

@@ -33,6 +33,7 @@
 // consecutive columns n of one row m and the epilogue stores 8 (bf16) or 16 (fp32) bytes per lane.
 #include "common.h"
 #include "gelu.h"
+#include "reduce.h"
 #include <stdlib.h>
 #include <type_traits>
 
@@ -1075,15 +1076,6 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
   }
 }
 
-// dbias[n] = sum over R row tiles of part[r][n] (fixed order: deterministic)
-__global__ __launch_bounds__(256) void colpart_reduce_kernel(const float* __restrict__ part, int R, int N,
-                                                             bf16_t* __restrict__ out) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += part[(int64_t)r * N + n];
-  out[n] = f2bf(s);
-}
 
 // rows per group of tile_of's walk, dividing the block's rows.  Measured on the flagship's NT shapes
 // (profiles/r4/r4_gemm_grp_ab.log, PDT_GEMM_GRP forces one): short K (<= 4096: the A panels of an item are
@@ -1143,7 +1135,7 @@ PDT_API int pdt_gemm_ok(int layout, int64_t M, int64_t N, int64_t K, int64_t lda
 }
 
 // Fused-epilogue GEMM.  epi: 0 plain, 1 bias, 2 bias+GELU (aux_out = pre-activation), 3 dGELU (aux = the
-// pre-activation, dbias = column sums of the result; ws >= (M / 256) * N floats), 4 is internal.
+// GELU derivative, dbias = column sums of the result; ws >= (M / 256 + 64) * N floats), 4 is internal.
 // splits > 1 (plain only): fp32 slabs in ws (splits * M * N floats) + a reduce pass.
 PDT_API int pdt_gemm_bf16(int layout, int epi, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
                           int64_t lda, int64_t ldb, int64_t ldc, const void* bias, const void* aux, void* aux_out,
@@ -1170,9 +1162,9 @@ PDT_API int pdt_gemm_bf16(int layout, int epi, const void* A, const void* B, voi
     gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, s>>>(ws, (bf16_t*)C, n4, splits, M * N);
     if (ldc != N) return (int)hipErrorInvalidValue;   // slab reduce writes a dense [M, N]
   }
-  if (epi == E_DGELU) {
-    colpart_reduce_kernel<<<(int)((N + 255) / 256), 256, 0, s>>>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias);
-  }
+  if (epi == E_DGELU)   // dbias = the R = M / 256 tile partials summed in a fixed two-level order (deterministic);
+    // a one-level pass (one thread per column, 32 workgroups at N = 8192) ran 0.15 ms: latency-bound
+    red::col_reduce<bf16_t>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias, ws + (M / TM) * N, 0, s);
   return (int)hipGetLastError();
 }
 
@@ -1205,9 +1197,9 @@ PDT_API int pdt_gemm2_bf16(int layout, int epi, const void* A, const void* B, vo
     const int64_t n4 = M * N / 4;
     gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 256 * 16), 256, 0, s>>>(ws, (bf16_t*)C, n4, splits, M * N);
   }
-  if (epi == E_DGELU) {
-    colpart_reduce_kernel<<<(int)((N + 255) / 256), 256, 0, s>>>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias);
-  }
+  if (epi == E_DGELU)   // dbias = the R = M / 256 tile partials summed in a fixed two-level order (deterministic);
+    // a one-level pass (one thread per column, 32 workgroups at N = 8192) ran 0.15 ms: latency-bound
+    red::col_reduce<bf16_t>(ws, (int)(M / TM), (int)N, (bf16_t*)dbias, ws + (M / TM) * N, 0, s);
   return (int)hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ _SIGS = {
                            c_int, c_int, c_float, c_int, c_void_p],
     "pdt_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
-                           c_void_p, c_void_p, c_int, c_void_p],
+                           c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "pdt_flash_attn_colsum_ws_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "pdt_flash_attn_set_variant": [c_int, c_int],
     "pdt_flash_attn_set_order": [c_int],
@@ -108,7 +108,7 @@ _SIGS = {
     "pdt_bn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_eval_coef": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
-    "pdt_bn_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_bn_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p],
     "pdt_bn_bwd_reduce": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_bwd_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

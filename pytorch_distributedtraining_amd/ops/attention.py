@@ -44,26 +44,41 @@ def _fwd(q, k, v, causal, scale):
     return o, lse
 
 
+def _dout_colsum(do):
+    """fp32 column sums of dO over (batch, query) rows -> [H*D]: stashed by the Linear whose data gradient dO is
+    (``stash_dx_colsum``, computed there as db W without touching dO), else one column-sum pass."""
+    cs = take_dx_colsum(do)
+    if cs is not None:
+        return cs
+    from .activations import _colsum, colsum_ok
+    d2 = do.reshape(-1, do.shape[-2] * do.shape[-1])
+    if d2.is_contiguous() and colsum_ok(d2.shape[1]):
+        return _colsum(d2, torch.float32)
+    return d2.float().sum(0)
+
+
 def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, bias_grad=False):
     """dq, dk, dv; with ``bias_grad`` also returns the fp32 column sums of the stored dq | dk | dv rows
-    ([H*D + 2*Hkv*D], the bias gradient of the packed qkv projection) from per-workgroup partials of the
-    backward kernels themselves, or None where the current kernel variant does not produce them."""
+    ([H*D + 2*Hkv*D], the bias gradient of the packed qkv projection): the q part from per-workgroup partials of
+    the dQ kernel, the k part exactly 0 and the v part from the column sums of dO (softmax identities, see
+    pdt_flash_attn_bwd); None where the current kernel variant does not produce them."""
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     delta = torch.empty((2, B, H, Sq), dtype=torch.float32, device=q.device)   # [delta | -lse*log2e]
-    do = do if (do.stride(-1) == 1 and all(s % 8 == 0 for s in do.stride()[:-1])) else do.contiguous()
-    strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
-                           + _strides(dk) + _strides(dv), dtype=torch.int64)
-    ws = db = None
+    ws = db = cso = None
     if bias_grad:
         n = int(_lib.require().pdt_flash_attn_colsum_ws_floats(B, H, Hkv, Sq, Sk, D))
         if n > 0:
             ws = torch.empty(n, dtype=torch.float32, device=q.device)
             db = torch.empty((H + 2 * Hkv) * D, dtype=torch.float32, device=q.device)
+            cso = _dout_colsum(do)
+    do = do if (do.stride(-1) == 1 and all(s % 8 == 0 for s in do.stride()[:-1])) else do.contiguous()
+    strides = torch.tensor(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
+                           + _strides(dk) + _strides(dv), dtype=torch.int64)
     _lib.call("pdt_flash_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), delta.data_ptr(), strides.data_ptr(),
               B, H, Hkv, Sq, Sk, D, float(scale), 1 if causal else 0, _lib.ptr(ws), _lib.ptr(db),
-              _lib.dtype_code(torch.float32), _lib.stream_handle(q.device))
+              _lib.dtype_code(torch.float32), _lib.ptr(cso), _lib.stream_handle(q.device))
     return db
 
 
@@ -109,6 +124,25 @@ class _FlashAttnPackedFn(torch.autograd.Function):
 
 
 _BIAS_GRADS: dict = {}
+_DX_COLSUMS: dict = {}
+
+
+def _stash(table, grad, colsum):
+    for key in [k for k, (ref, _, _) in table.items() if ref() is None]:
+        del table[key]
+    table[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum, grad._version)
+
+
+def _take(table, t):
+    ent = table.pop(t.untyped_storage().data_ptr(), None)
+    if ent is None:
+        return None
+    src, colsum, version = ent[0](), ent[1], ent[2]
+    if (src is None or src.untyped_storage().data_ptr() != t.untyped_storage().data_ptr()
+            or src.numel() != t.numel() or colsum.numel() != t.shape[-1] * (t.shape[-2] if t.dim() == 4 else 1)
+            or t.data_ptr() != src.data_ptr() or src._version != version or t._version != version):
+        return None
+    return colsum
 
 
 def stash_bias_grad(grad, colsum):
@@ -116,23 +150,24 @@ def stash_bias_grad(grad, colsum):
     whose output received that gradient: its backward takes them (``take_bias_grad``) instead of summing dY
     again.  Keyed by the buffer's storage; the entry holds the buffer weakly and dies with it, and records the
     buffer's version counter (shared by its views), so an in-place write between stash and take voids it."""
-    for key in [k for k, (ref, _, _) in _BIAS_GRADS.items() if ref() is None]:
-        del _BIAS_GRADS[key]
-    _BIAS_GRADS[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum, grad._version)
+    _stash(_BIAS_GRADS, grad, colsum)
 
 
 def take_bias_grad(dy):
     """The stashed column sums for ``dy`` (a 2-D [rows, N] view of a stashed gradient buffer, unmodified since
     the stash), once; else None (the caller sums dY itself)."""
-    ent = _BIAS_GRADS.pop(dy.untyped_storage().data_ptr(), None)
-    if ent is None:
-        return None
-    src, colsum, version = ent[0](), ent[1], ent[2]
-    if (src is None or src.untyped_storage().data_ptr() != dy.untyped_storage().data_ptr()
-            or src.numel() != dy.numel() or dy.dim() != 2 or colsum.numel() != dy.shape[1]
-            or dy.data_ptr() != src.data_ptr() or src._version != version or dy._version != version):
-        return None
-    return colsum
+    return _take(_BIAS_GRADS, dy) if dy.dim() == 2 else None
+
+
+def stash_dx_colsum(dx, colsum):
+    """Column sums of a Linear's data gradient ``dx`` (= db W, computed by that Linear from its bias gradient) for
+    the attention backward that consumes dx as dO (``take_dx_colsum``): the v part of the qkv bias gradient."""
+    _stash(_DX_COLSUMS, dx, colsum)
+
+
+def take_dx_colsum(do):
+    """The stashed fp32 [H*D] column sums of ``do`` ([B, S, H, D] or [rows, H*D] over a stashed buffer), once."""
+    return _take(_DX_COLSUMS, do) if do.dim() in (2, 4) else None
 
 
 _FRESH_GRADS = weakref.WeakValueDictionary()
@@ -213,12 +248,16 @@ def flash_attn(q, k, v, causal: bool = True, scale: float | None = None):
 
 def flash_attn_qkvpacked(qkv, causal: bool = True, scale: float | None = None, bias_grad: bool = False):
     """qkv [B, S, 3, H, D] -> o [B, S, H, D].  ``bias_grad``: qkv is the output of a Linear with a bias (GPT-2's
-    c_attn) -- the backward kernels also sum their dq / dk / dv rows per column and hand that bias gradient to the
+    c_attn) -- the backward also produces that bias gradient (q part: the dQ kernel's column sums; k part: 0; v
+    part: colsum(dO), stashed by a biased Linear consuming o -- GPT-2's c_proj -- as db W) and hands it to the
     Linear's backward (``take_bias_grad``), which then skips its own column-sum pass over dqkv."""
     scale = 1.0 / math.sqrt(qkv.shape[-1]) if scale is None else scale
     if not qkv.is_cuda:
         return _reference(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal, scale)
-    return _FlashAttnPackedFn.apply(qkv, causal, scale, bias_grad)
+    o = _FlashAttnPackedFn.apply(qkv, causal, scale, bias_grad)
+    if bias_grad:
+        o._pdt_dx_colsum = True     # the Linear consuming o stashes colsum(dO) for this backward (ops.linear)
+    return o
 
 
 def set_kernel_variant(fwd: int = 0, bwd: int = 0) -> tuple:

@@ -2,7 +2,8 @@
 config 2).  ``BatchNormAct2d`` subclasses nn.BatchNorm2d -- same parameters, buffers and
 state_dict keys (torchvision checkpoints load) -- and adds ``act`` ('relu' or None) and an optional
 ``residual`` input, so a ResNet block's ``relu(bn3(conv3(h)) + identity)`` is ONE forward pass over HBM
-instead of three (csrc/kernels/batchnorm.hip), and its backward two instead of four.
+instead of three (csrc/kernels/batchnorm.hip), and its backward two instead of four (after a residual add the
+ReLU mask travels as 1 bit per element instead of re-reading the bf16 output).
 
 Cross-rank statistics (SyncBatchNorm semantics, torch/nn/modules/_functions.py:36-200) when ``comm`` is set:
 one all-reduce of 2C+1 doubles in forward and 2C doubles in backward (``parallel.syncbn.convert_sync_batchnorm``
@@ -46,9 +47,12 @@ class _BNActFn(torch.autograd.Function):
                   _lib.ptr(bias), coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
                   _lib.ptr(running_mean), _lib.ptr(running_var), stream)
         y = torch.empty_like(x, memory_format=torch.channels_last)
+        # ReLU after a residual add: the backward's mask can not be recomputed from x, so the apply writes it as
+        # bits (1/16 of the bytes of reading y back in both backward passes)
+        mbits = torch.empty((rows, c // 8), dtype=torch.uint8, device=dev) if relu and res is not None else None
         _lib.call("pdt_bn_apply", x.data_ptr(), _lib.ptr(res), coef[2].data_ptr(), coef[3].data_ptr(), y.data_ptr(),
-                  rows, c, 1 if relu else 0, stream)
-        ctx.save_for_backward(x, y, weight, coef, stats[2 * c:])
+                  rows, c, 1 if relu else 0, _lib.ptr(mbits), stream)
+        ctx.save_for_backward(x, mbits if mbits is not None else y, weight, coef, stats[2 * c:])
         ctx.relu, ctx.comm, ctx.has_res = relu, comm, res is not None
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return y
@@ -69,8 +73,9 @@ class _BNActFn(torch.autograd.Function):
         gw = pg[0] if ctx.has_w and ctx.needs_input_grad[2] else None
         gb = pg[1] if ctx.has_b and ctx.needs_input_grad[3] else None
         # ReLU mask: recomputed from x with the forward's scale / shift when there is no residual (y is not
-        # read: one bf16 stream less in both passes); from the saved output after a residual add
-        mask = 0 if not ctx.relu else (1 if ctx.has_res else 2)
+        # read: one bf16 stream less in both passes); from the forward's mask bits after a residual add (``y`` is
+        # then that uint8 [rows, C / 8] tensor)
+        mask = 0 if not ctx.relu else (3 if ctx.has_res else 2)
         _lib.call("pdt_bn_bwd_reduce", dy.data_ptr(), y.data_ptr(), x.data_ptr(), coef[0].data_ptr(),
                   coef[1].data_ptr(), coef[2].data_ptr(), rows, c, mask, ws.data_ptr(), sums.data_ptr(),
                   _lib.ptr(gw), _lib.ptr(gb), stream)

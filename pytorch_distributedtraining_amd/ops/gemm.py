@@ -83,12 +83,12 @@ def gemm_nt_gelu(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor):
 
 def gemm_nt_dgelu(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor, bias_dtype=torch.bfloat16):
     """(g, db): g = (a b^T) * d bf16 [M, N] (d = the GELU derivative ``gemm_nt_gelu`` returned), db = g.sum(0)
-    (fp32 partial per 256-row tile, reduced in a fixed order)."""
+    (fp32 partial per 256-row tile, reduced in a fixed two-level order)."""
     m, k = a.shape
     n = b.shape[0]
     g = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     db = torch.empty(n, dtype=torch.bfloat16, device=a.device)
-    ws = torch.empty((m // 256) * n, dtype=torch.float32, device=a.device)
+    ws = torch.empty((m // 256 + 64) * n, dtype=torch.float32, device=a.device)   # partials + 2nd reduce level
     _launch(L_NT, E_DGELU, a, b, g, m, n, k, aux=d, dbias=db, ws=ws)
     return g, db.to(bias_dtype)
 

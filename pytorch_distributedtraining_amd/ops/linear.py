@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .activations import _colsum, colsum_ok
-from .attention import take_bias_grad
+from .attention import stash_dx_colsum, take_bias_grad
 from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 from .gemm import gemm_tt, tt_ok, tt_splits
@@ -295,6 +295,9 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        # x is (a view of) a flash-attention output whose backward wants colsum(dX) (ops.attention._dout_colsum)
+        base = x._base if x._base is not None else x
+        ctx.dx_colsum = bias is not None and getattr(base, "_pdt_dx_colsum", False)
         x2 = x.reshape(-1, x.shape[-1])
         if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
             return _as_output(nt_matmul(x2, weight, bias), (*x.shape[:-1], weight.shape[0]))
@@ -331,12 +334,17 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dx = torch.mm(dy2, w)
             dx = dx.view(*dy.shape[:-1], w.shape[1])
+        dbf = None
         if want_db:
             db = take_bias_grad(dy2)      # summed by the kernel that produced dY (flash attention's backward)
             if db is not None:
-                db = db.to(w.dtype)
+                dbf, db = db, db.to(w.dtype)
             else:
                 db = _colsum(dy2, w.dtype) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.sum(0).to(w.dtype)
+        if ctx.dx_colsum and dx is not None and db is not None:
+            # colsum(dX) = colsum(dY W) = db W: the attention backward's v-bias gradient without a pass over dX
+            dbf = dbf if dbf is not None and dbf.dtype == torch.float32 else db.float()
+            stash_dx_colsum(dx, dbf @ w.float())
         return dx, dw, db
 
 

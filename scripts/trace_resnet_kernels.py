@@ -53,16 +53,21 @@ def main():
     torch.backends.cudnn.benchmark = True
     mb = int(os.environ.get("MB", "256"))
     model = resnet50().to(dev).to(memory_format=torch.channels_last)
-    model = DistributedDataParallel(model, comm=Comm(), reduce_dtype=torch.bfloat16)
+    # PDT_RESNET_AUTOCAST=0: the bf16 compute copy (bench.py's other arm) instead of fp32 weights under autocast
+    autocast = os.environ.get("PDT_RESNET_AUTOCAST", "1") == "1"
+    model = DistributedDataParallel(model, comm=Comm(), reduce_dtype=torch.bfloat16,
+                                    compute_dtype=None if autocast else torch.bfloat16)
     params = model.optimizer_parameters()
     opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
     x = torch.randn(mb, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    if not autocast:
+        x = x.bfloat16()
     y = torch.randint(0, 1000, (mb,), device=dev)
     crit = torch.nn.CrossEntropyLoss()
 
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = crit(model(x), y)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            loss = crit(model(x).float(), y)
         loss.backward()
         _, coef, _ = clip_grad_norm_(params, 1.0, comm=model.comm, sharded=False, apply=False)
         opt.step(grad_scale=coef)
@@ -78,6 +83,7 @@ def main():
         step()
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) * 1000 / n
+    print(json.dumps({"autocast": autocast}), flush=True)
     print(json.dumps({"unprofiled_step_ms": round(step_ms, 3), "samples_per_s": round(mb * 1000 / step_ms, 1)}),
           flush=True)
 

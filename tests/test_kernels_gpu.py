@@ -258,8 +258,7 @@ def test_flash_attn_packed_flagship_b96_full_rows():
     g = got[0]
     db = take_bias_grad(g.view(B * S, 3 * H * D))
     assert db is not None
-    want = g.view(B * S, 3 * H * D).float().sum(0)
-    assert float((db.float() - want).abs().max()) < 2e-3 * float(want.abs().max()) + 1e-2
+    _check_qkv_bias_grad(db, g.view(B * S, 3, H * D), do.reshape(B * S, H * D), H, H)
     for b in (0, B - 1):
         x = qkv[b:b + 1].detach().float().requires_grad_()
         orf = _attn_ref(x[:, :, 0], x[:, :, 1], x[:, :, 2], True, 1 / math.sqrt(D))
@@ -312,12 +311,32 @@ def test_flash_attn_qkvpacked_matches_unpacked():
     assert torch.equal(qkv.grad, x.grad)
 
 
+def _check_qkv_bias_grad(db, g, do, H, Hkv):
+    """db = [q | k | v] bias gradient from the attention backward: q part = the column sums of the stored dq rows
+    (g [rows, 3, H*D] the stored packed gradient), k part exactly 0 (the row softmax cancels a key bias), v part =
+    the column sums of dO folded over each kv head's query heads (softmax rows sum to 1) -- which the column sums
+    of the stored (bf16-rounded) dv approximate."""
+    hd = g.shape[-1]
+    D = hd // H
+    kvd = Hkv * D
+    dbq, dbk, dbv = db[:hd].float(), db[hd:hd + kvd].float(), db[hd + kvd:].float()
+    wq = g[:, 0].float().sum(0)
+    assert float((dbq - wq).abs().max()) <= 1e-5 * float(wq.abs().max()) + 1e-3
+    assert torch.equal(dbk, torch.zeros_like(dbk))
+    wv = do.float().sum(0).view(Hkv, H // Hkv, D).sum(1).reshape(-1)
+    assert float((dbv - wv).abs().max()) <= 1e-5 * float(wv.abs().max()) + 1e-3
+    sv = g[:, 2, :kvd].float().sum(0)            # what the stored dv rows sum to: the same up to bf16 rounding
+    assert float((dbv - sv).abs().max()) <= 2e-2 * float(sv.abs().max()) + 0.5
+
+
 @pytest.mark.parametrize("bwd", [0, 3, 8])
 @pytest.mark.parametrize("D,S,B", [(128, 1024, 3), (64, 300, 2), (128, 200, 2)])
 def test_attn_bias_grad_from_backward_kernels(D, S, B, bwd):
-    """The qkv projection's bias gradient summed by the attention backward kernels (per-workgroup column sums
-    of the stored dq / dk / dv rows + a column reduce) equals the column sum of the gradient they stored; through
-    a biased Linear (GPT-2's c_attn) the Linear takes it instead of summing dY, and its bias gradient matches."""
+    """The qkv projection's bias gradient from the attention backward (_check_qkv_bias_grad: q part from the dQ
+    kernel's per-workgroup column sums + a column reduce, k part 0, v part from colsum(dO)), against the fp32
+    reference gradient too; through a biased Linear (GPT-2's c_attn) the Linear takes it instead of summing dY;
+    with a biased Linear consuming the attention output (GPT-2's c_proj) colsum(dO) comes from that Linear's
+    stash (db W) instead of a pass over dO."""
     from pytorch_distributedtraining_amd.ops import attention as A
     from pytorch_distributedtraining_amd.ops.linear import Linear
     H = 4
@@ -328,11 +347,28 @@ def test_attn_bias_grad_from_backward_kernels(D, S, B, bwd):
         scale = D ** -0.5
         o, lse = A._fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], True, scale)
         dqkv = torch.empty_like(qkv)
-        got = A._bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, torch.randn_like(o), dqkv[:, :, 0],
+        do = torch.randn_like(o)
+        got = A._bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0],
                      dqkv[:, :, 1], dqkv[:, :, 2], True, scale, bias_grad=True)
         assert got is not None and got.dtype == torch.float32
-        want = dqkv.float().reshape(B * S, 3 * H * D).sum(0)
-        assert rel_err(got, want) < 1e-5, rel_err(got, want)
+        _check_qkv_bias_grad(got, dqkv.reshape(B * S, 3, H * D), do.reshape(B * S, H * D), H, H)
+        x = qkv.detach().float().requires_grad_()
+        _attn_ref(x[:, :, 0], x[:, :, 1], x[:, :, 2], True, scale).backward(do.float())
+        ref = x.grad.reshape(B * S, 3 * H * D).sum(0)
+        assert float((got - ref).abs().max()) < 2e-2 * float(ref.abs().max()) + 0.05
+        # through a Linear consuming the attention output: the stashed colsum(dO) is taken, and equals the pass
+        C = H * D
+        proj = Linear(C, C).to(DEV).bfloat16()
+        q2 = qkv.detach().requires_grad_() * 1.0      # non-leaf: its gradient buffer is the attention's own
+        gqkv, gdo = [], []
+        q2.register_hook(gqkv.append)
+        o2 = A.flash_attn_qkvpacked(q2, causal=True, bias_grad=True)
+        o2.register_hook(gdo.append)
+        proj(o2.reshape(B, S, C)).backward(torch.randn(B, S, C, device=DEV, dtype=torch.bfloat16))
+        assert not [e for e in A._DX_COLSUMS.values() if e[0]() is not None]     # taken by the attention
+        db2 = A.take_bias_grad(gqkv[0].view(B * S, 3 * C))
+        assert db2 is not None
+        _check_qkv_bias_grad(db2, gqkv[0].view(B * S, 3, C), gdo[0].reshape(B * S, C), H, H)
         # end to end through a biased Linear: the stash is consumed, the bias gradient matches the column sum
         C = H * D
         lin = Linear(C, 3 * C).to(DEV).bfloat16()
