@@ -204,6 +204,15 @@ __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t voff, const 
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :: "s"(m0), "v"(voff), "s"(rsrc));   // m0: reserved, never allocated by hipcc
 }
+// the same with the LDS destination already a wave-uniform byte address
+__device__ __forceinline__ void dma16_m0(const v4i& rsrc, uint32_t voff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(m0), "v"(voff), "s"(rsrc));
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
+// a value every lane holds equally (block coordinates, tile counters): keep it -- and everything derived from it,
+// the 64-bit tile addresses included -- in SGPRs / on the scalar ALU instead of the VALU
+__device__ __forceinline__ int sgpr(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ void dma4_asm(const v4i& rsrc, uint32_t voff, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds_dst);
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
@@ -226,7 +235,9 @@ struct DmaLane {
   static constexpr int RW = TILE / NW, RPI = 1024 / (D * 2), NI = RW / RPI, LPR = 64 / RPI;
   static_assert(NI >= 1 && RW % RPI == 0, "tile rows per wave must be whole DMA instructions");
   uint32_t off_[NI];
+  uint32_t woff_;   // this wave's byte offset inside a staged tile (wave-uniform: an SGPR)
   __device__ __forceinline__ void init(int64_t row_stride, int w, int lane) {
+    woff_ = (uint32_t)sgpr(RW * w * D * 2);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int row = RW * w + RPI * i + lane / LPR;
@@ -241,8 +252,10 @@ struct DmaLane {
     const int bytes = rows_left > 0 ? (int)((int64_t)(rows_left - 1) * row_stride * 2 + D * 2) : 0;
     if constexpr (ASM) {
       const v4i rsrc = make_rsrc(base + (int64_t)row0 * row_stride, bytes);
+      // m0 = stage base (scalar) + wave offset (SGPR) + piece immediate: no per-issue VALU address math
+      const uint32_t m0 = lds_u32(lds) + woff_;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) dma16_asm(rsrc, off(i, w), lds + (RW * w + RPI * i) * D);
+      for (int i = 0; i < NI; ++i) dma16_m0(rsrc, off(i, w), m0 + RPI * i * D * 2);
     } else {
 #if __HIP_DEVICE_COMPILE__   // the buffer-resource type exists only in the device pass
       const __amdgpu_buffer_rsrc_t rsrc =
@@ -538,9 +551,9 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
-  const int qb = remap ? bc.t : (int)blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
+  const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
+  const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
+  const int hk = sgpr(hq / (p.H / p.Hkv));
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
   const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
@@ -655,9 +668,9 @@ __global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
-  const int qb = remap ? bc.t : (int)blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
+  const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
+  const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
+  const int hk = sgpr(hq / (p.H / p.Hkv));
   const int off = p.Sk - p.Sq;
   const int q0 = qb * BM, qw = q0 + w * 32, qrow = qw + c32;
   const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
@@ -936,8 +949,8 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(false, p.order, 1);   // causal: low key blocks see the most queries
   const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hk = remap ? bc.h : (int)blockIdx.y;
-  const int kb = remap ? bc.t : (int)blockIdx.x;
+  const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hk = sgpr(remap ? bc.h : (int)blockIdx.y);
+  const int kb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int group = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   const int kw = kb * 128 + w * 32, key = kw + c32;
@@ -976,16 +989,19 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   DmaLane<D> lq, lg;
   lq.init(p.q_ss, w, lane);
   lg.init(p.do_ss, w, lane);
-  auto issue = [&](int it, int buf) {
-    const int hi = it / qtiles, q0 = qstart + (it % qtiles) * TILE;
-    const int hq = hk * group + hi;
+  // (query head, query tile) of the next tile to stage / of the tile being computed, advanced by counters
+  // (wave-uniform: no integer division -- a VALU sequence -- per tile)
+  int iss_hi = 0, iss_qi = 0, cur_qi = 0;
+  auto issue = [&](int buf) {
+    const int q0 = sgpr(qstart + iss_qi * TILE), hq = sgpr(hk * group + iss_hi);
     bf16_t* base = smem + buf * 2 * TE;
     lq.issue(p.q + b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w);
     lg.issue(p.dout + b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE, w);
     if (w == 0) dma_f32_row(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][0], lane);
     if (w == 1) dma_f32_row(p.delta + ((int64_t)b * p.H + hq) * p.Sq, q0, p.Sq, sstat[buf][1], lane);
+    if (++iss_qi == qtiles) { iss_qi = 0; ++iss_hi; }
   };
-  if (total > 0) issue(0, 0);
+  if (total > 0) issue(0);
 
   for (int it = 0; it < total; it += 2) {
 #pragma unroll
@@ -993,8 +1009,9 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
       const int cur = it + u;
       if (cur >= total) break;
       dma_barrier();
-      if (cur + 1 < total) issue(cur + 1, 1 - u);
-      const int q0 = qstart + (cur % qtiles) * TILE;
+      if (cur + 1 < total) issue(1 - u);
+      const int q0 = sgpr(qstart + cur_qi * TILE);
+      if (++cur_qi == qtiles) cur_qi = 0;
       if (CAUSAL && q0 + TILE - 1 + off < kw) continue;         // every query of the tile precedes these keys
       const bf16_t* Qs = smem + u * 2 * TE;
       const float* Ls = sstat[u][0];
@@ -1119,9 +1136,9 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
-  const int qb = remap ? bc.t : (int)blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
+  const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
+  const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
+  const int hk = sgpr(hq / (p.H / p.Hkv));
   const int off = p.Sk - p.Sq;
   const int q0 = qb * 128, qw = q0 + w * 32, qrow = qw + c32;
   const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
@@ -1214,9 +1231,9 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
   const bool remap = CAUSAL || p.order == 1;
-  const int b = remap ? bc.b : (int)blockIdx.z, hq = remap ? bc.h : (int)blockIdx.y;
-  const int qb = remap ? bc.t : (int)blockIdx.x;
-  const int hk = hq / (p.H / p.Hkv);
+  const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
+  const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
+  const int hk = sgpr(hq / (p.H / p.Hkv));
   const int off = p.Sk - p.Sq;
   const int q0 = qb * BM, qw = q0 + w * 32, qrow = qw + c32;
   const bf16_t* Qp = p.q + b * p.q_sb + hq * p.q_sh;
