@@ -48,6 +48,9 @@ def parse():
                     help="with activation checkpointing: 'all', a layer count, or 'auto' = recompute only as many "
                          "layers as the HBM needs (sized after the first warm-up step)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--resnet-graph", type=int, default=0,
+                    help="resnet50-ddp (and the ResNet secondary): capture the whole DDP step in a HIP graph "
+                         "(fwd, bwd, clip, fused AdamW; at N > 1 the bucket all-reduces too)")
     ap.add_argument("--secondary", type=int, default=1,
                     help="gpt2-fsdp: also measure BASELINE.json's ResNet-50 DDP metric at the same world size "
                          "(JSON 'secondary')")
@@ -510,7 +513,8 @@ def bench_resnet(args, comm, dev, world, rank, guarded=False):
     model = DistributedDataParallel(model, comm=comm, reduce_dtype=None if cpu else torch.bfloat16,
                                     compute_dtype=None if autocast else torch.bfloat16)
     params = model.optimizer_parameters()
-    opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4)
+    graph = bool(args.resnet_graph) and not cpu and (world == 1 or comm.backend == "nccl")
+    opt = FusedAdamW(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-8, weight_decay=1e-4, capturable=graph)
     crit = torch.nn.CrossEntropyLoss()
 
     def step():
@@ -519,7 +523,7 @@ def bench_resnet(args, comm, dev, world, rank, guarded=False):
         loss.backward()
         _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
         opt.step(grad_scale=coef)
-        opt.zero_grad(set_to_none=True)
+        opt.zero_grad(set_to_none=not graph)
 
     if guarded:
         try:
@@ -539,6 +543,23 @@ def bench_resnet(args, comm, dev, world, rank, guarded=False):
             err = e
         agree(comm, dev, err, "first step")
 
+    if graph:
+        from pytorch_distributedtraining_amd.utils.graphs import GraphedStep
+
+        def body(xs, ys):
+            opt.zero_grad(set_to_none=False)          # gradients keep their addresses across replays
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+                loss = crit(model(xs).float(), ys)
+            loss.backward()
+            _, coef, _ = clip_grad_norm_(params, args.grad_clip, comm=comm, sharded=False, apply=False)
+            opt.step(grad_scale=coef)
+            return loss.detach()
+        if world > 1:
+            model.prepare_capture()
+        graphed = GraphedStep(body, x, y, warmup=2)
+
+        def step():                                   # noqa: F811 - the graphed replacement
+            graphed(x, y)
     dt = timed_loop(step, args, comm, dev)
     sps = world * mb * args.steps / dt
     name = "ResNet-18 DDP CPU/gloo" if cpu else "ResNet-50 DDP"
@@ -547,7 +568,7 @@ def bench_resnet(args, comm, dev, world, rank, guarded=False):
             "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             **comm_fields(world), "vs_baseline": None, "dtype": "fp32" if cpu else "bf16", "data": "synthetic",
             "config": {"model": "resnet18" if cpu else "resnet50", "global_batch": world * mb, "seq_len": None,
-                       "parallelism": f"dp{world}", "image": "3x224x224"}}
+                       "parallelism": f"dp{world}", "image": "3x224x224", "hip_graph": graph}}
 
 
 def bench_swinir(args, comm, dev, world, rank):

@@ -10,7 +10,7 @@
 // Row-major [N, K] = dY[M, N]^T X[M, K] is the column-major product D[K, N] = op(A) op(B) with A = X
 // (column-major [K, M], op N) and B = dY (column-major [N, M], op T); the bias gradient runs along n = N.
 // Plans (descriptors + the algorithm) are cached per shape; the first call of a shape outside graph capture
-// times up to 8 heuristic candidates and keeps the fastest.  Workspace: one 64 MiB device buffer per device.
+// times up to 8 (plain / bias: 16) heuristic candidates and keeps the fastest.  Workspace: one 64 MiB device buffer per device.
 // The library resolves at run time to the libhipblaslt.so.1 torch already mapped (same soname).
 #include "common.h"
 #include <hipblaslt/hipblaslt.h>
@@ -104,9 +104,12 @@ int build(Plan& p, hipblasLtHandle_t h, int epi, int trans, int64_t m, int64_t n
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   const uint64_t wsb = WS_BYTES;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
-  p.cands.resize(8);
+  // plain / bias GEMMs (ops.linear's NT products) time a wider candidate list than the fused-epilogue ones
+  const int want = (epi == 0 || epi == 1) ? 16 : 8;
+  p.cands.resize(want);
   int got = 0;
-  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.a, p.b, p.d, p.d, pref, 8, p.cands.data(), &got);
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.a, p.b, p.d, p.d, pref, want, p.cands.data(),
+                                                              &got);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || got <= 0) return -3;   // epilogue / type combination not supported
   p.cands.resize(got);

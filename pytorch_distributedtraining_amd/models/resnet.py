@@ -5,7 +5,8 @@ downsample.{0,1}, fc) so torchvision checkpoints load with ``strict=True``.  Con
 MIOpen (framework layer); use ``channels_last`` + bf16 autocast on MI355X.  With ``fused_bn=True`` (default)
 every BatchNorm is an ``ops.batchnorm.BatchNormAct2d`` (an nn.BatchNorm2d subclass) that fuses the
 following ReLU and, at the end of a block, the residual add into one channels-last HIP pass
-(``relu(bn3(conv3(h)) + identity)``); ``fused_bn=False`` builds the plain nn.BatchNorm2d / nn.ReLU model
+(``relu(bn3(conv3(h)) + identity)``), and the stem's max pool keeps a 1-byte window slot instead of an int64
+argmax (``ops.pool``); ``fused_bn=False`` builds the plain nn.BatchNorm2d / nn.ReLU model
 (the stock-torch baseline).  ``parallel.syncbn.convert_sync_batchnorm`` makes either cross-rank.
 Written from the published architecture (He et al. 2015), random init.
 """
@@ -16,6 +17,7 @@ import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import Conv2d1x1
+from ..ops.pool import MaxPool2d
 
 
 def _bn(c, act, fused):
@@ -94,7 +96,7 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(64, "relu", fused_bn)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool2d(3, stride=2, padding=1) if fused_bn else nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)

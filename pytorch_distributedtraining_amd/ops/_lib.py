@@ -104,6 +104,13 @@ _SIGS = {
     "pdt_xgmi_wallclock_khz": [],
     "pdt_bn_ws_floats": [c_int],
     "pdt_bn_ok": [c_int],
+    "pdt_maxpool_ok": [c_int, c_int, c_int, c_int],
+    "pdt_bn_stats_finalize": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pdt_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_void_p],
+    "pdt_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_void_p],
     "pdt_bn_stats": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "pdt_bn_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_void_p],

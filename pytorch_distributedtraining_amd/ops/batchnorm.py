@@ -39,13 +39,17 @@ class _BNActFn(torch.autograd.Function):
         dev, stream = x.device, _lib.stream_handle(x.device)
         ws = _workspace(c, dev)
         stats = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-        _lib.call("pdt_bn_stats", x.data_ptr(), rows, c, ws.data_ptr(), stats.data_ptr(), stream)
-        if comm is not None and comm.world_size > 1:
-            comm.all_reduce(stats, "sum")
         coef = torch.empty(4, c, dtype=torch.float32, device=dev)        # mean, invstd, scale, shift
-        _lib.call("pdt_bn_finalize", stats.data_ptr(), c, float(eps), float(momentum), _lib.ptr(weight),
-                  _lib.ptr(bias), coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
-                  _lib.ptr(running_mean), _lib.ptr(running_var), stream)
+        if comm is not None and comm.world_size > 1:
+            _lib.call("pdt_bn_stats", x.data_ptr(), rows, c, ws.data_ptr(), stats.data_ptr(), stream)
+            comm.all_reduce(stats, "sum")
+            _lib.call("pdt_bn_finalize", stats.data_ptr(), c, float(eps), float(momentum), _lib.ptr(weight),
+                      _lib.ptr(bias), coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
+                      _lib.ptr(running_mean), _lib.ptr(running_var), stream)
+        else:       # local statistics: the combine and the finalize are one kernel
+            _lib.call("pdt_bn_stats_finalize", x.data_ptr(), rows, c, ws.data_ptr(), stats.data_ptr(), float(eps),
+                      float(momentum), _lib.ptr(weight), _lib.ptr(bias), coef[0].data_ptr(), coef[1].data_ptr(),
+                      coef[2].data_ptr(), coef[3].data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), stream)
         y = torch.empty_like(x, memory_format=torch.channels_last)
         # ReLU after a residual add: the backward's mask can not be recomputed from x, so the apply writes it as
         # bits (1/16 of the bytes of reading y back in both backward passes)

@@ -53,19 +53,55 @@ def _nt_hip_ok(a2: torch.Tensor, w: torch.Tensor, bias) -> bool:
             and G.nt_ok(a2, w) and a2.shape[1] // 64 >= 2 and w.shape[0] % 8 == 0)
 
 
+# PDT_NT_LT: "auto" -- the library side of nt_matmul's choice is the faster of torch's hipBLASLt call (its
+# heuristic's first algorithm) and ops.blaslt's tuned plan (16 heuristic candidates timed once per shape); "0"
+# (default): torch's call only -- on the flagship the tuned plans tied torch's pick (150.3 / 150.2k vs 150.7 /
+# 149.9k tokens/s interleaved, profiles/r5/r5e_nt_lt_ab.log)
+LT_NT = os.environ.get("PDT_NT_LT", "0")
+_LT_CHOICE: dict = {}
+
+
+def _lt_linear(a2, w, bias):
+    """a2 [M, K] @ w[N, K]^T (+ bias) on the tuned hipBLASLt plan, or None (no algorithm for the combination).
+    Column-major: D[N, M] = W^T(op T on col-major [K, N]) . A(col-major [K, M])."""
+    from . import blaslt as LT
+    m, k = a2.shape
+    n = w.shape[0]
+    y = torch.empty(m, n, dtype=a2.dtype, device=a2.device)
+    if not LT.lt_matmul(LT.EPI_BIAS if bias is not None else LT.EPI_NONE, 1, n, m, k, w, a2, y, bias):
+        return None
+    return y
+
+
+def _library_linear(a2, w, bias, key):
+    """hipBLASLt for a2 @ w^T (+ bias): torch's call, or the tuned plan where it was measured faster."""
+    if LT_NT != "0" and a2.is_cuda and a2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+            and a2.is_contiguous() and w.is_contiguous() and (bias is None or bias.dtype == torch.bfloat16):
+        c = _LT_CHOICE.get(key)
+        if c is None and not torch.cuda.is_current_stream_capturing():
+            c = _LT_CHOICE[key] = _lt_linear(a2, w, bias) is not None and \
+                timed_choice(lambda: _lt_linear(a2, w, bias), lambda: F.linear(a2, w, bias), 0.99)
+        if c:
+            y = _lt_linear(a2, w, bias)
+            if y is not None:
+                return y
+    return F.linear(a2, w, bias)
+
+
 def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
     """a2 [M, K] @ w[N, K]^T (+ bias): the hand NT GEMM (ops.gemm.gemm_nt) or hipBLASLt, per shape as timed."""
+    key = (tuple(a2.shape), tuple(w.shape), bias is not None, a2.device)
     if _nt_hip_ok(a2, w, bias):
         from . import gemm as G
         if HIP_NT == "1":
             return G.gemm_nt(a2, w, bias)
-        key = (tuple(a2.shape), tuple(w.shape), bias is not None, a2.device)
         c = _NT_CHOICE.get(key)
         if c is None and not torch.cuda.is_current_stream_capturing():
-            c = _NT_CHOICE[key] = timed_choice(lambda: G.gemm_nt(a2, w, bias), lambda: F.linear(a2, w, bias), 0.99)
+            c = _NT_CHOICE[key] = timed_choice(lambda: G.gemm_nt(a2, w, bias),
+                                               lambda: _library_linear(a2, w, bias, key), 0.99)
         if c:
             return G.gemm_nt(a2, w, bias)
-    return F.linear(a2, w, bias)
+    return _library_linear(a2, w, bias, key)
 
 
 def _tall_skinny(m: int, n: int, k: int) -> bool:

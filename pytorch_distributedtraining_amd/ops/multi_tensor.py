@@ -62,7 +62,8 @@ class TensorTable:
                     # elementwise over the storage: any dense layout works if every column shares it
                     assert _dense(t), "multi-tensor kernels need dense (non-overlapping) tensors"
                     assert t.numel() == self.numels[i]
-                    assert t.stride() == ref.stride() or t.dim() <= 1, "multi-tensor columns must share a layout"
+                    assert t.dim() <= 1 or all(a == b for a, b, k in zip(t.stride(), ref.stride(), ref.shape) if k != 1), \
+                        "multi-tensor columns must share a layout"   # (a size-1 dimension's stride is arbitrary)
                     meta[i, j] = t.data_ptr()
             meta[i, 5] = self.numels[i]
         if self.nblocks:

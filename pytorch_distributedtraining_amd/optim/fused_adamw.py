@@ -25,13 +25,23 @@ import torch
 from torch.optim import Optimizer
 
 from ..ops import multi_tensor as mt
+from ..ops.multi_tensor import _dense
 from ._grads import grad_of
+
+
+def _same_layout(g, p) -> bool:
+    """Same element order in memory: strides equal wherever the size is not 1 (a size-1 dimension's stride is
+    arbitrary -- a contiguous [Cout, Cin, 1, 1] gradient of a channels_last 1x1-conv weight is already in its order,
+    and autograd's layout contract accepts it as is)."""
+    return g.shape == p.shape and all(gs == ps for gs, ps, n in zip(g.stride(), p.stride(), p.shape) if n != 1)
 
 
 def _like(g, p):
     """The gradient in the parameter's memory layout (the kernel walks storage linearly)."""
-    if g.stride() == p.stride() or p.dim() <= 1:
-        return g if g.is_contiguous() or p.dim() > 1 else g.contiguous()
+    if p.dim() <= 1:
+        return g if g.is_contiguous() else g.contiguous()
+    if _same_layout(g, p) and _dense(g):
+        return g
     return torch.empty_like(p, dtype=g.dtype).copy_(g)
 
 

@@ -204,6 +204,10 @@ class DistributedDataParallel(nn.Module):
             # They are never cast at all (a round trip through bf16 would round values loaded before wrapping).
             _cast_except_batchnorm(module, compute_dtype)
         self.params = [p for p in module.parameters() if p.requires_grad]
+        # one process and fp32 parameters: no collective reads the buckets, so the gradients stay where autograd
+        # puts them -- AccumulateGrad STEALS each freshly produced gradient (no kernel) instead of adding it into a
+        # zeroed bucket view (one add launch per parameter per step: 161 for ResNet-50, ~0.7 ms)
+        self._steal_grads = self.comm.world_size == 1 and compute_dtype is None
         if self.comm.world_size > 1:
             self.comm.broadcast_coalesced([p.data for p in self.params] + [b for b in module.buffers()])
         self._build(order=None)
@@ -238,8 +242,9 @@ class DistributedDataParallel(nn.Module):
             for li, gi in enumerate(gidx):
                 self.param_group[gi] = (g, li)
             self.groups.append(g)
-        for g in self.groups:
-            g.attach_grads()
+        if not self._steal_grads:
+            for g in self.groups:
+                g.attach_grads()
         self._arm_readiness()
 
     def _arm_readiness(self):
@@ -361,7 +366,7 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
-        if self.params and self.params[0].grad is None:
+        if self.params and self.params[0].grad is None and not self._steal_grads:
             # zero_grad(set_to_none=True) dropped the bucket views: zero the flats and re-attach
             for g in self.groups:
                 g.flat_grad.zero_()
@@ -395,6 +400,13 @@ class DistributedDataParallel(nn.Module):
         return self.optimizer_parameters()
 
     def zero_grad(self, set_to_none: bool = False):
+        if self._steal_grads:
+            for p in self.params:
+                if set_to_none:
+                    p.grad = None
+                elif p.grad is not None:
+                    p.grad.zero_()
+            return
         for g in self.groups:
             g.flat_grad.zero_()
 

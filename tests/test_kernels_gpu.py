@@ -298,6 +298,21 @@ def test_hand_gemm_nt_3stage_full_grid_production_shapes(N, K):
         assert int(bad.sum()) == 0, int(bad.sum())
 
 
+@pytest.mark.parametrize("m,n,k,bias", [(4096, 2048, 2048, False), (4096, 6144, 2048, True), (1000, 768, 3072, True)])
+def test_tuned_hipblaslt_linear_matches_torch(m, n, k, bias):
+    """ops.linear's library arm through the tuned hipBLASLt plan (ops.blaslt, every heuristic candidate timed)
+    equals torch's F.linear up to accumulation order, with and without the bias epilogue."""
+    from pytorch_distributedtraining_amd.ops import linear as L
+    torch.manual_seed(m + n + k)
+    a = torch.randn(m, k, device=DEV).bfloat16()
+    w = (torch.randn(n, k, device=DEV) * k ** -0.5).bfloat16()
+    b = torch.randn(n, device=DEV).bfloat16() if bias else None
+    got = L._lt_linear(a, w, b)
+    assert got is not None and got.shape == (m, n)
+    want = a.float() @ w.float().t() + (b.float() if bias else 0)
+    assert rel_err(got, want) < 1e-2, rel_err(got, want)
+
+
 def test_flash_attn_qkvpacked_matches_unpacked():
     from pytorch_distributedtraining_amd.ops import flash_attn, flash_attn_qkvpacked
     qkv = torch.randn(2, 300, 3, 4, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -1154,6 +1169,29 @@ def test_fused_batchnorm_relu_resnet_layer_shape(res):
         assert rel_err(r.grad, rr.grad) < 1e-2
     assert rel_err(bn.weight.grad, ref.weight.grad) < 1e-2
     assert rel_err(bn.bias.grad, ref.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 24, 17, 15), 3, 2, 1),
+                                         ((2, 16, 9, 9), 2, 2, 0), ((1, 8, 10, 12), 3, 1, 1)])
+def test_maxpool_nhwc_matches_torch(shape, k, s, p):
+    """ops.pool.MaxPool2d (1-byte window slot, gather backward) vs torch's max_pool2d on the same bf16 values in
+    fp32: forward bitwise, the input gradient on exactly the same elements (first maximum in scan order on ties, as
+    torch) and equal up to bf16 rounding; the ResNet stem shape included.  Ties are forced by quantising the input."""
+    from pytorch_distributedtraining_amd.ops.pool import MaxPool2d
+    torch.manual_seed(sum(shape) + k)
+    x = (torch.randn(shape, device=DEV) * 4).round().div(4).bfloat16().to(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = MaxPool2d(k, stride=s, padding=p)(x)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == torch.bfloat16
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, k, s, p)
+    yr.backward(dy.float())
+    assert torch.equal(y.float(), yr)
+    # the same windows win; their dy sums (<= 4 terms) differ from torch's scatter-add order by fp32 rounding only
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+    assert torch.equal(x.grad.float() != 0, xr.grad != 0)
 
 
 def test_resnet50_fused_bn_matches_plain_model():
