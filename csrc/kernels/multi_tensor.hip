@@ -203,6 +203,21 @@ __global__ __launch_bounds__(MT_THREADS) void cast_f32_bf16_mt_kernel(const int6
   for (int64_t j = beg + threadIdx.x; j < end; j += MT_THREADS) D[j] = f2bf(S[j]);
 }
 
+// dst <- src over a tensor list (ptr0 = dst, ptr1 = src, same element type; src 0 -> dst zero-filled): gathers
+// per-parameter gradients into a flat buffer in ONE launch (parallel/ddp.py, single-process compute-copy mode)
+template <typename T>
+__global__ __launch_bounds__(MT_THREADS) void copy_mt_kernel(const int64_t* __restrict__ meta, const int* __restrict__ blk,
+                                                             int chunk) {
+  const int t = blk[2 * blockIdx.x], c = blk[2 * blockIdx.x + 1];
+  const int64_t* mt = meta + (int64_t)t * MT_META;
+  T* __restrict__ D = reinterpret_cast<T*>(mt[0]);
+  const T* __restrict__ S = reinterpret_cast<const T*>(mt[1]);
+  const int64_t n = mt[5];
+  const int64_t beg = (int64_t)c * chunk;
+  const int64_t end = beg + chunk < n ? beg + chunk : n;
+  for (int64_t j = beg + threadIdx.x; j < end; j += MT_THREADS) D[j] = S ? S[j] : T(0);
+}
+
 // Device step counter of a param group: +1 unless the (all-reduced) found_inf flag says the step is skipped
 // (torch.amp.GradScaler skips optimizer.step() on overflow, so Adam's bias-correction step must not move).
 __global__ void step_inc_kernel(float* __restrict__ dstep, const int* __restrict__ found_inf) {
@@ -264,5 +279,17 @@ PDT_API int pdt_scale_mt(const int64_t* meta, const int* blk, int nblocks, int c
 PDT_API int pdt_cast_f32_bf16_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, hipStream_t stream) {
   if (nblocks <= 0) return 0;
   cast_f32_bf16_mt_kernel<<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  return (int)hipGetLastError();
+}
+
+// elem_bytes 2 (bf16 / fp16) or 4 (fp32)
+PDT_API int pdt_copy_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, int elem_bytes, hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  if (elem_bytes == 4)
+    copy_mt_kernel<uint32_t><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  else if (elem_bytes == 2)
+    copy_mt_kernel<uint16_t><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  else
+    return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }

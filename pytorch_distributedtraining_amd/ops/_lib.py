@@ -41,6 +41,7 @@ _SIGS = {
     "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "pdt_cast_f32_bf16_mt": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "pdt_copy_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_int, c_float, c_int, c_int, c_int, c_void_p],
     "pdt_norm_bwd_workspace_floats": [c_int, c_int],

@@ -255,3 +255,31 @@ def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
         dst.copy_(src)
         return
     _lib.call("pdt_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), _lib.stream_handle(src.device))
+
+
+def copy_(dsts: Sequence[torch.Tensor], srcs: Sequence[torch.Tensor | None], name: str = "copy") -> None:
+    """dst.copy_(src) for every pair (same dtype, same element order; a None src zero-fills its dst) in ONE
+    launch on CUDA -- e.g. per-parameter gradients gathered into a flat buffer."""
+    if not dsts:
+        return
+    dev = dsts[0].device
+    if dev.type != "cuda":
+        for d, s in zip(dsts, srcs):
+            d.zero_() if s is None else d.copy_(s)
+        return
+    for d, s in zip(dsts, srcs):
+        assert s is None or (s.dtype == d.dtype and s.numel() == d.numel())
+    key = TensorTable.make_key([list(dsts), list(srcs)])
+    cached = _cache._tables.get(name)
+    if torch.cuda.is_current_stream_capturing() and (cached is None or cached.key() != key):
+        # a new pointer set while a HIP graph is captured: no table upload is allowed -- torch's foreach copy
+        pairs = [(d, s) for d, s in zip(dsts, srcs) if s is not None]
+        if pairs:
+            torch._foreach_copy_([d for d, _ in pairs], [s for _, s in pairs])
+        zs = [d for d, s in zip(dsts, srcs) if s is None]
+        if zs:
+            torch._foreach_zero_(zs)
+        return
+    t = _cache.get(name, [list(dsts), list(srcs)])
+    _lib.call("pdt_copy_mt", t.meta.data_ptr(), t.blk.data_ptr(), t.nblocks, t.chunk, dsts[0].element_size(),
+              _lib.stream_handle(dev))

@@ -134,7 +134,10 @@ class FusedAdamW(Optimizer):
                     continue
                 rest.append(p)
         for zero in flats.values():
-            zero()
+            if getattr(zero, "_pdt_set_to_none", False):
+                zero(set_to_none)      # an engine that keeps per-parameter gradients (DDP._steal_grads)
+            else:
+                zero()
         if views:
             torch._foreach_zero_(views)
         if set_to_none:

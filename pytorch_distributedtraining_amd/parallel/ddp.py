@@ -122,6 +122,34 @@ class _FlatGroup:
             m._pdt_zero_grad = self.flat_grad.zero_   # optimizer.zero_grad() clears the accumulated flat grad
             self.master = m
 
+    def gather_grads(self):
+        """Single-process gradient stealing (DistributedDataParallel._steal_grads) with a compute copy: the
+        parameters' own (stolen) gradients -> the flat the fp32 master reads, in ONE multi-tensor launch; a
+        parameter that received no gradient gets zeros."""
+        from ..ops import multi_tensor as mt
+        dsts = [_pview(self.flat_grad, p, self.offset_of[li]) for li, p in enumerate(self.params)]
+        srcs = [p.grad for p in self.params]
+        same = [s is None or all(a == b for a, b, n in zip(s.stride(), d.stride(), d.shape) if n != 1)
+                for s, d in zip(srcs, dsts)]
+        if all(same):
+            mt.copy_(dsts, srcs, name=("ddp_gather", id(self)))
+        else:
+            for s_, d in zip(srcs, dsts):
+                d.zero_() if s_ is None else d.copy_(s_)
+
+    def drop_grads(self, set_to_none: bool = True):
+        """zero_grad for a stealing compute-copy group: set_to_none -> the next backward's gradients are stolen
+        again; otherwise they are zeroed in place (addresses kept: HIP-graph replay)."""
+        if set_to_none:
+            for p in self.params:
+                p.grad = None
+        else:
+            gs = [p.grad for p in self.params if p.grad is not None]
+            if gs:
+                torch._foreach_zero_(gs)
+        self.flat_grad.zero_()
+    drop_grads._pdt_set_to_none = True
+
     def attach_grads(self):
         for li, p in enumerate(self.params):
             o = self.offset_of[li]
@@ -204,10 +232,12 @@ class DistributedDataParallel(nn.Module):
             # They are never cast at all (a round trip through bf16 would round values loaded before wrapping).
             _cast_except_batchnorm(module, compute_dtype)
         self.params = [p for p in module.parameters() if p.requires_grad]
-        # one process and fp32 parameters: no collective reads the buckets, so the gradients stay where autograd
-        # puts them -- AccumulateGrad STEALS each freshly produced gradient (no kernel) instead of adding it into a
-        # zeroed bucket view (one add launch per parameter per step: 161 for ResNet-50, ~0.7 ms)
-        self._steal_grads = self.comm.world_size == 1 and compute_dtype is None
+        # one process: no collective reads the buckets, so the gradients stay where autograd puts them --
+        # AccumulateGrad STEALS each freshly produced gradient (no kernel) instead of adding it into a zeroed
+        # bucket view (one add launch per parameter per step: 161 for ResNet-50, ~0.7 ms).  With a compute copy
+        # the fp32 masters read the flat: one multi-tensor gather fills it at the end of each backward.
+        self._steal_grads = self.comm.world_size == 1
+        self._gather_queued = False
         if self.comm.world_size > 1:
             self.comm.broadcast_coalesced([p.data for p in self.params] + [b for b in module.buffers()])
         self._build(order=None)
@@ -245,6 +275,10 @@ class DistributedDataParallel(nn.Module):
         if not self._steal_grads:
             for g in self.groups:
                 g.attach_grads()
+        elif self.compute_dtype is not None:
+            for g in self.groups:
+                if g.master is not None:
+                    g.master._pdt_zero_grad = g.drop_grads      # bound method: _pdt_set_to_none via __func__
         self._arm_readiness()
 
     def _arm_readiness(self):
@@ -373,7 +407,31 @@ class DistributedDataParallel(nn.Module):
                 g.attach_grads()
         if self.broadcast_buffers and self.comm.world_size > 1 and self.module.training:
             self._sync_buffers()
-        return self.module(*args, **kwargs)
+        out = self.module(*args, **kwargs)
+        if self._steal_grads and self.compute_dtype is not None and torch.is_grad_enabled():
+            self._arm_gather(out)
+        return out
+
+    def _arm_gather(self, out):
+        """Queue the compute-copy gradient gather to run once the backward through ``out`` has finished."""
+        ts = [out] if torch.is_tensor(out) else [t for t in (out.values() if isinstance(out, dict) else out)
+                                                  if torch.is_tensor(t)] if isinstance(out, (tuple, list, dict)) else []
+        for t in ts:
+            if t.requires_grad:
+                ref = weakref.ref(self)
+                t.register_hook(lambda g, ref=ref: ref()._queue_gather() or g)
+                return
+
+    def _queue_gather(self):
+        if not self._gather_queued:
+            self._gather_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._gather)
+
+    def _gather(self):
+        self._gather_queued = False
+        for g in self.groups:
+            if g.master is not None:
+                g.gather_grads()
 
     def _sync_buffers(self):
         sync_buffers(self.module, self.comm, self, self.buffer_sync)
@@ -400,6 +458,10 @@ class DistributedDataParallel(nn.Module):
         return self.optimizer_parameters()
 
     def zero_grad(self, set_to_none: bool = False):
+        if self._steal_grads and self.compute_dtype is not None:
+            for g in self.groups:
+                g.drop_grads(set_to_none)
+            return
         if self._steal_grads:
             for p in self.params:
                 if set_to_none:

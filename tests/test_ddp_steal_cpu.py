@@ -1,0 +1,68 @@
+"""Single-process DDP keeps gradients where autograd puts them (parallel/ddp.py ``_steal_grads``): AccumulateGrad
+steals each fresh gradient instead of adding it into a zeroed bucket view.  With fp32 parameters the optimizer
+reads the per-parameter gradients; with a bf16 compute copy one multi-tensor gather (queued at the end of every
+backward) fills the flat the fp32 masters read.  Checked against a plain module: gradients, accumulation over two
+backwards (no_sync), zero_grad, and AdamW steps (FusedAdamW on CPU)."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from pytorch_distributedtraining_amd.optim import FusedAdamW
+from pytorch_distributedtraining_amd.parallel.comm import Comm
+from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _pg():
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29671")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    yield
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(12, 32), torch.nn.BatchNorm1d(32), torch.nn.ReLU(),
+                               torch.nn.Linear(32, 5))
+
+
+@pytest.mark.parametrize("compute_dtype", [None, torch.bfloat16])
+def test_single_process_ddp_steals_gradients(compute_dtype):
+    ref = _model()
+    ddp = DistributedDataParallel(copy.deepcopy(ref), comm=Comm(), compute_dtype=compute_dtype)
+    assert ddp._steal_grads
+    if compute_dtype is not None:
+        ref = ref.to(compute_dtype)
+        for m in ref.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.float()
+    xs = [torch.randn(16, 12) for _ in range(2)]
+    # two backwards accumulate (the second under no_sync, as a gradient-accumulation micro-step)
+    with ddp.no_sync():
+        ddp(xs[0].to(compute_dtype or torch.float32)).float().square().mean().backward()
+    ddp(xs[1].to(compute_dtype or torch.float32)).float().square().mean().backward()
+    for x in xs:
+        ref(x.to(compute_dtype or torch.float32)).float().square().mean().backward()
+    for p, q in zip(ddp.module.parameters(), ref.parameters()):
+        assert p.grad is not None and p.grad._base is None            # autograd's own tensor, not a bucket view
+        torch.testing.assert_close(p.grad.float(), q.grad.float(), rtol=1e-2, atol=1e-3)
+    if compute_dtype is not None:
+        for g in ddp.groups:                                           # the gather filled the masters' flat
+            for li, p in enumerate(g.params):
+                o = g.offset_of[li]
+                torch.testing.assert_close(g.flat_grad[o:o + p.numel()].view_as(p.grad).float(), p.grad.float())
+    opt = FusedAdamW(ddp.optimizer_parameters(), lr=1e-2)
+    opt.step()
+    opt.zero_grad()
+    assert all(p.grad is None for p in ddp.module.parameters())
+    if compute_dtype is not None:
+        assert all(float(g.flat_grad.abs().sum()) == 0.0 for g in ddp.groups)
+    # a second step steals again
+    ddp(xs[0].to(compute_dtype or torch.float32)).float().square().mean().backward()
+    assert all(p.grad is not None for p in ddp.module.parameters())
+    opt.zero_grad(set_to_none=False)                                   # graph-replay form: zeroed in place
+    assert all(p.grad is None or float(p.grad.abs().sum()) == 0.0 for p in ddp.module.parameters())
