@@ -124,6 +124,9 @@ struct AttnParams {
   int fuse_delta;
   // A/B switch (PDT_FA_MASK_ALL=1): every backward tile takes the masked path (the pre-dispatch code)
   int mask_all;
+  // timing diagnostics only (PDT_FA_DIAG, results WRONG when set): bit 0 dK/dV kernel skips its K / V prologue
+  // loads, bit 1 its dK / dV stores; bit 2 the dQ kernel skips its Q / dO / O prologue loads, bit 3 its dQ stores
+  int diag;
 };
 
 // delta of this lane's query row from its dO fragments (gf, already in registers) and the O row; written with
@@ -246,6 +249,17 @@ struct DmaLane {
     }
   }
   __device__ __forceinline__ uint32_t off(int i, int) const { return off_[i]; }
+  // the same with the stage's LDS byte address given (no generic-pointer round trip)
+  __device__ __forceinline__ void issue_at(const bf16_t* base, int64_t row_stride, int row0, int nrows, uint32_t lds,
+                                           int w) const {
+    static_assert(ASM, "issue_at: inline-asm DMA only");
+    const int rows_left = nrows - row0;
+    const int bytes = rows_left > 0 ? (int)((int64_t)(rows_left - 1) * row_stride * 2 + D * 2) : 0;
+    const v4i rsrc = make_rsrc(base + (int64_t)row0 * row_stride, bytes);
+    const uint32_t m0 = lds + woff_;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) dma16_m0(rsrc, off(i, w), m0 + RPI * i * D * 2);
+  }
   __device__ __forceinline__ void issue(const bf16_t* base, int64_t row_stride, int row0, int nrows, bf16_t* lds,
                                         int w) const {
     const int rows_left = nrows - row0;
@@ -317,7 +331,21 @@ __device__ __forceinline__ BlockCoord grouped_coord(int lin, int nt, int nh, int
 __device__ __forceinline__ bool grouped_ok(int order, int nh, int nb, int grp) {
   return order == 1 && !(((nh / grp) * nb) & 7);
 }
+// order 2: the tile index cycles fastest (heaviest first within each cycle): consecutive workgroups get different
+// amounts of causal work, so they finish -- and start their HBM-bound prologues -- at different times instead of
+// every CU loading its Q / dO (K / V) rows in the same burst (a measured A/B: PDT_FA_CYCLE)
+__device__ __forceinline__ BlockCoord cycled(bool heavy_is_high) {
+  const int nt = gridDim.x, nh = gridDim.y;
+  const int lin = blockIdx.x + nt * (blockIdx.y + nh * blockIdx.z);
+  const int tr = lin % nt, rest = lin / nt;
+  BlockCoord c;
+  c.t = heavy_is_high ? nt - 1 - tr : tr;
+  c.h = rest % nh;
+  c.b = rest / nh;
+  return c;
+}
 __device__ __forceinline__ BlockCoord block_order(bool heavy_is_high, int order, int grp) {
+  if (order == 2) return cycled(heavy_is_high);
   if (!grouped_ok(order, gridDim.y, gridDim.z, grp)) return heavy_first(heavy_is_high);
   return grouped_coord(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y, grp,
                        heavy_is_high);
@@ -550,7 +578,7 @@ __global__ __launch_bounds__(NT, 2) void fa_fwd_v5_kernel(AttnParams p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
-  const bool remap = CAUSAL || p.order == 1;
+  const bool remap = CAUSAL || p.order != 0;
   const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
   const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int hk = sgpr(hq / (p.H / p.Hkv));
@@ -667,7 +695,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_fwd_v7_kernel(AttnParams p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
-  const bool remap = CAUSAL || p.order == 1;
+  const bool remap = CAUSAL || p.order != 0;
   const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
   const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int hk = sgpr(hq / (p.H / p.Hkv));
@@ -789,6 +817,13 @@ __global__ __launch_bounds__(NT) void fa_bwd_delta_kernel(AttnParams p) {
 __device__ __forceinline__ void dma_f32_row(const float* src, int row0, int nrows, float* lds, int lane) {
   const int left = nrows - row0;
   dma4_asm(make_rsrc(src + row0, left > 0 ? left * 4 : 0), (uint32_t)lane * 4, lds);
+}
+
+__device__ __forceinline__ void dma_f32_row_at(const float* src, int row0, int nrows, uint32_t lds, int lane) {
+  const int left = nrows - row0;
+  const v4i rsrc = make_rsrc(src + row0, left > 0 ? left * 4 : 0);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "s"(lds), "v"((uint32_t)lane * 4), "s"(rsrc));
 }
 
 // transposed-fragment offsets for a [TILE][D] swizzled image (rows kb + 4(g>>1) + q (+8), column
@@ -948,7 +983,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(false, p.order, 1);   // causal: low key blocks see the most queries
-  const bool remap = CAUSAL || p.order == 1;
+  const bool remap = CAUSAL || p.order != 0;
   const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hk = sgpr(remap ? bc.h : (int)blockIdx.y);
   const int kb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int group = p.H / p.Hkv;
@@ -961,7 +996,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
   u16x8 kf[KS], vf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    if (key < p.Sk) {
+    if (key < p.Sk && !(p.diag & 1)) {
       kf[ks] = *reinterpret_cast<const u16x8*>(Kp + (int64_t)key * p.k_ss + 16 * ks + 8 * h);
       vf[ks] = *reinterpret_cast<const u16x8*>(Vp + (int64_t)key * p.v_ss + 16 * ks + 8 * h);
     } else {
@@ -1027,8 +1062,210 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dkdv_v3_kernel(AttnParams p) {
     }
   }
   acc_fence();
-  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, key < p.Sk);
-  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, key < p.Sk);
+  const bool st = key < p.Sk && !(p.diag & 2);
+  store_row16<DT>(p.dk + b * p.dk_sb + hk * p.dk_sh + (int64_t)key * p.dk_ss, dk, p.scale, h, st);
+  store_row16<DT>(p.dv + b * p.dv_sb + hk * p.dv_sh + (int64_t)key * p.dv_ss, dv, 1.0f, h, st);
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK/dV, persistent (default where eligible; v3 above: PDT_FA_DKDV=3).  At the flagship shape a v3 workgroup computes ~9 query
+// tiles, and with one workgroup per CU (320 registers per lane) nothing overlaps its prologue (the K / V fragments
+// of its 128 keys from HBM, the first Q / dO tile) or its epilogue (the dK / dV stores): measured as a fixed cost
+// of 0.46 ms of the kernel's 1.41 ms (S 1024 vs 8192 at equal tokens, profiles/r5/r5h_attn_fixed_cost.txt).  Here
+// one workgroup per CU walks a stream of (key block, query tile) pairs across work items:
+//   * the tile ring continues across items -- the last tile of item i stages the first Q / dO tile of item i+1;
+//   * the next item's K / V fragments are loaded into a second register set during that last tile;
+//   * the dK / dV stores are buffer stores with a range-checked resource (rows past Sk dropped, no branch), so
+//     their count is fixed and the next item's first barrier waits with vmcnt(#stores) -- for everything issued
+//     before them -- instead of draining the stores too.
+// Items are dealt heavy-first (low key blocks see the most queries under the causal mask) in snake order.
+// ------------------------------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ void store_row16_rs(__amdgpu_buffer_rsrc_t rs, uint32_t row_byte, const f32x16 (&acc)[DT],
+                                               float scale, int h) {
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      unsigned a[2], c[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int g0 = 2 * pr, g1 = 2 * pr + 1;
+        a[k] = (unsigned)f2bf(acc[dt][4 * g0 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g0 + 2 * k + 1] * scale) << 16);
+        c[k] = (unsigned)f2bf(acc[dt][4 * g1 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g1 + 2 * k + 1] * scale) << 16);
+        const auto r = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+        a[k] = r[0];
+        c[k] = r[1];
+      }
+      u32x4 v;
+      v[0] = a[0]; v[1] = a[1]; v[2] = c[0]; v[3] = c[1];
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(row_byte + (uint32_t)(dt * 32 + 16 * pr + 8 * h) * 2u), 0, 0);
+    }
+}
+
+struct KvItem {
+  int b, hk, kb, qstart, qtiles, total;
+};
+
+template <int D, bool CAUSAL>
+__device__ __forceinline__ KvItem kv_item(const AttnParams& p, int j) {
+  const int bh = p.B * p.Hkv, group = p.H / p.Hkv, off = p.Sk - p.Sq;
+  KvItem it;
+  it.kb = sgpr(j / bh);
+  const int rest = j - it.kb * bh;
+  it.b = sgpr(rest / p.Hkv);
+  it.hk = sgpr(rest - it.b * p.Hkv);
+  it.qstart = CAUSAL ? max(0, it.kb * 128 - off) / TILE * TILE : 0;
+  it.qtiles = p.Sq > it.qstart ? (p.Sq - it.qstart + TILE - 1) / TILE : 0;
+  it.total = it.qtiles * group;
+  return it;
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_p_kernel(AttnParams p, int nitems) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D, NSTORE = 2 * 2 * DT;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];        // [buf][Q | dO]
+  __shared__ __attribute__((aligned(16))) bf16_t kvs[2][2 * TE];      // [K | V][128 key rows, two tile images]
+  __shared__ __attribute__((aligned(16))) float sstat[2][2][TILE];    // [buf][lse | delta]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int group = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * LOG2E;
+  auto item_of = [&](int r) { return r * G + ((r & 1) ? G - 1 - bid : bid); };   // snake over the heavy-first order
+
+  int r = 0;
+  const int j0 = item_of(0);
+  if (j0 >= nitems) return;
+  KvItem cur = kv_item<D, CAUSAL>(p, j0);
+
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+
+  DmaLane<D> lq, lg;
+  lq.init(p.q_ss, w, lane);
+  lg.init(p.do_ss, w, lane);
+  const uint32_t sm0 = lds_u32(smem), ss0 = lds_u32(&sstat[0][0][0]), kv0 = lds_u32(&kvs[0][0]);
+  auto issue = [&](const KvItem& it, int hi, int qi, int buf) {
+    const int q0 = sgpr(it.qstart + qi * TILE), hq = sgpr(it.hk * group + hi);
+    const uint32_t base = sm0 + (uint32_t)(buf * 2 * TE * 2);
+    lq.issue_at(p.q + it.b * p.q_sb + hq * p.q_sh, p.q_ss, q0, p.Sq, base, w);
+    lg.issue_at(p.dout + it.b * p.do_sb + hq * p.do_sh, p.do_ss, q0, p.Sq, base + TE * 2, w);
+    const uint32_t sb = ss0 + (uint32_t)(buf * 2 * TILE * 4);
+    if (w == 0)
+      dma_f32_row_at(p.delta + (int64_t)p.B * p.H * p.Sq + ((int64_t)it.b * p.H + hq) * p.Sq, q0, p.Sq, sb, lane);
+    if (w == 1) dma_f32_row_at(p.delta + ((int64_t)it.b * p.H + hq) * p.Sq, q0, p.Sq, sb + TILE * 4, lane);
+  };
+  // an item's 128 K and V rows into kvs (two tile images each; rows past Sk read 0 from the range check)
+  // (lane offsets computed here, once per item: no registers held for them across the tile loop)
+  auto issue_kv = [&](const KvItem& it) {
+    DmaLane<D> l;
+    const bf16_t* Kp = p.k + it.b * p.k_sb + it.hk * p.k_sh;
+    const bf16_t* Vp = p.v + it.b * p.v_sb + it.hk * p.v_sh;
+    l.init(p.k_ss, w, lane);
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+      l.issue_at(Kp, p.k_ss, it.kb * 128 + half * TILE, p.Sk, kv0 + (uint32_t)(half * TE * 2), w);
+    l.init(p.v_ss, w, lane);
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+      l.issue_at(Vp, p.v_ss, it.kb * 128 + half * TILE, p.Sk, kv0 + (uint32_t)((2 * TE + half * TE) * 2), w);
+  };
+  // this wave's 32 key rows: image w / 2, rows 32 (w % 2) + c32 (swizzle phase = c32's)
+  u16x8 kf[KS], vf[KS];
+  auto read_kv = [&]() {
+    const bf16_t* kb_ = &kvs[0][0] + (w >> 1) * TE + (w & 1) * 32 * D;
+    const bf16_t* vb_ = &kvs[1][0] + (w >> 1) * TE + (w & 1) * 32 * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *reinterpret_cast<const u16x8*>(kb_ + roff[ks]);
+      vf[ks] = *reinterpret_cast<const u16x8*>(vb_ + roff[ks]);
+    }
+  };
+  auto store_item = [&](const KvItem& it, const f32x16 (&dk_)[DT], const f32x16 (&dv_)[DT]) {
+    const int rows = min(128, p.Sk - it.kb * 128);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.dk + it.b * p.dk_sb + it.hk * p.dk_sh + (int64_t)it.kb * 128 * p.dk_ss), (short)0,
+        (int)(((int64_t)(rows - 1) * p.dk_ss + D) * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.dv + it.b * p.dv_sb + it.hk * p.dv_sh + (int64_t)it.kb * 128 * p.dv_ss), (short)0,
+        (int)(((int64_t)(rows - 1) * p.dv_ss + D) * 2), 0x00020000);
+    const int row = w * 32 + c32;
+    store_row16_rs<DT>(rk, (uint32_t)(row * p.dk_ss * 2), dk_, p.scale, h);
+    store_row16_rs<DT>(rv, (uint32_t)(row * p.dv_ss * 2), dv_, 1.0f, h);
+  };
+  // every item has >= 1 query tile: the host launches this kernel only for Sq, Sk > 0 (causal: the first query
+  // tile that sees key block kb starts below Sq for every kb < Sk / 128)
+
+  // prologue: the first item's K / V and first Q / dO tile
+  issue_kv(cur);
+  issue(cur, 0, 0, 0);
+  dma_barrier();
+  read_kv();
+
+  // The item loop is the outer loop; the tile loop inside it is v3's, unrolled by the 2-deep ring with the buffer
+  // a compile-time constant.  Every item has an EVEN number of query tiles (host condition: Sq, Sk multiples of 128
+  // and Sq == Sk under the causal mask), so each item starts on buffer 0 and the last tile (buffer 1) stages the
+  // next item's first tile into buffer 0.  The epilogue and the accumulator reset sit outside the tile loop.
+  bool first_item = true;
+  for (;;) {
+    f32x16 dk[DT], dv[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+    int iss_hi = 0, iss_qi = 1;        // next tile of this item to stage (tile 0 already is)
+    if (iss_qi == cur.qtiles) { iss_qi = 0; ++iss_hi; }
+    const int jn = item_of(r + 1);
+    const int kw = cur.kb * 128 + w * 32, key = kw + c32;
+    int cur_qi = 0;
+    for (int ct = 0; ct < cur.total; ct += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 0 && ct == 0) {
+          if (!first_item) {
+            // everything issued before the previous item's NSTORE dK / dV stores (this tile's DMA, this item's
+            // K / V rows) has landed; the stores themselves may still be in flight
+            vm_wait<NSTORE>();
+            __syncthreads();
+            read_kv();
+          }
+        } else {
+          dma_barrier();
+        }
+        if (ct + u + 1 < cur.total) {
+          issue(cur, iss_hi, iss_qi, 1 - u);
+          if (++iss_qi == cur.qtiles) { iss_qi = 0; ++iss_hi; }
+        } else if (jn < nitems) {
+          const KvItem nx = kv_item<D, CAUSAL>(p, jn);
+          issue(nx, 0, 0, 1 - u);        // the next item's first tile and K / V rows ride this tile's compute
+          issue_kv(nx);
+        }
+        const int q0 = sgpr(cur.qstart + cur_qi * TILE);
+        if (++cur_qi == cur.qtiles) cur_qi = 0;
+        if (CAUSAL && q0 + TILE - 1 + off < kw) continue;         // every query of the tile precedes these keys
+        const bf16_t* Qs = smem + u * 2 * TE;
+        const float* Ls = sstat[u][0];
+        const int tmask = CAUSAL ? key - off - q0 - 4 * h : -1;
+        const int tsq = p.Sq - q0 - 4 * h;
+        if (CAUSAL && (p.mask_all || kw + 31 - off - q0 > 0))
+          BwdKVTile<D, CAUSAL>::template run<true>(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2, tmask,
+                                                   tsq, h);
+        else
+          BwdKVTile<D, CAUSAL>::template run<false>(Qs, Qs + TE, Ls, Ls + TILE, kf, vf, roff, toff, dk, dv, sl2,
+                                                    tmask, tsq, h);
+      }
+    }
+    acc_fence();
+    store_item(cur, dk, dv);
+    if (jn >= nitems) return;
+    ++r;
+    cur = kv_item<D, CAUSAL>(p, jn);
+    first_item = false;
+  }
 }
 
 // dQ kernels: the per-element select inside every tile's softmax steps (1) or the dS post-mask on diagonal tiles
@@ -1135,7 +1372,7 @@ __global__ __launch_bounds__(NT, OCC) void fa_bwd_dq_v3_kernel(AttnParams p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
-  const bool remap = CAUSAL || p.order == 1;
+  const bool remap = CAUSAL || p.order != 0;
   const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
   const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int hk = sgpr(hq / (p.H / p.Hkv));
@@ -1230,7 +1467,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
   const BlockCoord bc = block_order(true, p.order, p.H / p.Hkv);
-  const bool remap = CAUSAL || p.order == 1;
+  const bool remap = CAUSAL || p.order != 0;
   const int b = sgpr(remap ? bc.b : (int)blockIdx.z), hq = sgpr(remap ? bc.h : (int)blockIdx.y);
   const int qb = sgpr(remap ? bc.t : (int)blockIdx.x);
   const int hk = sgpr(hq / (p.H / p.Hkv));
@@ -1257,7 +1494,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   u16x8 qf[KS], gf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < p.Sq) {
+    if (qrow < p.Sq && !(p.diag & 4)) {
       qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
       gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
     } else {
@@ -1266,7 +1503,7 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     }
   }
   const float nlse2 = qrow < p.Sq ? -p.lse[((int64_t)b * p.H + hq) * p.Sq + qrow] * LOG2E : -INFINITY;
-  const float dl = p.fuse_delta ? row_delta<KS>(p, gf, b, hq, qrow, h)
+  const float dl = (p.diag & 4) ? 0.f : p.fuse_delta ? row_delta<KS>(p, gf, b, hq, qrow, h)
                                 : (qrow < p.Sq ? p.delta[((int64_t)b * p.H + hq) * p.Sq + qrow] : 0.f);
   retire(qf);
   retire(gf);
@@ -1302,7 +1539,8 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
     }
     stage = stage + 1 == NBUF ? 0 : stage + 1;
   }
-  if (p.cs_q == nullptr) {
+  if (p.diag & 8) {
+  } else if (p.cs_q == nullptr) {
     store_row16<DT>(p.dq + b * p.dq_sb + hq * p.dq_sh + (int64_t)qrow * p.dq_ss, dq, p.scale, h, qrow < p.Sq);
   } else {
     float vals[DT * 16];
@@ -1330,6 +1568,28 @@ int block_order_mode(int B, int Hkv, int Sk, int D) {
   if (g_order >= 0) return g_order;
   const int64_t unit = (int64_t)Sk * D * 4, total = unit * B * Hkv;
   return (unit <= (1 << 20) && total > ((int64_t)384 << 20)) ? 1 : 0;
+}
+
+// dK/dV kernel: persistent (default where every item has an even tile count; flagship layer 1.41 -> 1.26 ms,
+// profiles/r5/r5m_dkdv_persistent_ab.txt) or v3 (PDT_FA_DKDV=3)
+int g_dkdv_variant = -1;
+int dkdv_items(const AttnParams& p) { return p.B * p.Hkv * ((p.Sk + 127) / 128); }
+bool dkdv_persistent(const AttnParams& p) {
+  if (g_dkdv_variant < 0) { const char* e = getenv("PDT_FA_DKDV"); g_dkdv_variant = e ? atoi(e) : 0; }
+  // every item must have an even number of query tiles (the kernel's ring parity): Sq, Sk multiples of 128, and
+  // Sq == Sk (no key / query offset) for the causal mask -- the shapes every model here runs
+  return g_dkdv_variant != 3 && p.Sq > 0 && p.Sq % 128 == 0 && p.Sk % 128 == 0 && p.Sq == p.Sk;
+}
+int dkdv_grid(const AttnParams& p) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      n = 256;
+    return n;
+  }();
+  const int n = dkdv_items(p);
+  return n < cus ? n : cus;        // one workgroup per CU (320 registers per lane: one wave per SIMD)
 }
 
 int fwd_variant() {
@@ -1378,9 +1638,14 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   AttnParams kv = p, qp = p;               // per-kernel block order (p.order bit 1: dK/dV, bit 2: dQ)
   kv.order = (p.order >> 1) & 1;
   qp.order = (p.order >> 2) & 1;
+  static const int cyc = [] { const char* e = getenv("PDT_FA_CYCLE"); return e ? atoi(e) : 0; }();
+  if (cyc & 2) kv.order = 2;
+  if (cyc & 4) qp.order = 2;
   kv.fuse_delta = 0;
   static const int mask_all = [] { const char* e = getenv("PDT_FA_MASK_ALL"); return e && atoi(e) != 0 ? 1 : 0; }();
   kv.mask_all = qp.mask_all = mask_all;
+  static const int diag = [] { const char* e = getenv("PDT_FA_DIAG"); return e ? atoi(e) : 0; }();
+  kv.diag = qp.diag = diag;
   static const bool fuse = [] { const char* e = getenv("PDT_FA_FUSE_DELTA"); return !e || atoi(e) != 0; }();
   qp.fuse_delta = fuse ? 1 : 0;
   if (!fuse) fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
@@ -1388,12 +1653,14 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
     if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
     else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
-    fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+    else fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
   } else {
     if (variant == 3) fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     else if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
     else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
-    fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+    else fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
   }
   return (int)hipGetLastError();
 }
@@ -1503,6 +1770,15 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
 PDT_API int pdt_flash_attn_set_order(int order) {
   if (order >= 0 || order == -2) g_order = order == -2 ? -1 : order;
   return g_order;
+}
+
+// dK/dV kernel: 4 persistent, 3 v3, 0 keeps, -1 restores the default; returns the setting
+PDT_API int pdt_flash_attn_set_dkdv(int v) {
+  (void)dkdv_items(AttnParams{});
+  if (g_dkdv_variant < 0) { const char* e = getenv("PDT_FA_DKDV"); g_dkdv_variant = e ? atoi(e) : 0; }
+  if (v > 0) g_dkdv_variant = v;
+  if (v == -1) g_dkdv_variant = 0;
+  return g_dkdv_variant;
 }
 
 // select kernel variants (0 keeps the current choice, -1 restores the default); returns fwd * 32 + bwd of the

@@ -313,6 +313,36 @@ def test_tuned_hipblaslt_linear_matches_torch(m, n, k, bias):
     assert rel_err(got, want) < 1e-2, rel_err(got, want)
 
 
+@pytest.mark.parametrize("B,S,H,Hkv,D", [(96, 1024, 16, 16, 128), (3, 512, 8, 2, 128), (4, 384, 4, 4, 64)])
+def test_persistent_dkdv_matches_v3(B, S, H, Hkv, D):
+    """The persistent dK/dV kernel (items streamed across one workgroup per CU, next item's K / V and first tile
+    staged under the current item's last tile, range-checked buffer stores) is bitwise equal to v3 -- the same
+    tile body in the same order per key block -- at the flagship shape, GQA, and head dim 64."""
+    from pytorch_distributedtraining_amd.ops import _lib
+    from pytorch_distributedtraining_amd.ops import attention as A
+    lib = _lib.require()
+    torch.manual_seed(B + S + H + D)
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    scale = D ** -0.5
+    o, lse = A._fwd(q, k, v, True, scale)
+    do = torch.randn_like(o)
+    outs = []
+    try:
+        for variant in (3, 4):
+            lib.pdt_flash_attn_set_dkdv(variant)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            dk.fill_(float("nan"))
+            dv.fill_(float("nan"))
+            A._bwd(q, k, v, o, lse, do, dq, dk, dv, True, scale)
+            outs.append((dq, dk, dv))
+    finally:
+        lib.pdt_flash_attn_set_dkdv(-1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_flash_attn_qkvpacked_matches_unpacked():
     from pytorch_distributedtraining_amd.ops import flash_attn, flash_attn_qkvpacked
     qkv = torch.randn(2, 300, 3, 4, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
