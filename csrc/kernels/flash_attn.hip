@@ -1317,11 +1317,16 @@ struct BwdQTile {
   // softmax steps of every tile; otherwise ``diag`` (wave-uniform: the tile crosses the causal diagonal or Sk)
   // masks the finished dS registers in three short branches -- the interior tiles issue no mask VALU at all and
   // the body stays ONE copy (a second unrolled body cost 20 % in instruction-cache misses)
-  template <bool MASK>
+  struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+  };
+  // after_a(): runs once the S / dP chains (the only readers of qf / gf) have issued -- the persistent kernel
+  // loads the next item's Q / dO rows into qf / gf there, under stages B and C
+  template <bool MASK, typename Hook = NoHook>
   __device__ __forceinline__ static void run(const bf16_t* Ks, const bf16_t* Vs, const u16x8 (&qf)[KS],
                                              const u16x8 (&gf)[KS], const int (&roff)[KS], const int (&toff)[DT][2],
                                              f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim,
-                                             bool diag = false) {
+                                             bool diag = false, const Hook& after_a = Hook()) {
     f32x16 s[2], dp[2];
     u16x8 df[2][2];
     const f32x16 z = zero16();
@@ -1338,6 +1343,7 @@ struct BwdQTile {
       ka = kn; va = vn;
       __builtin_amdgcn_sched_barrier(0);
     }
+    after_a();
     if (!MASK && diag) mask_ds<0, 16>(dp[0], 0, lim);
     df[0][0] = pack8(dp[0], 0); df[0][1] = pack8(dp[0], 1);
 #pragma unroll
@@ -1551,6 +1557,278 @@ __global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_v4_kernel(AttnParams p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// dQ, persistent (OPT-IN: PDT_FA_DQP=1 or pdt_flash_attn_set_dqp(1); v4 stays the default).  v4's workgroup loads
+// the Q / dO rows of its 256 queries (and the O rows for delta) in a prologue nothing overlaps -- 0.37 ms of the
+// kernel's 1.01 at the flagship shape (profiles/r5/r5h_attn_fixed_cost.txt).  Here one workgroup per CU walks
+// (batch, head, query block) items heavy-first in snake order: the K / V ring continues across items (the last
+// tile stages the next item's first tile), the next item's Q / dO rows load under the epilogue and the next ring
+// wait, its O rows DMA into LDS beside its first K / V tile (delta fused as in v4), and dQ leaves through
+// range-checked buffer stores whose count is fixed, so the next item's first ring wait leaves them in flight.
+// Measured at the flagship shape (profiles/r5/r5o_dq_persistent_ab.txt): 0.912 ms + the 0.171 ms delta pass with
+// delta unfused, 1.163 ms fused, against v4's 1.04-1.07 ms -- the hidden prologue is paid back in register
+// pressure (256 VGPRs, 16-34 spilled) -- so it stays opt-in.  Requires an even tile count per item: Sq a multiple
+// of 256 and Sq == Sk under the causal mask (4 (qb + 1) tiles), Sk a multiple of 128 otherwise.
+// ------------------------------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ void store_row16_vals_rs(__amdgpu_buffer_rsrc_t rs, uint32_t row_byte, const f32x16 (&acc)[DT],
+                                                    float scale, int h, bool ok, float (&v)[DT * 16]) {
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      unsigned a[2], c[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int g0 = 2 * pr, g1 = 2 * pr + 1;
+        a[k] = (unsigned)f2bf(acc[dt][4 * g0 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g0 + 2 * k + 1] * scale) << 16);
+        c[k] = (unsigned)f2bf(acc[dt][4 * g1 + 2 * k] * scale) | ((unsigned)f2bf(acc[dt][4 * g1 + 2 * k + 1] * scale) << 16);
+        const auto r = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+        a[k] = r[0];
+        c[k] = r[1];
+      }
+      u32x4 q;
+      q[0] = a[0]; q[1] = a[1]; q[2] = c[0]; q[3] = c[1];
+      __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(row_byte + (uint32_t)(dt * 32 + 16 * pr + 8 * h) * 2u), 0, 0);
+      const float m = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[(dt * 2 + pr) * 8 + 2 * k] = m * __uint_as_float(q[k] << 16);
+        v[(dt * 2 + pr) * 8 + 2 * k + 1] = m * __uint_as_float(q[k] & 0xffff0000u);
+      }
+    }
+}
+
+struct QItem {
+  int b, hq, hk, qb, ntiles;
+};
+
+template <bool CAUSAL>
+__device__ __forceinline__ QItem q_item(const AttnParams& p, int j, int nqb) {
+  const int bh = p.B * p.H, off = p.Sk - p.Sq;
+  QItem it;
+  const int rank = sgpr(j / bh);
+  const int rest = j - rank * bh;
+  it.qb = sgpr(nqb - 1 - rank);                       // heavy first: high query blocks see the most keys
+  it.b = sgpr(rest / p.H);
+  it.hq = sgpr(rest - it.b * p.H);
+  it.hk = it.hq / (p.H / p.Hkv);
+  const int kend = CAUSAL ? min(p.Sk, it.qb * 256 + 256 + off) : p.Sk;
+  it.ntiles = kend > 0 ? (kend + TILE - 1) / TILE : 0;
+  return it;
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(NT8, 1) void fa_bwd_dq_p_kernel(AttnParams p, int nitems, int nqb) {
+  constexpr int KS = D / 16, DT = D / 32, TE = TILE * D, NW = 8, NSTORE = 2 * DT;
+  using Dma = DmaLane<D, true, NW>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TE];   // [stage][K | V]
+  __shared__ __attribute__((aligned(16))) float csl[NW * D];         // column-sum scratch (the ring stays live)
+  __shared__ __attribute__((aligned(16))) bf16_t osm[4 * TE];        // the item's 256 O rows (fused delta)
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c32 = lane & 31;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * LOG2E;
+  auto item_of = [&](int r) { return r * G + ((r & 1) ? G - 1 - bid : bid); };
+
+  int r = 0;
+  const int j0 = item_of(0);
+  if (j0 >= nitems) return;
+  QItem cur = q_item<CAUSAL>(p, j0, nqb);
+
+  Dma lk, lv;
+  lk.init(p.k_ss, w, lane);
+  lv.init(p.v_ss, w, lane);
+  const uint32_t sm0 = lds_u32(smem);
+  auto issue = [&](const QItem& it, int t, int stage) {
+    const bf16_t* Kp = p.k + it.b * p.k_sb + it.hk * p.k_sh;
+    const bf16_t* Vp = p.v + it.b * p.v_sb + it.hk * p.v_sh;
+    const uint32_t base = sm0 + (uint32_t)(stage * 2 * TE * 2);
+    lk.issue_at(Kp, p.k_ss, t * TILE, p.Sk, base, w);
+    lv.issue_at(Vp, p.v_ss, t * TILE, p.Sk, base + TE * 2, w);
+  };
+  // the item's O rows -> osm (4 swizzled 64-row tiles, as K / V): issued beside the item's first K / V tile, so
+  // the wait that lands that tile lands them too and no register holds them across the previous epilogue
+  // (prefetching them into registers there spilled 92)
+  const uint32_t os0 = lds_u32(osm);
+  Dma lo;   // its lane offsets carry O's row stride (a packed projection's K rows are 3x longer)
+  lo.init(p.o_ss, w, lane);
+  auto issue_o = [&](const QItem& it) {
+    if (!p.fuse_delta) return;
+    const bf16_t* Op = p.o + it.b * p.o_sb + it.hq * p.o_sh;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lo.issue_at(Op, p.o_ss, it.qb * 256 + i * TILE, p.Sq, os0 + (uint32_t)(i * TE * 2), w);
+  };
+  u16x8 qf[KS], gf[KS];
+  // this lane's query row of item it: Q / dO fragments and, for the fused delta, the natural lse (rows past Sq:
+  // zeros / +inf); with the separate delta pass, -lse*log2(e) and delta straight from it
+  // (returns {-lse*log2(e), delta or 0}: values, not captured references -- written through the lambdas'
+  // references they lived in scratch and every tile reloaded them)
+  auto load_rows = [&](const QItem& it) -> float2 {
+    const int qrow = it.qb * 256 + w * 32 + c32;
+    const bool ok = qrow < p.Sq;
+    const bf16_t* Qp = p.q + it.b * p.q_sb + it.hq * p.q_sh;
+    const bf16_t* Gp = p.dout + it.b * p.do_sb + it.hq * p.do_sh;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ok) {
+        qf[ks] = *reinterpret_cast<const u16x8*>(Qp + (int64_t)qrow * p.q_ss + 16 * ks + 8 * h);
+        gf[ks] = *reinterpret_cast<const u16x8*>(Gp + (int64_t)qrow * p.do_ss + 16 * ks + 8 * h);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { qf[ks][k] = 0; gf[ks][k] = 0; }
+      }
+    }
+    const int64_t ri = ((int64_t)it.b * p.H + it.hq) * p.Sq + qrow;
+    if (p.fuse_delta) return make_float2(ok ? -p.lse[ri] * LOG2E : -INFINITY, 0.f);
+    // the delta pass stored -lse * log2(e)
+    return make_float2(ok ? p.delta[(int64_t)p.B * p.H * p.Sq + ri] : -INFINITY, ok ? p.delta[ri] : 0.f);
+  };
+  int roff[KS];
+  const int F = swz_f<D>(c32);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = c32 * D + (((2 * ks + h) ^ F) << 3);
+  int toff[DT][2];
+  tr_offsets<D>(lane, toff);
+
+  // fused delta = rowsum(dO * O) once osm has landed (rows past Sq: the DMA range check zero-filled them); the
+  // h == 0 lane hands delta and the log2-domain lse to the dK/dV kernel (as the per-item kernel's row_delta does)
+  auto finish_rows = [&](const QItem& it, float nlse2, float dl) -> float {
+    if (!p.fuse_delta) return dl;
+    const int qrow = it.qb * 256 + w * 32 + c32;
+    const bf16_t* Os = osm + w * 32 * D;   // this lane's row sits in 64-row tile w / 2, at row (w & 1) * 32 + c32
+    float acc = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 o = *reinterpret_cast<const u16x8*>(Os + roff[ks]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += bf2f(o[e]) * bf2f(gf[ks][e]);
+    }
+    acc += __shfl_xor(acc, 32, 64);
+    if (qrow < p.Sq && h == 0) {
+      const int64_t idx = ((int64_t)it.b * p.H + it.hq) * p.Sq + qrow;
+      p.delta[idx] = acc;
+      p.delta[(int64_t)p.B * p.H * p.Sq + idx] = nlse2;
+    }
+    return acc;
+  };
+
+  issue(cur, 0, 0);
+  issue_o(cur);
+  float2 rl = load_rows(cur);
+  float nlse2 = rl.x, dl = rl.y;
+  bool first_item = true;
+  for (;;) {
+    f32x16 dq[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dq[dt] = zero16();
+    const int jn = item_of(r + 1);
+    const bool more = jn < nitems;
+    const QItem nx = q_item<CAUSAL>(p, more ? jn : j0, nqb);
+    const int q0 = cur.qb * 256, qw = q0 + w * 32, qrow = qw + c32;
+    const int lim0 = min(p.Sk - 1, CAUSAL ? qrow + off : p.Sk - 1) - 4 * h;
+    for (int t = 0; t < cur.ntiles; t += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tt = t + u;
+        if (tt == 0) {
+          // everything issued before the previous item's dQ / column-sum stores has landed (this tile's DMA, the
+          // O rows, this item's Q / dO rows); the stores may still be in flight.  osm is read here and
+          // overwritten at the LAST tile's issue: ntiles >= 2 (Sq % 256 == 0, Sk % 128 == 0), so a barrier of a
+          // later tile separates every wave's read from that DMA
+          if (first_item) vm_wait<0>();
+          else if (w < 2 && p.cs_q != nullptr) vm_wait<NSTORE + 1>();   // + the column-sum partial store
+          else vm_wait<NSTORE>();
+          __syncthreads();
+          dl = finish_rows(cur, nlse2, dl);
+        } else {
+          vm_wait<0>();
+          __syncthreads();
+        }
+        const bool last = tt + 1 == cur.ntiles;
+        if (!last) issue(cur, tt + 1, 1 - u);
+        else if (more) { issue(nx, 0, 1 - u); issue_o(nx); }
+        const int k0 = tt * TILE;
+        if (!(CAUSAL && k0 > qw + 31 + off)) {
+          const bf16_t* Ks = smem + u * 2 * TE;
+          const bool diag = (k0 + TILE > p.Sk) || (CAUSAL && k0 + TILE - 1 > qw + off);
+          BwdQTile<D, CAUSAL>::template run<false>(Ks, Ks + TE, qf, gf, roff, toff, dq, sl2, nlse2, dl, lim0 - k0,
+                                                   diag);
+        }
+      }
+    }
+    // the next item's Q / dO rows load under the epilogue (loading them right after the last tile's S / dP chains
+    // kept them live beside stages B / C: 191 spilled registers)
+    if (more) rl = load_rows(nx);
+    // epilogue: dQ rows (buffer stores: rows past Sq dropped by the range check) + this item's column sums, one
+    // 32-column block (dt) at a time so only 16 values per lane are live beside the prefetched qf / gf
+    {
+      const int rows = min(256, p.Sq - q0);
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.dq + cur.b * p.dq_sb + cur.hq * p.dq_sh + (int64_t)q0 * p.dq_ss), (short)0,
+          (int)(((int64_t)(rows - 1) * p.dq_ss + D) * 2), 0x00020000);
+      const uint32_t row_byte = (uint32_t)((w * 32 + c32) * p.dq_ss * 2);
+      const bool cs = p.cs_q != nullptr;
+      const float m = qrow < p.Sq ? 1.f : 0.f;
+      if (cs) lds_barrier();              // every wave is past its last read of csl (previous item)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float v[16];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          unsigned a[2], c[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int g0 = 2 * pr, g1 = 2 * pr + 1;
+            a[k] = (unsigned)f2bf(dq[dt][4 * g0 + 2 * k] * p.scale) |
+                   ((unsigned)f2bf(dq[dt][4 * g0 + 2 * k + 1] * p.scale) << 16);
+            c[k] = (unsigned)f2bf(dq[dt][4 * g1 + 2 * k] * p.scale) |
+                   ((unsigned)f2bf(dq[dt][4 * g1 + 2 * k + 1] * p.scale) << 16);
+            const auto rr = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+            a[k] = rr[0];
+            c[k] = rr[1];
+          }
+          u32x4 qv;
+          qv[0] = a[0]; qv[1] = a[1]; qv[2] = c[0]; qv[3] = c[1];
+          __builtin_amdgcn_raw_buffer_store_b128(qv, rq, (int)(row_byte + (uint32_t)(dt * 32 + 16 * pr + 8 * h) * 2u),
+                                                 0, 0);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[pr * 8 + 2 * k] = m * __uint_as_float(qv[k] << 16);
+            v[pr * 8 + 2 * k + 1] = m * __uint_as_float(qv[k] & 0xffff0000u);
+          }
+        }
+        if (cs) {
+          // sum over the 32 rows of this half-wave: reduce-scatter 16 -> 1 value per lane (masks 16..2), then the
+          // xor-1 partner; lane c32 then holds value index c32 >> 1 = column dt*32 + 8h + (i & 7) + 16 (i >> 3)
+          colsum32_step<16, 16, 16>(v, c32);
+          v[0] += __shfl_xor(v[0], 1, 64);
+          if (!(c32 & 1)) {
+            const int i = c32 >> 1;
+            csl[w * D + dt * 32 + 8 * h + (i & 7) + 16 * (i >> 3)] = v[0];
+          }
+        }
+      }
+      if (cs) {
+        lds_barrier();
+        if ((int)threadIdx.x < D) {
+          float t = 0.f;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) t += csl[q * D + threadIdx.x];
+          p.cs_q[((int64_t)cur.b * nqb + cur.qb) * p.H * D + cur.hq * D + threadIdx.x] = t;
+        }
+      }
+    }
+    if (!more) return;
+    ++r;
+    cur = nx;
+    nlse2 = rl.x;
+    dl = rl.y;
+    first_item = false;
+  }
+}
+
 // kernel-variant selection: PDT_FA_FWD / PDT_FA_BWD env at first use, or pdt_flash_attn_set_variant()
 int g_fwd_variant = -1, g_bwd_variant = -1, g_order = -1;
 // block order bitmask (bit 0 forward, bit 1 dK/dV, bit 2 dQ): PDT_FA_ORDER / pdt_flash_attn_set_order, else
@@ -1569,6 +1847,15 @@ int block_order_mode(int B, int Hkv, int Sk, int D) {
   const int64_t unit = (int64_t)Sk * D * 4, total = unit * B * Hkv;
   return (unit <= (1 << 20) && total > ((int64_t)384 << 20)) ? 1 : 0;
 }
+
+// dQ kernel: persistent (opt-in, PDT_FA_DQP=1) or the dQ variant below (default)
+int g_dqp = -1;
+bool dq_persistent(const AttnParams& p, int causal) {
+  if (g_dqp < 0) { const char* e = getenv("PDT_FA_DQP"); g_dqp = e ? atoi(e) : 0; }
+  if (!g_dqp || p.Sq <= 0 || p.Sq % 256 != 0) return false;
+  return causal ? p.Sq == p.Sk : p.Sk % 128 == 0;
+}
+int dq_items(const AttnParams& p) { return p.B * p.H * (p.Sq / 256); }
 
 // dK/dV kernel: persistent (default where every item has an even tile count; flagship layer 1.41 -> 1.26 ms,
 // profiles/r5/r5m_dkdv_persistent_ab.txt) or v3 (PDT_FA_DKDV=3)
@@ -1647,8 +1934,23 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
   static const int diag = [] { const char* e = getenv("PDT_FA_DIAG"); return e ? atoi(e) : 0; }();
   kv.diag = qp.diag = diag;
   static const bool fuse = [] { const char* e = getenv("PDT_FA_FUSE_DELTA"); return !e || atoi(e) != 0; }();
+  const bool dqp = dq_persistent(p, causal) && bwd_variant(D) == 9;
   qp.fuse_delta = fuse ? 1 : 0;
-  if (!fuse) fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
+  if (!qp.fuse_delta) fa_bwd_delta_kernel<D><<<(rows * (D / 8) + NT - 1) / NT, NT, 0, st>>>(p);
+  if (dqp) {
+    const int n = dq_items(p);
+    const int g = n < dkdv_grid(p) ? n : dkdv_grid(p);
+    if (causal) fa_bwd_dq_p_kernel<D, true><<<g, NT8, 0, st>>>(qp, n, p.Sq / 256);
+    else fa_bwd_dq_p_kernel<D, false><<<g, NT8, 0, st>>>(qp, n, p.Sq / 256);
+    if (causal) {
+      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+      else fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
+    } else {
+      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+      else fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
+    }
+    return (int)hipGetLastError();
+  }
   if (causal) {
     if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
@@ -1770,6 +2072,16 @@ PDT_API int pdt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
 PDT_API int pdt_flash_attn_set_order(int order) {
   if (order >= 0 || order == -2) g_order = order == -2 ? -1 : order;
   return g_order;
+}
+
+// dQ kernel: 1 persistent where eligible, 2 the dQ variant of pdt_flash_attn_set_variant, -1 restores the
+// default; returns the setting
+PDT_API int pdt_flash_attn_set_dqp(int v) {
+  if (g_dqp < 0) { const char* e = getenv("PDT_FA_DQP"); g_dqp = e ? atoi(e) : 0; }
+  if (v == 1) g_dqp = 1;
+  if (v == 2) g_dqp = 0;
+  if (v == -1) { const char* e = getenv("PDT_FA_DQP"); g_dqp = e ? atoi(e) : 0; }
+  return g_dqp;
 }
 
 // dK/dV kernel: 4 persistent, 3 v3, 0 keeps, -1 restores the default; returns the setting

@@ -79,6 +79,7 @@ _SIGS = {
                            c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "pdt_flash_attn_colsum_ws_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "pdt_flash_attn_set_dkdv": [c_int],
+    "pdt_flash_attn_set_dqp": [c_int],
     "pdt_flash_attn_set_variant": [c_int, c_int],
     "pdt_flash_attn_set_order": [c_int],
     "pdt_win_attn_grid": [c_int],

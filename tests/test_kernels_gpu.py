@@ -343,6 +343,46 @@ def test_persistent_dkdv_matches_v3(B, S, H, Hkv, D):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal", [(96, 1024, 16, 16, 128, True), (3, 512, 8, 2, 128, True),
+                                                 (2, 512, 4, 4, 64, True), (2, 256, 4, 4, 128, False)])
+def test_persistent_dq_matches_v4(B, S, H, Hkv, D, causal):
+    """The persistent dQ kernel (items streamed per CU, the K / V ring across items, the next item's Q / dO rows
+    loaded under the epilogue, O rows DMA'd to LDS for the fused delta) against the one-workgroup-per-item dQ
+    kernel: dQ, dK / dV (which read the delta rows the dQ kernel hands over) and the q part of the packed-projection
+    bias gradient, at the flagship shape, GQA, head dim 64 and full attention.  The packed cases give K rows 3x
+    O's stride.  Delta is summed in a different order: equal up to fp32 rounding."""
+    from pytorch_distributedtraining_amd.ops import _lib
+    from pytorch_distributedtraining_amd.ops import attention as A
+    lib = _lib.require()
+    torch.manual_seed(B + S + H + D)
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16) if H == Hkv else None
+    if qkv is not None:
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    else:
+        q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+        k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+        v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    scale = D ** -0.5
+    o, lse = A._fwd(q, k, v, causal, scale)
+    do = torch.randn_like(o)
+    outs = []
+    try:
+        for variant in (2, 1):
+            lib.pdt_flash_attn_set_dqp(variant)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            dq.fill_(float("nan"))
+            db = A._bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, bias_grad=H == Hkv)
+            outs.append((dq, dk, dv, db))
+    finally:
+        lib.pdt_flash_attn_set_dqp(-1)
+    (dq0, dk0, dv0, db0), (dq1, dk1, dv1, db1) = outs
+    assert not torch.isnan(dq1).any()
+    assert rel_err(dq1, dq0) < 2e-3, rel_err(dq1, dq0)
+    assert rel_err(dk1, dk0) < 2e-3 and rel_err(dv1, dv0) < 2e-3
+    if db0 is not None:
+        assert rel_err(db1, db0) < 2e-3, rel_err(db1, db0)
+
+
 def test_flash_attn_qkvpacked_matches_unpacked():
     from pytorch_distributedtraining_amd.ops import flash_attn, flash_attn_qkvpacked
     qkv = torch.randn(2, 300, 3, 4, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
