@@ -681,7 +681,7 @@ struct ItemOps {
 // results through the 32 KiB of LDS past the ring (4 rounds of 64 rows, full-row 16-byte stores) and the stores
 // drain under the next item's first K-steps (its first wait counts them: vmcnt(16 + stores)).
 // DIAG = 1 (diagnostic builds only, pdt_gemm_stamps_bf16): wave 0 stamps s_memtime at each item's start, after
-// its main loop and after its epilogue into p.aux_out (uint64 [item][8]: [3] = s_memrealtime at item start, [4..7] =
+// its main loop and after its epilogue into p.ws (uint64 [item][8]: [3] = s_memrealtime at item start, [4..7] =
 // the stamped loop's own phase stamps: start, prologue wait done, first K-step done, tail entry)
 // -- for the phase shares of an item, never for timing the production kernel.
 __device__ __forceinline__ uint64_t stamp() {
@@ -804,6 +804,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
                [vob1] "v"(vob1), [rd0] "v"(rd0), [rdx] "v"(rd1)                                                  \
                : PDT_KLOOP_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99")
 
+  // (Workgroups run their items in near lockstep, so their epilogues' stores arrive together; delaying phase groups
+  // of them by 6-24 us at start measured 1-4 % SLOWER on c_fc / c_proj, profiles/r5/r5p_gemm_stagger_ab.txt: the
+  // lockstep walk is what lets an XCD's workgroups share A / B panels in L2.)
   ItemOps<LAYOUT> cur;
   int item = blockIdx.x;
   cur.init(p, item, ntiles);
@@ -985,7 +988,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_asm_kernel(GemmArgs p) {
     if (DIAG) {
       const uint64_t st2 = stamp();
       if (tid == 0) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(p.aux_out) + 8 * (int64_t)item;
+        uint64_t* d = reinterpret_cast<uint64_t*>(p.ws) + 8 * (int64_t)item;
         d[0] = st0; d[1] = st1; d[2] = st2; d[3] = rt0;
         for (int i = 0; i < 4; ++i) d[4 + i] = ((uint64_t)ph[2 * i + 1] << 32) | ph[2 * i];
       }
@@ -1203,18 +1206,34 @@ PDT_API int pdt_gemm2_bf16(int layout, int epi, const void* A, const void* B, vo
   return (int)hipGetLastError();
 }
 
+PDT_API int pdt_gemm_stamps_epi_bf16(int layout, int epi, const void* A, const void* B, void* C, int64_t M, int64_t N,
+                                     int64_t K, int64_t lda, int64_t ldb, const void* bias, void* aux_out,
+                                     void* stamps, hipStream_t s);
 // Instrumented build (results unchanged): the plain-epilogue kernel with phase stamps (DIAG above) into `stamps`
 // (uint64 [items][4]) -- scripts/gemm_stamps.py.
 PDT_API int pdt_gemm_stamps_bf16(int layout, const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
                                  int64_t lda, int64_t ldb, void* stamps, hipStream_t s) {
   if (!pdt_gemm_ok(layout, M, N, K, lda, ldb, 1) || K < 2 * KB || !stamps) return (int)hipErrorInvalidValue;
+  return pdt_gemm_stamps_epi_bf16(layout, E_PLAIN, A, B, C, M, N, K, lda, ldb, nullptr, nullptr, stamps, s);
+}
+
+// The same for the bias / GELU epilogues (NT only): bias [N], aux_out [M, N] (GELU's derivative)
+PDT_API int pdt_gemm_stamps_epi_bf16(int layout, int epi, const void* A, const void* B, void* C, int64_t M, int64_t N,
+                                     int64_t K, int64_t lda, int64_t ldb, const void* bias, void* aux_out,
+                                     void* stamps, hipStream_t s) {
+  if (!pdt_gemm_ok(layout, M, N, K, lda, ldb, 1) || K < 2 * KB || !stamps) return (int)hipErrorInvalidValue;
+  if (epi != E_PLAIN && (layout != L_NT || !bias || (epi == E_GELU && !aux_out) || (epi != E_BIAS && epi != E_GELU)))
+    return (int)hipErrorInvalidValue;
   GemmArgs a{};
-  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux_out = (bf16_t*)stamps;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.ws = (float*)stamps;
+  a.bias = (const bf16_t*)bias; a.aux_out = (bf16_t*)aux_out;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = N; a.k_per_split = (int)K;
   a.xpr = xcd_cut((int)(M / TM), (int)(N / TN));
   a.grp = xcd_grp((int)(M / TM), (int)(N / TN), (int)K, a.xpr);
   const dim3 grid(persist_grid((int)((M / TM) * (N / TN))), 1);
-  if (layout == L_NT) gemm_asm_kernel<L_NT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
-  else gemm_asm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
+  if (layout == L_TT) gemm_asm_kernel<L_TT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
+  else if (epi == E_BIAS) gemm_asm_kernel<L_NT, E_BIAS, 1><<<grid, NTH, 0, s>>>(a);
+  else if (epi == E_GELU) gemm_asm_kernel<L_NT, E_GELU, 1><<<grid, NTH, 0, s>>>(a);
+  else gemm_asm_kernel<L_NT, E_PLAIN, 1><<<grid, NTH, 0, s>>>(a);
   return (int)hipGetLastError();
 }

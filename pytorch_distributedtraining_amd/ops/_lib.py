@@ -142,6 +142,8 @@ _SIGS = {
                       c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_gemm_stamps_bf16": [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                              c_void_p, c_void_p],
+    "pdt_gemm_stamps_epi_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64,
+                                 c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_gemm2_bf16": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_syncbn_stats": [c_void_p, c_int64, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p],
