@@ -15,7 +15,7 @@ dev = torch.device("cuda")
 TOK = int(os.environ.get("TOK", str(96 * 1024)))
 
 
-def run(name, layout, M, N, K, epi=0):
+def run(name, layout, M, N, K, ek=0):
     if layout == 0:
         a = torch.randn(M, K, device=dev).bfloat16()
         b = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
@@ -28,10 +28,10 @@ def run(name, layout, M, N, K, epi=0):
     items = (M // 256) * (N // 256)
     st = torch.zeros(items, 8, dtype=torch.int64, device=dev)
     bias = torch.randn(N, device=dev).bfloat16()
-    aux = torch.empty_like(c) if epi == 2 else None
+    aux = torch.empty_like(c) if ek == 2 else None
     for _ in range(3):
-        _lib.call("pdt_gemm_stamps_epi_bf16", layout, epi, a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda,
-                  ldb, bias.data_ptr() if epi else None, aux.data_ptr() if aux is not None else None, st.data_ptr(),
+        _lib.call("pdt_gemm_stamps_epi_bf16", layout, ek, a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda,
+                  ldb, bias.data_ptr() if ek else None, aux.data_ptr() if aux is not None else None, st.data_ptr(),
                   _lib.stream_handle(dev))
     torch.cuda.synchronize()
     s = st.cpu().double()
@@ -62,7 +62,7 @@ def run(name, layout, M, N, K, epi=0):
     out_ph = {"pre_asm_cyc": med(pre), "prologue_wait_cyc_first_item": med(pro, ~later),
               "prologue_wait_cyc_later_items": med(pro, later), "kstep0_cyc": med(k0),
               "kstep0_cyc_later_items": med(k0, later), "steady_kstep_cyc": med(mid), "tail_kstep_cyc": med(tail)}
-    out = {"case": name, "epi": epi, "shape": [M, N, K], "items": items, "k_steps": T, **out_ph,
+    out = {"case": name, "epi": ek, "shape": [M, N, K], "items": items, "k_steps": T, **out_ph,
            "loop_cyc_median": float(loop.median()), "loop_cyc_per_kstep": float(loop.median()) / T,
            "epi_cyc_median": float(epi.median()), "epi_cyc_p90": float(epi.quantile(0.9)),
            "gap_cyc_median": float(torch.tensor(gaps).median()) if gaps else None, "clock_hz": clk}

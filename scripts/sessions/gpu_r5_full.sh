@@ -16,5 +16,8 @@ run() {  # name, seconds, cmd...
 run pytest_gpu 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
 run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $?
 run bench 500 python bench.py || exit $?
-run rocprof 500 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o bench --output-format csv -- python bench.py --steps 3 --warmup 1 --secondary 0 || exit $?
+run rocprof 500 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 3 --warmup 3 --secondary 0 --overlap-probe 0 || exit $?
+f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
+python3 scripts/trace_kernels.py "$f" --marker adamw_mt_kernel --last 3 --top 45 > $OUT/steady.txt && head -20 $OUT/steady.txt
+rm -f "$f"
 exit 0
