@@ -1122,7 +1122,7 @@ __device__ __forceinline__ KvItem kv_item(const AttnParams& p, int j) {
 }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_p_kernel(AttnParams p, int nitems) {
+__global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_p_kernel(AttnParams p, int nitems, int upr) {
   constexpr int KS = D / 16, DT = D / 32, TE = TILE * D, NSTORE = 2 * 2 * DT;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TE];        // [buf][Q | dO]
   __shared__ __attribute__((aligned(16))) bf16_t kvs[2][2 * TE];      // [K | V][128 key rows, two tile images]
@@ -1133,7 +1133,19 @@ __global__ __launch_bounds__(NT, 1) void fa_bwd_dkdv_p_kernel(AttnParams p, int 
   const int group = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   const float sl2 = p.scale * LOG2E;
-  auto item_of = [&](int r) { return r * G + ((r & 1) ? G - 1 - bid : bid); };   // snake over the heavy-first order
+  // upr == 0: snake over the heavy-first order (item j = kb * B * Hkv + unit).  upr > 0 (unit-local order): the
+  // nkb / 2 workgroups of one (batch, kv head) unit sit on one XCD (ids b, b + 8, ... share an XCD) and each runs
+  // key blocks kb = i and nkb - 1 - i of it back to back (causal: 16 - 2 i + 2 + 2 i query tiles, every pair the
+  // same), so the unit's key blocks stream its Q / dO tiles together out of that XCD's L2 instead of 256 unrelated
+  // streams from HBM; upr = units per XCD per round
+  const int nkb = (p.Sk + 127) / 128, bh = p.B * p.Hkv;
+  auto item_of = [&](int r) {
+    if (upr == 0) return r * G + ((r & 1) ? G - 1 - bid : bid);
+    const int loc = bid >> 3, pi = loc % (nkb >> 1), slot = loc / (nkb >> 1);
+    const int u = ((r >> 1) * upr + slot) * 8 + (bid & 7);
+    if (u >= bh) return nitems;
+    return ((r & 1) ? nkb - 1 - pi : pi) * bh + u;
+  };
 
   int r = 0;
   const int j0 = item_of(0);
@@ -1867,6 +1879,17 @@ bool dkdv_persistent(const AttnParams& p) {
   // Sq == Sk (no key / query offset) for the causal mask -- the shapes every model here runs
   return g_dkdv_variant != 3 && p.Sq > 0 && p.Sq % 128 == 0 && p.Sk % 128 == 0 && p.Sq == p.Sk;
 }
+// unit-local item order of the persistent dK/dV kernel (see fa_bwd_dkdv_p_kernel): units per XCD per round, or 0
+// for the snake order -- needs an even key-block count, a grid of whole XCD rows of pairs (G / 8 a multiple of
+// nkb / 2) and at least as many units as the grid hosts at once.  PDT_FA_DKDV_ORDER=0 forces the snake order.
+int dkdv_upr(const AttnParams& p, int grid) {
+  static const int forced = [] { const char* e = getenv("PDT_FA_DKDV_ORDER"); return e ? atoi(e) : -1; }();
+  if (forced == 0) return 0;
+  const int nkb = (p.Sk + 127) / 128, half = nkb / 2;
+  if (nkb < 2 || nkb % 2 || grid % 8 || (grid / 8) % half) return 0;
+  const int upr = (grid / 8) / half;
+  return p.B * p.Hkv >= 8 * upr ? upr : 0;
+}
 int dkdv_grid(const AttnParams& p) {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1943,10 +1966,10 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
     if (causal) fa_bwd_dq_p_kernel<D, true><<<g, NT8, 0, st>>>(qp, n, p.Sq / 256);
     else fa_bwd_dq_p_kernel<D, false><<<g, NT8, 0, st>>>(qp, n, p.Sq / 256);
     if (causal) {
-      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p), dkdv_upr(kv, dkdv_grid(p)));
       else fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
     } else {
-      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+      if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p), dkdv_upr(kv, dkdv_grid(p)));
       else fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
     }
     return (int)hipGetLastError();
@@ -1955,13 +1978,13 @@ int launch_bwd(const AttnParams& p, int causal, hipStream_t st) {
     if (variant == 3) fa_bwd_dq_v3_kernel<D, true><<<gq, NT, 0, st>>>(qp);
     else if (variant == 8) fa_bwd_dq_v4_kernel<D, true, 3><<<gq8, NT8, 0, st>>>(qp);
     else fa_bwd_dq_v4_kernel<D, true, 2><<<gq8, NT8, 0, st>>>(qp);
-    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, true><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p), dkdv_upr(kv, dkdv_grid(p)));
     else fa_bwd_dkdv_v3_kernel<D, true, 1><<<gkv, NT, 0, st>>>(kv);
   } else {
     if (variant == 3) fa_bwd_dq_v3_kernel<D, false><<<gq, NT, 0, st>>>(qp);
     else if (variant == 8) fa_bwd_dq_v4_kernel<D, false, 3><<<gq8, NT8, 0, st>>>(qp);
     else fa_bwd_dq_v4_kernel<D, false, 2><<<gq8, NT8, 0, st>>>(qp);
-    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p));
+    if (dkdv_persistent(p)) fa_bwd_dkdv_p_kernel<D, false><<<dkdv_grid(p), NT, 0, st>>>(kv, dkdv_items(p), dkdv_upr(kv, dkdv_grid(p)));
     else fa_bwd_dkdv_v3_kernel<D, false, 1><<<gkv, NT, 0, st>>>(kv);
   }
   return (int)hipGetLastError();

@@ -313,11 +313,14 @@ def test_tuned_hipblaslt_linear_matches_torch(m, n, k, bias):
     assert rel_err(got, want) < 1e-2, rel_err(got, want)
 
 
-@pytest.mark.parametrize("B,S,H,Hkv,D", [(96, 1024, 16, 16, 128), (3, 512, 8, 2, 128), (4, 384, 4, 4, 64)])
+@pytest.mark.parametrize("B,S,H,Hkv,D", [(96, 1024, 16, 16, 128), (3, 512, 8, 2, 128), (4, 384, 4, 4, 64),
+                                         (64, 512, 4, 4, 128), (64, 512, 8, 2, 64)])
 def test_persistent_dkdv_matches_v3(B, S, H, Hkv, D):
     """The persistent dK/dV kernel (items streamed across one workgroup per CU, next item's K / V and first tile
     staged under the current item's last tile, range-checked buffer stores) is bitwise equal to v3 -- the same
-    tile body in the same order per key block -- at the flagship shape, GQA, and head dim 64."""
+    tile body in the same order per key block -- at the flagship shape, GQA, and head dim 64.  The flagship and
+    the two B64 cases (a full round and two rounds of units on a 256-CU grid) run the unit-local item order
+    (paired key blocks of one unit per XCD), the others the snake order."""
     from pytorch_distributedtraining_amd.ops import _lib
     from pytorch_distributedtraining_amd.ops import attention as A
     lib = _lib.require()
