@@ -37,7 +37,7 @@ struct Plan {
 struct State {
   hipblasLtHandle_t handle = nullptr;
   void* ws = nullptr;
-  std::map<std::tuple<int, int, int64_t, int64_t, int64_t, int, int>, Plan> plans;
+  std::map<std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int>, Plan> plans;   // (..., C given)
 };
 
 std::mutex g_mu;
@@ -118,11 +118,13 @@ int build(Plan& p, hipblasLtHandle_t h, int epi, int trans, int64_t m, int64_t n
   return 0;
 }
 
+// C (optional, same layout as D, never D itself): D = op(A) op(B) + C, the accumulate input read in the kernel's
+// epilogue (beta = 1) -- a residual stream added where the GEMM writes its output
 int run(State& s, Plan& p, const hipblasLtMatmulAlgo_t& algo, size_t ws, const void* A, const void* B, void* D,
-        hipStream_t st) {
-  const float alpha = 1.f, beta = 0.f;
-  return hipblasLtMatmul(s.handle, p.desc, &alpha, A, p.a, B, p.b, &beta, D, p.d, D, p.d, &algo, s.ws, ws, st) ==
-                 HIPBLAS_STATUS_SUCCESS ? 0 : -4;
+        hipStream_t st, const void* C = nullptr) {
+  const float alpha = 1.f, beta = C ? 1.f : 0.f;
+  return hipblasLtMatmul(s.handle, p.desc, &alpha, A, p.a, B, p.b, &beta, C ? C : D, p.d, D, p.d, &algo, s.ws, ws,
+                         st) == HIPBLAS_STATUS_SUCCESS ? 0 : -4;
 }
 
 }  // namespace
@@ -131,13 +133,15 @@ int run(State& s, Plan& p, const hipblasLtMatmulAlgo_t& algo, size_t ws, const v
 // row-major mapping.  bias: epilogue 1/2 input [m], epilogue 3 output (bias gradient) [m].  aux: epilogue 2
 // output / epilogue 3 input, same layout as D.  Returns 0, a hipError_t, or a negative hipBLASLt code
 // (-3: no algorithm for this epilogue/type combination -- the caller falls back to separate kernels).
-PDT_API int pdt_lt_matmul(int epilogue, int trans, int64_t m, int64_t n, int64_t k, const void* A, const void* B,
-                          void* D, void* bias, int bias_dt, void* aux, int io_dt, int tune, hipStream_t st) {
+static int lt_matmul_impl(int epilogue, int trans, int64_t m, int64_t n, int64_t k, const void* A, const void* B,
+                          const void* C, void* D, void* bias, int bias_dt, void* aux, int io_dt, int tune,
+                          hipStream_t st) {
   std::lock_guard<std::mutex> g(g_mu);
   int err = 0;
   State* s = state_for_device(err);
   if (!s) return err ? err : -1;
-  const auto key = std::make_tuple(epilogue, trans, m, n, k, io_dt, bias_dt);
+  if (C && (C == D || (epilogue != 0 && epilogue != 1))) return (int)hipErrorInvalidValue;
+  const auto key = std::make_tuple(epilogue, trans, m, n, k, io_dt, bias_dt, C ? 1 : 0);
   auto it = s->plans.find(key);
   if (it == s->plans.end()) {
     Plan p;
@@ -164,9 +168,9 @@ PDT_API int pdt_lt_matmul(int epilogue, int trans, int64_t m, int64_t n, int64_t
     float best = 1e30f;
     for (auto& c : p.cands) {
       if (c.workspaceSize > WS_BYTES) continue;
-      if (run(*s, p, c.algo, c.workspaceSize, A, B, D, st)) continue;
+      if (run(*s, p, c.algo, c.workspaceSize, A, B, D, st, C)) continue;
       hipEventRecord(e0, st);
-      for (int r = 0; r < 3; ++r) run(*s, p, c.algo, c.workspaceSize, A, B, D, st);
+      for (int r = 0; r < 3; ++r) run(*s, p, c.algo, c.workspaceSize, A, B, D, st, C);
       hipEventRecord(e1, st);
       hipEventSynchronize(e1);
       float ms = 0.f;
@@ -181,9 +185,21 @@ PDT_API int pdt_lt_matmul(int epilogue, int trans, int64_t m, int64_t n, int64_t
     hipEventDestroy(e1);
     p.tuned = true;
   }
-  const int rc = run(*s, p, p.algo, p.ws, A, B, D, st);
+  const int rc = run(*s, p, p.algo, p.ws, A, B, D, st, C);
   if (rc) return rc;
   return (int)hipGetLastError();
+}
+
+PDT_API int pdt_lt_matmul(int epilogue, int trans, int64_t m, int64_t n, int64_t k, const void* A, const void* B,
+                          void* D, void* bias, int bias_dt, void* aux, int io_dt, int tune, hipStream_t st) {
+  return lt_matmul_impl(epilogue, trans, m, n, k, A, B, nullptr, D, bias, bias_dt, aux, io_dt, tune, st);
+}
+
+// The same with an accumulate input: D = op(A) op(B) (+ bias) + C, C a distinct buffer of D's layout (epilogue
+// 0 or 1 only) -- e.g. a projection GEMM that adds the residual stream as it writes.
+PDT_API int pdt_lt_matmul_c(int epilogue, int trans, int64_t m, int64_t n, int64_t k, const void* A, const void* B,
+                            const void* C, void* D, void* bias, int bias_dt, int io_dt, int tune, hipStream_t st) {
+  return lt_matmul_impl(epilogue, trans, m, n, k, A, B, C, D, bias, bias_dt, nullptr, io_dt, tune, st);
 }
 
 // Diagnostics: number of heuristic algorithms hipBLASLt offers for a combination (<0: descriptor error).

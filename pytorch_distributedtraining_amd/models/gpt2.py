@@ -22,7 +22,7 @@ import torch.nn as nn
 from ..ops import bias_gelu, cross_entropy, flash_attn_qkvpacked
 from ..ops.embedding import Embedding
 from ..ops.fp8 import fp8_enabled, fp8_gelu_mlp, fp8_gelu_mlp_ok, fp8_recompute_safe
-from ..ops.linear import Linear, gelu_mlp, gelu_mlp_ok, linear, linear_bias_gelu, linear_bias_gelu_ok
+from ..ops.linear import Linear, gelu_mlp, gelu_mlp_ok, linear, linear_bias_gelu, linear_bias_gelu_ok, linear_residual
 from ..ops.norms import LayerNorm
 
 
@@ -57,6 +57,18 @@ GPT2_CONFIGS = {
 
 # attention c_proj bias folded into ln_2's fused residual-add kernel (its gradient from the norm backward's pass)
 FOLD_PROJ_BIAS = os.environ.get("PDT_FOLD_PROJ_BIAS", "1") == "1"
+# residual adds in the projection GEMMs (hipBLASLt's accumulate input reads the stream in the epilogue): the norms
+# then read one stream and write one output instead of summing two (``ops.norms.norm_pass``).  Flagship shapes
+# (profiles/r5/r5u_resid_gemm_ab.txt): attention c_proj 604 -> 641 us, MLP c_proj 2,156 -> 2,152 us, each norm
+# 292 -> 178 us: 649.8 / 653.5 -> 646.9 / 649.0 ms per step.  PDT_RESID_GEMM=0 restores the norm-side adds.
+RESID_GEMM = os.environ.get("PDT_RESID_GEMM", "1") == "1"
+
+
+def _resid_mode(x, mlp) -> bool:
+    """Projection GEMMs add the residual stream (RESID_GEMM): bf16 on the GPU, the fused MLP path, no fp8."""
+    return (RESID_GEMM and FOLD_PROJ_BIAS and x.is_cuda and x.dtype == torch.bfloat16 and not fp8_enabled()
+            and not torch.is_autocast_enabled("cuda")
+            and gelu_mlp_ok(x, mlp.c_fc.weight, mlp.c_fc.bias, mlp.c_proj.weight, mlp.c_proj.bias))
 
 
 def gpt2_config(name: str, **overrides) -> GPT2Config:
@@ -73,15 +85,18 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = Linear(cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x, fold_bias: bool = False):
+    def forward(self, x, fold_bias: bool = False, residual=None):
         """Attention branch output; with ``fold_bias`` the pair (c_proj(y) without its bias, the bias) for a
         consumer that adds the bias itself (the block's fused residual-add + LayerNorm, whose backward then
-        returns the bias gradient from its own pass instead of a separate column sum over dY)."""
+        returns the bias gradient from its own pass instead of a separate column sum over dY); with ``residual``
+        the stream plus the branch, summed by the c_proj GEMM."""
         B, S, C = x.shape
         qkv = self.c_attn(x).view(B, S, 3, self.n_head, self.head_dim)
         # c_attn's bias gradient comes out of the attention backward kernels (per-workgroup column sums of the
         # dq / dk / dv rows they store), not from a separate pass over the [tokens, 3C] gradient
         y = flash_attn_qkvpacked(qkv, causal=True, bias_grad=self.c_attn.bias is not None).reshape(B, S, C)
+        if residual is not None:
+            return linear_residual(y, self.c_proj.weight, self.c_proj.bias, residual)
         if fold_bias:
             return self.c_proj.matmul(y), self.c_proj.bias
         return self.c_proj(y)
@@ -93,7 +108,9 @@ class MLP(nn.Module):
         self.c_fc = Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
+        if residual is not None:   # (the caller checked _resid_mode) + the stream, summed by the c_proj GEMM
+            return gelu_mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias, residual)
         if fp8_enabled():
             m1, m2 = self.c_fc._fp8_meta(x), self.c_proj._fp8_meta(x)
             if m1 is not None and m2 is not None and fp8_gelu_mlp_ok(x, self.c_fc.weight, self.c_fc.bias,
@@ -122,11 +139,17 @@ class GPT2Block(nn.Module):
     def forward(self, x, pending=None, pending_colsum=False):
         """(x, pending) -> (x', mlp_out): the residual adds are fused into the following LayerNorm
         kernels (``pending`` is the previous block's branch output not yet added to the stream;
-        ``pending_colsum``: it came from a biased Linear, whose bias gradient ln_1's backward sums)."""
+        ``pending_colsum``: it came from a biased Linear, whose bias gradient ln_1's backward sums).
+        RESID_GEMM mode: (x, None) -> (x'', None), the branch outputs added to the stream by the projection GEMMs
+        and the norms reading the summed stream (``pending`` None: x already holds the previous block's MLP)."""
         if pending is None:
-            h = self.ln_1(x)
+            h, x = self.ln_1.forward_pass(x, r_colsum=pending_colsum)
         else:
             h, x = self.ln_1.forward_add(x, pending, r_colsum=pending_colsum and FOLD_PROJ_BIAS)
+        if _resid_mode(h, self.mlp):
+            x = self.attn(h, residual=x)
+            y, x = self.ln_2.forward_pass(x, r_colsum=self.attn.c_proj.bias is not None)
+            return self.mlp(y, residual=x), None
         if FOLD_PROJ_BIAS:
             a, a_bias = self.attn(h, fold_bias=True)   # c_proj's bias joins the residual sum in ln_2's kernel
             y, x = self.ln_2.forward_add(x, a, a_bias)
@@ -194,7 +217,10 @@ class GPT2LMHeadModel(nn.Module):
             else:
                 x, pending = blk(x, pending, colsum)
         last = self._mlp_proj_bias[-1] and not fp8_enabled() and FOLD_PROJ_BIAS
-        x, _ = self.ln_f.forward_add(x, pending, r_colsum=last)
+        if pending is None:       # RESID_GEMM: the last MLP's c_proj already added its output to the stream
+            x, _ = self.ln_f.forward_pass(x, r_colsum=last)
+        else:
+            x, _ = self.ln_f.forward_add(x, pending, r_colsum=last)
         logits = linear(x, self.wte.weight)     # tied head (framework linear: transposed-layout dgrad)
         if labels is None:
             return logits

@@ -36,6 +36,8 @@ _SIGS = {
     "pdt_lt_probe": [c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, c_int],
     "pdt_lt_matmul": [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_int, c_int, c_void_p],
+    "pdt_lt_matmul_c": [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_int, c_int, c_int, c_void_p],
     "pdt_embedding_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_int64, c_void_p],
     "pdt_l2norm_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "pdt_clip_coef": [c_void_p, c_float, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],

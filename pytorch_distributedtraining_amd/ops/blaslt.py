@@ -35,6 +35,26 @@ def lt_matmul(epi: int, trans: int, m: int, n: int, k: int, a, b, d, bias=None) 
     return True
 
 
+def linear_residual(a2: torch.Tensor, w: torch.Tensor, bias, r2: torch.Tensor):
+    """a2 [M, K] @ w[N, K]^T (+ bias) + r2 [M, N] in ONE hipBLASLt GEMM (the residual read in its epilogue, beta =
+    1) into a new tensor, or None (no algorithm).  Column-major: D[N, M] = W^T(op T on col-major [K, N]) . A."""
+    m, k = a2.shape
+    n = w.shape[0]
+    d = torch.empty(m, n, dtype=a2.dtype, device=a2.device)
+    epi = EPI_BIAS if bias is not None else EPI_NONE
+    key = ("c", epi, m, n, k, d.dtype, None if bias is None else bias.dtype)
+    if key in _UNSUPPORTED:
+        return None
+    rc = _lib.require().pdt_lt_matmul_c(epi, 1, n, m, k, w.data_ptr(), a2.data_ptr(), r2.data_ptr(), d.data_ptr(),
+                                        _lib.ptr(bias), _lib.dtype_code(bias.dtype) if bias is not None else 0,
+                                        _lib.dtype_code(d.dtype), 1 if TUNE else 0, _lib.stream_handle(d.device))
+    if rc == -3:
+        _UNSUPPORTED.add(key)
+        return None
+    _lib.check(rc, "pdt_lt_matmul_c")
+    return d
+
+
 def wgrad_bgrad(dy2: torch.Tensor, x2: torch.Tensor):
     """(dW [N, K], db [N]) = (dY^T X, colsum dY) for contiguous bf16 dY [M, N], X [M, K] in ONE GEMM, or None."""
     m_rows, n = dy2.shape

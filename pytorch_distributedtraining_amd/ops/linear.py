@@ -384,6 +384,72 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+def _lin_residual_fwd(x2, w, b, r2):
+    """x2 W^T (+ b) + r2 in one hipBLASLt GEMM (C = r2), else the GEMM and an add."""
+    from .blaslt import linear_residual as _lt_residual
+    if x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and r2.dtype == torch.bfloat16 \
+            and (b is None or b.dtype == torch.bfloat16) and w.is_contiguous() and r2.is_contiguous():
+        d = _lt_residual(x2, w, b, r2)
+        if d is not None:
+            return d
+    return torch.addmm(r2, x2, w.t()) if b is None else F.linear(x2, w, b) + r2
+
+
+class _LinearResidualFn(torch.autograd.Function):
+    """out = x W^T (+ b) + r: the residual stream added by the GEMM that writes the projection (hipBLASLt's
+    accumulate input), so the following norm reads one stream instead of summing two.  Backward: dr = dout (the
+    same buffer), dW / dx as ``_LinearFn``, db from the following norm's pass (``take_bias_grad``) when it summed
+    it, else a column sum."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, r):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        base = x._base if x._base is not None else x
+        ctx.dx_colsum = bias is not None and getattr(base, "_pdt_dx_colsum", False)
+        n = weight.shape[0]
+        x2 = x.reshape(-1, x.shape[-1])
+        x2 = x2 if x2.is_contiguous() else x2.contiguous()
+        r2 = r.reshape(-1, n)
+        r2 = r2 if r2.is_contiguous() else r2.contiguous()
+        return _as_output(_lin_residual_fwd(x2, weight, bias, r2), (*x.shape[:-1], n))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            x2 = x2 if x2.is_contiguous() else x2.contiguous()
+            dw = _wgrad_result(w, dy2, x2)
+        if ctx.needs_input_grad[0]:
+            if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
+                dx = nt_matmul(dy2, transpose16(w))
+            else:
+                dx = torch.mm(dy2, w)
+            dx = dx.view(*dy.shape[:-1], w.shape[1])
+        if ctx.has_bias and (ctx.needs_input_grad[2] or ctx.dx_colsum):
+            dbf = take_bias_grad(dy2)
+            if dbf is None:
+                dbf = _colsum(dy2, torch.float32) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.float().sum(0)
+            db = dbf.to(w.dtype)
+            if ctx.dx_colsum and dx is not None:
+                stash_dx_colsum(dx, dbf.float() @ w.float())
+            if not ctx.needs_input_grad[2]:
+                db = None
+        return dx, dw, db, (dy if ctx.needs_input_grad[3] else None)
+
+
+def linear_residual(x, weight, bias, r):
+    """x W^T (+ bias) + r with the add in the GEMM (``_LinearResidualFn``); plain ops off the GPU path."""
+    if x.is_cuda and x.dtype == weight.dtype == r.dtype and x.dtype in (torch.bfloat16, torch.float32) \
+            and (bias is None or bias.dtype == x.dtype) and not torch.is_autocast_enabled("cuda"):
+        return _LinearResidualFn.apply(x, weight, bias, r)
+    return linear(x, weight, bias) + r
+
+
 FUSED_GELU = os.environ.get("PDT_FUSED_GELU", "1") == "1"
 
 
@@ -469,14 +535,19 @@ class _GeluMlpFn(torch.autograd.Function):
     pass (DGELU epilogue: a multiply by the kept derivative) -- no separate sweep over the [tokens, 4d] hidden."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, r=None):
         from . import gemm as G
         x2 = x.reshape(-1, x.shape[-1])
         x2 = x2 if x2.is_contiguous() and x2.data_ptr() % 16 == 0 else x2.contiguous()
         y1, d1 = G.gemm_nt_gelu(x2, w1, b1)
-        out = F.linear(y1, w2, b2)
+        if r is None:
+            out = F.linear(y1, w2, b2)
+        else:   # + the residual stream, added by the c_proj GEMM itself (``linear_residual``)
+            r2 = r.reshape(-1, w2.shape[0])
+            out = _lin_residual_fwd(y1, w2, b2, r2 if r2.is_contiguous() else r2.contiguous())
         ctx.save_for_backward(x2, w1, d1, y1, w2)
         ctx.xshape = x.shape
+        ctx.has_r = r is not None
         return _as_output(out, (*x.shape[:-1], w2.shape[0]))
 
     @staticmethod
@@ -500,11 +571,13 @@ class _GeluMlpFn(torch.autograd.Function):
             else:
                 dx = torch.mm(dpre, w1)
             dx = dx.view(*ctx.xshape)
-        return dx, dw1, (db1 if ctx.needs_input_grad[2] else None), dw2, db2
+        dr = dout if ctx.has_r and ctx.needs_input_grad[5] else None
+        return dx, dw1, (db1 if ctx.needs_input_grad[2] else None), dw2, db2, dr
 
 
-def gelu_mlp(x, w1, b1, w2, b2):
-    return _GeluMlpFn.apply(x, w1, b1, w2, b2)
+def gelu_mlp(x, w1, b1, w2, b2, residual=None):
+    """gelu_tanh(x W1^T + b1) W2^T + b2 (+ residual, added by the c_proj GEMM)."""
+    return _GeluMlpFn.apply(x, w1, b1, w2, b2, residual)
 
 
 def linear(x, weight, bias=None):

@@ -113,6 +113,42 @@ class _AddNormFn(torch.autograd.Function):
         return dx, dx, drb, dw, db, None, None, None
 
 
+class _NormPassFn(torch.autograd.Function):
+    """(y, x) = (norm(x), x): the residual stream passes through so that its LATER use's gradient ds comes back
+    here and is folded into dx by the same backward pass (no separate add over the stream); ``r_colsum``: x came
+    from a biased Linear that added the residual itself (``ops.linear.linear_residual``) -- the backward sums dx
+    per column in the same pass and stashes it as that Linear's bias gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, rms, r_colsum):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        x2 = x2 if x2.is_contiguous() else x2.contiguous()
+        y, mean, rstd, _ = _norm_fwd(x2, weight, bias, eps, rms)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.has_bias, ctx.rms, ctx.r_colsum = bias is not None, rms, r_colsum
+        return y.view(shape), x
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        x2, w, mean, rstd = ctx.saved_tensors
+        n = x2.shape[-1]
+        shape = dy.shape if dy is not None else ds.shape
+        dy2 = dy.reshape(-1, n).contiguous() if dy is not None else torch.zeros_like(x2)
+        ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
+        dx, dw, db, dcs = _norm_bwd(dy2, x2, w, mean, rstd, ctx.has_bias, ctx.rms, dres2=ds2, need_ds=ctx.r_colsum)
+        if ctx.r_colsum:
+            stash_bias_grad(dx, dcs)
+        return dx.view(shape), dw, db, None, None, None
+
+
+def norm_pass(x, weight, bias=None, eps=1e-5, rms=False, r_colsum=False):
+    """(norm(x), x) with the stream's later gradient folded into this norm's backward pass (``_NormPassFn``)."""
+    if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
+        return (rms_norm(x, weight, eps) if rms else layer_norm(x, weight, bias, eps)), x
+    return _NormPassFn.apply(x, weight, bias, eps, rms, bool(r_colsum))
+
+
 def add_norm(x, r, weight, bias=None, eps=1e-5, rms=False, r_bias=None, r_colsum=False):
     """Fused residual add + LayerNorm/RMSNorm: returns (norm(x + r + r_bias), x + r + r_bias); ``r_bias``
     (optional, [N], the norm's parameter dtype) is the bias of the Linear that produced r.  ``r_colsum``: r came
@@ -173,6 +209,10 @@ class LayerNorm(nn.Module):
     def forward_add(self, x, r, r_bias=None, r_colsum=False):
         """(LN(x + r + r_bias), x + r + r_bias) with one kernel pass (``add_norm``)."""
         return _ln_forward_add(self, x, r, rms=False, r_bias=r_bias, r_colsum=r_colsum)
+
+    def forward_pass(self, x, r_colsum=False):
+        """(LN(x), x) for a stream the producing GEMM already summed (``norm_pass``)."""
+        return norm_pass(x, self.weight, getattr(self, "bias", None), self.eps, False, r_colsum)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"

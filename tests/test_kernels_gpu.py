@@ -630,13 +630,18 @@ def test_resnet_ddp_bf16_compute_copy_keeps_batchnorm_fp32():
         assert abs(a - b) < 3e-2 * abs(b), losses
 
 
-def test_gpt2_every_grad_matches_fp32_reference():
+@pytest.mark.parametrize("resid", [False, True])
+def test_gpt2_every_grad_matches_fp32_reference(resid, monkeypatch):
     """Per-parameter gradients of the bf16 GPT-2 on the HIP kernels vs the fp32 torch model -- in particular the
     biases whose gradients come from fused passes: c_attn (attention backward column sums), attention c_proj
     (ln_2's residual-bias backward), MLP c_proj (the next ln_1 / ln_f backward's column sums, stashed for the
-    Linear), c_fc (bias-GELU backward)."""
+    Linear), c_fc (bias-GELU backward).  resid: the projection GEMMs add the residual stream (hipBLASLt's
+    accumulate input) and the norms pass the stream through (``norm_pass``), their backward folding the later
+    gradient in and summing the projection biases' gradients."""
     from pytorch_distributedtraining_amd.models import build_gpt2
+    from pytorch_distributedtraining_amd.models import gpt2 as G2
     from pytorch_distributedtraining_amd.ops import attention as A
+    monkeypatch.setattr(G2, "RESID_GEMM", resid)
     torch.manual_seed(0)
     ref = build_gpt2("gpt2-tiny", n_embd=256, n_head=2, n_layer=3)
     x = torch.randint(0, 512, (4, 129))
@@ -645,12 +650,44 @@ def test_gpt2_every_grad_matches_fp32_reference():
     m.load_state_dict(ref.state_dict())
     m = m.to(DEV).bfloat16()
     xd = x.to(DEV)
+    if resid:
+        h = m.wte(xd[:, :-1])
+        assert G2._resid_mode(h, m.h[0].mlp)                                 # the residual GEMM path runs
     m(xd[:, :-1], labels=xd[:, 1:]).backward()
     assert not [e for e in A._BIAS_GRADS.values() if e[0]() is not None]      # every stashed colsum consumed
     grads = dict(ref.named_parameters())
     for n, p in m.named_parameters():
         g, want = p.grad.float().cpu(), grads[n].grad
         assert rel_err(g, want) < 4e-2, (n, rel_err(g, want))
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_linear_residual_and_norm_pass_match_fp32(bias):
+    """linear_residual (x W^T + b + r in one hipBLASLt GEMM) and norm_pass ((LN(s), s) with the stream's later
+    gradient folded into the norm backward) against fp32 autograd, values and every gradient."""
+    from pytorch_distributedtraining_amd.ops.linear import linear_residual
+    from pytorch_distributedtraining_amd.ops.norms import norm_pass
+    torch.manual_seed(3)
+    M, K, N = 1024, 512, 768
+    x = torch.randn(M, K, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16().requires_grad_()
+    b = torch.randn(N, device=DEV).bfloat16().requires_grad_() if bias else None
+    r = torch.randn(M, N, device=DEV).bfloat16().requires_grad_()
+    g = (torch.rand(N, device=DEV) + 0.5).bfloat16().requires_grad_()
+    beta = torch.randn(N, device=DEV).bfloat16().requires_grad_()
+    s = linear_residual(x, w, b, r)
+    y, s2 = norm_pass(s, g, beta, 1e-5)
+    dy, ds = torch.randn_like(y), torch.randn_like(s2)
+    (y.float() * dy.float()).sum().add_((s2.float() * ds.float()).sum()).backward()
+    leaves = [x, w, r, g, beta] + ([b] if bias else [])
+    refs = [t.detach().float().requires_grad_() for t in leaves]
+    xr, wr, rr, gr, br = refs[:5]
+    sr = xr @ wr.t() + rr + (refs[5] if bias else 0)
+    yr = torch.nn.functional.layer_norm(sr, (N,), gr, br, 1e-5)
+    (yr * dy.float()).sum().add_((sr * ds.float()).sum()).backward()
+    assert rel_err(s, sr) < 1e-2 and rel_err(y, yr) < 2e-2
+    for t, tr in zip(leaves, refs):
+        assert rel_err(t.grad, tr.grad) < 2e-2, (t.shape, rel_err(t.grad, tr.grad))
 
 
 @pytest.mark.parametrize("layout", ["nchw", "nhwc"])
