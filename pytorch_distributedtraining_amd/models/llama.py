@@ -22,10 +22,11 @@ from ..ops import cross_entropy, rope_tables, swiglu
 from ..ops.attention import flash_attn_gqa_packed
 from ..ops.rope import apply_rope_qk_
 from ..ops.embedding import Embedding
-from ..ops.fp8 import fp8_recompute_safe
-from ..ops.linear import Linear
+from ..ops.fp8 import fp8_enabled, fp8_recompute_safe
+from ..ops.linear import Linear, linear_residual
 from ..ops.norms import RMSNorm, rms_norm
 from ..utils import recompute
+from . import gpt2 as _gpt2
 
 
 @dataclass
@@ -73,7 +74,7 @@ class Attention(nn.Module):
         self.wqkv = Linear(cfg.dim, (self.h + 2 * self.hkv) * self.d, bias=False)
         self.wo = Linear(self.h * self.d, cfg.dim, bias=False)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, cos, sin, residual=None):
         B, S, _ = x.shape
         qkv = apply_rope_qk_(self.wqkv(x), self.h, self.hkv, self.d, cos, sin)
         qkv = qkv.view(B, S, self.h + 2 * self.hkv, self.d)
@@ -85,6 +86,8 @@ class Attention(nn.Module):
         r = getattr(o, "_pdt_recipe", None)          # selective recompute: wo's saved input is the same forward
         if r is not None:
             recompute.tag(o2, r[0], r[1], view=lambda t: t.reshape(B, S, self.h * self.d))
+        if residual is not None:   # + the residual stream, added by the wo GEMM (ops.linear.linear_residual)
+            return linear_residual(o2, self.wo.weight, None, residual)
         return self.wo(o2)
 
 
@@ -94,10 +97,12 @@ class FeedForward(nn.Module):
         self.w13 = Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)
         self.w2 = Linear(cfg.ffn_dim, cfg.dim, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
         g = self.w13(x)
         a = swiglu(g)
         recompute.tag(a, recompute.Recipe(lambda: swiglu(g)))   # (only inside selective_recompute)
+        if residual is not None:
+            return linear_residual(a, self.w2.weight, None, residual)
         return self.w2(a)
 
 
@@ -111,7 +116,17 @@ class LlamaBlock(nn.Module):
 
     def forward(self, x, cos, sin, pending=None):
         """(x, pending) -> (x', ffn_out); residual adds fused into the next RMSNorm kernel.  Inside
-        ``utils.recompute.selective_recompute()`` the norm outputs are saved as recipes over the residual stream."""
+        ``utils.recompute.selective_recompute()`` the norm outputs are saved as recipes over the residual stream.
+        RESID_GEMM mode: (x, None) -> (x'', None), wo and w2 add their outputs to the stream in the GEMM and the
+        norms pass the summed stream through (``ops.norms.norm_pass``)."""
+        if _resid_mode(x):
+            h, x = self.attention_norm.forward_pass(x) if pending is None else \
+                self.attention_norm.forward_add(x, pending)
+            _tag_norm(h, x, self.attention_norm)
+            x = self.attention(h, cos, sin, residual=x)
+            y, x = self.ffn_norm.forward_pass(x)
+            _tag_norm(y, x, self.ffn_norm)
+            return self.feed_forward(y, residual=x), None
         if pending is None:
             h = self.attention_norm(x)
         else:
@@ -120,6 +135,12 @@ class LlamaBlock(nn.Module):
         y, x = self.ffn_norm.forward_add(x, self.attention(h, cos, sin))
         _tag_norm(y, x, self.ffn_norm)
         return x, self.feed_forward(y)
+
+
+def _resid_mode(x) -> bool:
+    """wo / w2 add the residual stream in their GEMMs (PDT_RESID_GEMM, models.gpt2): bf16 on the GPU, no fp8."""
+    return (_gpt2.RESID_GEMM and x.is_cuda and x.dtype == torch.bfloat16 and not fp8_enabled()
+            and not torch.is_autocast_enabled("cuda"))
 
 
 def _tag_norm(out, s, norm):

@@ -242,3 +242,7 @@ class RMSNorm(nn.Module):
 
     def forward_add(self, x, r, r_bias=None, r_colsum=False):
         return _ln_forward_add(self, x, r, rms=True, r_bias=r_bias, r_colsum=r_colsum)
+
+    def forward_pass(self, x, r_colsum=False):
+        """(RMSNorm(x), x) for a stream the producing GEMM already summed (``norm_pass``)."""
+        return norm_pass(x, self.weight, None, self.eps, True, r_colsum)
