@@ -37,6 +37,8 @@ for _ in range(it):
     if mode in ("all", "nt"):
         G.gemm_nt_gelu(x, w, b)          # c_fc forward + bias + GELU epilogue
         G.gemm_nt(dy, w2)                # c_proj forward (K = 8192)
+    if mode in ("all", "nt", "dgelu"):
+        G.gemm_nt_dgelu(x, w, dy)        # c_proj data gradient + GELU backward + c_fc bias gradient epilogue
     if mode in ("all", "lt"):
         torch.mm(x, w.t())               # c_fc forward on hipBLASLt
         torch.mm(dy, w2.t())             # c_proj forward on hipBLASLt
