@@ -72,6 +72,9 @@ _SIGS = {
     "pdt_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "pdt_transpose16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_ce_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_int, c_void_p],
+    "pdt_ce_fwd_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_int,
+                        c_void_p],
+    "pdt_ce_scale": [c_void_p, c_void_p, c_int64, c_int, c_int64, c_int, c_void_p],
     "pdt_ce_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int64, c_int64,
                    c_int, c_int, c_void_p],
     "pdt_flash_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

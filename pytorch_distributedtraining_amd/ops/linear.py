@@ -35,6 +35,8 @@ from .gemm import gemm_tt, tt_ok, tt_splits
 from .grad_slots import claim, is_sharded_param
 
 _WGRAD_CHUNK = 4096
+# PDT_DX_COLSUM_STASH=0: the attention backward sums dO itself instead of taking the consuming Linear's db W
+_DX_STASH = os.environ.get("PDT_DX_COLSUM_STASH", "1") == "1"
 
 
 # PDT_NT_HIP: "auto" (default: per shape, the hand NT GEMM where it timed >= 1 % faster than hipBLASLt on the shape's
@@ -364,12 +366,13 @@ class _LinearFn(torch.autograd.Function):
             if not x2.is_contiguous():
                 x2 = x2.contiguous()
             dw = _wgrad_result(w, dy2, x2)
+        dx2 = None
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
-                dx = nt_matmul(dy2, transpose16(w))
+                dx2 = nt_matmul(dy2, transpose16(w))
             else:
-                dx = torch.mm(dy2, w)
-            dx = dx.view(*dy.shape[:-1], w.shape[1])
+                dx2 = torch.mm(dy2, w)
+            dx = dx2.view(*dy.shape[:-1], w.shape[1])
         dbf = None
         if want_db:
             db = take_bias_grad(dy2)      # summed by the kernel that produced dY (flash attention's backward)
@@ -377,10 +380,12 @@ class _LinearFn(torch.autograd.Function):
                 dbf, db = db, db.to(w.dtype)
             else:
                 db = _colsum(dy2, w.dtype) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.sum(0).to(w.dtype)
-        if ctx.dx_colsum and dx is not None and db is not None:
-            # colsum(dX) = colsum(dY W) = db W: the attention backward's v-bias gradient without a pass over dX
+        if ctx.dx_colsum and _DX_STASH and dx is not None and db is not None:
+            # colsum(dX) = colsum(dY W) = db W: the attention backward's v-bias gradient without a pass over dX.
+            # Stashed on the GEMM's own output, not on the view returned: the engine drops the Python object of
+            # what a backward returns (a weak reference to it dies), the base's survives through the view
             dbf = dbf if dbf is not None and dbf.dtype == torch.float32 else db.float()
-            stash_dx_colsum(dx, dbf @ w.float())
+            stash_dx_colsum(dx2, dbf @ w.float())
         return dx, dw, db
 
 
@@ -419,24 +424,24 @@ class _LinearResidualFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
-        dx = dw = db = None
+        dx = dx2 = dw = db = None
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             x2 = x2 if x2.is_contiguous() else x2.contiguous()
             dw = _wgrad_result(w, dy2, x2)
         if ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
-                dx = nt_matmul(dy2, transpose16(w))
+                dx2 = nt_matmul(dy2, transpose16(w))
             else:
-                dx = torch.mm(dy2, w)
-            dx = dx.view(*dy.shape[:-1], w.shape[1])
+                dx2 = torch.mm(dy2, w)
+            dx = dx2.view(*dy.shape[:-1], w.shape[1])
         if ctx.has_bias and (ctx.needs_input_grad[2] or ctx.dx_colsum):
             dbf = take_bias_grad(dy2)
             if dbf is None:
                 dbf = _colsum(dy2, torch.float32) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.float().sum(0)
             db = dbf.to(w.dtype)
-            if ctx.dx_colsum and dx is not None:
-                stash_dx_colsum(dx, dbf.float() @ w.float())
+            if ctx.dx_colsum and _DX_STASH and dx2 is not None:   # (on the base: see _LinearFn)
+                stash_dx_colsum(dx2, dbf.float() @ w.float())
             if not ctx.needs_input_grad[2]:
                 db = None
         return dx, dw, db, (dy if ctx.needs_input_grad[3] else None)

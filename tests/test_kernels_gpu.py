@@ -126,6 +126,33 @@ def test_cross_entropy(V, dt):
     assert rel_err(x.grad, xr.grad) < (2e-2 if dt == torch.bfloat16 else 1e-4)
 
 
+@pytest.mark.parametrize("V,reduction,gscale", [(50304, "mean", 1.0), (50304, "mean", 2.5), (1000, "sum", 1.0),
+                                                (50304, "sum", 0.5), (128256, "mean", 1.0)])
+def test_cross_entropy_inplace_forward_gradient(V, reduction, gscale):
+    """inplace_backward on bf16 logits (the LM heads' call): where the row fits one workgroup's registers the
+    forward writes (softmax - onehot) [/ count] over the logits in its single read and the backward only applies a
+    non-unit upstream gradient -- loss and gradient against fp32 torch, ignore_index rows zero; Llama-3's
+    128,256-column vocabulary takes the two-pass path."""
+    from pytorch_distributedtraining_amd.ops import cross_entropy
+    torch.manual_seed(V)
+    base = (3 * torch.randn(300, V, device=DEV)).bfloat16()
+    t = torch.randint(0, V, (300,), device=DEV)
+    t[7] = -100
+    xr = base.float().requires_grad_()
+    lr = F.cross_entropy(xr, t, ignore_index=-100, reduction=reduction)
+    (lr * gscale).backward()
+    leaf = base.clone().requires_grad_()
+    x = leaf * 1.0                                  # a non-leaf logits buffer, as a model's head output
+    grads = []
+    x.register_hook(grads.append)
+    loss = cross_entropy(x, t, reduction=reduction, inplace_backward=True)
+    assert abs(loss.item() - lr.item()) < 2e-3 * max(1, abs(lr.item()))
+    (loss * gscale).backward()
+    g = grads[0]
+    assert rel_err(g, xr.grad) < 2e-2, rel_err(g, xr.grad)
+    assert float(g[7].float().abs().max()) == 0.0
+
+
 def _attn_ref(q, k, v, causal, scale):
     H, Hkv = q.shape[2], k.shape[2]
     qt, kt, vt = (t.float().transpose(1, 2) for t in (q, k, v))
@@ -399,11 +426,13 @@ def test_flash_attn_qkvpacked_matches_unpacked():
     assert torch.equal(qkv.grad, x.grad)
 
 
-def _check_qkv_bias_grad(db, g, do, H, Hkv):
+def _check_qkv_bias_grad(db, g, do, H, Hkv, v_rel=1e-5):
     """db = [q | k | v] bias gradient from the attention backward: q part = the column sums of the stored dq rows
     (g [rows, 3, H*D] the stored packed gradient), k part exactly 0 (the row softmax cancels a key bias), v part =
     the column sums of dO folded over each kv head's query heads (softmax rows sum to 1) -- which the column sums
-    of the stored (bf16-rounded) dv approximate."""
+    of the stored (bf16-rounded) dv approximate.  v_rel: when colsum(dO) came from the consuming Linear's stash
+    (db W in fp32, the exact product) rather than a pass over the bf16-rounded dO, the two differ by dO's
+    rounding summed over the rows (~0.3 % of the largest column here)."""
     hd = g.shape[-1]
     D = hd // H
     kvd = Hkv * D
@@ -412,7 +441,7 @@ def _check_qkv_bias_grad(db, g, do, H, Hkv):
     assert float((dbq - wq).abs().max()) <= 1e-5 * float(wq.abs().max()) + 1e-3
     assert torch.equal(dbk, torch.zeros_like(dbk))
     wv = do.float().sum(0).view(Hkv, H // Hkv, D).sum(1).reshape(-1)
-    assert float((dbv - wv).abs().max()) <= 1e-5 * float(wv.abs().max()) + 1e-3
+    assert float((dbv - wv).abs().max()) <= v_rel * float(wv.abs().max()) + 1e-3
     sv = g[:, 2, :kvd].float().sum(0)            # what the stored dv rows sum to: the same up to bf16 rounding
     assert float((dbv - sv).abs().max()) <= 2e-2 * float(sv.abs().max()) + 0.5
 
@@ -456,7 +485,7 @@ def test_attn_bias_grad_from_backward_kernels(D, S, B, bwd):
         assert not [e for e in A._DX_COLSUMS.values() if e[0]() is not None]     # taken by the attention
         db2 = A.take_bias_grad(gqkv[0].view(B * S, 3 * C))
         assert db2 is not None
-        _check_qkv_bias_grad(db2, gqkv[0].view(B * S, 3, C), gdo[0].reshape(B * S, C), H, H)
+        _check_qkv_bias_grad(db2, gqkv[0].view(B * S, 3, C), gdo[0].reshape(B * S, C), H, H, v_rel=1e-2)
         # end to end through a biased Linear: the stash is consumed, the bias gradient matches the column sum
         C = H * D
         lin = Linear(C, 3 * C).to(DEV).bfloat16()
@@ -653,8 +682,14 @@ def test_gpt2_every_grad_matches_fp32_reference(resid, monkeypatch):
     if resid:
         h = m.wte(xd[:, :-1])
         assert G2._resid_mode(h, m.h[0].mlp)                                 # the residual GEMM path runs
+    from pytorch_distributedtraining_amd.ops import activations as ACT
+    passes = []
+    orig = ACT._colsum
+    monkeypatch.setattr(ACT, "_colsum", lambda x, dt: passes.append(tuple(x.shape)) or orig(x, dt))
     m(xd[:, :-1], labels=xd[:, 1:]).backward()
     assert not [e for e in A._BIAS_GRADS.values() if e[0]() is not None]      # every stashed colsum consumed
+    if resid:   # colsum(dO) for the v-bias came from c_proj's stash (db W), no pass over dO (the norm-side add
+        assert not passes, passes   # path runs c_proj bias-free: the attention backward sums dO itself)
     grads = dict(ref.named_parameters())
     for n, p in m.named_parameters():
         g, want = p.grad.float().cpu(), grads[n].grad
