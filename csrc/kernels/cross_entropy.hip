@@ -181,10 +181,17 @@ __global__ __launch_bounds__(256) void ce_scale_kernel(T* __restrict__ g, const 
 PDT_API int pdt_ce_fwd_grad(void* logits, const int64_t* target, float* loss, float* lse, const float* inv_count,
                             int64_t rows, int V, int64_t ldl, int dt, int ignore_index, hipStream_t st) {
   if (rows <= 0) return 0;
-  // up to 65,536 columns (GPT-2's 50,304; a 1024-thread variant for Llama-3's 128,256 spilled at 128 VGPRs)
+  // up to 65,536 columns (GPT-2's 50,304; 16 slabs of 1,024 threads for Llama-3's 128,256 spilled at 128 VGPRs).
+  // 1,024 threads x 8 slabs (106 VGPRs: 16 waves per CU) or 512 x 16 (180 VGPRs: 8 waves); PDT_CE_FUSED_NTH
+  static const int nth = [] { const char* e = getenv("PDT_CE_FUSED_NTH"); return e ? atoi(e) : 1024; }();
   if (V % 8 || ldl % 8 || (reinterpret_cast<uintptr_t>(logits) & 15) || V > 512 * 8 * 16) return -1;
   if (dt != kBF16) return -1;   // fp32 logits: 2x the registers per element; the two-pass path
-  ce_fwd_grad_kernel<512, 16><<<rows, 512, 0, st>>>((bf16_t*)logits, target, loss, lse, inv_count, V, ldl, ignore_index);
+  if (nth == 512)
+    ce_fwd_grad_kernel<512, 16><<<rows, 512, 0, st>>>((bf16_t*)logits, target, loss, lse, inv_count, V, ldl,
+                                                       ignore_index);
+  else
+    ce_fwd_grad_kernel<1024, 8><<<rows, 1024, 0, st>>>((bf16_t*)logits, target, loss, lse, inv_count, V, ldl,
+                                                        ignore_index);
   return (int)hipGetLastError();
 }
 
