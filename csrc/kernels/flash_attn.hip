@@ -1329,16 +1329,11 @@ struct BwdQTile {
   // softmax steps of every tile; otherwise ``diag`` (wave-uniform: the tile crosses the causal diagonal or Sk)
   // masks the finished dS registers in three short branches -- the interior tiles issue no mask VALU at all and
   // the body stays ONE copy (a second unrolled body cost 20 % in instruction-cache misses)
-  struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
-  };
-  // after_a(): runs once the S / dP chains (the only readers of qf / gf) have issued -- the persistent kernel
-  // loads the next item's Q / dO rows into qf / gf there, under stages B and C
-  template <bool MASK, typename Hook = NoHook>
+  template <bool MASK>
   __device__ __forceinline__ static void run(const bf16_t* Ks, const bf16_t* Vs, const u16x8 (&qf)[KS],
                                              const u16x8 (&gf)[KS], const int (&roff)[KS], const int (&toff)[DT][2],
                                              f32x16 (&dq)[DT], float sl2, float nlse2, float dl, int lim,
-                                             bool diag = false, const Hook& after_a = Hook()) {
+                                             bool diag = false) {
     f32x16 s[2], dp[2];
     u16x8 df[2][2];
     const f32x16 z = zero16();
@@ -1355,7 +1350,6 @@ struct BwdQTile {
       ka = kn; va = vn;
       __builtin_amdgcn_sched_barrier(0);
     }
-    after_a();
     if (!MASK && diag) mask_ds<0, 16>(dp[0], 0, lim);
     df[0][0] = pack8(dp[0], 0); df[0][1] = pack8(dp[0], 1);
 #pragma unroll
