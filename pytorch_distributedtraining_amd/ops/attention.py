@@ -130,6 +130,12 @@ _DX_COLSUMS: dict = {}
 def _stash(table, grad, colsum):
     for key in [k for k, (ref, _, _) in table.items() if ref() is None]:
         del table[key]
+    # a backward's RETURNED tensor loses its Python object once the engine takes it (a weak reference to it dies
+    # before the consumer's backward runs); the base it views keeps its object, so hold that when it spans the
+    # same elements
+    base = grad._base
+    if base is not None and base.data_ptr() == grad.data_ptr() and base.numel() == grad.numel():
+        grad = base
     table[grad.untyped_storage().data_ptr()] = (weakref.ref(grad), colsum, grad._version)
 
 
