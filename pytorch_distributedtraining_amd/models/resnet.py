@@ -12,6 +12,8 @@ Written from the published architecture (He et al. 2015), random init.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -35,6 +37,12 @@ def conv1x1(cin, cout, stride=1, fused=False):
         return Conv2d1x1(cin, cout)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
+
+
+# the downsample blocks fork x too (PDT_RESNET_FORK_DS=1: their downsample conv's data gradient joins conv1's dgrad
+# GEMM as its C operand) -- measured 0.6-1 % SLOWER than autograd's separate add over those 4 block inputs
+# (9,217 / 9,169 vs 9,252 / 9,276 samples/s, profiles/r5/r5_resnet_fork_ds_ab.txt), so off by default
+FORK_DOWNSAMPLE = os.environ.get("PDT_RESNET_FORK_DS", "0") == "1"
 
 class BasicBlock(nn.Module):
     expansion = 1
@@ -74,9 +82,11 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        if self.fused and self.downsample is None and hasattr(self.conv1, "forward_fork"):
-            # conv1 and the identity share x: their two input gradients are summed inside conv1's dgrad GEMM
-            h, idt = self.conv1.forward_fork(x)
+        if self.fused and hasattr(self.conv1, "forward_fork") and (self.downsample is None or FORK_DOWNSAMPLE):
+            # conv1 and the identity (or the downsample branch) share x: their two input gradients are summed
+            # inside conv1's dgrad GEMM instead of by a separate add over the block input's gradient
+            h, xa = self.conv1.forward_fork(x)
+            idt = xa if self.downsample is None else self.downsample(xa)
             return self.bn3(self.conv3(self.bn2(self.conv2(self.bn1(h)))), residual=idt)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused:

@@ -1387,20 +1387,30 @@ def test_resnet50_fused_bn_matches_plain_model():
         assert rel_err(ga, gr) < 2 * rel_err(gb, gr) + 5e-2, name
 
 
-def test_resnet_bottleneck_fork_sums_identity_gradient_in_dgrad():
-    """Bottlenecks without downsample run conv1 + identity through one Function (the identity's input gradient
-    is the C operand of conv1's dgrad GEMM): gradients of the input and of every parameter vs fp32, with the
-    residual branch live (bn3 gamma != 0, unlike the zero-init default).  Three BNs deep, bf16 rounding alone
-    is several percent, so the bound is stock bf16 autocast's own error on the same block."""
-    from pytorch_distributedtraining_amd.models.resnet import Bottleneck
+@pytest.mark.parametrize("down", [False, True])
+def test_resnet_bottleneck_fork_sums_identity_gradient_in_dgrad(down, monkeypatch):
+    """Bottlenecks run conv1 + the identity (or the downsample branch, ``down``: 1x1 stride-2 conv + BN) through
+    one Function (the other branch's input gradient is the C operand of conv1's dgrad GEMM): gradients of the
+    input and of every parameter vs fp32, with the residual branch live (bn3 gamma != 0, unlike the zero-init
+    default).  Three BNs deep, bf16 rounding alone is several percent, so the bound is stock bf16 autocast's own
+    error on the same block."""
+    from pytorch_distributedtraining_amd.models import resnet as R
+    monkeypatch.setattr(R, "FORK_DOWNSAMPLE", True)      # (opt-in for downsample blocks)
     torch.manual_seed(3)
-    blk = Bottleneck(256, 64).to(DEV).to(memory_format=torch.channels_last)
+
+    def make(fused):
+        ds = None
+        if down:
+            ds = torch.nn.Sequential(R.conv1x1(256, 512, 2, fused=fused), R._bn(512, None, fused))
+        return R.Bottleneck(256, 128 if down else 64, 2 if down else 1, ds, fused=fused).to(DEV).to(
+            memory_format=torch.channels_last)
+    blk = make(True)
     for m in blk.modules():
         if isinstance(m, torch.nn.BatchNorm2d):
             torch.nn.init.uniform_(m.weight, 0.5, 1.5)
             torch.nn.init.uniform_(m.bias, -0.2, 0.2)
-    stock = Bottleneck(256, 64, fused=False).to(DEV).to(memory_format=torch.channels_last)
-    ref = Bottleneck(256, 64, fused=False).to(DEV).to(memory_format=torch.channels_last)
+    stock = make(False)
+    ref = make(False)
     stock.load_state_dict(blk.state_dict())
     ref.load_state_dict(blk.state_dict())
     x0 = torch.randn(16, 256, 28, 28, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
