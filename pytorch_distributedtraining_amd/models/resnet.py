@@ -38,11 +38,11 @@ def conv1x1(cin, cout, stride=1, fused=False):
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
-
 # the downsample blocks fork x too (PDT_RESNET_FORK_DS=1: their downsample conv's data gradient joins conv1's dgrad
 # GEMM as its C operand) -- measured 0.6-1 % SLOWER than autograd's separate add over those 4 block inputs
 # (9,217 / 9,169 vs 9,252 / 9,276 samples/s, profiles/r5/r5_resnet_fork_ds_ab.txt), so off by default
 FORK_DOWNSAMPLE = os.environ.get("PDT_RESNET_FORK_DS", "0") == "1"
+
 
 class BasicBlock(nn.Module):
     expansion = 1
