@@ -541,7 +541,9 @@ int bwd_partial_rows(int rows, int N) {
   // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
   // a few rows per wave (so the row prefetch pays) while covering the chip: ~2 waves per SIMD
   if (small_rows(N)) return grid_for(rows, SM_RPB * 8, 512);
-  static const int cap = [] { const char* e = getenv("PDT_NORM_BWD_WG"); return e ? atoi(e) : 512; }();
+  // 256 partial-row workgroups: the flagship step 668.1 / 669.7 -> 664.8 / 669.3 ms against 512, the norm_pass
+  // backward alone 360-405 -> 377-386 us (profiles/r5/r5v_norm_grid_ab.txt); PDT_NORM_BWD_WG overrides
+  static const int cap = [] { const char* e = getenv("PDT_NORM_BWD_WG"); return e ? atoi(e) : 256; }();
   if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB * 4, cap);
   return grid_for(rows, 1, 512);
 }
