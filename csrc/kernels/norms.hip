@@ -517,10 +517,11 @@ int launch_fwd(const void* x, const void* res, const void* rb, void* sum_out, co
     norm_fwd_small<T, W, RMS><<<grid_for(rows, SM_RPB, 256 * 16), NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N,
                                                                               eps);
   } else if (N % 8 == 0 && N <= 8192) {
-    // workgroups per CU: 32 (plain) / 96 (fused residual add) -- GPT-2 1.3B norms at 96 x 1024 tokens, 2,048
-    // columns: plain 178 -> 167 us, residual add 291 -> 250 us against 16 (profiles/r5/r5v_norm_grid_ab.txt)
+    // workgroups per CU: 64 (plain) / 96 (fused residual add) -- GPT-2 1.3B norms at 96 x 1024 tokens, 2,048
+    // columns: plain 178 (16) -> 167.8 (32) -> 164.9 us (64), residual add 291 -> 250 us (96)
+    // (profiles/r5/r5v_norm_grid_ab.txt)
     static const int cap_env = [] { const char* e = getenv("PDT_NORM_FWD_WG_PER_CU"); return e ? atoi(e) : 0; }();
-    const int cap = cap_env > 0 ? cap_env : (res != nullptr ? 96 : 32);
+    const int cap = cap_env > 0 ? cap_env : (res != nullptr ? 96 : 64);
     const int grid = grid_for(rows, RPB, 256 * cap);
     const int iters = (N + 511) / 512;
 #define PDT_NF(I) norm_fwd_kernel<T, W, I, RMS><<<grid, NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N, eps)
