@@ -238,6 +238,10 @@ def timed_loop(step_fn, args, comm, dev):
         if i == 0:
             torch_cuda.synchronize(dev)
             log(f"[bench] warmup step 0 done")
+    # per-shape kernel picks were timed per rank inside the warm-up; agree them over the engine's group here,
+    # where every rank arrives together (ops/picks.py), so all ranks time the same kernels
+    from pytorch_distributedtraining_amd.ops import picks
+    picks.agree(comm)
     comm.barrier()
     torch_cuda.synchronize(dev)
     comm.reset_stats()
@@ -360,7 +364,8 @@ def bench_gpt2(args, comm, dev, world, rank):
         else:
             model = build_gpt2(name, n_positions=max(1024, S), activation_checkpointing=bool(args.act_ckpt))
     nparams = model.num_params()
-    flops_tok = model.flops_per_token(S)
+    flops_tok = model.flops_per_token(S)                    # causal attention: the FLOPs the model needs
+    flops_tok_full = model.flops_per_token(S, causal=False)  # every score counted (full-matrix convention)
     if fsdp:
         strat = ShardingStrategy.FULL_SHARD if args.reshard else ShardingStrategy.SHARD_GRAD_OP
         model = FullyShardedDataParallel(model, sharding_strategy=strat, mixed_precision=MixedPrecision(),
@@ -450,7 +455,9 @@ def bench_gpt2(args, comm, dev, world, rank):
     tokens = world * mb * S * args.steps
     tps = tokens / dt
     log(f"[bench] {name} params={nparams/1e9:.3f}B loss={float(state['loss'].item()):.4f} "
-        f"step={1000*dt/args.steps:.1f}ms MFU(bf16 2.5PF/GPU)={tps*flops_tok/world/2.5e15*100:.1f}%")
+        f"step={1000*dt/args.steps:.1f}ms MFU(bf16 2.5PF/GPU, causal attention FLOPs)="
+        f"{tps*flops_tok/world/2.5e15*100:.1f}% (full-matrix attention FLOPs: "
+        f"{tps*flops_tok_full/world/2.5e15*100:.1f}%)")
     metric = "tokens/sec GPT-2-1.3B FSDP (whole node)" if fsdp and name == "gpt2-1.3b" else \
         f"tokens/sec {name} {'FSDP' if fsdp else 'DDP'} (whole node)"
     if llama:
@@ -460,6 +467,9 @@ def bench_gpt2(args, comm, dev, world, rank):
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", **comm_fields(world), "vs_baseline": None,
             "dtype": "fp8-linears" if args.fp8 else "bf16", "data": "synthetic",
+            "mfu": {"causal_attention_flops": round(tps * flops_tok / world / 2.5e15, 4),
+                    "full_attention_flops": round(tps * flops_tok_full / world / 2.5e15, 4),
+                    "peak": "2.5 PFLOP/s dense bf16 per GPU"},
             "config": {"model": name, "global_batch": world * mb, "seq_len": S, "parallelism": par,
                        "micro_batch_per_gpu": mb, "params": nparams, "hip_graph": graph, "sharding": "full_shard" if args.reshard else
                        "shard_grad_op", "optimizer": "fused AdamW + global-norm clip",

@@ -195,11 +195,14 @@ class GPT2LMHeadModel(nn.Module):
             n -= self.wpe.weight.numel()
         return n
 
-    def flops_per_token(self, seq_len: int) -> float:
-        """6N + attention (12 L S d) training FLOPs per token (causal halving not applied)."""
+    def flops_per_token(self, seq_len: int, causal: bool = True) -> float:
+        """Training FLOPs per token: 6N (N without the position table) + attention.  Attention is QK^T and PV,
+        4 S d per token per layer forward, x3 for training = 12 L S d with every score computed; a causal mask
+        makes half of them useful, so the default (``causal=True``) counts 6 L S d -- the work this model
+        actually needs.  ``causal=False`` is the full-matrix convention some MFU figures use."""
         c = self.config
         n = self.num_params(non_embedding=True)
-        return 6 * n + 12 * c.n_layer * seq_len * c.n_embd
+        return 6 * n + (6 if causal else 12) * c.n_layer * seq_len * c.n_embd
 
     def forward(self, input_ids, labels=None):
         B, S = input_ids.shape
@@ -224,7 +227,8 @@ class GPT2LMHeadModel(nn.Module):
         logits = linear(x, self.wte.weight)     # tied head (framework linear: transposed-layout dgrad)
         if labels is None:
             return logits
-        return cross_entropy(logits, labels, inplace_backward=True)
+        # training: the gradient is written over the (dead) logits in the forward's single read; eval keeps them
+        return cross_entropy(logits, labels, inplace_backward=True, grad_in_forward=self.training)
 
 
 def build_gpt2(name: str = "gpt2-124m", **overrides) -> GPT2LMHeadModel:

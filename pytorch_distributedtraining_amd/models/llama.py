@@ -177,10 +177,12 @@ class Llama(nn.Module):
     def num_params(self):
         return sum(p.numel() for p in self.parameters())
 
-    def flops_per_token(self, seq_len):
+    def flops_per_token(self, seq_len, causal: bool = True):
+        """6N (N without the embedding table) + causal attention 6 L S d (12 L S d with ``causal=False``): see
+        ``GPT2.flops_per_token``."""
         c = self.config
         n = self.num_params() - self.tok_embeddings.weight.numel()
-        return 6 * n + 12 * c.n_layers * seq_len * c.dim
+        return 6 * n + (6 if causal else 12) * c.n_layers * seq_len * c.dim
 
     def to_portable_state_dict(self, sd: dict) -> dict:
         """This module's (fused) state dict -> the Meta layout (``export_meta_state_dict``)."""
@@ -211,7 +213,8 @@ class Llama(nn.Module):
         logits = self.output(h)
         if labels is None:
             return logits
-        return cross_entropy(logits, labels, inplace_backward=True)
+        # training: the gradient is written over the (dead) logits in the forward's single read; eval keeps them
+        return cross_entropy(logits, labels, inplace_backward=True, grad_in_forward=self.training)
 
 
 def build_llama(name="llama3-8b", **overrides) -> Llama:

@@ -85,6 +85,6 @@ def prefer_bgradb(dy2: torch.Tensor, x2: torch.Tensor, separate) -> bool:
         _CHOICE[key] = False
         return False
 
-    from .linear import timed_choice
-    c = _CHOICE[key] = timed_choice(lambda: wgrad_bgrad(dy2, x2), separate)
+    from .picks import timed_choice
+    c = _CHOICE[key] = timed_choice(lambda: wgrad_bgrad(dy2, x2), separate, table=_CHOICE, key=key, name="bgradb")
     return c

@@ -213,8 +213,8 @@ def _c1_pick(key, gemm_fn, miopen_fn):
     if c is None:
         if torch.cuda.is_current_stream_capturing():
             return True
-        from .linear import timed_choice
-        c = _C1_CHOICE[key] = timed_choice(gemm_fn, miopen_fn)
+        from .picks import timed_choice
+        c = _C1_CHOICE[key] = timed_choice(gemm_fn, miopen_fn, table=_C1_CHOICE, key=key, name="conv1x1")
     return c
 
 

@@ -33,6 +33,7 @@ from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 from .gemm import gemm_tt, tt_ok, tt_splits
 from .grad_slots import claim, is_sharded_param
+from .picks import timed_choice
 
 _WGRAD_CHUNK = 4096
 # PDT_DX_COLSUM_STASH=0: the attention backward sums dO itself instead of taking the consuming Linear's db W
@@ -82,7 +83,8 @@ def _library_linear(a2, w, bias, key):
         c = _LT_CHOICE.get(key)
         if c is None and not torch.cuda.is_current_stream_capturing():
             c = _LT_CHOICE[key] = _lt_linear(a2, w, bias) is not None and \
-                timed_choice(lambda: _lt_linear(a2, w, bias), lambda: F.linear(a2, w, bias), 0.99)
+                timed_choice(lambda: _lt_linear(a2, w, bias), lambda: F.linear(a2, w, bias), 0.99,
+                             table=_LT_CHOICE, key=key, name="lt")
         if c:
             y = _lt_linear(a2, w, bias)
             if y is not None:
@@ -100,7 +102,8 @@ def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
         c = _NT_CHOICE.get(key)
         if c is None and not torch.cuda.is_current_stream_capturing():
             c = _NT_CHOICE[key] = timed_choice(lambda: G.gemm_nt(a2, w, bias),
-                                               lambda: _library_linear(a2, w, bias, key), 0.99)
+                                               lambda: _library_linear(a2, w, bias, key), 0.99,
+                                               table=_NT_CHOICE, key=key, name="nt")
         if c:
             return G.gemm_nt(a2, w, bias)
     return _library_linear(a2, w, bias, key)
@@ -130,35 +133,6 @@ HIP_WGRAD = os.environ.get("PDT_WGRAD_HIP", "auto")
 _WGRAD_CHOICE: dict = {}
 
 
-def _timed_ms(fn, iters: int = 3) -> float:
-    fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1)
-
-
-def timed_choice(fa, fb, margin: float = 1.0) -> bool:
-    """Whether ``fa`` runs faster than ``margin`` x ``fb`` -- the per-shape kernel picks (hand GEMM vs hipBLASLt,
-    1x1 conv as GEMM vs MIOpen, BGRADB).  Decided IDENTICALLY on every rank: each rank times both arms (a timing
-    can overlap in-flight bucket collectives and differ between ranks), then the times are summed over the default
-    process group -- one 2-float all-reduce, issued in the same order by every rank since every rank meets the
-    same shapes in the same order -- so all ranks run the same kernels and reduce bitwise-comparable gradients.
-    The env switches of each pick (PDT_NT_HIP, PDT_WGRAD_HIP, PDT_CONV1X1) pin the choice outright."""
-    ta, tb = _timed_ms(fa), _timed_ms(fb)
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else \
-            torch.device("cpu")
-        t = torch.tensor([ta, tb], dtype=torch.float64, device=dev)
-        dist.all_reduce(t)
-        ta, tb = (float(v) for v in t.tolist())
-    return ta < margin * tb
-
-
 def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, ragged: bool = False) -> bool:
     """Hand kernel vs hipBLASLt for this weight-gradient shape.  Measured, not assumed: the two trade places
     by shape and by box (GPT-2 1.3B attention projection +12 %, fc1 +3 %, Llama-3 8B qkv -14 % on one box;
@@ -172,7 +146,8 @@ def _prefer_hip_wgrad(dy2: torch.Tensor, x2: torch.Tensor, ragged: bool = False)
             return True
         # against the path wgrad() would otherwise take (split-K batched GEMM for small outputs, else one GEMM)
         hip = hip_wgrad_ragged if ragged else hip_wgrad
-        c = _WGRAD_CHOICE[key] = timed_choice(lambda: hip(dy2, x2), lambda: _library_wgrad(dy2, x2, torch.bfloat16))
+        c = _WGRAD_CHOICE[key] = timed_choice(lambda: hip(dy2, x2), lambda: _library_wgrad(dy2, x2, torch.bfloat16),
+                                                    table=_WGRAD_CHOICE, key=key, name="wgrad")
     return c
 
 

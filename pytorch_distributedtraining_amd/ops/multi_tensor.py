@@ -103,6 +103,14 @@ class TableCache:
             self._tables[name] = t
         return t
 
+    def retain(self, keep) -> None:
+        """Drop every cached table whose name fails ``keep(name)`` (its device table is freed with it)."""
+        for n in [n for n in self._tables if not keep(n)]:
+            del self._tables[n]
+
+    def __len__(self):
+        return len(self._tables)
+
 
 _cache = TableCache()
 

@@ -214,6 +214,7 @@ class FusedAdamW(Optimizer):
                     st = self._init_state(p)
                     st["step"] += 1
                     buckets.setdefault((grad_of(p).dtype, -int(st["step"].item()), p.device), []).append(p)
+            used = set()
             for (gdt, ckey, dev), ps in buckets.items():
                 dstep = counters.get(ckey)
                 step = -ckey if dstep is None else 1
@@ -229,7 +230,9 @@ class FusedAdamW(Optimizer):
                 table = None
                 if dev.type == "cuda":
                     cols = [ps, grads, ms, vs, lps if has_lp else [None] * len(ps)]
-                    table = self._tables.get((gi, gdt, ckey if dstep is not None else 0), cols)
+                    name = (gi, gdt, ckey if dstep is not None else 0)
+                    used.add(name)
+                    table = self._tables.get(name, cols)
                 mt.adamw_step(ps, grads, ms, vs, lr=lr, beta1=beta1, beta2=beta2, eps=group["eps"],
                               weight_decay=group["weight_decay"], step=max(step, 1),
                               decoupled=group.get("decoupled", True), grad_scale=grad_scale, found_inf=found_inf,
@@ -240,4 +243,8 @@ class FusedAdamW(Optimizer):
                 for p in ps:
                     if getattr(p, "_pdt_lp_shard", None) is not None:
                         p._pdt_lp_version = p._version   # compute copy already refreshed by the kernel
+            if buckets:
+                # tables of this group's counters that no longer exist (a split counter, a reloaded checkpoint)
+                # are dropped, so their device tables do not pile up over a long run
+                self._tables.retain(lambda n, gi=gi: n[0] != gi or n in used)
         return loss

@@ -414,13 +414,22 @@ class DistributedDataParallel(nn.Module):
 
     def _arm_gather(self, out):
         """Queue the compute-copy gradient gather to run once the backward through ``out`` has finished."""
-        ts = [out] if torch.is_tensor(out) else [t for t in (out.values() if isinstance(out, dict) else out)
-                                                  if torch.is_tensor(t)] if isinstance(out, (tuple, list, dict)) else []
-        for t in ts:
-            if t.requires_grad:
+        from torch.utils._pytree import tree_leaves
+        leaves = [out] if torch.is_tensor(out) else tree_leaves(out)
+        if not any(torch.is_tensor(t) for t in leaves) and hasattr(out, "__dict__"):
+            leaves = tree_leaves(vars(out))          # dataclass / plain object outputs: walk their fields
+        for t in leaves:
+            if torch.is_tensor(t) and t.requires_grad:
                 ref = weakref.ref(self)
                 t.register_hook(lambda g, ref=ref: ref()._queue_gather() or g)
                 return
+        # nothing to hook: if a backward still runs (through a tensor this walk could not see) the masters would
+        # step on zero gradients -- say so once instead of failing silently
+        if self.module.training and not getattr(self, "_warned_no_hook", False):
+            self._warned_no_hook = True
+            warnings.warn("DistributedDataParallel(compute_dtype=...): no grad-requiring tensor found in the model "
+                          f"output ({type(out).__name__}); the master-gradient gather is not queued for this forward",
+                          stacklevel=3)
 
     def _queue_gather(self):
         if not self._gather_queued:

@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from ..data.loader import DeviceDataLoader
+from ..ops import picks
 from ..ops.fp8 import fp8_autocast
 from ..optim import FusedAdamW, GradScaler, clip_grad_norm_
 from ..parallel.comm import Comm
@@ -394,6 +395,11 @@ class Trainer:
         with prof.range("pdt.optimizer_step"):
             self._step()
         self._optimizer_steps += 1
+        if self._optimizer_steps <= 3 and self.comm.world_size > 1 and not (
+                torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            # the kernel picks timed inside the first steps' forward / backward, agreed over THIS engine's group
+            # at a point every rank reaches together (ops/picks.py) -- never from inside autograd
+            picks.agree(self.comm)
         if self.comm.debug and self._optimizer_steps % self._verify_every == 0:
             self.comm.verify_consistency(f"after optimizer step {self._optimizer_steps}")
         return True
@@ -501,8 +507,13 @@ class Trainer:
             return
         t = self._ema.reshape(1).clone()
         if self.world_size_ > 1:
-            self.comm.reduce(t, dst=int(self.logger.info_rank if not isinstance(self.logger.info_rank, (list, tuple))
-                                        else self.logger.info_rank[0]), op="avg")
+            ir = self.logger.info_rank
+            if isinstance(ir, int) or (isinstance(ir, (list, tuple)) and len(ir) == 1):
+                # one printing rank: reduce to it only
+                self.comm.reduce(t, dst=int(ir if isinstance(ir, int) else ir[0]), op="avg")
+            else:
+                # several printing ranks ('all', a list, or None = every rank's logger decides): each needs the mean
+                self.comm.all_reduce(t, "avg")
         if not self.logger.will_print():
             return
         parts = (prepend_msg, postpend_msg)

@@ -27,7 +27,7 @@ def run(fused):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        CE.cross_entropy(x, t, inplace_backward=True).backward()
+        CE.cross_entropy(x, t, grad_in_forward=True).backward()
         e1.record()
         e1.synchronize()
         if i >= 2:

@@ -18,9 +18,10 @@ from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
 @pytest.fixture(scope="module", autouse=True)
 def _pg():
     if not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29671")
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        # file rendezvous: no fixed TCP port to collide with under pytest-xdist
+        import tempfile
+        d = tempfile.mkdtemp()
+        dist.init_process_group("gloo", init_method="file://" + os.path.join(d, "rdzv"), rank=0, world_size=1)
     yield
 
 
@@ -66,3 +67,28 @@ def test_single_process_ddp_steals_gradients(compute_dtype):
     assert all(p.grad is not None for p in ddp.module.parameters())
     opt.zero_grad(set_to_none=False)                                   # graph-replay form: zeroed in place
     assert all(p.grad is None or float(p.grad.abs().sum()) == 0.0 for p in ddp.module.parameters())
+
+
+class _Nested(torch.nn.Module):
+    """Returns its prediction nested two levels deep in a dataclass-like object: the master-gradient gather must
+    still be queued (only the top level of a tuple/list/dict was searched)."""
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(12, 5)
+
+    def forward(self, x):
+        from dataclasses import dataclass
+
+        @dataclass
+        class Out:
+            extras: dict
+        return Out(extras={"aux": [torch.zeros(1), {"pred": self.lin(x)}]})
+
+
+def test_single_process_ddp_gathers_through_nested_outputs():
+    ddp = DistributedDataParallel(_Nested(), comm=Comm(), compute_dtype=torch.bfloat16)
+    x = torch.randn(8, 12, dtype=torch.bfloat16)
+    out = ddp(x)
+    out.extras["aux"][1]["pred"].float().square().mean().backward()
+    nz = sum(float(g.flat_grad.abs().sum()) for g in ddp.groups if g.master is not None)
+    assert nz > 0, "master gradients stayed zero: the gather was never queued"

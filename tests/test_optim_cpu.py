@@ -102,3 +102,34 @@ def test_zero_grad_fills_a_bucket_flat_only_when_it_owns_every_view():
     flat.fill_(2.0)
     opt_both.zero_grad()
     assert torch.equal(flat, torch.zeros(10)) and b.grad._base is flat
+
+
+@pytest.mark.gpu
+def test_device_tables_do_not_pile_up_when_counters_split():
+    """tables were keyed by id(counter) and never evicted; a counter split (a parameter skipping steps)
+    or a checkpoint reload left dead device tables behind.  Only the live counters' tables stay cached."""
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in [(64, 32), (32,), (128,)]]
+    opt = FusedAdamW(ps, capturable=True, **KW)
+    for it in range(12):
+        for i, p in enumerate(ps):
+            p.grad = None if (i == 1 and it % 3 != 0) else torch.randn_like(p)
+        opt.step()
+        assert len(opt._tables) <= len(opt._dsteps)
+    sd = copy.deepcopy(opt.state_dict())
+    for _ in range(3):                    # repeated reloads: each rebuilds the counters
+        opt.load_state_dict(sd)
+        for p in ps:
+            p.grad = torch.randn_like(p)
+        opt.step()
+        assert len(opt._tables) <= len(opt._dsteps)
+
+
+def test_table_cache_retain():
+    from pytorch_distributedtraining_amd.ops.multi_tensor import TableCache
+    tc = TableCache()
+    a, b = torch.zeros(4), torch.zeros(8)
+    tc.get((0, "x", 1), [[a]])
+    tc.get((0, "x", 2), [[b]])
+    tc.get((1, "x", 3), [[b]])
+    tc.retain(lambda n: n[0] != 0 or n == (0, "x", 2))
+    assert len(tc) == 2
