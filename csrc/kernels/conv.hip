@@ -12,6 +12,8 @@
 // The im2col kernel reads ANY input strides (NCHW images, the NHWC-strided views SwinIR produces from
 // [B, L, C] token tensors, channels_last gradients), so no layout copy precedes it, and writes 16-byte
 // rows of 8 consecutive K entries per thread.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace pdt;
@@ -113,11 +115,13 @@ PDT_API int pdt_im2col3x3(const void* x, int64_t sn, int64_t sc, int64_t sh, int
 // partition.  REVERSE maps back (inverse permutation) and optionally adds the residual.
 // ------------------------------------------------------------------------------------------------
 namespace {
-template <bool REVERSE, bool RES>
-__global__ __launch_bounds__(256) void window_perm_kernel(const bf16_t* __restrict__ src, const bf16_t* __restrict__ res,
-                                                          bf16_t* __restrict__ dst, int64_t rows, int C, int H, int W,
+// T = bf16_t (8-byte chunks of 4) or float (16-byte chunks of 4: the fp32 model, the reference's precision)
+template <typename T, bool REVERSE, bool RES>
+__global__ __launch_bounds__(256) void window_perm_kernel(const T* __restrict__ src, const T* __restrict__ res,
+                                                          T* __restrict__ dst, int64_t rows, int C, int H, int W,
                                                           int ws, int shift) {
-  const int cpr = C / 4;                      // 8-byte chunks per row
+  typedef typename std::conditional<sizeof(T) == 2, u16x4, f32x4>::type V;
+  const int cpr = C / 4;                      // 4-element chunks per row
   const int nww = W / ws, per_img = H * W;
   const int64_t total = rows * cpr;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -146,31 +150,42 @@ __global__ __launch_bounds__(256) void window_perm_kernel(const bf16_t* __restri
     }
     const int64_t so = (REVERSE ? win_row : img_row) * C + ch * 4;
     const int64_t dof = (REVERSE ? img_row : win_row) * C + ch * 4;
-    u16x4 v = *reinterpret_cast<const u16x4*>(src + so);
+    V v = *reinterpret_cast<const V*>(src + so);
     if (RES) {
-      const u16x4 a = *reinterpret_cast<const u16x4*>(res + dof);
+      const V a = *reinterpret_cast<const V*>(res + dof);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = f2bf(bf2f(v[k]) + bf2f(a[k]));
+      for (int k = 0; k < 4; ++k) v[k] = from_f<T>(to_f<T>((T)v[k]) + to_f<T>((T)a[k]));
     }
-    *reinterpret_cast<u16x4*>(dst + dof) = v;
+    *reinterpret_cast<V*>(dst + dof) = v;
   }
 }
 }  // namespace
 
 // reverse = 0: windows = partition(roll(x, -shift)); reverse = 1: x = roll(reverse(windows), +shift) (+ res).
-// bf16, C % 4 == 0, H % ws == 0, W % ws == 0, 0 <= shift < ws.
-PDT_API int pdt_window_perm(const void* src, const void* res, void* dst, int64_t rows, int C, int H, int W, int ws,
-                            int shift, int reverse, hipStream_t st) {
+// C % 4 == 0, H % ws == 0, W % ws == 0, 0 <= shift < ws.
+namespace {
+template <typename T>
+int window_perm_launch(const void* src, const void* res, void* dst, int64_t rows, int C, int H, int W, int ws,
+                       int shift, int reverse, hipStream_t st) {
   if (C % 4 || H % ws || W % ws || shift < 0 || shift >= ws || rows % ((int64_t)H * W)) return (int)hipErrorInvalidValue;
   const int64_t total = rows * (C / 4);
   const int grid = grid_for(total, 256, 256 * 16);
   if (reverse) {
-    if (res) window_perm_kernel<true, true><<<grid, 256, 0, st>>>((const bf16_t*)src, (const bf16_t*)res, (bf16_t*)dst, rows, C, H, W, ws, shift);
-    else window_perm_kernel<true, false><<<grid, 256, 0, st>>>((const bf16_t*)src, nullptr, (bf16_t*)dst, rows, C, H, W, ws, shift);
+    if (res) window_perm_kernel<T, true, true><<<grid, 256, 0, st>>>((const T*)src, (const T*)res, (T*)dst, rows, C, H, W, ws, shift);
+    else window_perm_kernel<T, true, false><<<grid, 256, 0, st>>>((const T*)src, nullptr, (T*)dst, rows, C, H, W, ws, shift);
   } else {
-    window_perm_kernel<false, false><<<grid, 256, 0, st>>>((const bf16_t*)src, nullptr, (bf16_t*)dst, rows, C, H, W, ws, shift);
+    window_perm_kernel<T, false, false><<<grid, 256, 0, st>>>((const T*)src, nullptr, (T*)dst, rows, C, H, W, ws, shift);
   }
   return (int)hipGetLastError();
+}
+}  // namespace
+PDT_API int pdt_window_perm(const void* src, const void* res, void* dst, int64_t rows, int C, int H, int W, int ws,
+                            int shift, int reverse, hipStream_t st) {
+  return window_perm_launch<bf16_t>(src, res, dst, rows, C, H, W, ws, shift, reverse, st);
+}
+PDT_API int pdt_window_perm_f32(const void* src, const void* res, void* dst, int64_t rows, int C, int H, int W, int ws,
+                                int shift, int reverse, hipStream_t st) {
+  return window_perm_launch<float>(src, res, dst, rows, C, H, W, ws, shift, reverse, st);
 }
 
 // ------------------------------------------------------------------------------------------------

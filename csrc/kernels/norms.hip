@@ -256,6 +256,139 @@ __global__ __launch_bounds__(NT, OCC) void norm_bwd_kernel(const T* __restrict__
   }
 }
 
+// ---- wide rows (N > 2048, e.g. Llama-3 8B's d = 4,096): one ROW per workgroup, split over its 4 waves ----
+// The wave-per-row kernel above keeps a whole row (and the next one, prefetched) plus the per-column dgamma
+// partials in registers: at N = 4,096 that is > 256 VGPRs and the compiler spilled 200-540 of them to scratch
+// (300 us per call, ~1.8 TB/s at Llama's 16,384 x 4,096).  Here wave w owns columns [w N/4, (w+1) N/4): its
+// slice of the row (IT 512-column slabs, IT = N / 2048) and of the dgamma partials stays small, the two row
+// reductions cross waves through an 8-float LDS slot (double-buffered by row parity: one barrier per row), and
+// since the waves own disjoint columns each workgroup writes its partial row straight from registers.
+template <typename T, typename W, int IT, bool RMS, bool DRES, bool DSUM>
+__global__ __launch_bounds__(NT, 2) void norm_bwd_split_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                               const float* __restrict__ rstd_in,
+                                                               const T* __restrict__ dres, T* __restrict__ dx,
+                                                               float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                               float* __restrict__ ds_part, int rows, int N) {
+  __shared__ float red[2][2][RPB];          // [row parity][a, bsum][wave]
+  typedef typename Vec8<T>::raw_t raw_t;
+  typedef typename Vec8<W>::raw_t wraw_t;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float invN = 1.f / (float)N;
+  const int span = N / RPB;                 // columns per wave (a multiple of 8)
+  int cc[IT];
+  bool cv[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 512 + lane * 8;
+    cv[it] = c < span;
+    cc[it] = wid * span + (cv[it] ? c : span - 8);
+  }
+  float dwa[IT][8], dba[IT][8], dsa[DSUM ? IT : 1][8];
+  wraw_t wr[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dwa[it][k] = 0.f; dba[it][k] = 0.f; if constexpr (DSUM) dsa[it][k] = 0.f; }
+    wr[it] = Vec8<W>::load_raw(w + cc[it]);
+  }
+  raw_t cx[IT], cg[IT], cr[DRES ? IT : 1];
+  int row = blockIdx.x;
+  {
+    const int64_t r = min(row, rows - 1);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      cx[it] = Vec8<T>::load_raw(x + r * N + cc[it]);
+      cg[it] = Vec8<T>::load_raw(dy + r * N + cc[it]);
+      if constexpr (DRES) cr[it] = Vec8<T>::load_raw(dres + r * N + cc[it]);
+    }
+  }
+  int par = 0;
+  for (; row < rows; row += gridDim.x, par ^= 1) {
+    raw_t nx[IT], ng[IT], nr[DRES ? IT : 1];
+    const int64_t nrow = min(row + (int)gridDim.x, rows - 1);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      nx[it] = Vec8<T>::load_raw(x + nrow * N + cc[it]);
+      ng[it] = Vec8<T>::load_raw(dy + nrow * N + cc[it]);
+      if constexpr (DRES) nr[it] = Vec8<T>::load_raw(dres + nrow * N + cc[it]);
+    }
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      float xv[8], dv[8], wv[8];
+      Vec8<T>::unpack(cx[it], xv);
+      Vec8<T>::unpack(cg[it], dv);
+      Vec8<W>::unpack(wr[it], wv);
+      const float m = cv[it] ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[k] - mean) * rstd;
+        const float d = dv[k] * m;
+        const float g = d * wv[k];
+        a += g * xh;
+        bsum += g;
+        dwa[it][k] += d * xh;
+        dba[it][k] += d;
+      }
+    }
+    a = wave_sum(a);
+    if (!RMS) bsum = wave_sum(bsum);
+    if (lane == 0) {
+      red[par][0][wid] = a;
+      red[par][1][wid] = bsum;
+    }
+    __syncthreads();     // the slot of this parity is rewritten two rows later, after the next barrier
+    a = (red[par][0][0] + red[par][0][1] + red[par][0][2] + red[par][0][3]) * invN;
+    if (!RMS) bsum = (red[par][1][0] + red[par][1][1] + red[par][1][2] + red[par][1][3]) * invN;
+    T* dxr = dx + (int64_t)row * N;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      float xv[8], dv[8], wv[8], o[8];
+      Vec8<T>::unpack(cx[it], xv);
+      Vec8<T>::unpack(cg[it], dv);
+      Vec8<W>::unpack(wr[it], wv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[k] * wv[k] - (RMS ? 0.f : bsum) - (xv[k] - mean) * rstd * a);
+      if constexpr (DRES) {
+        float rv[8];
+        Vec8<T>::unpack(cr[it], rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += rv[k];
+      }
+      if constexpr (DSUM) {
+        const float m = cv[it] ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dsa[it][k] += m * to_f<T>(from_f<T>(o[k]));
+      }
+      if (cv[it]) Vec8<T>::store(dxr + cc[it], o);
+      cx[it] = nx[it];
+      cg[it] = ng[it];
+      if constexpr (DRES) cr[it] = nr[it];
+    }
+  }
+  // disjoint columns per wave: the workgroup's partial row straight from registers
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    if (!cv[it]) continue;
+    const int64_t o = (int64_t)blockIdx.x * N + cc[it];
+    *reinterpret_cast<f32x4*>(dw_part + o) = f32x4{dwa[it][0], dwa[it][1], dwa[it][2], dwa[it][3]};
+    *reinterpret_cast<f32x4*>(dw_part + o + 4) = f32x4{dwa[it][4], dwa[it][5], dwa[it][6], dwa[it][7]};
+    if (db_part) {
+      *reinterpret_cast<f32x4*>(db_part + o) = f32x4{dba[it][0], dba[it][1], dba[it][2], dba[it][3]};
+      *reinterpret_cast<f32x4*>(db_part + o + 4) = f32x4{dba[it][4], dba[it][5], dba[it][6], dba[it][7]};
+    }
+    if constexpr (DSUM) {
+      *reinterpret_cast<f32x4*>(ds_part + o) = f32x4{dsa[it][0], dsa[it][1], dsa[it][2], dsa[it][3]};
+      *reinterpret_cast<f32x4*>(ds_part + o + 4) = f32x4{dsa[it][4], dsa[it][5], dsa[it][6], dsa[it][7]};
+    }
+  }
+}
+// the split kernel's shape contract: 4 waves x IT slabs of 512 columns, each wave's span a multiple of 8
+__host__ __device__ constexpr bool split_rows_ok(int N) { return N > 2048 && N <= 16384 && N % (8 * RPB) == 0; }
+
 // ---- fallback: one block per row, streamed from global memory ----
 template <typename T, typename W, bool RMS>
 __global__ __launch_bounds__(NT) void norm_fwd_generic(const T* __restrict__ x, const T* __restrict__ res,
@@ -545,6 +678,12 @@ int bwd_partial_rows(int rows, int N) {
   // 256 partial-row workgroups: the flagship step 668.1 / 669.7 -> 664.8 / 669.3 ms against 512, the norm_pass
   // backward alone 360-405 -> 377-386 us (profiles/r5/r5v_norm_grid_ab.txt); PDT_NORM_BWD_WG overrides
   static const int cap = [] { const char* e = getenv("PDT_NORM_BWD_WG"); return e ? atoi(e) : 256; }();
+  if (split_rows_ok(N)) {
+    // one row per workgroup pass, 2 workgroups per CU resident: 512 partial rows (16 MB of fp32 partials at
+    // N = 4,096 against ~540 MB of row traffic); PDT_NORM_SPLIT_WG overrides
+    static const int scap = [] { const char* e = getenv("PDT_NORM_SPLIT_WG"); return e ? atoi(e) : 512; }();
+    return grid_for(rows, 4, scap);
+  }
   if (N % 8 == 0 && N <= 8192) return grid_for(rows, RPB * 4, cap);
   return grid_for(rows, 1, 512);
 }
@@ -559,8 +698,21 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   float* dwp = ws;
   float* dbp = (db != nullptr) ? ws + (int64_t)R * N : nullptr;
   float* dsp = (ds != nullptr) ? ws + (int64_t)2 * R * N : nullptr;
+  static const bool split_off = [] { const char* e = getenv("PDT_NORM_SPLIT"); return e && atoi(e) == 0; }();
   if (small_rows(N)) {
     norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N);
+  } else if (split_rows_ok(N) && !split_off) {
+    const int it = (N / RPB + 511) / 512;
+#define PDT_NS2(I, D, S) \
+  norm_bwd_split_kernel<T, W, I, RMS, D, S><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N)
+#define PDT_NS1(I, D) do { if (dsp) { PDT_NS2(I, D, true); } else { PDT_NS2(I, D, false); } } while (0)
+#define PDT_NS(I) do { if (DR) { PDT_NS1(I, true); } else { PDT_NS1(I, false); } } while (0)
+    if (it <= 2) PDT_NS(2);
+    else if (it <= 4) PDT_NS(4);
+    else PDT_NS(8);
+#undef PDT_NS
+#undef PDT_NS1
+#undef PDT_NS2
   } else if (N % 8 == 0 && N <= 8192) {
     const int iters = (N + 511) / 512;
     const size_t lds = (dsp ? 3 : 2) * (size_t)N * sizeof(float);

@@ -673,6 +673,405 @@ int mfma_blocks_per_head(int Bw, int H, int per_cu) {
   return need < want ? need : (want > 0 ? want : 1);
 }
 
+
+// ================================================================================================
+// fp32 MFMA path -- the reference's own precision (Stoke-DDP.py:247 trains SwinIR with fp16=None).  gfx950 has
+// f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32, an fmaf chain per output, 64 FLOP/clk/SIMD) and no xf32, so
+// these kernels keep full fp32 numerics while moving every product off the VALU.  Same structure as the bf16
+// kernels above -- one wave per (window, head), scores transposed (lane = query, registers = keys), the two-pass
+// backward -- with fp32 operands: a 32x32x2 fragment is ONE float per lane (A[row = l & 31][k = l >> 5],
+// B[k = l >> 5][col = l & 31]), read straight from per-wave LDS row tiles R[64][D + 1] (odd pitch for D even:
+// the 32 rows of a fragment hit distinct banks).  Products whose k runs over keys take the accumulator registers
+// as the B operand in the permuted key order key = acc_row(r, hh), and their A operand from the same row tile at
+// [key][min(l32, D)] -- column D is kept zero, so output rows (head dims) >= D come out zero for free.
+// ================================================================================================
+constexpr int BPF = 68;      // fp32 bias row pitch: 16-byte reads of 4 consecutive keys
+
+__device__ __forceinline__ f32x16 mfma2(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+template <int D> constexpr int f32_fwd_wave() { return 3 * 64 * (D + 1) + 16; }          // Q K V tiles, labels
+template <int D> constexpr int f32_bwd_wave() { return 4 * 64 * (D + 1) + 128 + 16; }    // Q K V dO, L, delta, labels
+template <int D> size_t f32_fwd_lds() { return sizeof(float) * (64 * BPF + 4 * f32_fwd_wave<D>()); }
+// (the wave tiles double as the [64][64] bias-gradient reduction area at the end of pass 1)
+template <int D> size_t f32_bwd_lds() {
+  return sizeof(float) * (64 * BPF + (4 * f32_bwd_wave<D>() > 64 * 64 ? 4 * f32_bwd_wave<D>() : 64 * 64));
+}
+
+template <int D>
+struct RowF {
+  float v[D];
+  __device__ __forceinline__ void load(const float* p) {      // 8-byte aligned: row offsets and D are even
+    const float2* s = reinterpret_cast<const float2*>(p);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) {
+      const float2 x = s[i];
+      v[2 * i] = x.x;
+      v[2 * i + 1] = x.y;
+    }
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < D; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void put(float* R, int t) const {
+    float* d = R + t * (D + 1);
+#pragma unroll
+    for (int i = 0; i < D; ++i) d[i] = v[i];
+    d[D] = 0.f;
+  }
+};
+// D-wide fp32 output row from an O^T-layout accumulator (register r = dim acc_row(r, hh), lane = token)
+template <int D>
+__device__ __forceinline__ void store_dims_f32(float* row, const f32x16& acc, float mul, int hh) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int dim = 8 * g + 4 * hh + 2 * pr;
+      if (dim < D) *reinterpret_cast<float2*>(row + dim) = float2{acc[4 * g + 2 * pr] * mul, acc[4 * g + 2 * pr + 1] * mul};
+    }
+}
+template <bool TRANSPOSE>
+__device__ __forceinline__ void stage_bias_f32(const float* g, float* s, int N) {
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+    const int r = e >> 6, c = e & 63;
+    s[(TRANSPOSE ? c : r) * BPF + (TRANSPOSE ? r : c)] = (r < N && c < N) ? g[r * N + c] : 0.f;
+  }
+}
+// S^T (or S) tile over the head dim: sum_s A[ra][2s + hh] B[rb][2s + hh]
+template <int D>
+__device__ __forceinline__ f32x16 dot_tile(const float* RA, int ra, const float* RB, int rb, int hh) {
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int s = 0; s < D / 2; ++s) acc = mfma2(RA[ra * (D + 1) + 2 * s + hh], RB[rb * (D + 1) + 2 * s + hh], acc);
+  return acc;
+}
+
+template <int D, int MK, bool FULL>
+__global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_f32(const float* __restrict__ qkv, const float* __restrict__ bias,
+                                                             const float* __restrict__ mask,
+                                                             const uint8_t* __restrict__ labels, int nw,
+                                                             float* __restrict__ o, float* __restrict__ lse, int Bw,
+                                                             int N, int H, float scale, int P) {
+  extern __shared__ __attribute__((aligned(16))) float smf32[];
+  constexpr int RP = D + 1;
+  const int C = H * D, C3 = 3 * C;
+  const int h = blockIdx.x % H, pb = blockIdx.x / H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int dcl = l32 < D ? l32 : D;
+  float* BR = smf32;                                      // [64][BPF] bias of head h, [q][key]
+  float* QR = smf32 + 64 * BPF + wv * f32_fwd_wave<D>();
+  float* KR = QR + 64 * RP;
+  float* VR = KR + 64 * RP;
+  uint8_t* LAB = reinterpret_cast<uint8_t*>(VR + 64 * RP);
+  stage_bias_f32<false>(bias + (int64_t)h * N * N, BR, N);
+  __syncthreads();
+
+  for (int bw = pb * 4 + wv; bw < Bw; bw += P * 4) {
+    {
+      RowF<D> q, k, v;
+      if (lane < N) {
+        const float* row = qkv + ((int64_t)bw * N + lane) * C3 + h * D;
+        q.load(row); k.load(row + C); v.load(row + 2 * C);
+      } else {
+        q.zero(); k.zero(); v.zero();
+      }
+      q.put(QR, lane); k.put(KR, lane); v.put(VR, lane);
+      if (MK == 2) LAB[lane] = lane < N ? labels[(int64_t)(bw % nw) * N + lane] : (uint8_t)255;
+    }
+    wave_sync();
+    const float* mw = MK == 1 ? mask + (int64_t)(bw % nw) * N * N : nullptr;
+    f32x16 p[2][2];
+    float lsum[2], mmax[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * qt + l32;
+      const int qc = FULL ? q : min(q, N - 1);
+      const uint32_t qlab = MK == 2 ? LAB[q] : 0u;
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        p[qt][kt] = dot_tile<D>(KR, 32 * kt + l32, QR, q, hh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {          // registers 4i..4i+3 = keys base..base+3
+          const int base = 32 * kt + 8 * i + 4 * hh;
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(BR + q * BPF + base);
+          f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+          if (MK == 2) {
+            mv = label_mask(LAB, base, qlab);
+          } else if (MK == 1) {
+            if (FULL) {
+              mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) mv[j] = base + j < N ? mw[qc * N + base + j] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * i + j;
+            float a = fmaf(p[qt][kt][r], scale, bv[j] + mv[j]);
+            if (!FULL) a = (base + j < N && q < N) ? a : -INFINITY;
+            p[qt][kt][r] = a;
+            m = fmaxf(m, a);
+          }
+        }
+      }
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const float msub = m == -INFINITY ? 0.f : m;
+      float l = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __expf(p[qt][kt][r] - msub);
+          p[qt][kt][r] = e;
+          l += e;
+        }
+      l += __shfl_xor(l, 32, 64);
+      lsum[qt] = l;
+      mmax[qt] = msub;
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      // O^T = V^T P^T: k runs over the keys in the accumulator order (lane half hh supplies key acc_row(r, hh))
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc = mfma2(VR[(32 * kt + acc_row(r, hh)) * RP + dcl], p[qt][kt][r], acc);
+      const int q = 32 * qt + l32;
+      if (FULL || q < N) {
+        store_dims_f32<D>(o + ((int64_t)bw * N + q) * C + h * D, acc, 1.f / lsum[qt], hh);
+        if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(lsum[qt]);
+      }
+    }
+    wave_sync();
+  }
+}
+
+template <int D, int MK, bool FULL, int PASS>
+__global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_f32(
+    const float* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask,
+    const uint8_t* __restrict__ labels, int nw,
+    const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P) {
+  extern __shared__ __attribute__((aligned(16))) float smb32[];
+  constexpr int RP = D + 1;
+  const int C = H * D, C3 = 3 * C;
+  const int h = blockIdx.x % H, pb = blockIdx.x / H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int dcl = l32 < D ? l32 : D;
+  float* BB = smb32;                    // [64][BPF] bias: pass 1 [q][key], pass 2 [key][q]
+  float* QR = BB + 64 * BPF + wv * f32_bwd_wave<D>();
+  float* KR = QR + 64 * RP;
+  float* VR = KR + 64 * RP;
+  float* GR = VR + 64 * RP;
+  float* SL = GR + 64 * RP;             // [64] lse
+  float* SD = SL + 64;                  // [64] delta
+  uint8_t* LAB = reinterpret_cast<uint8_t*>(SD + 64);
+  stage_bias_f32<PASS == 2>(bias + (int64_t)h * N * N, BB, N);
+  __syncthreads();
+  f32x16 dsacc[2][2];
+  if (PASS == 1) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) dsacc[x][y] = zero16();
+  }
+
+  for (int bw = pb * 4 + wv; bw < Bw; bw += P * 4) {
+    {
+      RowF<D> q, k, v, g, oo;
+      float L = 0.f, dl = 0.f;
+      if (lane < N) {
+        const int64_t tok = (int64_t)bw * N + lane;
+        const float* row = qkv + tok * C3 + h * D;
+        q.load(row); k.load(row + C); v.load(row + 2 * C);
+        g.load(dout + tok * C + h * D);
+        oo.load(o + tok * C + h * D);
+        L = lse[((int64_t)bw * H + h) * N + lane];
+#pragma unroll
+        for (int e = 0; e < D; ++e) dl = fmaf(g.v[e], oo.v[e], dl);
+      } else {
+        q.zero(); k.zero(); v.zero(); g.zero();
+      }
+      q.put(QR, lane); k.put(KR, lane); v.put(VR, lane); g.put(GR, lane);
+      SL[lane] = L;
+      SD[lane] = dl;
+      if (MK == 2) LAB[lane] = lane < N ? labels[(int64_t)(bw % nw) * N + lane] : (uint8_t)255;
+    }
+    wave_sync();
+    const float* mw = MK == 1 ? mask + (int64_t)(bw % nw) * N * N : nullptr;
+    if (PASS == 1) {
+      // lane = query (S^T layout): dS^T, dQ = dS K * scale, dS summed for the bias gradient
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int q = 32 * qt + l32;
+        const int qc = FULL ? q : min(q, N - 1);
+        const float Lq = SL[q], Dq = SD[q];
+        const uint32_t qlab = MK == 2 ? LAB[q] : 0u;
+        f32x16 ds[2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const f32x16 sc = dot_tile<D>(KR, 32 * kt + l32, QR, q, hh);
+          const f32x16 dp = dot_tile<D>(VR, 32 * kt + l32, GR, q, hh);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int base = 32 * kt + 8 * i + 4 * hh;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(BB + q * BPF + base);
+            f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+            if (MK == 2) {
+              mv = label_mask(LAB, base, qlab);
+            } else if (MK == 1) {
+              if (FULL) {
+                mv = *reinterpret_cast<const f32x4*>(mw + q * 64 + base);
+              } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) mv[j] = base + j < N ? mw[qc * N + base + j] : 0.f;
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * i + j;
+              const float a = fmaf(sc[r], scale, bv[j] + mv[j]);
+              float v = __expf(a - Lq) * (dp[r] - Dq);
+              if (!FULL) v = (base + j < N && q < N) ? v : 0.f;
+              ds[kt][r] = v;
+            }
+          }
+          dsacc[qt][kt] += ds[kt];
+        }
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc = mfma2(KR[(32 * kt + acc_row(r, hh)) * RP + dcl], ds[kt][r], acc);
+        if (FULL || q < N) store_dims_f32<D>(dqkv + ((int64_t)bw * N + q) * C3 + h * D, acc, scale, hh);
+      }
+    } else {
+      // lane = key (S layout): P and dS in one sweep; dV = P^T dO, dK = dS^T Q * scale
+#pragma unroll 1
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = 32 * kt + l32;
+        const int kc = FULL ? key : min(key, N - 1);
+        const uint32_t klab = MK == 2 ? LAB[key] : 0u;
+        f32x16 av = zero16(), ak = zero16();
+#pragma unroll 1
+        for (int qt = 0; qt < 2; ++qt) {
+          const f32x16 sc = dot_tile<D>(QR, 32 * qt + l32, KR, key, hh);
+          const f32x16 dp = dot_tile<D>(GR, 32 * qt + l32, VR, key, hh);
+          f32x16 pv, dv;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {        // registers 4i..4i+3 = queries base..base+3
+            const int base = 32 * qt + 8 * i + 4 * hh;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(BB + key * BPF + base);
+            const f32x4 L4 = *reinterpret_cast<const f32x4*>(SL + base);
+            const f32x4 D4 = *reinterpret_cast<const f32x4*>(SD + base);
+            f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+            if (MK == 2) {
+              mv = label_mask(LAB, base, klab);
+            } else if (MK == 1) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) mv[j] = (FULL || base + j < N) ? mw[(base + j) * N + kc] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * i + j;
+              const float a = fmaf(sc[r], scale, bv[j] + mv[j]);
+              float e = __expf(a - L4[j]);
+              if (!FULL) e = (key < N && base + j < N) ? e : 0.f;
+              pv[r] = e;
+              dv[r] = e * (dp[r] - D4[j]);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = (32 * qt + acc_row(r, hh)) * RP + dcl;
+            av = mfma2(GR[row], pv[r], av);
+            ak = mfma2(QR[row], dv[r], ak);
+          }
+        }
+        if (FULL || key < N) {
+          float* row = dqkv + ((int64_t)bw * N + key) * C3 + h * D;
+          store_dims_f32<D>(row + C, ak, scale, hh);
+          store_dims_f32<D>(row + 2 * C, av, 1.f, hh);
+        }
+      }
+    }
+    wave_sync();
+  }
+  if (PASS == 1) {
+    __syncthreads();
+    float* red = BB + 64 * BPF;          // [64][64] over the (now idle) wave tiles
+    for (int e = threadIdx.x; e < 64 * 64; e += WA_NT) red[e] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          atomicAdd(red + (32 * qt + l32) * 64 + 32 * kt + acc_row(r, hh), dsacc[qt][kt][r]);
+    __syncthreads();
+    float* dst = dbias_part + ((int64_t)pb * H + h) * N * N;
+    for (int e = threadIdx.x; e < N * N; e += WA_NT) dst[e] = red[(e / N) * 64 + e % N];
+  }
+}
+
+template <int D>
+int wa_f32_fwd_launch(const float* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, float* o,
+                      float* lse, int Bw, int N, int H, float scale, hipStream_t st) {
+  const int P = mfma_blocks_per_head(Bw, H, 4);
+  const size_t lds = f32_fwd_lds<D>();
+  const bool full = N == 64;
+#define PDT_WF(M, F) \
+  win_attn_fwd_f32<D, M, F><<<P * H, WA_NT, lds, st>>>(qkv, bias, mask, labels, nw, o, lse, Bw, N, H, scale, P)
+  if (labels) { if (full) PDT_WF(2, true); else PDT_WF(2, false); }
+  else if (mask) { if (full) PDT_WF(1, true); else PDT_WF(1, false); }
+  else { if (full) PDT_WF(0, true); else PDT_WF(0, false); }
+#undef PDT_WF
+  return (int)hipGetLastError();
+}
+template <int D>
+int wa_f32_bwd_launch(const float* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw,
+                      const float* o, const float* dout, const float* lse, float* dqkv, float* dbias_part, int Bw,
+                      int N, int H, float scale, hipStream_t st) {
+  const int P = mfma_blocks_per_head(Bw, H, 2);
+  const size_t lds = f32_bwd_lds<D>();
+  static bool attr = [] {
+    bool ok = true;
+    const void* fns[12] = {
+        (const void*)win_attn_bwd_f32<D, 1, true, 1>,  (const void*)win_attn_bwd_f32<D, 1, false, 1>,
+        (const void*)win_attn_bwd_f32<D, 0, true, 1>,  (const void*)win_attn_bwd_f32<D, 0, false, 1>,
+        (const void*)win_attn_bwd_f32<D, 1, true, 2>,  (const void*)win_attn_bwd_f32<D, 1, false, 2>,
+        (const void*)win_attn_bwd_f32<D, 0, true, 2>,  (const void*)win_attn_bwd_f32<D, 0, false, 2>,
+        (const void*)win_attn_bwd_f32<D, 2, true, 1>,  (const void*)win_attn_bwd_f32<D, 2, false, 1>,
+        (const void*)win_attn_bwd_f32<D, 2, true, 2>,  (const void*)win_attn_bwd_f32<D, 2, false, 2>};
+    for (const void* f : fns)
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f32_bwd_lds<D>()) == hipSuccess;
+    return ok;
+  }();
+  if (!attr) return (int)hipErrorInvalidValue;
+  const bool full = N == 64;
+#define PDT_WB(M, F, PS)                                                                                         \
+  win_attn_bwd_f32<D, M, F, PS><<<P * H, WA_NT, lds, st>>>(qkv, bias, mask, labels, nw, o, dout, lse, dqkv, dbias_part, \
+                                                           Bw, N, H, scale, P)
+  if (labels) {
+    if (full) { PDT_WB(2, true, 1); PDT_WB(2, true, 2); }
+    else { PDT_WB(2, false, 1); PDT_WB(2, false, 2); }
+  } else if (mask) {
+    if (full) { PDT_WB(1, true, 1); PDT_WB(1, true, 2); }
+    else { PDT_WB(1, false, 1); PDT_WB(1, false, 2); }
+  } else {
+    if (full) { PDT_WB(0, true, 1); PDT_WB(0, true, 2); }
+    else { PDT_WB(0, false, 1); PDT_WB(0, false, 2); }
+  }
+#undef PDT_WB
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // grid size the launcher uses (also the number of dbias partials the caller must allocate)
@@ -769,6 +1168,25 @@ PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const floa
 #define PDT_C(D)                                                                                                   \
   return wa_bwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, dout, lse, dqkv, dbias_part, Bw, N, H, \
                           scale, st)
+  PDT_WA_DISPATCH_D(d, PDT_C)
+#undef PDT_C
+}
+// fp32 MFMA path (same contract as the bf16 one; partials [pdt_win_attn_mfma_grid(Bw, H), H, N, N])
+PDT_API int pdt_win_attn_mfma32_ok(int N, int H, int d) { return mfma_ok(N, H, d, kBF16) ? 1 : 0; }
+PDT_API int pdt_win_attn_mfma32_fwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
+                                    float* o, float* lse, int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D) return wa_f32_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, st)
+  PDT_WA_DISPATCH_D(d, PDT_C)
+#undef PDT_C
+}
+PDT_API int pdt_win_attn_mfma32_bwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
+                                    const float* o, const float* dout, const float* lse, float* dqkv,
+                                    float* dbias_part, int Bw, int N, int H, int d, float scale, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+#define PDT_C(D)                                                                                                 \
+  return wa_f32_bwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, dout, lse, dqkv, dbias_part, Bw, N, \
+                              H, scale, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }

@@ -170,15 +170,17 @@ class SwinTransformerBlock(nn.Module):
     def forward(self, x, x_size):
         H, W = x_size
         B, L, C = x.shape
-        if self.attn.native and fused_window_ok(x, H, W, self.window_size, self.shift_size):
-            # roll + partition and reverse + roll + residual add as one permutation pass each
+        if self.attn.native and fused_window_ok(x, H, W, self.window_size, self.shift_size) and (
+                x.dtype == torch.bfloat16 or not torch.is_autocast_enabled()):
+            # roll + partition and reverse + roll + residual add as one permutation pass each (bf16, or fp32 --
+            # the reference's own precision -- when no autocast region would mix the two)
             if self.shift_size > 0:
                 mask = self._mask_for(H, W, x.device)
             else:
                 mask = None
-            h = self.norm1(x).to(torch.bfloat16)
+            h = self.norm1(x).to(x.dtype)
             win = window_partition_shifted(h, H, W, self.window_size, self.shift_size)
-            a = self.attn(win, mask=mask).to(torch.bfloat16)
+            a = self.attn(win, mask=mask).to(x.dtype)
             x = window_reverse_shifted_add(a, x, H, W, self.window_size, self.shift_size)
             return self.mlp(self.norm2(x), residual=x)
         sc = x

@@ -94,6 +94,11 @@ _SIGS = {
                               c_int, c_float, c_void_p],
     "pdt_win_attn_mfma_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "pdt_win_attn_mfma32_ok": [c_int, c_int, c_int],
+    "pdt_win_attn_mfma32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                c_int, c_float, c_void_p],
+    "pdt_win_attn_mfma32_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
     "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                          c_int, c_void_p],
     "pdt_win_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
@@ -129,6 +134,7 @@ _SIGS = {
     "pdt_bn_bwd_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_window_perm": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_window_perm_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,
                       c_int, c_void_p],
     "pdt_pixel_shuffle_affine_fwd": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int,

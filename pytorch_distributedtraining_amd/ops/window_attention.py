@@ -4,7 +4,8 @@
 ``softmax(q kᵀ · scale + rel_bias[h] + mask[w]) v`` straight from the fused qkv projection
 ``[Bw, N, 3C]`` and returns ``[Bw, N, C]`` ready for the output projection.  On MI355X this is one
 HIP kernel each way (``csrc/kernels/window_attn.hip``); the stock path would materialise the
-expanded bias+mask ``[Bw, h, N, N]`` and the scores in HBM.  The CPU path is the plain PyTorch
+expanded bias+mask ``[Bw, h, N, N]`` and the scores in HBM.  bf16 runs the bf16 MFMA kernels; fp32 (the reference's
+own training precision) runs exact-f32 MFMA kernels (``v_mfma_f32_32x32x2_f32``), not a reduced-precision cast.  The CPU path is the plain PyTorch
 formula (also the numerics reference in the GPU tests).
 """
 from __future__ import annotations
@@ -19,6 +20,7 @@ from . import _lib
 
 _MASK_T_CACHE: dict = {}
 USE_LABELS = os.environ.get("PDT_WIN_MASK_LABELS", "1") == "1"   # A/B switch: 0 = dense fp32 mask reads
+MFMA_F32 = os.environ.get("PDT_WIN_F32_MFMA", "1") == "1"        # A/B switch: 0 = fp32 on the VALU kernels
 
 
 def _mask_t(mask):
@@ -83,12 +85,17 @@ class _WindowAttnFn(torch.autograd.Function):
         o = torch.empty((Bw, N, C), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty((Bw, num_heads, N), dtype=torch.float32, device=qkv.device)
         lib = _lib.require()
-        ctx.mfma = bool(lib.pdt_win_attn_mfma_ok(N, num_heads, d, _lib.dtype_code(qkv.dtype)))
+        if qkv.dtype == torch.float32:
+            # fp32 (the reference's precision): exact-f32 MFMA kernels (v_mfma_f32_32x32x2_f32), VALU as fallback
+            ctx.mfma = "f32" if (MFMA_F32 and lib.pdt_win_attn_mfma32_ok(N, num_heads, d)) else None
+        else:
+            ctx.mfma = "bf16" if lib.pdt_win_attn_mfma_ok(N, num_heads, d, _lib.dtype_code(qkv.dtype)) else None
         if ctx.mfma:
             # MFMA kernels: dense bias [h, N(q), N(key)] and mask [nw, N, N], no transposed copies
             m = mask.float().contiguous() if mask is not None else None
             lab = _mask_labels(mask) if (mask is not None and USE_LABELS) else None
-            _lib.call("pdt_win_attn_mfma_fwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
+            _lib.call("pdt_win_attn_mfma_fwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_fwd", qkv.data_ptr(),
+                      bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
                       o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.stream_handle(qkv.device))
             ctx.save_for_backward(qkv, bias, o, lse)
             ctx.mask = (m, lab, nw)
@@ -115,7 +122,7 @@ class _WindowAttnFn(torch.autograd.Function):
             dqkv = torch.empty_like(qkv)
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
             do = do.contiguous().to(qkv.dtype)
-            _lib.call("pdt_win_attn_mfma_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
+            _lib.call("pdt_win_attn_mfma_bwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
                       o.data_ptr(),
                       do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
                       ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
@@ -157,11 +164,11 @@ def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float):
 # ------------------------------------------------------------------------------------------------
 def _perm(src, res, out_shape, H, W, ws, shift, reverse):
     C = src.shape[-1]
-    if src.dtype != torch.bfloat16 or (res is not None and res.dtype != torch.bfloat16):
-        raise TypeError("fused window permutation takes bf16 tensors")
+    if src.dtype not in (torch.bfloat16, torch.float32) or (res is not None and res.dtype != src.dtype):
+        raise TypeError("fused window permutation takes bf16 or fp32 tensors of one dtype")
     out = torch.empty(out_shape, dtype=src.dtype, device=src.device)
     rows = src.numel() // C
-    _lib.call("pdt_window_perm", src.data_ptr(), _lib.ptr(res), out.data_ptr(), rows, C, H, W, ws, shift,
+    _lib.call("pdt_window_perm" if src.dtype == torch.bfloat16 else "pdt_window_perm_f32", src.data_ptr(), _lib.ptr(res), out.data_ptr(), rows, C, H, W, ws, shift,
               1 if reverse else 0, _lib.stream_handle(src.device))
     return out
 
@@ -195,7 +202,7 @@ class _ReverseAddFn(torch.autograd.Function):
 
 
 def fused_window_ok(x, H, W, ws, shift) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.shape[1] == H * W and
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 3 and x.shape[1] == H * W and
             x.shape[2] % 4 == 0 and H % ws == 0 and W % ws == 0 and 0 <= shift < ws)
 
 

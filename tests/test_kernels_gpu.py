@@ -145,7 +145,10 @@ def test_cross_entropy_inplace_forward_gradient(V, reduction, gscale):
     x = leaf * 1.0                                  # a non-leaf logits buffer, as a model's head output
     grads = []
     x.register_hook(grads.append)
-    loss = cross_entropy(x, t, reduction=reduction, inplace_backward=True)
+    x0 = x.detach().clone()
+    probe = cross_entropy(x, t, reduction=reduction, inplace_backward=True)   # no grad_in_forward: logits intact
+    assert torch.equal(x.detach(), x0) and abs(probe.item() - lr.item()) < 2e-3 * max(1, abs(lr.item()))
+    loss = cross_entropy(x, t, reduction=reduction, grad_in_forward=True)
     assert abs(loss.item() - lr.item()) < 2e-3 * max(1, abs(lr.item()))
     (loss * gscale).backward()
     g = grads[0]
@@ -785,7 +788,7 @@ def test_ddp_bf16_engine_single_gpu_step():
 
 @pytest.mark.parametrize("rbias", [False, True])
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("N", [2048, 96, 4096, 60, 10240])
+@pytest.mark.parametrize("N", [2048, 96, 4096, 60, 10240, 3072, 8192, 16384])
 def test_fused_add_norm(rms, N, rbias):
     """Fused residual add (+ the producing Linear's bias, whose gradient is colsum(dx) from the same backward
     pass) + LayerNorm / RMSNorm against fp32 torch; N = 10240 takes the generic (one block per row) kernels."""
@@ -943,22 +946,23 @@ def test_pixel_shuffle_affine(dt, r, C):
     assert rel_err(y.grad, yr.grad) < tol
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("H,W,ws,shift,C", [(16, 24, 8, 4, 60), (14, 21, 7, 0, 12), (16, 16, 8, 3, 96)])
-def test_window_perm_fused(H, W, ws, shift, C):
+def test_window_perm_fused(H, W, ws, shift, C, dt):
     """Fused shifted-window partition / reverse(+residual) vs torch.roll + view/permute, values and grads."""
     from pytorch_distributedtraining_amd.ops.window_attention import (window_partition_shifted,
                                                                        window_reverse_shifted_add)
     from pytorch_distributedtraining_amd.models.swinir import window_partition, window_reverse
     torch.manual_seed(0)
     B = 3
-    x = torch.randn(B, H * W, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(B, H * W, C, device=DEV, dtype=dt, requires_grad=True)
     xr = x.detach().clone().requires_grad_(True)
     win = window_partition_shifted(x, H, W, ws, shift)
     wr = window_partition(torch.roll(xr.view(B, H, W, C), (-shift, -shift), (1, 2)), ws).view(-1, ws * ws, C)
     assert torch.equal(win, wr)
     a = torch.randn_like(win, requires_grad=True)
     ar = a.detach().clone().requires_grad_(True)
-    res = torch.randn(B, H * W, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    res = torch.randn(B, H * W, C, device=DEV, dtype=dt, requires_grad=True)
     resr = res.detach().clone().requires_grad_(True)
     out = window_reverse_shifted_add(a, res, H, W, ws, shift)
     outr = resr + torch.roll(window_reverse(ar.view(-1, ws, ws, C), ws, H, W), (shift, shift), (1, 2)).view(B, H * W, C)
@@ -1971,3 +1975,68 @@ def test_llama_selective_recompute_gpu_bitwise():
     assert torch.equal(l0, l1)
     assert all(torch.equal(a, b) for a, b in zip(g0, g1))
     assert len(runs) == 4 * 3
+
+
+@pytest.mark.parametrize("res", [(64, 64), (40, 24)])
+def test_window_attention_fp32_mfma_matches_fp32_reference(res):
+    """fp32 SwinIR (the reference's precision) on the exact-f32 MFMA kernels (v_mfma_f32_32x32x2_f32): forward,
+    dq/dk/dv and the relative-bias gradient against the fp32 torch formula and against the fp32 VALU kernels, with
+    the shift mask rebuilt from region labels, with the dense mask and unmasked."""
+    from pytorch_distributedtraining_amd.models.swinir import SwinTransformerBlock
+    from pytorch_distributedtraining_amd.ops import window_attention as WA
+    blk = SwinTransformerBlock(60, res, 6, window_size=8, shift_size=4)
+    mask = blk._mask(res).to(DEV)
+    nw = mask.shape[0]
+    Bw, N, h, d = 3 * nw, 64, 6, 10
+    torch.manual_seed(1)
+    qkv = torch.randn(Bw, N, 3 * h * d, device=DEV).requires_grad_()
+    rb = (0.5 * torch.randn(h, N, N, device=DEV)).requires_grad_()
+    g = torch.randn(Bw, N, h * d, device=DEV)
+    qr, br = qkv.detach().clone().requires_grad_(), rb.detach().clone().requires_grad_()
+    (WA.reference(qr, br, mask, h, d ** -0.5) * g).sum().backward()
+    ref = WA.reference(qr.detach(), br.detach(), mask, h, d ** -0.5)
+    for f32_mfma, labels, m in ((True, True, mask), (True, False, mask), (False, False, mask), (True, False, None)):
+        WA.MFMA_F32, WA.USE_LABELS = f32_mfma, labels
+        try:
+            qkv.grad = rb.grad = None
+            o = WA.window_attention(qkv, rb, m, h, d ** -0.5)
+            (o * g).sum().backward()
+        finally:
+            WA.MFMA_F32, WA.USE_LABELS = True, True
+        if m is None:
+            r2q, r2b = qkv.detach().clone().requires_grad_(), rb.detach().clone().requires_grad_()
+            (WA.reference(r2q, r2b, None, h, d ** -0.5) * g).sum().backward()
+            assert rel_err(o, WA.reference(qkv.detach(), rb.detach(), None, h, d ** -0.5)) < 1e-5
+            assert rel_err(qkv.grad, r2q.grad) < 1e-5 and rel_err(rb.grad, r2b.grad) < 1e-5
+            continue
+        assert rel_err(o, ref) < 1e-5, (f32_mfma, labels, rel_err(o, ref))
+        assert rel_err(qkv.grad, qr.grad) < 1e-5, (f32_mfma, labels, rel_err(qkv.grad, qr.grad))
+        assert rel_err(rb.grad, br.grad) < 1e-5, (f32_mfma, labels, rel_err(rb.grad, br.grad))
+
+
+@pytest.mark.parametrize("rms", [True, False])
+def test_norm_bwd_row_split_at_llama_shape(rms):
+    """Wide rows (N > 2048) take the row-split backward (one row per workgroup over its 4 waves, no register
+    spills): at Llama-3 8B's 16,384 x 4,096 with the stream gradient folded in (norm_pass), every dx row and the
+    weight (and bias) gradients against fp32 torch."""
+    from pytorch_distributedtraining_amd.ops.norms import norm_pass
+    torch.manual_seed(5)
+    M, N = 16384, 4096
+    s = torch.randn(M, N, device=DEV).bfloat16().requires_grad_()
+    g = (torch.rand(N, device=DEV) + 0.5).bfloat16().requires_grad_()
+    beta = None if rms else torch.randn(N, device=DEV).bfloat16().requires_grad_()
+    y, s2 = norm_pass(s, g, beta, 1e-5, rms=rms)
+    dy, ds = torch.randn_like(y), torch.randn_like(s2)
+    torch.autograd.backward([y, s2], [dy, ds])
+    sr, gr = s.detach().float().requires_grad_(), g.detach().float().requires_grad_()
+    br = None if rms else beta.detach().float().requires_grad_()
+    if rms:
+        yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * gr
+    else:
+        yr = F.layer_norm(sr, (N,), gr, br, 1e-5)
+    torch.autograd.backward([yr, sr], [dy.float(), ds.float()])
+    row_err = ((s.grad.float() - sr.grad).norm(dim=1) / sr.grad.norm(dim=1)).max().item()
+    assert row_err < 1e-2, row_err
+    assert rel_err(g.grad, gr.grad) < 1e-2
+    if not rms:
+        assert rel_err(beta.grad, br.grad) < 1e-2
