@@ -60,6 +60,11 @@ def parse():
                     help="cpu: plumbing rehearsal of any workload on gloo (tiny --model / --micro-batch)")
     ap.add_argument("--overlap-probe", type=int, default=1,
                     help="world > 1: after timing, measure exposed vs communication-only time (untimed)")
+    ap.add_argument("--rehearse-world", type=int, default=0,
+                    help="REHEARSAL, never a headline: run this rank's step as rank --rehearse-rank of a world of "
+                         "this size on ONE GPU over torch's 'fake' process group (collectives complete without "
+                         "moving data): per-rank compute ms/step, shard sizes and peak memory at world W")
+    ap.add_argument("--rehearse-rank", type=int, default=-1, help="rank to play (default: the last)")
     ap.add_argument("--loss", default="feat", choices=["feat", "mse"], help="swinir-stoke loss")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"], help="swinir-stoke precision")
     ap.add_argument("--graph", type=int, default=0,
@@ -107,6 +112,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_world > 1:
+        return rehearse(args)
     if args.workload == "resnet18-cpu" or args.device == "cpu":   # config 1 / CPU plumbing rehearsal
         dev = torch.device("cpu")
         if world > 1:
@@ -170,6 +177,63 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def rehearse(args):
+    """``--rehearse-world W``: one process on one GPU plays rank R of a world of W through torch's ``fake``
+    process-group backend.  Every engine takes its multi-rank code path -- the nccl-style branches of ``Comm``
+    (reduce_scatter_tensor with AVG, all_gather_into_tensor, all_reduce, barrier) with world-W shard shapes and
+    bucket plans -- while the collectives themselves move no data.  The line reports per-rank compute time,
+    collective counts / payload bytes per step and peak memory at world W.  It is a readiness rehearsal, NOT a
+    measurement of scaling: its metric says so and it never carries a headline value."""
+    import torch
+    import torch.distributed as dist
+    from torch.testing._internal.distributed.fake_pg import FakeStore
+
+    world = args.rehearse_world
+    rank = args.rehearse_rank if args.rehearse_rank >= 0 else world - 1
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("fake", rank=rank, world_size=world, store=FakeStore())
+    # the fake group leaves outputs untouched: an FSDP all-gather would hand the forward uninitialised weights
+    # (NaN loss -- and NaN / zero operands draw less power, so the GPU clocks up and the rehearsal reads ~16 %
+    # fast, profiles/r6/r6d_fake_world8_rehearsal.jsonl).  Fill every output the way the real collective would
+    # (this rank's payload in every slot / this rank's own chunk): real values, and the bytes a real
+    # all-gather / reduce-scatter writes into its output.
+    real_ag, real_rs = dist.all_gather_into_tensor, dist.reduce_scatter_tensor
+
+    def all_gather_into_tensor(out, inp, group=None, async_op=False):
+        w = real_ag(out, inp, group=group, async_op=async_op)
+        out.view(world, -1).copy_(inp.reshape(1, -1).expand(world, -1))
+        return w
+
+    def reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=None, async_op=False):
+        w = real_rs(out, inp, op=op, group=group, async_op=async_op)
+        out.view(-1).copy_(inp.reshape(world, -1)[rank])
+        return w
+    dist.all_gather_into_tensor, dist.reduce_scatter_tensor = all_gather_into_tensor, reduce_scatter_tensor
+    from pytorch_distributedtraining_amd.ops import _lib
+    _lib.require()
+    from pytorch_distributedtraining_amd.parallel import Comm
+    comm = Comm(xgmi=False)
+    args.overlap_probe, args.secondary, args.gpus = 0, 0, world
+    torch.manual_seed(1234)
+    if args.workload.startswith("gpt2") or args.workload.startswith("llama"):
+        res = bench_gpt2(args, comm, dev, world, rank)
+    elif args.workload == "swinir-stoke":
+        res = bench_swinir(args, comm, dev, world, rank)
+    else:
+        res = bench_resnet(args, comm, dev, world, rank)
+    out = {"metric": f"REHEARSAL per-rank compute ms/step at fake world {world} (rank {rank}, one GPU, collectives "
+                     f"move no data) -- {res['metric'].split(' (whole node)')[0]} -- not a measurement",
+           "value": res["ms_per_step"], "unit": "ms/step/rank", "higher_is_better": False, "rehearsal": True,
+           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+           "world": world, "rank": rank, "backend": comm.backend,
+           **{k: res[k] for k in ("collectives_per_step", "comm_bytes_per_step", "peak_mem_gb", "dtype", "config")
+              if k in res}}
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    return 0
 
 
 class SecondarySkipped(RuntimeError):
