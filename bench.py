@@ -417,8 +417,10 @@ def bench_gpt2(args, comm, dev, world, rank):
     # +1.3 % at 188 GB peak (128: +2.0 % at 243 GB -- not taken, leaves < 50 GB headroom;
     # profiles/r2_flagship_microbatch_64_96_128.log); Llama-3 8B with selective recompute on all 32 layers 8 -> 16
     # sequences 22.9k -> 24.9k tokens/s at 182 GB peak (AdamW's fixed 39 ms/step amortised;
-    # profiles/r5/r5_llama3_8b_ckpt_policy.jsonl)
-    mb = args.micro_batch or (16 if llama else 96 if fsdp else 64)
+    # profiles/r5/r5_llama3_8b_ckpt_policy.jsonl); 16 -> 32 sequences 25.2k -> 26.3k tokens/s at 231 GB peak (24: 25.9k,
+    # 206 GB; profiles/r6/r6e_microbatch_and_rehearsal.jsonl).  GPT-2 1.3B stays at 96: 112 / 128 sequences measured
+    # +0.4 % / -0.2 % at 216 / 244 GB (same file)
+    mb = args.micro_batch or (32 if llama else 96 if fsdp else 64)
     S = args.seq
     with torch.device(dev):
         if llama:

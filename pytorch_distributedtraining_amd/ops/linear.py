@@ -33,6 +33,7 @@ from .blaslt import prefer_bgradb, wgrad_bgrad
 from .fp8 import Fp8Meta, fp8_enabled, fp8_linear
 from .gemm import gemm_tt, tt_ok, tt_splits
 from .grad_slots import claim, is_sharded_param
+from .narrow import narrow_linear, narrow_ok
 from .picks import timed_choice
 
 _WGRAD_CHUNK = 4096
@@ -107,6 +108,37 @@ def nt_matmul(a2: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
         if c:
             return G.gemm_nt(a2, w, bias)
     return _library_linear(a2, w, bias, key)
+
+
+# PDT_NARROW: "auto" (default: per shape, the narrow HIP kernel where it timed faster than the library path),
+# "1" (always where it applies), "0" (never)
+NARROW = os.environ.get("PDT_NARROW", "auto")
+_NARROW_CHOICE: dict = {}
+
+
+def _prefer_narrow(x2: torch.Tensor, w: torch.Tensor, bias, role: str) -> bool:
+    """The narrow-GEMM kernel (ops.narrow) for a forward x W^T + b ("fwd") or a data gradient dY W ("dgrad") of a
+    narrow Linear, where it is measured faster than the library GEMM on the shape's first uncaptured call."""
+    if NARROW == "0":
+        return False
+    # dgrad: dY [M, N] . W [N, K] -- the kernel's B operand is W^T [K, N]
+    if not narrow_ok(x2, w, bias, transposed=role != "fwd"):
+        return False
+    if NARROW == "1":
+        return True
+    key = (role, tuple(x2.shape), tuple(w.shape), bias is not None, x2.device)
+    c = _NARROW_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        if role == "fwd":
+            fa = lambda: narrow_linear(x2, w, bias)                                  # noqa: E731
+            fb = lambda: F.linear(x2, w, bias)                                       # noqa: E731
+        else:
+            fa = lambda: narrow_linear(x2, w.t().contiguous(), None, w.dtype)        # noqa: E731
+            fb = lambda: (torch.mm(x2, w), _colsum(x2, w.dtype) if colsum_ok(x2.shape[1]) else None)  # noqa: E731
+        c = _NARROW_CHOICE[key] = timed_choice(fa, fb, table=_NARROW_CHOICE, key=key, name="narrow")
+    return c
 
 
 def _tall_skinny(m: int, n: int, k: int) -> bool:
@@ -312,6 +344,8 @@ class _LinearFn(torch.autograd.Function):
         base = x._base if x._base is not None else x
         ctx.dx_colsum = bias is not None and getattr(base, "_pdt_dx_colsum", False)
         x2 = x.reshape(-1, x.shape[-1])
+        if x2.is_contiguous() and _prefer_narrow(x2, weight, bias, "fwd"):
+            return _as_output(narrow_linear(x2, weight, bias)[0], (*x.shape[:-1], weight.shape[0]))
         if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
             return _as_output(nt_matmul(x2, weight, bias), (*x.shape[:-1], weight.shape[0]))
         return F.linear(x, weight, bias)
@@ -341,14 +375,25 @@ class _LinearFn(torch.autograd.Function):
             if not x2.is_contiguous():
                 x2 = x2.contiguous()
             dw = _wgrad_result(w, dy2, x2)
-        dx2 = None
-        if ctx.needs_input_grad[0]:
+        dx2 = dbf = None
+        if ctx.needs_input_grad[0] and _prefer_narrow(dy2, w, None, "dgrad"):
+            # narrow data gradient dY W = dY (W^T)^T on the HIP kernel; the bias gradient colsum(dY) from its read
+            # unless the kernel that produced dY already summed it (take_bias_grad)
+            pre = take_bias_grad(dy2) if want_db else None
+            dx2, cs = narrow_linear(dy2, w.t().contiguous(), None, w.dtype if (want_db and pre is None) else None)
+            dx = dx2.view(*dy.shape[:-1], w.shape[1])
+            if want_db:
+                if pre is not None:
+                    dbf, db = pre, pre.to(w.dtype)
+                else:
+                    db = cs
+                want_db = False
+        elif ctx.needs_input_grad[0]:
             if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
                 dx2 = nt_matmul(dy2, transpose16(w))
             else:
                 dx2 = torch.mm(dy2, w)
             dx = dx2.view(*dy.shape[:-1], w.shape[1])
-        dbf = None
         if want_db:
             db = take_bias_grad(dy2)      # summed by the kernel that produced dY (flash attention's backward)
             if db is not None:

@@ -1,0 +1,42 @@
+"""Narrow bf16 linears (in / out features <= 192, hundreds of thousands of rows) on ``csrc/kernels/narrow_gemm.hip``.
+
+SwinIR-S at the reference's Stoke config runs its attention projections on 294,912 tokens x C = 60 (qkv 60 -> 180,
+proj 60 -> 60; Stoke-DDP.py:206-208).  Those products are bandwidth-bound, and a library GEMM tiled for compute
+pays a macro tile's prologue / epilogue for two K-steps of MFMA work.  The HIP kernel keeps the weight in VGPRs,
+streams 16-row blocks through LDS and writes contiguous output blocks; its data-gradient use also returns the
+column sums of dY (the bias gradient) from the same read.  ``ops.linear`` times it against the library path per
+shape (``ops.picks``) and takes the faster.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def narrow_ok(x2: torch.Tensor, w: torch.Tensor, bias=None, transposed: bool = False) -> bool:
+    """Whether x2 @ w.T (+ bias) -- or x2 @ w with ``transposed`` (a data gradient dY W) -- fits the kernel."""
+    n_out, k_in = (w.shape[1], w.shape[0]) if transposed else (w.shape[0], w.shape[1])
+    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x2.dim() == 2
+            and w.dim() == 2 and x2.is_contiguous() and w.is_contiguous() and x2.shape[1] == k_in
+            and x2.data_ptr() % 16 == 0 and x2.shape[0] >= 16384 and _lib.available()):
+        return False
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        return False
+    return bool(_lib.require().pdt_narrow_gemm_ok(x2.shape[0], k_in, n_out))
+
+
+def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None):
+    """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192."""
+    M, K = x2.shape
+    N = w.shape[0]
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+    cs = ws = None
+    if colsum_dtype is not None:
+        lib = _lib.require()
+        cs = torch.empty(K, dtype=colsum_dtype, device=x2.device)
+        ws = torch.empty((lib.pdt_narrow_gemm_partials(M, K, N) + 64) * K, dtype=torch.float32, device=x2.device)
+    _lib.call("pdt_narrow_gemm", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N, _lib.ptr(cs),
+              _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws),
+              _lib.stream_handle(x2.device))
+    return y, cs

@@ -2040,3 +2040,43 @@ def test_norm_bwd_row_split_at_llama_shape(rms):
     assert rel_err(g.grad, gr.grad) < 1e-2
     if not rms:
         assert rel_err(beta.grad, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,N,bias", [(294912, 60, 180, True), (294912, 60, 60, True), (294912, 180, 60, False),
+                                        (20007, 60, 180, True), (16389, 120, 60, False), (40000, 188, 36, True),
+                                        (65536, 64, 128, False)])
+def test_narrow_gemm_matches_fp32(M, K, N, bias):
+    """Narrow linears (SwinIR's qkv / proj and their data gradients) on the HIP kernel: every output element against
+    fp32 torch, ragged tail blocks included, and the fused column sums of X (the data-gradient pass's bias gradient)."""
+    from pytorch_distributedtraining_amd.ops.narrow import narrow_linear, narrow_ok
+    torch.manual_seed(M % 97)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16() if bias else None
+    assert narrow_ok(x, w, b)
+    y, cs = narrow_linear(x, w, b, torch.float32)
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    err = ((y.float() - ref).abs() / (ref.abs() + 1e-2)).max().item()
+    assert rel_err(y, ref) < 5e-3 and err < 0.05, (rel_err(y, ref), err)
+    assert rel_err(cs, x.float().sum(0)) < 1e-5
+    y2, cs2 = narrow_linear(x, w, b)
+    assert cs2 is None and torch.equal(y2, y)
+
+
+def test_narrow_linear_module_grads_match_fp32(monkeypatch):
+    """ops.linear.Linear forced onto the narrow kernel (forward + data gradient with the fused bias gradient) against
+    fp32 autograd at SwinIR's qkv shape."""
+    from pytorch_distributedtraining_amd.ops import linear as L
+    monkeypatch.setattr(L, "NARROW", "1")
+    torch.manual_seed(0)
+    x = torch.randn(2, 147456, 60, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(180, 60, device=DEV) * 0.1).bfloat16().requires_grad_()
+    b = torch.randn(180, device=DEV).bfloat16().requires_grad_()
+    y = L.linear(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    (F.linear(xr, wr, br) * g.float()).sum().backward()
+    assert rel_err(y, F.linear(xr, wr, br)) < 5e-3
+    for t, r in ((x, xr), (w, wr), (b, br)):
+        assert rel_err(t.grad, r.grad) < 1e-2, rel_err(t.grad, r.grad)
