@@ -505,13 +505,33 @@ __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes
   return v;
 }
 
+// Swin's shifted-window permutation folded into the narrow-row norms (SwinIR-S, C = 60): image-order row r of
+// [B, H*W, C] <-> row img_to_win(r) of the window-ordered [B*nW, ws*ws, C] (torch.roll by -shift, then window
+// partition; the inverse of conv.hip's window_perm_kernel).  mode bit 0: the forward's y is written to / the
+// backward's dy is read from window-order rows (the block's norm1 feeds the qkv projection in window order);
+// bit 1: the forward's residual input is read from window-order rows / the backward also writes that residual's
+// gradient to window-order rows (norm2's x + attention output).  Each replaces a whole permutation pass.
+struct WinMap {
+  int H, W, ws, shift, mode;
+};
+__device__ __forceinline__ int64_t img_to_win(int64_t r, const WinMap& m) {
+  const int per_img = m.H * m.W;
+  const int64_t b = r / per_img;
+  const int t = (int)(r - b * per_img);
+  int h = t / m.W - m.shift, w = t % m.W - m.shift;
+  if (h < 0) h += m.H;
+  if (w < 0) w += m.W;
+  const int wh = h / m.ws, i = h - wh * m.ws, ww = w / m.ws, j = w - ww * m.ws;
+  return b * per_img + (int64_t)(wh * (m.W / m.ws) + ww) * m.ws * m.ws + i * m.ws + j;
+}
+
 template <typename T, typename W, bool RMS>
 __global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, const T* __restrict__ res,
                                                      const W* __restrict__ rb, T* __restrict__ sum_out,
                                                      const W* __restrict__ w,
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int rows, int N, float eps) {
+                                                     int rows, int N, float eps, WinMap wm) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
   const bool col_ok = c0 < N;
@@ -533,7 +553,7 @@ __global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, co
       Vec4<T>::load(x + row * N + c0, v);
       if (res != nullptr) {
         float r[4];
-        Vec4<T>::load(res + row * N + c0, r);
+        Vec4<T>::load(res + ((wm.mode & 2) ? img_to_win(row, wm) : row) * N + c0, r);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = to_f<T>(from_f<T>(v[k] + (r[k] + rbr[k])));   // the stored sum, rounded
         Vec4<T>::store(sum_out + row * N + c0, v);
@@ -553,7 +573,7 @@ __global__ __launch_bounds__(NT) void norm_fwd_small(const T* __restrict__ x, co
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = (v[k] - mean) * rstd * wr[k] + br[k];
-      Vec4<T>::store(y + row * N + c0, o);
+      Vec4<T>::store(y + ((wm.mode & 1) ? img_to_win(row, wm) : row) * N + c0, o);
     }
     if (row < rows && c0 == 0) {
       if (mean_out) mean_out[row] = mean;
@@ -568,7 +588,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
                                                      const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                      T* __restrict__ dx, float* __restrict__ dw_part,
                                                      float* __restrict__ db_part, float* __restrict__ ds_part,
-                                                     int rows, int N) {
+                                                     int rows, int N, WinMap wm, T* __restrict__ dr_win) {
   __shared__ __attribute__((aligned(16))) float sred[3][RPB][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane / SM_LPR, c0 = (lane % SM_LPR) * 4;
@@ -587,7 +607,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
     float mean = 0.f, rstd = 0.f;
     if (ok) {
       Vec4<T>::load(x + row * N + c0, xv);
-      Vec4<T>::load(dy + row * N + c0, g);
+      Vec4<T>::load(dy + ((wm.mode & 1) ? img_to_win(row, wm) : row) * N + c0, g);
       mean = RMS ? 0.f : mean_in[row];
       rstd = rstd_in[row];
     }
@@ -610,6 +630,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_small(const T* __restrict__ dy, c
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] += rstd * (gw[k] - bs - xh[k] * a);
       Vec4<T>::store(dx + row * N + c0, o);
+      if (wm.mode & 2) Vec4<T>::store(dr_win + img_to_win(row, wm) * N + c0, o);   // the residual's gradient
 #pragma unroll
       for (int k = 0; k < 4; ++k) dsa[k] += to_f<T>(from_f<T>(o[k]));
     }
@@ -643,12 +664,13 @@ using red::col_reduce;
 
 template <typename T, typename W, bool RMS>
 int launch_fwd(const void* x, const void* res, const void* rb, void* sum_out, const void* w, const void* b, void* y,
-               float* mean, float* rstd, int rows, int N, float eps, hipStream_t st) {
+               float* mean, float* rstd, int rows, int N, float eps, hipStream_t st, WinMap wm = {}) {
   const T* X = (const T*)x; const T* R = (const T*)res; T* S = (T*)sum_out; const W* RB = (const W*)rb;
   const W* Wt = (const W*)w; const W* B = (const W*)b; T* Y = (T*)y;
+  if (wm.mode != 0 && !small_rows(N)) return (int)hipErrorInvalidValue;   // window maps: narrow rows only
   if (small_rows(N)) {
     norm_fwd_small<T, W, RMS><<<grid_for(rows, SM_RPB, 256 * 16), NT, 0, st>>>(X, R, RB, S, Wt, B, Y, mean, rstd, rows, N,
-                                                                              eps);
+                                                                              eps, wm);
   } else if (N % 8 == 0 && N <= 8192) {
     // workgroups per CU: 64 (plain) / 96 (fused residual add) -- GPT-2 1.3B norms at 96 x 1024 tokens, 2,048
     // columns: plain 178 (16) -> 167.8 (32) -> 164.9 us (64), residual add 291 -> 250 us (96)
@@ -691,7 +713,10 @@ int bwd_partial_rows(int rows, int N) {
 // workspace: fp32, >= (3 * bwd_partial_rows(rows, N) + 192) * N floats
 template <typename T, typename W, bool RMS>
 int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
-               void* dx, void* dw, void* db, void* ds, float* ws, int rows, int N, int accumulate, hipStream_t st) {
+               void* dx, void* dw, void* db, void* ds, float* ws, int rows, int N, int accumulate, hipStream_t st,
+               WinMap wm = {}, void* dr_win = nullptr) {
+  if (wm.mode != 0 && !small_rows(N)) return (int)hipErrorInvalidValue;
+  if ((wm.mode & 2) && dr_win == nullptr) return (int)hipErrorInvalidValue;
   const T* DY = (const T*)dy; const T* X = (const T*)x; const W* Wt = (const W*)w; T* DX = (T*)dx;
   const T* DR = (const T*)dres;
   const int R = bwd_partial_rows(rows, N);
@@ -700,7 +725,8 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   float* dsp = (ds != nullptr) ? ws + (int64_t)2 * R * N : nullptr;
   static const bool split_off = [] { const char* e = getenv("PDT_NORM_SPLIT"); return e && atoi(e) == 0; }();
   if (small_rows(N)) {
-    norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N);
+    norm_bwd_small<T, W, RMS><<<R, NT, 0, st>>>(DY, X, Wt, mean, rstd, DR, DX, dwp, dbp, dsp, rows, N, wm,
+                                                 (T*)dr_win);
   } else if (split_rows_ok(N) && !split_off) {
     const int it = (N / RPB + 511) / 512;
 #define PDT_NS2(I, D, S) \
@@ -768,6 +794,41 @@ PDT_API int pdt_norm_fwd(const void* x, const void* res, const void* res_bias, v
   if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);   \
   if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);     \
   if (xdt == kF32 && wdt == kBF16) return launch_fwd<float, bf16_t, R>(x, res, res_bias, sum_out, w, b, y, mean, rstd, rows, N, eps, st);
+  if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
+#undef PDT_DISPATCH
+  return (int)hipErrorInvalidValue;
+}
+
+// The same with Swin's window permutation folded in (WinMap above; narrow rows, N <= 64): mode bit 0 = y written to
+// window-order rows, bit 1 = res read from window-order rows.  rows = B * H * W image-order rows.
+PDT_API int pdt_norm_fwd_win(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
+                             float* mean, float* rstd, int rows, int N, float eps, int xdt, int wdt, int rms, int H,
+                             int W_, int ws, int shift, int mode, hipStream_t st) {
+  if (!small_rows(N) || ws <= 0 || H % ws || W_ % ws || shift < 0 || shift >= ws || rows % (H * W_) ||
+      ((mode & 2) && (!res || !sum_out)))
+    return (int)hipErrorInvalidValue;
+  const WinMap wm{H, W_, ws, shift, mode};
+#define PDT_DISPATCH(R)                                                                                                 \
+  if (xdt == kBF16 && wdt == kBF16) return launch_fwd<bf16_t, bf16_t, R>(x, res, nullptr, sum_out, w, b, y, mean, rstd, rows, N, eps, st, wm); \
+  if (xdt == kBF16 && wdt == kF32) return launch_fwd<bf16_t, float, R>(x, res, nullptr, sum_out, w, b, y, mean, rstd, rows, N, eps, st, wm);   \
+  if (xdt == kF32 && wdt == kF32) return launch_fwd<float, float, R>(x, res, nullptr, sum_out, w, b, y, mean, rstd, rows, N, eps, st, wm);
+  if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
+#undef PDT_DISPATCH
+  return (int)hipErrorInvalidValue;
+}
+
+// mode bit 0 = dy read from window-order rows; bit 1 = dr_win (window-order rows) also receives dx -- the gradient
+// of a residual input the forward read through the map.
+PDT_API int pdt_norm_bwd_win(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                             const void* dres, void* dx, void* dw, void* db, float* ws, int rows, int N, int xdt, int wdt,
+                             int rms, int H, int W_, int wsz, int shift, int mode, void* dr_win, hipStream_t st) {
+  if (!small_rows(N) || wsz <= 0 || H % wsz || W_ % wsz || shift < 0 || shift >= wsz || rows % (H * W_))
+    return (int)hipErrorInvalidValue;
+  const WinMap wm{H, W_, wsz, shift, mode};
+#define PDT_DISPATCH(R)                                                                                                 \
+  if (xdt == kBF16 && wdt == kBF16) return launch_bwd<bf16_t, bf16_t, R>(dy, x, w, mean, rstd, dres, dx, dw, db, nullptr, ws, rows, N, 0, st, wm, dr_win); \
+  if (xdt == kBF16 && wdt == kF32) return launch_bwd<bf16_t, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, nullptr, ws, rows, N, 0, st, wm, dr_win);   \
+  if (xdt == kF32 && wdt == kF32) return launch_bwd<float, float, R>(dy, x, w, mean, rstd, dres, dx, dw, db, nullptr, ws, rows, N, 0, st, wm, dr_win);
   if (rms) { PDT_DISPATCH(true) } else { PDT_DISPATCH(false) }
 #undef PDT_DISPATCH
   return (int)hipErrorInvalidValue;

@@ -27,12 +27,14 @@ from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
 from ..ops.linear import Linear, linear
 from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
-from ..ops.norms import LayerNorm
+from ..ops.norms import LayerNorm, add_layer_norm_from_windows, layer_norm_to_windows, window_norm_ok
 from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
                                     window_reverse_shifted_add)
 
 # PDT_SWINIR_FUSED_TAIL=0: stock PixelShuffle + de-normalisation (A/B of the fused HIP tail)
 _FUSED_TAIL = os.environ.get("PDT_SWINIR_FUSED_TAIL", "1") == "1"
+# PDT_SWIN_WINDOW_NORMS=0: separate roll / partition / reverse(+residual) passes instead of the window-mapped norms
+WINDOW_NORMS = os.environ.get("PDT_SWIN_WINDOW_NORMS", "1") == "1"
 
 
 def window_partition(x, ws):
@@ -178,10 +180,19 @@ class SwinTransformerBlock(nn.Module):
                 mask = self._mask_for(H, W, x.device)
             else:
                 mask = None
+            ws, ss = self.window_size, self.shift_size
+            if WINDOW_NORMS and window_norm_ok(x, H, W, ws, ss) and self.norm1.weight.dtype == self.norm2.weight.dtype:
+                # the roll / partition / reverse permutations ride inside the two LayerNorms (ops.norms WinMap):
+                # norm1 writes window order, norm2 reads the attention output from window order
+                win = layer_norm_to_windows(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, H, W, ws, ss)
+                a = self.attn(win, mask=mask).to(x.dtype)
+                y, s = add_layer_norm_from_windows(x, a, self.norm2.weight, self.norm2.bias, self.norm2.eps, H, W,
+                                                   ws, ss)
+                return self.mlp(y, residual=s)
             h = self.norm1(x).to(x.dtype)
-            win = window_partition_shifted(h, H, W, self.window_size, self.shift_size)
+            win = window_partition_shifted(h, H, W, ws, ss)
             a = self.attn(win, mask=mask).to(x.dtype)
-            x = window_reverse_shifted_add(a, x, H, W, self.window_size, self.shift_size)
+            x = window_reverse_shifted_add(a, x, H, W, ws, ss)
             return self.mlp(self.norm2(x), residual=x)
         sc = x
         x = self.norm1(x).view(B, H, W, C)

@@ -47,6 +47,11 @@ _SIGS = {
     "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_int, c_float, c_int, c_int, c_int, c_void_p],
     "pdt_norm_bwd_workspace_floats": [c_int, c_int],
+    "pdt_norm_fwd_win": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                         c_float, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_norm_bwd_win": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                         c_void_p],
     "pdt_norm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_colsum_ws_floats": [c_int, c_int],

@@ -142,6 +142,103 @@ class _NormPassFn(torch.autograd.Function):
         return dx.view(shape), dw, db, None, None, None
 
 
+# ------------------------------------------------------------------------------------------------
+# Swin blocks: the shifted-window permutation folded into the narrow-row LayerNorms (csrc/kernels/norms.hip WinMap).
+# norm1 writes its output rows straight into window order (the qkv projection's input) and its backward reads dy
+# from window order; norm2 reads the attention output from window order as its residual input and its backward
+# writes that input's gradient back in window order.  The block then has no separate roll / partition / reverse
+# pass in either direction.
+# ------------------------------------------------------------------------------------------------
+def window_norm_ok(x, H: int, W: int, ws: int, shift: int) -> bool:
+    C = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 3 and x.shape[1] == H * W
+            and C <= 64 and C % 4 == 0 and H % ws == 0 and W % ws == 0 and 0 <= shift < ws and _lib.available())
+
+
+def _win_norm_fwd(x2, res2, w, b, eps, geom, mode):
+    rows, n = x2.shape
+    H, W, ws, shift = geom
+    y = torch.empty_like(x2)
+    s = torch.empty_like(x2) if res2 is not None else None
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x2.device)
+    _lib.call("pdt_norm_fwd_win", x2.data_ptr(), _lib.ptr(res2), _lib.ptr(s), w.data_ptr(), _lib.ptr(b), y.data_ptr(),
+              mean.data_ptr(), rstd.data_ptr(), rows, n, float(eps), _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype),
+              0, H, W, ws, shift, mode, _lib.stream_handle(x2.device))
+    return y, s, mean, rstd
+
+
+def _win_norm_bwd(dy2, x2, w, mean, rstd, need_b, dres2, geom, mode):
+    rows, n = x2.shape
+    H, W, ws, shift = geom
+    lib = _lib.require()
+    dx = torch.empty_like(x2)
+    dr = torch.empty_like(x2) if mode & 2 else None
+    dw = torch.empty_like(w)
+    db = torch.empty_like(w) if need_b else None
+    wsp = torch.empty(lib.pdt_norm_bwd_workspace_floats(rows, n), dtype=torch.float32, device=x2.device)
+    _lib.call("pdt_norm_bwd_win", dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+              _lib.ptr(dres2), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), wsp.data_ptr(), rows, n,
+              _lib.dtype_code(x2.dtype), _lib.dtype_code(w.dtype), 0, H, W, ws, shift, mode, _lib.ptr(dr),
+              _lib.stream_handle(x2.device))
+    return dx, dr, dw, db
+
+
+class _NormToWindowsFn(torch.autograd.Function):
+    """y_win = window_partition(roll(LayerNorm(x), -shift)) -- [B, H*W, C] in, [B*nW, ws*ws, C] out, one pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, geom):
+        B, L, C = x.shape
+        x2 = x.reshape(-1, C).contiguous()
+        y, _, mean, rstd = _win_norm_fwd(x2, None, weight, bias, eps, geom, 1)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.geom, ctx.has_bias, ctx.shape = geom, bias is not None, x.shape
+        ws = geom[2]
+        return y.view(-1, ws * ws, C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        dx, _, dw, db = _win_norm_bwd(dy.reshape(-1, x2.shape[1]).contiguous(), x2, w, mean, rstd, ctx.has_bias, None,
+                                      ctx.geom, 1)
+        return dx.view(ctx.shape), dw, db, None, None
+
+
+class _AddNormFromWindowsFn(torch.autograd.Function):
+    """(LayerNorm(s), s) with s = x + roll(window_reverse(a_win), +shift): the attention output joins the residual
+    stream inside the norm's read; backward returns d(s) for x and the same values in window order for a_win."""
+
+    @staticmethod
+    def forward(ctx, x, a_win, weight, bias, eps, geom):
+        B, L, C = x.shape
+        x2 = x.reshape(-1, C).contiguous()
+        a2 = a_win.reshape(-1, C).contiguous()
+        y, s, mean, rstd = _win_norm_fwd(x2, a2, weight, bias, eps, geom, 2)
+        ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.geom, ctx.has_bias, ctx.shape, ctx.wshape = geom, bias is not None, x.shape, a_win.shape
+        return y.view(x.shape), s.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, w, mean, rstd = ctx.saved_tensors
+        n = s.shape[-1]
+        dy2 = dy.reshape(-1, n).contiguous() if dy is not None else torch.zeros_like(s)
+        ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
+        dx, dr, dw, db = _win_norm_bwd(dy2, s, w, mean, rstd, ctx.has_bias, ds2, ctx.geom, 2)
+        return dx.view(ctx.shape), dr.view(ctx.wshape), dw, db, None, None
+
+
+def layer_norm_to_windows(x, weight, bias, eps, H, W, ws, shift):
+    """LayerNorm of [B, H*W, C] written in shifted-window order [B*nW, ws*ws, C] (see window_norm_ok)."""
+    return _NormToWindowsFn.apply(x, weight, bias, eps, (H, W, ws, shift))
+
+
+def add_layer_norm_from_windows(x, a_win, weight, bias, eps, H, W, ws, shift):
+    """(LayerNorm(s), s), s = x + the window-ordered ``a_win`` put back in image order (see window_norm_ok)."""
+    return _AddNormFromWindowsFn.apply(x, a_win, weight, bias, eps, (H, W, ws, shift))
+
+
 def norm_pass(x, weight, bias=None, eps=1e-5, rms=False, r_colsum=False):
     """(norm(x), x) with the stream's later gradient folded into this norm's backward pass (``_NormPassFn``)."""
     if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
