@@ -138,6 +138,8 @@ _SIGS = {
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pdt_bn_bwd_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "pdt_conv3x3_igemm_ok": [c_int, c_int, c_int, c_int, c_int],
+    "pdt_conv3x3_igemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_narrow_gemm_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_partials": [c_int64, c_int, c_int],
     "pdt_narrow_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p,

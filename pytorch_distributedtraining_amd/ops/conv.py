@@ -1,4 +1,9 @@
-"""3x3 / stride 1 / pad 1 convolution lowered to im2col (HIP kernel) + one hipBLASLt GEMM per pass.
+"""3x3 / stride 1 / pad 1 convolution: an implicit-GEMM HIP kernel for narrow NHWC bf16 channels, else im2col (HIP
+kernel) + one hipBLASLt GEMM per pass.
+
+Narrow channels (<= 64, bf16, NHWC-contiguous; SwinIR-S's 60 -> 60 body convolutions): ``csrc/kernels/conv_igemm.hip``
+forward and data gradient (the same kernel on dY with the flipped weight), picked per shape against the im2col path;
+the weight gradient keeps the im2col + row-split GEMM below.  Otherwise:
 
 For the small-channel convolutions of SwinIR-S (3->60, 60->60, 60->12 at 18 x 128 x 128)
 MIOpen has no implicit-GEMM solver in bf16 and runs its naive direct kernels (the weight gradients alone
@@ -15,6 +20,8 @@ The output is returned channels_last ([N, Cout, H, W] view of an NHWC buffer): S
 parameters / state_dict keys are unchanged.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
@@ -60,17 +67,74 @@ def _nhwc_rows(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(N * H * W, C)
 
 
+# ---- implicit GEMM (csrc/kernels/conv_igemm.hip): narrow channels (<= 64), NHWC, bf16 -- no im2col matrix at all
+IGEMM = os.environ.get("PDT_CONV_IGEMM", "auto")     # "auto": per shape, timed against im2col + GEMM; "0" / "1"
+_IG_CHOICE: dict = {}
+
+
+def _nhwc_contig(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous()
+
+
+def _igemm_ok(t: torch.Tensor, ci: int, co: int) -> bool:
+    N, _, H, W = t.shape
+    return (IGEMM != "0" and t.is_cuda and t.dtype == torch.bfloat16 and _nhwc_contig(t) and t.data_ptr() % 8 == 0
+            and bool(_lib.require().pdt_conv3x3_igemm_ok(N, H, W, ci, co)))
+
+
+def _w_taps(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> [Cout, 9 taps x 64] bf16 (channels zero-padded to 64), the igemm kernel's weight."""
+    co, ci = w.shape[0], w.shape[1]
+    m = w.permute(0, 2, 3, 1)                                       # [co, kh, kw, ci]
+    return F.pad(m, (0, 64 - ci)).reshape(co, 9 * 64).to(torch.bfloat16).contiguous()
+
+
+def _w_taps_flip(w: torch.Tensor) -> torch.Tensor:
+    """Data-gradient weight: w'[ci][kh][kw][co] = w[co][ci][2-kh][2-kw], channels (co) padded to 64."""
+    co, ci = w.shape[0], w.shape[1]
+    m = w.flip(2, 3).permute(1, 2, 3, 0)                            # [ci, kh, kw, co]
+    return F.pad(m, (0, 64 - co)).reshape(ci, 9 * 64).to(torch.bfloat16).contiguous()
+
+
+def _igemm(t: torch.Tensor, wk: torch.Tensor, bias, co: int) -> torch.Tensor:
+    """3x3 conv of the NHWC-contiguous [N, C, H, W] ``t`` with the prepared tap weight -> channels_last output."""
+    N, C, H, W = t.shape
+    y = torch.empty((N, H, W, co), dtype=torch.bfloat16, device=t.device)
+    _lib.call("pdt_conv3x3_igemm", t.data_ptr(), wk.data_ptr(), _lib.ptr(bias), y.data_ptr(), N, H, W, C, co,
+              _lib.stream_handle(t.device))
+    return y.permute(0, 3, 1, 2)
+
+
+def _prefer_igemm(key, fa, fb) -> bool:
+    if IGEMM == "1":
+        return True
+    c = _IG_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        from .picks import timed_choice
+        c = _IG_CHOICE[key] = timed_choice(fa, fb, table=_IG_CHOICE, key=key, name="conv_igemm")
+    return c
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         N, C, H, W = x.shape
         co = weight.shape[0]
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        if _igemm_ok(x, C, co) and (bias is None or bias.dtype == torch.bfloat16):
+            wk = _w_taps(weight)
+            kp = _round8(9 * C)
+            if _prefer_igemm(("fwd", tuple(x.shape), co, x.device), lambda: _igemm(x, wk, bias, co),
+                             lambda: torch.addmm(bias, _im2col(x, kp), _w_rows(weight, kp)) if bias is not None
+                             else _im2col(x, kp) @ _w_rows(weight, kp)):
+                return _igemm(x, wk, bias, co)
         kp = _round8(9 * C)
         cols = _im2col(x, kp)
         wm = _w_rows(weight, kp)
         y = torch.addmm(bias, cols, wm) if bias is not None else cols @ wm
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
         return y.view(N, H, W, co).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -95,6 +159,12 @@ class _Conv3x3Fn(torch.autograd.Function):
                 dym.float().sum(0).to(weight.dtype)
         if ctx.needs_input_grad[0]:
             kq = _round8(9 * co)
+            dyc = dym.view(N, H, W, co).permute(0, 3, 1, 2)         # NHWC-contiguous view of dY
+            if _igemm_ok(dyc, co, C):
+                wf = _w_taps_flip(weight)
+                if _prefer_igemm(("dgrad", tuple(dy.shape), C, dy.device), lambda: _igemm(dyc, wf, None, C),
+                                 lambda: _im2col(dy, kq) @ _w_flip_rows(weight.to(dy.dtype), kq)):
+                    return _igemm(dyc, wf, None, C), dw, db
             dcols = _im2col(dy, kq)
             dxm = dcols @ _w_flip_rows(weight.to(dy.dtype), kq)    # [P, Cin]
             dx = dxm.view(N, H, W, C).permute(0, 3, 1, 2)

@@ -2116,3 +2116,28 @@ def test_window_mapped_norms_match_permute_path(H, W, ws, shift, dt):
     assert rel_err(win, winr) < tol and rel_err(s, sr) < tol and rel_err(y, yr) < tol
     for t, r in ((x, xr), (w1, w1r), (b1, b1r), (w2, w2r), (b2, b2r)):
         assert rel_err(t.grad, r.grad) < 2 * tol, rel_err(t.grad, r.grad)
+
+
+@pytest.mark.parametrize("mode", ["1", "0"])
+@pytest.mark.parametrize("N,H,W,cin,cout", [(2, 32, 48, 60, 60), (3, 16, 16, 60, 12), (1, 24, 32, 32, 64),
+                                             (18, 128, 128, 60, 60)])
+def test_conv3x3_implicit_gemm_matches_fp32(N, H, W, cin, cout, mode, monkeypatch):
+    """Implicit-GEMM 3x3 conv (csrc/kernels/conv_igemm.hip; forced on, and forced off for the im2col reference path)
+    on the NHWC token views SwinIR feeds its convolutions: output, input, weight and bias gradients vs F.conv2d in
+    fp32, the last case at the reference's Stoke shape (18 x 128 x 128, 60 -> 60)."""
+    from pytorch_distributedtraining_amd.ops import conv as CV
+    monkeypatch.setattr(CV, "IGEMM", mode)
+    torch.manual_seed(N + cout)
+    x = torch.randn(N, H * W, cin, device=DEV).transpose(1, 2).reshape(N, cin, H, W).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(cout, cin, 3, 3, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(cout, device=DEV)).bfloat16().requires_grad_()
+    y = CV.conv3x3(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr, wr, br, 1, 1)
+    yr.backward(dy.float())
+    assert y.shape == yr.shape and y.permute(0, 2, 3, 1).is_contiguous()
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2 and rel_err(b.grad, br.grad) < 2e-2
