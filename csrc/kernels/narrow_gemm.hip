@@ -175,6 +175,135 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
   }
 }
 
+// ---- weight gradient dW[NO][KI] = dY[M, NO]^T X[M, KI] (the tall-skinny product of the same narrow Linears) ----
+// Both operands are token-major, and the MFMA's reduction index is the token: a workgroup of 8 waves stages 64-row
+// blocks of dY and X as plain row-major LDS images (contiguous 16-byte loads, double-buffered, one barrier per
+// block) and every fragment is two ds_read_b64_tr_b16 transposed reads (4 rows x 16 columns per 16-lane group,
+// delivered column-major).  The NO/16 x KI/16 output tiles are dealt round-robin to the 8 waves; each workgroup
+// writes one fp32 partial [NO][KI], folded by the caller's fixed-order column reduce.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+constexpr int WG_WAVES = 8;
+constexpr int WG_ROWS = 64;                    // rows per block: 2 MFMA K-steps (32 rows each)
+
+__device__ __forceinline__ u16x8 tr_frag(const bf16_t* base, int pitch, int lg, int l16, int c0, int r0) {
+  // rows r0 + 8 lg + q (first read) and r0 + 8 lg + 4 + q (second), columns c0 + 4 p, for lane 4 q + p of the
+  // 16-lane group
+  const int q = l16 >> 2, pp = l16 & 3;
+  const bf16_t* p0 = base + (r0 + 8 * lg + q) * pitch + c0 + 4 * pp;
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)p0);
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p0 + 4 * pitch));
+  return __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int NP, int KP>
+struct WgradCfg {
+  static constexpr int PN = NP + 8, PK = KP + 8;                 // LDS row pitches (elements), 16-byte rows
+  static constexpr int BUF = WG_ROWS * (PN + PK);                // one dY + X block image
+  static constexpr int TILES = (NP / 16) * (KP / 16);
+  static constexpr int TPW = (TILES + WG_WAVES - 1) / WG_WAVES; // tiles per wave
+  static constexpr int CHY = (WG_ROWS * NP / 8 + 64 * WG_WAVES - 1) / (64 * WG_WAVES);   // 16-B chunks / thread
+  static constexpr int CHX = (WG_ROWS * KP / 8 + 64 * WG_WAVES - 1) / (64 * WG_WAVES);
+};
+
+// 16-byte chunks of a 32-row block of a row-major [M, C] bf16 matrix (zero past M) -> registers
+template <int CH>
+__device__ __forceinline__ void wg_load(const bf16_t* __restrict__ A, int64_t M, int C, int64_t r0, int t,
+                                        u16x8 (&v)[CH]) {
+  const int64_t tot = (M - r0 < WG_ROWS ? M - r0 : WG_ROWS) * (int64_t)C;   // valid elements of the block
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int c = t + 64 * WG_WAVES * i;
+    u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (8 * (int64_t)c + 8 <= tot) {
+      z = *reinterpret_cast<const u16x8*>(A + r0 * C + 8 * (int64_t)c);
+    } else if (8 * (int64_t)c < tot) {         // C % 4 == 0: a last half chunk
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(A + r0 * C + 8 * (int64_t)c);
+      z[0] = lo[0]; z[1] = lo[1]; z[2] = lo[2]; z[3] = lo[3];
+    }
+    v[i] = z;
+  }
+}
+template <int CH>
+__device__ __forceinline__ void wg_put(bf16_t* img, int pitch, int C, int t, const u16x8 (&v)[CH]) {
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int c = t + 64 * WG_WAVES * i;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = 8 * c + 4 * h;
+      if (e < WG_ROWS * C) {
+        const int r = e / C, col = e - r * C;
+        *reinterpret_cast<u16x4*>(img + r * pitch + col) = u16x4{v[i][4 * h], v[i][4 * h + 1], v[i][4 * h + 2], v[i][4 * h + 3]};
+      }
+    }
+  }
+}
+
+template <int NP, int KP>
+__global__ __launch_bounds__(64 * WG_WAVES, 1) void narrow_wgrad_kernel(const bf16_t* __restrict__ dY,
+                                                                        const bf16_t* __restrict__ X,
+                                                                        float* __restrict__ part, int64_t M, int NO,
+                                                                        int KI) {
+  typedef WgradCfg<NP, KP> Cfg;
+  extern __shared__ __attribute__((aligned(16))) bf16_t wsm[];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  // zero both images once: padding columns (NO .. NP-1, KI .. KP-1) stay zero
+  for (int e = t; e < 2 * Cfg::BUF; e += 64 * WG_WAVES) wsm[e] = 0;
+  f32x4 acc[Cfg::TPW];
+#pragma unroll
+  for (int i = 0; i < Cfg::TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nblk = (M + WG_ROWS - 1) / WG_ROWS;
+  u16x8 vy[Cfg::CHY], vx[Cfg::CHX];
+  int64_t blk = blockIdx.x;
+  if (blk < nblk) {
+    wg_load<Cfg::CHY>(dY, M, NO, blk * WG_ROWS, t, vy);
+    wg_load<Cfg::CHX>(X, M, KI, blk * WG_ROWS, t, vx);
+  }
+  __syncthreads();
+  for (int it = 0; blk < nblk; blk += gridDim.x, ++it) {
+    bf16_t* ys = wsm + (it & 1) * Cfg::BUF;
+    bf16_t* xs = ys + WG_ROWS * Cfg::PN;
+    wg_put<Cfg::CHY>(ys, Cfg::PN, NO, t, vy);
+    wg_put<Cfg::CHX>(xs, Cfg::PK, KI, t, vx);
+    if (blk + gridDim.x < nblk) {
+      wg_load<Cfg::CHY>(dY, M, NO, (blk + gridDim.x) * WG_ROWS, t, vy);
+      wg_load<Cfg::CHX>(X, M, KI, (blk + gridDim.x) * WG_ROWS, t, vx);
+    }
+    __syncthreads();    // this block's images are written (the other buffer was last read before this barrier)
+#pragma unroll
+    for (int i = 0; i < Cfg::TPW; ++i) {
+      const int tile = wv + WG_WAVES * i;
+      if (tile < Cfg::TILES) {
+        const int tn = tile / (KP / 16), tk = tile - tn * (KP / 16);
+#pragma unroll
+        for (int ks = 0; ks < WG_ROWS / 32; ++ks)
+          acc[i] = mfma16(tr_frag(ys, Cfg::PN, lg, l16, 16 * tn, 32 * ks), tr_frag(xs, Cfg::PK, lg, l16, 16 * tk, 32 * ks),
+                          acc[i]);
+      }
+    }
+  }
+  // C[n = 16 tn + 4 lg + r][k = 16 tk + l16] -> this workgroup's partial [NO][KI]
+  float* dst = part + (int64_t)blockIdx.x * NO * KI;
+#pragma unroll
+  for (int i = 0; i < Cfg::TPW; ++i) {
+    const int tile = wv + WG_WAVES * i;
+    if (tile < Cfg::TILES) {
+      const int tn = tile / (KP / 16), tk = tile - tn * (KP / 16);
+      const int k = 16 * tk + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * tn + 4 * lg + r;
+        if (n < NO && k < KI) dst[n * KI + k] = acc[i][r];
+      }
+    }
+  }
+}
+
+template <int NP, int KP>
+size_t wgrad_lds() { return sizeof(bf16_t) * 2 * (size_t)WgradCfg<NP, KP>::BUF; }
+
 inline int pad_to(int v, int q) { return (v + q - 1) / q * q; }
 
 // resident workgroups: 4 per CU for the small (64 x 64) weight (115 VGPRs), 2 otherwise (up to 250 VGPRs);
@@ -224,5 +353,42 @@ PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void
     if (wdt == kBF16) red::col_reduce<bf16_t>(part, R, KI, (bf16_t*)colsum_out, ws2, 0, st);
     else red::col_reduce<float>(part, R, KI, (float*)colsum_out, ws2, 0, st);
   }
+  return (int)hipGetLastError();
+}
+
+// ---- dW [NO, KI] (wdt: kF32 or kBF16) = dY[M, NO]^T X[M, KI]; dY, X contiguous, 16-byte aligned; NO, KI <= 192,
+// multiples of 4.  ws >= pdt_narrow_wgrad_ws_floats(M, NO, KI) floats.
+namespace {
+// two workgroups per CU (their blocks' loads overlap each other's MFMAs and barriers)
+int wgrad_grid(int64_t M) {
+  const int64_t nblk = (M + WG_ROWS - 1) / WG_ROWS;
+  return (int)(nblk < 512 ? nblk : 512);
+}
+}  // namespace
+PDT_API int pdt_narrow_wgrad_ok(int64_t M, int NO, int KI) {
+  return (M > 0 && NO >= 4 && NO <= 192 && KI >= 4 && KI <= 192 && NO % 4 == 0 && KI % 4 == 0) ? 1 : 0;
+}
+PDT_API int64_t pdt_narrow_wgrad_ws_floats(int64_t M, int NO, int KI) {
+  return ((int64_t)wgrad_grid(M) + 64) * NO * KI;
+}
+PDT_API int pdt_narrow_wgrad(const void* dY, const void* X, void* dW, int64_t M, int NO, int KI, int wdt, float* ws,
+                             hipStream_t st) {
+  if (!pdt_narrow_wgrad_ok(M, NO, KI) || ((uintptr_t)dY & 15) || ((uintptr_t)X & 15)) return (int)hipErrorInvalidValue;
+  const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
+  const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
+  const int grid = wgrad_grid(M);
+#define PDT_WG(NP_, KP_)                                                                                       \
+  narrow_wgrad_kernel<NP_, KP_><<<grid, 64 * WG_WAVES, wgrad_lds<NP_, KP_>(), st>>>(                          \
+      (const bf16_t*)dY, (const bf16_t*)X, ws, M, NO, KI)
+#define PDT_WG_K(NP_) \
+  do { if (KP == 64) PDT_WG(NP_, 64); else if (KP == 128) PDT_WG(NP_, 128); else PDT_WG(NP_, 192); } while (0)
+  if (NP == 64) PDT_WG_K(64);
+  else if (NP == 128) PDT_WG_K(128);
+  else PDT_WG_K(192);
+#undef PDT_WG_K
+#undef PDT_WG
+  float* ws2 = ws + (int64_t)grid * NO * KI;
+  if (wdt == kBF16) red::col_reduce<bf16_t>(ws, grid, NO * KI, (bf16_t*)dW, ws2, 0, st);
+  else red::col_reduce<float>(ws, grid, NO * KI, (float*)dW, ws2, 0, st);
   return (int)hipGetLastError();
 }

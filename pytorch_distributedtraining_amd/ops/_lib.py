@@ -140,6 +140,9 @@ _SIGS = {
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_conv3x3_igemm_ok": [c_int, c_int, c_int, c_int, c_int],
     "pdt_conv3x3_igemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_narrow_wgrad_ok": [c_int64, c_int, c_int],
+    "pdt_narrow_wgrad_ws_floats": [c_int64, c_int, c_int],
+    "pdt_narrow_wgrad": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p],
     "pdt_narrow_gemm_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_partials": [c_int64, c_int, c_int],
     "pdt_narrow_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p,
@@ -178,7 +181,7 @@ _SIGS = {
                              c_int64, c_int, c_int64, c_int, c_int, c_void_p],
 }
 
-_RET64 = {"pdt_swin_mlp_ws_floats", "pdt_fp8_gelu_bwd_ws_floats", "pdt_flash_attn_colsum_ws_floats"}
+_RET64 = {"pdt_swin_mlp_ws_floats", "pdt_narrow_wgrad_ws_floats", "pdt_fp8_gelu_bwd_ws_floats", "pdt_flash_attn_colsum_ws_floats"}
 
 F32, BF16, F16, F64 = 0, 1, 2, 3
 

@@ -40,3 +40,25 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
               _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws),
               _lib.stream_handle(x2.device))
     return y, cs
+
+
+def narrow_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> bool:
+    """dW = dy2^T x2 with both operands token-major bf16 and both feature counts narrow (<= 192)."""
+    return (dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.dim() == 2
+            and x2.dim() == 2 and dy2.shape[0] == x2.shape[0] and dy2.is_contiguous() and x2.is_contiguous()
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0 and dy2.shape[0] >= 16384
+            and out_dtype in (torch.float32, torch.bfloat16) and _lib.available()
+            and bool(_lib.require().pdt_narrow_wgrad_ok(dy2.shape[0], dy2.shape[1], x2.shape[1])))
+
+
+def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """dW [N, K] = dy2[M, N]^T x2[M, K] on the narrow weight-gradient kernel (transposed LDS reads, one fp32
+    partial per workgroup, fixed-order reduce)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    lib = _lib.require()
+    out = torch.empty((N, K), dtype=out_dtype, device=dy2.device)
+    ws = torch.empty(lib.pdt_narrow_wgrad_ws_floats(M, N, K), dtype=torch.float32, device=dy2.device)
+    _lib.call("pdt_narrow_wgrad", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), M, N, K, _lib.dtype_code(out_dtype),
+              ws.data_ptr(), _lib.stream_handle(dy2.device))
+    return out

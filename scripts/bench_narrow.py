@@ -10,7 +10,8 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 from pytorch_distributedtraining_amd.ops.activations import _colsum  # noqa: E402
-from pytorch_distributedtraining_amd.ops.narrow import narrow_linear  # noqa: E402
+from pytorch_distributedtraining_amd.ops.linear import _library_wgrad  # noqa: E402
+from pytorch_distributedtraining_amd.ops.narrow import narrow_linear, narrow_wgrad  # noqa: E402
 
 
 def t_ms(fn, it=20):
@@ -40,6 +41,15 @@ for name, K, N, bias, role in [("qkv fwd", 60, 180, True, "fwd"), ("proj fwd", 6
         tn = t_ms(lambda: narrow_linear(x, w, None, torch.bfloat16))
         wl = w.t().contiguous()
         tl = t_ms(lambda: (torch.mm(x, wl), _colsum(x, torch.bfloat16)))
+    gb = (M * K + M * N) * 2 / 1e9
+    print(json.dumps({"op": name, "M": M, "K": K, "N": N, "narrow_us": round(1000 * tn, 1),
+                      "library_us": round(1000 * tl, 1), "narrow_TBps": round(gb / tn, 2),
+                      "speedup": round(tl / tn, 2)}), flush=True)
+for name, N, K in [("qkv wgrad", 180, 60), ("proj wgrad", 60, 60)]:
+    dy = torch.randn(M, N, device=dev).bfloat16()
+    x = torch.randn(M, K, device=dev).bfloat16()
+    tn = t_ms(lambda: narrow_wgrad(dy, x, torch.bfloat16))
+    tl = t_ms(lambda: _library_wgrad(dy, x, torch.bfloat16))
     gb = (M * K + M * N) * 2 / 1e9
     print(json.dumps({"op": name, "M": M, "K": K, "N": N, "narrow_us": round(1000 * tn, 1),
                       "library_us": round(1000 * tl, 1), "narrow_TBps": round(gb / tn, 2),

@@ -2141,3 +2141,20 @@ def test_conv3x3_implicit_gemm_matches_fp32(N, H, W, cin, cout, mode, monkeypatc
     assert rel_err(y, yr) < 1e-2
     assert rel_err(x.grad, xr.grad) < 2e-2
     assert rel_err(w.grad, wr.grad) < 2e-2 and rel_err(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(294912, 180, 60), (294912, 60, 60), (20011, 60, 180), (65536, 128, 36),
+                                   (16400, 192, 192)])
+def test_narrow_wgrad_matches_fp32(M, N, K):
+    """Tall-skinny weight gradient dW = dY^T X on the narrow kernel (transposed LDS fragment reads): fp32 and bf16
+    outputs against the fp32 product, ragged row counts included."""
+    from pytorch_distributedtraining_amd.ops.narrow import narrow_wgrad, narrow_wgrad_ok
+    torch.manual_seed(M % 89 + N)
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    ref = dy.float().t() @ x.float()
+    for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 8e-3)):
+        assert narrow_wgrad_ok(dy, x, dt)
+        g = narrow_wgrad(dy, x, dt)
+        assert g.dtype == dt and g.shape == (N, K)
+        assert rel_err(g, ref) < tol, (dt, rel_err(g, ref))
