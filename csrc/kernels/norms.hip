@@ -696,7 +696,11 @@ int launch_fwd(const void* x, const void* res, const void* rb, void* sum_out, co
 int bwd_partial_rows(int rows, int N) {
   // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
   // a few rows per wave (so the row prefetch pays) while covering the chip: ~2 waves per SIMD
-  if (small_rows(N)) return grid_for(rows, SM_RPB * 8, 512);
+  if (small_rows(N)) {
+    // PDT_NORM_SMALL_BWD_WG overrides the workgroup cap of the narrow-row backward
+    static const int scap = [] { const char* e = getenv("PDT_NORM_SMALL_BWD_WG"); return e ? atoi(e) : 512; }();
+    return grid_for(rows, SM_RPB * 8, scap);
+  }
   // 256 partial-row workgroups: the flagship step 668.1 / 669.7 -> 664.8 / 669.3 ms against 512, the norm_pass
   // backward alone 360-405 -> 377-386 us (profiles/r5/r5v_norm_grid_ab.txt); PDT_NORM_BWD_WG overrides
   static const int cap = [] { const char* e = getenv("PDT_NORM_BWD_WG"); return e ? atoi(e) : 256; }();

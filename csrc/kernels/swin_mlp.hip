@@ -20,6 +20,7 @@
 // dW1 / dW2, accumulate over all the workgroup's tokens in registers and write one fp32 partial per
 // workgroup; a column-sum kernel adds the partials (deterministic, no atomics).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pdt {
 namespace {
@@ -371,8 +372,10 @@ PDT_API int64_t pdt_swin_mlp_ws_floats(int nb) {
   return ((int64_t)nb + (nb + RED_SLICE - 1) / RED_SLICE) * 2 * HPAD * CPAD;
 }
 PDT_API int pdt_swin_mlp_bwd_blocks(int64_t T) {
+  // one workgroup per CU by default (fp32 partials stay 16 MB); PDT_SWIN_MLP_BWD_WG overrides
+  static const int cap = [] { const char* e = getenv("PDT_SWIN_MLP_BWD_WG"); return e ? atoi(e) : 256; }();
   const int64_t ch = (T + 63) / 64;
-  return (int)(ch < 256 ? ch : 256);   // one workgroup per CU: fp32 partials stay 16 MB
+  return (int)(ch < cap ? ch : cap);
 }
 
 // y = MLP(x) (+ res when non-null, same [T, C] layout as y)
