@@ -697,8 +697,9 @@ int bwd_partial_rows(int rows, int N) {
   // enough waves to cover HBM latency (the row kernel holds ~120 VGPRs at N = 2048: 4 waves/SIMD)
   // a few rows per wave (so the row prefetch pays) while covering the chip: ~2 waves per SIMD
   if (small_rows(N)) {
-    // PDT_NORM_SMALL_BWD_WG overrides the workgroup cap of the narrow-row backward
-    static const int scap = [] { const char* e = getenv("PDT_NORM_SMALL_BWD_WG"); return e ? atoi(e) : 512; }();
+    // 1024 workgroups: SwinIR-S bf16 426.3 -> 433.5 samples/s against 512 (2048: 433.1;
+    // profiles/r6/r6k_grid_ab.jsonl); PDT_NORM_SMALL_BWD_WG overrides
+    static const int scap = [] { const char* e = getenv("PDT_NORM_SMALL_BWD_WG"); return e ? atoi(e) : 1024; }();
     return grid_for(rows, SM_RPB * 8, scap);
   }
   // 256 partial-row workgroups: the flagship step 668.1 / 669.7 -> 664.8 / 669.3 ms against 512, the norm_pass
