@@ -304,6 +304,224 @@ __global__ __launch_bounds__(64 * WG_WAVES, 1) void narrow_wgrad_kernel(const bf
 template <int NP, int KP>
 size_t wgrad_lds() { return sizeof(bf16_t) * 2 * (size_t)WgradCfg<NP, KP>::BUF; }
 
+// ---- fp32 family (the reference's own precision: Stoke-DDP.py trains with fp16=None) on v_mfma_f32_16x16x4_f32,
+// exact f32 (an fmaf chain per output): A / B fragments are ONE float per lane (A[row = l & 15][k = l >> 4],
+// B[k = l >> 4][col = l & 15]), so the weight tile and the X / dY tiles are plain row-major fp32 LDS images with odd
+// row pitches (b32 fragment reads of 16 rows land on distinct banks).  Structure as the bf16 kernels above: the
+// forward / data gradient keep the weight in LDS (shared by 8 waves), each wave streams 16-row blocks; the weight
+// gradient reduces 64-row blocks of dY and X, tiles dealt to the waves, one fp32 partial per workgroup.
+constexpr int NW32 = 8;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int KP, int NP>
+struct Narrow32Cfg {
+  static constexpr int BPF = KP + 1;                        // weight row pitch (floats)
+  static constexpr int XPF = KP + 1;                        // X tile row pitch
+  static constexpr int WAVE = (16 * XPF > 16 * NP ? 16 * XPF : 16 * NP);   // X tile, aliased by the Y staging
+  static constexpr int CH = (4 * KP + 63) / 64;              // 16-byte X chunks per lane per block (upper bound)
+};
+
+template <int KP, int NP>
+__global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const float* __restrict__ X,
+                                                                       const float* __restrict__ B,
+                                                                       const float* __restrict__ bias,
+                                                                       float* __restrict__ Y,
+                                                                       float* __restrict__ colsum_part, int64_t M,
+                                                                       int KI, int NO) {
+  typedef Narrow32Cfg<KP, NP> Cfg;
+  constexpr int NT = NP / 16;
+  extern __shared__ __attribute__((aligned(16))) float n32[];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  float* Bs = n32;                                           // [NP][BPF], zero outside [NO, KI]
+  float* Xs = n32 + NP * Cfg::BPF + wv * Cfg::WAVE;          // [16][XPF]; after the MFMAs: Y staging [16][NO]
+  for (int e = t; e < NP * Cfg::BPF; e += 64 * NW32) {
+    const int n = e / Cfg::BPF, k = e - n * Cfg::BPF;
+    Bs[e] = (n < NO && k < KI) ? B[(int64_t)n * KI + k] : 0.f;
+  }
+  float bcol[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = 16 * nt + l16;
+    bcol[nt] = (bias != nullptr && n < NO) ? bias[n] : 0.f;
+  }
+  float cs[3] = {0.f, 0.f, 0.f};
+  __syncthreads();
+  const int64_t nblk = (M + 15) / 16;
+  const int64_t gw = (int64_t)blockIdx.x * NW32 + wv, nwaves = (int64_t)gridDim.x * NW32;
+  f32x4 ch[Cfg::CH];
+  auto load = [&](int64_t blk) {
+    const int64_t r0 = blk * 16;
+    const int rows = M - r0 < 16 ? (int)(M - r0) : 16;
+    const int n4 = rows * KI / 4;                            // KI % 4 == 0: 16-byte chunks never straddle rows
+#pragma unroll
+    for (int i = 0; i < Cfg::CH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < n4) ch[i] = *reinterpret_cast<const f32x4*>(X + r0 * KI + 4 * c);
+    }
+  };
+  if (gw < nblk) load(gw);
+  for (int64_t blk = gw; blk < nblk; blk += nwaves) {
+    const int rows = M - blk * 16 < 16 ? (int)(M - blk * 16) : 16;
+    wave_sync();
+    // the X tile: rows < `rows` from the chunks, columns KI .. KP-1 and rows >= `rows` zero
+    for (int e = lane; e < 16 * Cfg::XPF; e += 64) Xs[e] = 0.f;
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < Cfg::CH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < rows * KI / 4) {
+        const int r = (4 * c) / KI, col = 4 * c - r * KI;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Xs[r * Cfg::XPF + col + e] = ch[i][e];
+      }
+    }
+    if (blk + nwaves < nblk) load(blk + nwaves);
+    wave_sync();
+    if (colsum_part != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int c = lane + 64 * j;
+        if (c < KI)
+          for (int r = 0; r < rows; ++r) cs[j] += Xs[r * Cfg::XPF + c];
+      }
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int ks = 0; ks < KP / 4; ++ks) {
+      const float a = Xs[l16 * Cfg::XPF + 4 * ks + lg];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma4(a, Bs[(16 * nt + l16) * Cfg::BPF + 4 * ks + lg], acc[nt]);
+    }
+    wave_sync();                                             // X tile reads done: the staging aliases it
+    float* Ys = Xs;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = 16 * nt + l16;
+      if (n < NO) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ys[(4 * lg + r) * NO + n] = acc[nt][r] + bcol[nt];
+      }
+    }
+    wave_sync();
+    float* dst = Y + blk * 16 * NO;
+    const int n4 = rows * NO / 4;
+    for (int c = lane; c < n4; c += 64) *reinterpret_cast<f32x4*>(dst + 4 * c) = *reinterpret_cast<const f32x4*>(Ys + 4 * c);
+  }
+  if (colsum_part != nullptr) {
+    float* dstp = colsum_part + gw * KI;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = lane + 64 * j;
+      if (c < KI) dstp[c] = cs[j];
+    }
+  }
+}
+
+template <int NP, int KP>
+struct Wgrad32Cfg {
+  static constexpr int PN = NP + 1, PK = KP + 1;
+  static constexpr int BUF = 64 * (PN + PK);
+  static constexpr int TILES = (NP / 16) * (KP / 16);
+  static constexpr int TPW = (TILES + NW32 - 1) / NW32;
+  static constexpr int CHY = (64 * NP / 4 + 64 * NW32 - 1) / (64 * NW32);
+  static constexpr int CHX = (64 * KP / 4 + 64 * NW32 - 1) / (64 * NW32);
+};
+
+template <int CH>
+__device__ __forceinline__ void w32_load(const float* __restrict__ A, int64_t M, int C, int64_t r0, int t,
+                                         f32x4 (&v)[CH]) {
+  const int64_t rows = M - r0 < 64 ? M - r0 : 64;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int c = t + 64 * NW32 * i;
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if (4 * (int64_t)c < rows * C) z = *reinterpret_cast<const f32x4*>(A + r0 * C + 4 * (int64_t)c);
+    v[i] = z;
+  }
+}
+template <int CH>
+__device__ __forceinline__ void w32_put(float* img, int pitch, int C, int t, const f32x4 (&v)[CH]) {
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int c = t + 64 * NW32 * i;
+    if (4 * c < 64 * C) {
+      const int r = (4 * c) / C, col = 4 * c - r * C;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) img[r * pitch + col + e] = v[i][e];
+    }
+  }
+}
+
+template <int NP, int KP>
+__global__ __launch_bounds__(64 * NW32, 1) void narrow_wgrad_f32_kernel(const float* __restrict__ dY,
+                                                                        const float* __restrict__ X,
+                                                                        float* __restrict__ part, int64_t M, int NO,
+                                                                        int KI) {
+  typedef Wgrad32Cfg<NP, KP> Cfg;
+  extern __shared__ __attribute__((aligned(16))) float w32[];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  for (int e = t; e < 2 * Cfg::BUF; e += 64 * NW32) w32[e] = 0.f;     // padding columns stay zero
+  f32x4 acc[Cfg::TPW];
+#pragma unroll
+  for (int i = 0; i < Cfg::TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nblk = (M + 63) / 64;
+  f32x4 vy[Cfg::CHY], vx[Cfg::CHX];
+  int64_t blk = blockIdx.x;
+  if (blk < nblk) {
+    w32_load<Cfg::CHY>(dY, M, NO, blk * 64, t, vy);
+    w32_load<Cfg::CHX>(X, M, KI, blk * 64, t, vx);
+  }
+  __syncthreads();
+  for (int it = 0; blk < nblk; blk += gridDim.x, ++it) {
+    float* ys = w32 + (it & 1) * Cfg::BUF;
+    float* xs = ys + 64 * Cfg::PN;
+    w32_put<Cfg::CHY>(ys, Cfg::PN, NO, t, vy);
+    w32_put<Cfg::CHX>(xs, Cfg::PK, KI, t, vx);
+    if (blk + gridDim.x < nblk) {
+      w32_load<Cfg::CHY>(dY, M, NO, (blk + gridDim.x) * 64, t, vy);
+      w32_load<Cfg::CHX>(X, M, KI, (blk + gridDim.x) * 64, t, vx);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < Cfg::TPW; ++i) {
+      const int tile = wv + NW32 * i;
+      if (tile < Cfg::TILES) {
+        const int tn = tile / (KP / 16), tk = tile - tn * (KP / 16);
+#pragma unroll 4
+        for (int ks = 0; ks < 16; ++ks)        // 64 rows = 16 K-steps of 4 tokens
+          acc[i] = mfma4(ys[(4 * ks + lg) * Cfg::PN + 16 * tn + l16], xs[(4 * ks + lg) * Cfg::PK + 16 * tk + l16],
+                         acc[i]);
+      }
+    }
+  }
+  float* dst = part + (int64_t)blockIdx.x * NO * KI;
+#pragma unroll
+  for (int i = 0; i < Cfg::TPW; ++i) {
+    const int tile = wv + NW32 * i;
+    if (tile < Cfg::TILES) {
+      const int tn = tile / (KP / 16), tk = tile - tn * (KP / 16);
+      const int k = 16 * tk + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * tn + 4 * lg + r;
+        if (n < NO && k < KI) dst[n * KI + k] = acc[i][r];
+      }
+    }
+  }
+}
+
+template <int KP, int NP>
+size_t narrow32_lds() { return sizeof(float) * ((size_t)NP * Narrow32Cfg<KP, NP>::BPF + (size_t)NW32 * Narrow32Cfg<KP, NP>::WAVE); }
+template <int NP, int KP>
+size_t wgrad32_lds() { return sizeof(float) * 2 * (size_t)Wgrad32Cfg<NP, KP>::BUF; }
+
 inline int pad_to(int v, int q) { return (v + q - 1) / q * q; }
 
 // resident workgroups: 4 per CU for the small (64 x 64) weight (115 VGPRs), 2 otherwise (up to 250 VGPRs);
@@ -390,5 +608,92 @@ PDT_API int pdt_narrow_wgrad(const void* dY, const void* X, void* dW, int64_t M,
   float* ws2 = ws + (int64_t)grid * NO * KI;
   if (wdt == kBF16) red::col_reduce<bf16_t>(ws, grid, NO * KI, (bf16_t*)dW, ws2, 0, st);
   else red::col_reduce<float>(ws, grid, NO * KI, (float*)dW, ws2, 0, st);
+  return (int)hipGetLastError();
+}
+
+// ---- fp32: Y [M, NO] = X [M, KI] . B [NO, KI]^T (+ bias [NO]); colsum_out (nullable, fp32 [KI]) as the bf16 entry,
+// ws >= (pdt_narrow_gemm_f32_partials(M) + 64) * KI floats.  X, Y contiguous, 16-byte aligned; KI, NO <= 192, % 4.
+namespace {
+int narrow32_grid(int64_t M) {
+  const int64_t nblk = (M + 15) / 16;
+  const int64_t wg = (nblk + NW32 - 1) / NW32;
+  return (int)(wg < 256 ? wg : 256);                         // one 8-wave workgroup per CU (the LDS weight tile)
+}
+template <int KP, int NP>
+bool narrow32_attr() {
+  static const bool ok =
+      hipFuncSetAttribute((const void*)narrow_gemm_f32_kernel<KP, NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)narrow32_lds<KP, NP>()) == hipSuccess;
+  return ok;
+}
+template <int NP, int KP>
+bool wgrad32_attr() {
+  static const bool ok =
+      hipFuncSetAttribute((const void*)narrow_wgrad_f32_kernel<NP, KP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)wgrad32_lds<NP, KP>()) == hipSuccess;
+  return ok;
+}
+}  // namespace
+PDT_API int pdt_narrow_gemm_f32_partials(int64_t M) { return narrow32_grid(M) * NW32; }
+// the weight tile plus 8 waves' X tiles must fit the 160 KiB of LDS
+PDT_API int pdt_narrow_gemm_f32_ok(int64_t M, int KI, int NO) {
+  if (M <= 0 || KI < 4 || KI > 192 || NO < 4 || NO > 192 || KI % 4 || NO % 4) return 0;
+  const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
+  const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
+  const size_t lds = sizeof(float) * ((size_t)NP * (KP + 1) + (size_t)NW32 * (16 * (KP + 1) > 16 * NP ? 16 * (KP + 1) : 16 * NP));
+  return lds <= 160 * 1024 ? 1 : 0;
+}
+PDT_API int pdt_narrow_wgrad_f32_ok(int64_t M, int NO, int KI) {
+  if (!pdt_narrow_wgrad_ok(M, NO, KI)) return 0;
+  const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
+  const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
+  return sizeof(float) * 2 * 64 * (size_t)(NP + 1 + KP + 1) <= 160 * 1024 ? 1 : 0;
+}
+PDT_API int pdt_narrow_gemm_f32(const float* X, const float* B, const float* bias, float* Y, int64_t M, int KI, int NO,
+                                float* colsum_out, float* ws, hipStream_t st) {
+  if (!pdt_narrow_gemm_f32_ok(M, KI, NO) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15)) return (int)hipErrorInvalidValue;
+  const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
+  const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
+  const int grid = narrow32_grid(M);
+  float* part = colsum_out ? ws : nullptr;
+#define PDT_N32(KP_, NP_)                                                                                         \
+  do {                                                                                                            \
+    if (!narrow32_attr<KP_, NP_>()) return (int)hipErrorInvalidValue;                                             \
+    narrow_gemm_f32_kernel<KP_, NP_><<<grid, 64 * NW32, narrow32_lds<KP_, NP_>(), st>>>(X, B, bias, Y, part, M, KI, NO); \
+  } while (0)
+#define PDT_N32_N(KP_) \
+  do { if (NP == 64) PDT_N32(KP_, 64); else if (NP == 128) PDT_N32(KP_, 128); else PDT_N32(KP_, 192); } while (0)
+  if (KP == 64) PDT_N32_N(64);
+  else if (KP == 128) PDT_N32_N(128);
+  else PDT_N32_N(192);
+#undef PDT_N32_N
+#undef PDT_N32
+  if (colsum_out) {
+    const int R = grid * NW32;
+    red::col_reduce<float>(part, R, KI, colsum_out, ws + (int64_t)R * KI, 0, st);
+  }
+  return (int)hipGetLastError();
+}
+// fp32 dW [NO, KI] = dY^T X; ws >= pdt_narrow_wgrad_ws_floats(M, NO, KI) floats
+PDT_API int pdt_narrow_wgrad_f32(const float* dY, const float* X, float* dW, int64_t M, int NO, int KI, float* ws,
+                                 hipStream_t st) {
+  if (!pdt_narrow_wgrad_f32_ok(M, NO, KI) || ((uintptr_t)dY & 15) || ((uintptr_t)X & 15))
+    return (int)hipErrorInvalidValue;
+  const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
+  const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
+  const int grid = wgrad_grid(M);
+#define PDT_W32(NP_, KP_)                                                                                       \
+  do {                                                                                                          \
+    if (!wgrad32_attr<NP_, KP_>()) return (int)hipErrorInvalidValue;                                            \
+    narrow_wgrad_f32_kernel<NP_, KP_><<<grid, 64 * NW32, wgrad32_lds<NP_, KP_>(), st>>>(dY, X, ws, M, NO, KI); \
+  } while (0)
+#define PDT_W32_K(NP_) \
+  do { if (KP == 64) PDT_W32(NP_, 64); else if (KP == 128) PDT_W32(NP_, 128); else PDT_W32(NP_, 192); } while (0)
+  if (NP == 64) PDT_W32_K(64);
+  else if (NP == 128) PDT_W32_K(128);
+  else PDT_W32_K(192);
+#undef PDT_W32_K
+#undef PDT_W32
+  red::col_reduce<float>(ws, grid, NO * KI, dW, ws + (int64_t)grid * NO * KI, 0, st);
   return (int)hipGetLastError();
 }

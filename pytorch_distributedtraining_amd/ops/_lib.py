@@ -140,6 +140,12 @@ _SIGS = {
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_conv3x3_igemm_ok": [c_int, c_int, c_int, c_int, c_int],
     "pdt_conv3x3_igemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_narrow_gemm_f32_ok": [c_int64, c_int, c_int],
+    "pdt_narrow_gemm_f32_partials": [c_int64],
+    "pdt_narrow_gemm_f32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p,
+                            c_void_p],
+    "pdt_narrow_wgrad_f32_ok": [c_int64, c_int, c_int],
+    "pdt_narrow_wgrad_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p],
     "pdt_narrow_wgrad_ok": [c_int64, c_int, c_int],
     "pdt_narrow_wgrad_ws_floats": [c_int64, c_int, c_int],
     "pdt_narrow_wgrad": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -1,4 +1,5 @@
-"""Narrow bf16 linears (in / out features <= 192, hundreds of thousands of rows) on ``csrc/kernels/narrow_gemm.hip``.
+"""Narrow linears (in / out features <= 192, hundreds of thousands of rows) on ``csrc/kernels/narrow_gemm.hip``:
+bf16 on 16x16x32 bf16 MFMAs, fp32 (the reference's precision) on exact-f32 16x16x4 MFMAs.
 
 SwinIR-S at the reference's Stoke config runs its attention projections on 294,912 tokens x C = 60 (qkv 60 -> 180,
 proj 60 -> 60; Stoke-DDP.py:206-208).  Those products are bandwidth-bound, and a library GEMM tiled for compute
@@ -17,19 +18,32 @@ from . import _lib
 def narrow_ok(x2: torch.Tensor, w: torch.Tensor, bias=None, transposed: bool = False) -> bool:
     """Whether x2 @ w.T (+ bias) -- or x2 @ w with ``transposed`` (a data gradient dY W) -- fits the kernel."""
     n_out, k_in = (w.shape[1], w.shape[0]) if transposed else (w.shape[0], w.shape[1])
-    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x2.dim() == 2
+    dt = x2.dtype
+    if not (x2.is_cuda and dt in (torch.bfloat16, torch.float32) and w.dtype == dt and x2.dim() == 2
             and w.dim() == 2 and x2.is_contiguous() and w.is_contiguous() and x2.shape[1] == k_in
             and x2.data_ptr() % 16 == 0 and x2.shape[0] >= 16384 and _lib.available()):
         return False
-    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+    if bias is not None and (bias.dtype != dt or not bias.is_contiguous()):
         return False
-    return bool(_lib.require().pdt_narrow_gemm_ok(x2.shape[0], k_in, n_out))
+    lib = _lib.require()
+    ok = lib.pdt_narrow_gemm_ok if dt == torch.bfloat16 else lib.pdt_narrow_gemm_f32_ok
+    return bool(ok(x2.shape[0], k_in, n_out))
 
 
 def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None):
     """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192."""
     M, K = x2.shape
     N = w.shape[0]
+    if x2.dtype == torch.float32:      # exact-f32 MFMA kernels (v_mfma_f32_16x16x4_f32)
+        lib = _lib.require()
+        y = torch.empty((M, N), dtype=torch.float32, device=x2.device)
+        cs = ws = None
+        if colsum_dtype is not None:
+            cs = torch.empty(K, dtype=torch.float32, device=x2.device)
+            ws = torch.empty((lib.pdt_narrow_gemm_f32_partials(M) + 64) * K, dtype=torch.float32, device=x2.device)
+        _lib.call("pdt_narrow_gemm_f32", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N,
+                  _lib.ptr(cs), _lib.ptr(ws), _lib.stream_handle(x2.device))
+        return y, (cs.to(colsum_dtype) if cs is not None else None)
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
     cs = ws = None
     if colsum_dtype is not None:
@@ -44,11 +58,15 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
 
 def narrow_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> bool:
     """dW = dy2^T x2 with both operands token-major bf16 and both feature counts narrow (<= 192)."""
-    return (dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.dim() == 2
+    dt = dy2.dtype
+    if not (dy2.is_cuda and dt in (torch.bfloat16, torch.float32) and x2.dtype == dt and dy2.dim() == 2
             and x2.dim() == 2 and dy2.shape[0] == x2.shape[0] and dy2.is_contiguous() and x2.is_contiguous()
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0 and dy2.shape[0] >= 16384
-            and out_dtype in (torch.float32, torch.bfloat16) and _lib.available()
-            and bool(_lib.require().pdt_narrow_wgrad_ok(dy2.shape[0], dy2.shape[1], x2.shape[1])))
+            and out_dtype in (torch.float32, torch.bfloat16) and _lib.available()):
+        return False
+    lib = _lib.require()
+    ok = lib.pdt_narrow_wgrad_ok if dt == torch.bfloat16 else lib.pdt_narrow_wgrad_f32_ok
+    return bool(ok(dy2.shape[0], dy2.shape[1], x2.shape[1]))
 
 
 def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
@@ -57,8 +75,13 @@ def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) ->
     M, N = dy2.shape
     K = x2.shape[1]
     lib = _lib.require()
-    out = torch.empty((N, K), dtype=out_dtype, device=dy2.device)
     ws = torch.empty(lib.pdt_narrow_wgrad_ws_floats(M, N, K), dtype=torch.float32, device=dy2.device)
+    if dy2.dtype == torch.float32:
+        out = torch.empty((N, K), dtype=torch.float32, device=dy2.device)
+        _lib.call("pdt_narrow_wgrad_f32", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), M, N, K, ws.data_ptr(),
+                  _lib.stream_handle(dy2.device))
+        return out.to(out_dtype)
+    out = torch.empty((N, K), dtype=out_dtype, device=dy2.device)
     _lib.call("pdt_narrow_wgrad", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), M, N, K, _lib.dtype_code(out_dtype),
               ws.data_ptr(), _lib.stream_handle(dy2.device))
     return out

@@ -2042,20 +2042,25 @@ def test_norm_bwd_row_split_at_llama_shape(rms):
         assert rel_err(beta.grad, br.grad) < 1e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,K,N,bias", [(294912, 60, 180, True), (294912, 60, 60, True), (294912, 180, 60, False),
                                         (20007, 60, 180, True), (16389, 120, 60, False), (40000, 188, 36, True),
-                                        (65536, 64, 128, False)])
-def test_narrow_gemm_matches_fp32(M, K, N, bias):
-    """Narrow linears (SwinIR's qkv / proj and their data gradients) on the HIP kernel: every output element against
-    fp32 torch, ragged tail blocks included, and the fused column sums of X (the data-gradient pass's bias gradient)."""
+                                        (65536, 64, 128, False), (294912, 120, 60, True), (294912, 60, 120, True)])
+def test_narrow_gemm_matches_fp32(M, K, N, bias, dt):
+    """Narrow linears (SwinIR's qkv / proj / MLP and their data gradients) on the HIP kernels -- bf16 MFMA, and exact-f32
+    MFMA for fp32 (the reference's precision): every output element against fp32 torch, ragged tail blocks included,
+    and the fused column sums of X (the data-gradient pass's bias gradient)."""
     from pytorch_distributedtraining_amd.ops.narrow import narrow_linear, narrow_ok
     torch.manual_seed(M % 97)
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    w = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
-    b = torch.randn(N, device=DEV).bfloat16() if bias else None
+    x = torch.randn(M, K, device=DEV).to(dt)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(dt)
+    b = torch.randn(N, device=DEV).to(dt) if bias else None
     assert narrow_ok(x, w, b)
     y, cs = narrow_linear(x, w, b, torch.float32)
     ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    if dt == torch.float32:
+        ref = (x.double() @ w.double().t() + (b.double() if bias else 0)).float()
+        assert y.dtype == torch.float32 and rel_err(y, ref) < 1e-6, rel_err(y, ref)
     err = ((y.float() - ref).abs() / (ref.abs() + 1e-2)).max().item()
     assert rel_err(y, ref) < 5e-3 and err < 0.05, (rel_err(y, ref), err)
     assert rel_err(cs, x.float().sum(0)) < 1e-5
@@ -2143,16 +2148,17 @@ def test_conv3x3_implicit_gemm_matches_fp32(N, H, W, cin, cout, mode, monkeypatc
     assert rel_err(w.grad, wr.grad) < 2e-2 and rel_err(b.grad, br.grad) < 2e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,N,K", [(294912, 180, 60), (294912, 60, 60), (20011, 60, 180), (65536, 128, 36),
-                                   (16400, 192, 192)])
-def test_narrow_wgrad_matches_fp32(M, N, K):
-    """Tall-skinny weight gradient dW = dY^T X on the narrow kernel (transposed LDS fragment reads): fp32 and bf16
-    outputs against the fp32 product, ragged row counts included."""
+                                   (16400, 128, 128), (294912, 120, 60), (294912, 60, 120)])
+def test_narrow_wgrad_matches_fp32(M, N, K, dt):
+    """Tall-skinny weight gradient dW = dY^T X on the narrow kernels (bf16: transposed LDS fragment reads; fp32: exact-f32
+    MFMA): fp32 and bf16 outputs against the fp32 product, ragged row counts included."""
     from pytorch_distributedtraining_amd.ops.narrow import narrow_wgrad, narrow_wgrad_ok
     torch.manual_seed(M % 89 + N)
-    dy = torch.randn(M, N, device=DEV).bfloat16()
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    ref = dy.float().t() @ x.float()
+    dy = torch.randn(M, N, device=DEV).to(dt)
+    x = torch.randn(M, K, device=DEV).to(dt)
+    ref = dy.float().t() @ x.float() if dt == torch.bfloat16 else (dy.double().t() @ x.double()).float()
     for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 8e-3)):
         assert narrow_wgrad_ok(dy, x, dt)
         g = narrow_wgrad(dy, x, dt)
