@@ -218,6 +218,22 @@ __global__ __launch_bounds__(MT_THREADS) void copy_mt_kernel(const int64_t* __re
   for (int64_t j = beg + threadIdx.x; j < end; j += MT_THREADS) D[j] = S ? S[j] : T(0);
 }
 
+// dst += src for every (dst, src) pair of the table (fp32 arithmetic; a null src adds nothing) -- per-parameter
+// gradients accumulated into a flat buffer in ONE launch (DDP gradient stealing across accumulation micro-steps)
+template <typename T>
+__global__ __launch_bounds__(MT_THREADS) void add_mt_kernel(const int64_t* __restrict__ meta, const int* __restrict__ blk,
+                                                            int chunk) {
+  const int t = blk[2 * blockIdx.x], c = blk[2 * blockIdx.x + 1];
+  const int64_t* mt = meta + (int64_t)t * MT_META;
+  T* __restrict__ D = reinterpret_cast<T*>(mt[0]);
+  const T* __restrict__ S = reinterpret_cast<const T*>(mt[1]);
+  if (S == nullptr) return;
+  const int64_t n = mt[5];
+  const int64_t beg = (int64_t)c * chunk;
+  const int64_t end = beg + chunk < n ? beg + chunk : n;
+  for (int64_t j = beg + threadIdx.x; j < end; j += MT_THREADS) D[j] = from_f<T>(to_f<T>(D[j]) + to_f<T>(S[j]));
+}
+
 // Device step counter of a param group: +1 unless the (all-reduced) found_inf flag says the step is skipped
 // (torch.amp.GradScaler skips optimizer.step() on overflow, so Adam's bias-correction step must not move).
 __global__ void step_inc_kernel(float* __restrict__ dstep, const int* __restrict__ found_inf) {
@@ -279,6 +295,18 @@ PDT_API int pdt_scale_mt(const int64_t* meta, const int* blk, int nblocks, int c
 PDT_API int pdt_cast_f32_bf16_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, hipStream_t stream) {
   if (nblocks <= 0) return 0;
   cast_f32_bf16_mt_kernel<<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  return (int)hipGetLastError();
+}
+
+// dt: kBF16 or kF32
+PDT_API int pdt_add_mt(const int64_t* meta, const int* blk, int nblocks, int chunk, int dt, hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  if (dt == kF32)
+    add_mt_kernel<float><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  else if (dt == kBF16)
+    add_mt_kernel<bf16_t><<<nblocks, MT_THREADS, 0, stream>>>(meta, blk, chunk);
+  else
+    return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -54,11 +54,30 @@ class PerceptualLoss(nn.Module):
 
     def forward(self, outputs, targets):
         self.features.eval()
-        fo, ft = self._taps(outputs), self._taps(targets.detach())
-        loss = self.pixel_weight * F.l1_loss(outputs, targets)
+        targets = targets.detach()
+        if outputs.dim() == 4 and targets.shape == outputs.shape and targets.stride() != outputs.stride() and \
+                outputs.is_contiguous(memory_format=torch.channels_last):
+            # a channels-last model output (the NHWC conv path): run the target branch in the same layout, so the
+            # feature maps pair up element for element (fused L1) and both branches take the same conv kernels
+            targets = targets.contiguous(memory_format=torch.channels_last)
+        fo, ft = self._taps(outputs), self._taps(targets)
+        # fused L1 (ops.l1): mean |a - b| and its gradient in one read, in the maps' own dtype (autocast would run
+        # F.l1_loss as fp32 copies + four elementwise passes over each 18 x 64 x 256 x 256 map)
+        loss = self.pixel_weight * _l1(outputs, targets.detach())
         for w, a, b in zip(self.weights, fo, ft):
-            loss = loss + w * F.l1_loss(a, b)
+            loss = loss + w * _l1(a, b)
         return loss
+
+
+def _l1(a, b):
+    if a.is_cuda:
+        from ..ops.l1 import l1_loss
+        b = b.to(a.dtype) if b.dtype != a.dtype else b
+        if b.stride() != a.stride():
+            cl = a.dim() == 4 and a.is_contiguous(memory_format=torch.channels_last)
+            b = b.contiguous(memory_format=torch.channels_last) if cl else b.contiguous()
+        return l1_loss(a, b)
+    return F.l1_loss(a, b)
 
 
 _feat = None

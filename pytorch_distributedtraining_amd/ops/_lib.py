@@ -44,6 +44,7 @@ _SIGS = {
     "pdt_scale_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "pdt_cast_f32_bf16_mt": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "pdt_copy_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "pdt_add_mt": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "pdt_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_int, c_float, c_int, c_int, c_int, c_void_p],
     "pdt_norm_bwd_workspace_floats": [c_int, c_int],
@@ -140,6 +141,8 @@ _SIGS = {
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_conv3x3_igemm_ok": [c_int, c_int, c_int, c_int, c_int],
     "pdt_conv3x3_igemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_l1_partials": [c_int64],
+    "pdt_l1_fwd_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p],
     "pdt_narrow_gemm_f32_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_f32_partials": [c_int64],
     "pdt_narrow_gemm_f32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p,

@@ -265,6 +265,24 @@ def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
     _lib.call("pdt_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), _lib.stream_handle(src.device))
 
 
+def add_(dsts: Sequence[torch.Tensor], srcs: Sequence[torch.Tensor | None], name: str = "add") -> None:
+    """dst += src for every pair (same dtype, same element order; a None src adds nothing) in ONE launch on CUDA
+    (bf16 / fp32) -- per-parameter gradients accumulated into a flat buffer."""
+    pairs = [(d, s) for d, s in zip(dsts, srcs) if s is not None]
+    if not pairs:
+        return
+    dev = pairs[0][0].device
+    if dev.type != "cuda" or pairs[0][0].dtype not in (torch.bfloat16, torch.float32) or \
+            torch.cuda.is_current_stream_capturing():
+        torch._foreach_add_([d for d, _ in pairs], [s for _, s in pairs])
+        return
+    for d, s in pairs:
+        assert s.dtype == d.dtype and s.numel() == d.numel()
+    t = _cache.get(name, [[d for d, _ in pairs], [s for _, s in pairs]])
+    _lib.call("pdt_add_mt", t.meta.data_ptr(), t.blk.data_ptr(), t.nblocks, t.chunk, _lib.dtype_code(pairs[0][0].dtype),
+              _lib.stream_handle(dev))
+
+
 def copy_(dsts: Sequence[torch.Tensor], srcs: Sequence[torch.Tensor | None], name: str = "copy") -> None:
     """dst.copy_(src) for every pair (same dtype, same element order; a None src zero-fills its dst) in ONE
     launch on CUDA -- e.g. per-parameter gradients gathered into a flat buffer."""

@@ -124,18 +124,25 @@ class _FlatGroup:
 
     def gather_grads(self):
         """Single-process gradient stealing (DistributedDataParallel._steal_grads) with a compute copy: the
-        parameters' own (stolen) gradients -> the flat the fp32 master reads, in ONE multi-tensor launch; a
-        parameter that received no gradient gets zeros."""
+        parameters' own (stolen) gradients are ADDED to the flat the fp32 master reads, in ONE multi-tensor launch,
+        and then dropped, so the next backward (an accumulation micro-step) steals fresh gradients again instead of
+        autograd adding into every parameter's .grad with one kernel each (227 launches per SwinIR-S step).  The flat
+        is zeroed by zero_grad / drop_grads, so it holds the accumulated gradient.  Under HIP-graph capture the
+        gradients stay attached (their addresses are part of the graph)."""
         from ..ops import multi_tensor as mt
         dsts = [_pview(self.flat_grad, p, self.offset_of[li]) for li, p in enumerate(self.params)]
         srcs = [p.grad for p in self.params]
         same = [s is None or all(a == b for a, b, n in zip(s.stride(), d.stride(), d.shape) if n != 1)
                 for s, d in zip(srcs, dsts)]
         if all(same):
-            mt.copy_(dsts, srcs, name=("ddp_gather", id(self)))
+            mt.add_(dsts, srcs, name=("ddp_gather", id(self)))
         else:
             for s_, d in zip(srcs, dsts):
-                d.zero_() if s_ is None else d.copy_(s_)
+                if s_ is not None:
+                    d.add_(s_)
+        if not (self.flat_grad.is_cuda and torch.cuda.is_current_stream_capturing()):
+            for p in self.params:
+                p.grad = None
 
     def drop_grads(self, set_to_none: bool = True):
         """zero_grad for a stealing compute-copy group: set_to_none -> the next backward's gradients are stolen

@@ -27,6 +27,7 @@ from ..data.loader import DeviceDataLoader
 from ..ops import picks
 from ..ops.fp8 import fp8_autocast
 from ..optim import FusedAdamW, GradScaler, clip_grad_norm_
+from ..optim._grads import grad_of
 from ..parallel.comm import Comm
 from ..utils import checkpoint as ckpt
 from ..utils import profiling as prof
@@ -414,10 +415,11 @@ class Trainer:
         norm_type = self.grad_clip.norm_type if isinstance(self.grad_clip, ClipGradNormConfig) else 2.0
         if isinstance(self.grad_clip, ClipGradConfig):
             for p in params:
-                if p.grad is not None:
+                g = grad_of(p)         # a compute-dtype master's gradient is its engine's flat (_pdt_grad)
+                if g is not None:
                     if self.scaler is not None:
-                        p.grad.mul_(inv_scale)
-                    p.grad.clamp_(-self.grad_clip.clip_value, self.grad_clip.clip_value)
+                        g.mul_(inv_scale)
+                    g.clamp_(-self.grad_clip.clip_value, self.grad_clip.clip_value)
             inv_scale = 1.0
         need_stats = self.scaler is not None or max_norm > 0
         coef = found = None

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6 (m): which torch kernels remain in the SwinIR bf16 step (full names).
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out/r6_m
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/tr -o run -- python3 bench.py --workload swinir-stoke --loss feat --steps 4 --warmup 3 --overlap-probe 0 > $OUT/tr.log 2>&1 || exit 1
+f=$(find $OUT/tr -name "*kernel_trace.csv" | head -1)
+python3 scripts/trace_torch_kernels.py "$f" > $OUT/torch_kernels.txt && cut -c1-330 $OUT/torch_kernels.txt
+rm -f "$f"
+exit 0

@@ -1,4 +1,5 @@
 """Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (MI355X)."""
+import contextlib
 import math
 
 import pytest
@@ -2164,3 +2165,80 @@ def test_narrow_wgrad_matches_fp32(M, N, K, dt):
         g = narrow_wgrad(dy, x, dt)
         assert g.dtype == dt and g.shape == (N, K)
         assert rel_err(g, ref) < tol, (dt, rel_err(g, ref))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,cl", [((18, 64, 64, 64), True), ((3, 5, 7), False), ((1000003,), False)])
+def test_fused_l1_loss_matches_torch(shape, cl, dt):
+    """ops.l1.l1_loss (one read: mean |a - b| and sign(a - b) / n) against F.l1_loss in fp32, channels_last maps and
+    a ragged element count included; the upstream gradient scales the stored sign."""
+    from pytorch_distributedtraining_amd.ops.l1 import l1_loss
+    torch.manual_seed(len(shape))
+    a = torch.randn(shape, device=DEV)
+    b = torch.randn(shape, device=DEV)
+    if cl:
+        a, b = a.to(memory_format=torch.channels_last), b.to(memory_format=torch.channels_last)
+    a = a.to(dt).requires_grad_()
+    b = b.to(dt)
+    loss = l1_loss(a, b)
+    (2.5 * loss).backward()
+    ar = a.detach().float().requires_grad_()
+    ref = F.l1_loss(ar, b.float())
+    (2.5 * ref).backward()
+    assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+    assert rel_err(a.grad, ar.grad) < (1e-2 if dt == torch.bfloat16 else 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_multi_tensor_add_matches_torch(dt):
+    """ops.multi_tensor.add_ (pdt_add_mt): dst += src over a table of ragged tensors in one launch, None skipped."""
+    from pytorch_distributedtraining_amd.ops import multi_tensor as mt
+    torch.manual_seed(0)
+    sizes = [1, 7, 4096, 100003, 60, 3 * 65536 + 5]
+    dsts = [torch.randn(n, device="cuda").to(dt) for n in sizes]
+    srcs = [torch.randn(n, device="cuda").to(dt) if i != 2 else None for i, n in enumerate(sizes)]
+    ref = [(d.float() + (s.float() if s is not None else 0)).to(dt) for d, s in zip(dsts, srcs)]
+    mt.add_(dsts, srcs, name=("test_add", dt))
+    mt.add_(dsts, [None] * len(dsts), name=("test_add_none", dt))
+    for d, r in zip(dsts, ref):
+        torch.testing.assert_close(d, r, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_ddp_steal_accumulates_micro_steps_on_gpu():
+    """Single-process DDP with a bf16 compute copy on the GPU: every micro-step's stolen gradients are added into the
+    masters' flat by the multi-tensor add and dropped, so the flat equals the sum over micro-steps."""
+    import copy
+    import tempfile
+
+    import torch.distributed as dist
+
+    from pytorch_distributedtraining_amd.parallel.comm import Comm
+    from pytorch_distributedtraining_amd.parallel.ddp import DistributedDataParallel
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method="file://" + tempfile.mkdtemp() + "/rdzv", rank=0, world_size=1)
+        created = True
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.GELU(), torch.nn.Linear(128, 32)).cuda()
+        ref = copy.deepcopy(net).to(torch.bfloat16)
+        ddp = DistributedDataParallel(net, comm=Comm(), compute_dtype=torch.bfloat16)
+        xs = [torch.randn(256, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
+        for i, x in enumerate(xs):
+            ctx = ddp.no_sync() if i < len(xs) - 1 else contextlib.nullcontext()
+            with ctx:
+                ddp(x).float().square().mean().backward()
+            assert all(p.grad is None for p in ddp.module.parameters())
+        for x in xs:
+            ref(x).float().square().mean().backward()
+        refs = dict(zip(ddp.module.parameters(), ref.parameters()))
+        for g in ddp.groups:
+            for li, p in enumerate(g.params):
+                o = g.offset_of[li]
+                torch.testing.assert_close(g.flat_grad[o:o + p.numel()].view_as(p).float(), refs[p].grad.float(),
+                                           rtol=3e-2, atol=3e-3)
+    finally:
+        if created:
+            dist.destroy_process_group()
