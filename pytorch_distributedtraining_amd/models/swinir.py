@@ -28,13 +28,15 @@ from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
 from ..ops.linear import Linear, linear
 from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
 from ..ops.norms import LayerNorm, add_layer_norm_from_windows, layer_norm_to_windows, window_norm_ok
-from ..ops.window_attention import (fused_window_ok, window_attention, window_partition_shifted,
-                                    window_reverse_shifted_add)
+from ..ops.window_attention import (fused_window_ok, window_attention, window_attention_table,
+                                    window_partition_shifted, window_reverse_shifted_add)
 
 # PDT_SWINIR_FUSED_TAIL=0: stock PixelShuffle + de-normalisation (A/B of the fused HIP tail)
 _FUSED_TAIL = os.environ.get("PDT_SWINIR_FUSED_TAIL", "1") == "1"
 # PDT_SWIN_WINDOW_NORMS=0: separate roll / partition / reverse(+residual) passes instead of the window-mapped norms
 WINDOW_NORMS = os.environ.get("PDT_SWIN_WINDOW_NORMS", "1") == "1"
+# PDT_SWIN_REL_TABLE_KERNELS=0: relative-position bias gathered / scattered by torch ops (A/B)
+REL_TABLE_KERNELS = os.environ.get("PDT_SWIN_REL_TABLE_KERNELS", "1") == "1"
 
 
 def window_partition(x, ws):
@@ -93,9 +95,13 @@ class WindowAttention(nn.Module):
             # fused HIP window attention: reads the qkv projection in place, never materialises the
             # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
             qkv = self.qkv(x)
-            bias = _RelBiasGather.apply(self.relative_position_bias_table, self.relative_position_index.view(-1))
-            bias = bias.view(N, N, h)
-            out = window_attention(qkv, bias.permute(2, 0, 1), mask, h, self.scale)
+            if REL_TABLE_KERNELS:
+                # the table gather and its gradient scatter fused into two small kernels (ops.window_attention)
+                out = window_attention_table(qkv, self.relative_position_bias_table, self.relative_position_index,
+                                             mask, h, self.scale)
+            else:
+                bias = _RelBiasGather.apply(self.relative_position_bias_table, self.relative_position_index.view(-1))
+                out = window_attention(qkv, bias.view(N, N, h).permute(2, 0, 1), mask, h, self.scale)
             return self.proj(out)
         qkv = self.qkv(x).reshape(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]

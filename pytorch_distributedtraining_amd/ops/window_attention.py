@@ -113,6 +113,12 @@ class _WindowAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
+        dqkv, part = _WindowAttnFn._backward_parts(ctx, do)
+        return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
+
+    @staticmethod
+    def _backward_parts(ctx, do):
+        """(dqkv, per-workgroup bias-gradient partials [G, h, N, N] fp32)."""
         if ctx.mfma:
             qkv, bias, o, lse = ctx.saved_tensors
             m, lab, nw = ctx.mask
@@ -126,7 +132,7 @@ class _WindowAttnFn(torch.autograd.Function):
                       o.data_ptr(),
                       do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
                       ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
-            return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
+            return dqkv, part
         qkv, bias, bias_t, o, lse = ctx.saved_tensors
         m, m_t, nw = ctx.mask
         Bw, N, C3 = qkv.shape
@@ -139,7 +145,71 @@ class _WindowAttnFn(torch.autograd.Function):
         _lib.call("pdt_win_attn_bwd", qkv.data_ptr(), bias.data_ptr(), bias_t.data_ptr(), _lib.ptr(m), _lib.ptr(m_t),
                   nw, o.data_ptr(), do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N, ctx.h,
                   d, float(ctx.scale), _lib.dtype_code(qkv.dtype), _lib.stream_handle(qkv.device))
-        return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
+        return dqkv, part
+
+
+_CSR_CACHE: dict = {}
+
+
+def _rel_csr(index, rows: int):
+    """(idx int32 [N*N], off int32 [rows + 1], pos int32 [N*N]) for a relative-position index buffer: the entries
+    that read each table row, in ascending order -- built once per index buffer (host, first call)."""
+    key = (index.data_ptr(), index._version, tuple(index.shape), index.device, rows)
+    ent = _CSR_CACHE.get(key)
+    if ent is not None and ent[0]() is index:
+        return ent[1]
+    if len(_CSR_CACHE) > 64:
+        _CSR_CACHE.clear()
+    flat = index.reshape(-1).to(torch.int64).cpu()
+    order = torch.argsort(flat, stable=True)
+    counts = torch.bincount(flat, minlength=rows)
+    off = torch.zeros(rows + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(counts, 0)
+    dev = index.device
+    out = (flat.to(torch.int32).to(dev), off.to(torch.int32).to(dev), order.to(torch.int32).to(dev))
+    _CSR_CACHE[key] = (weakref.ref(index), out)
+    return out
+
+
+class _WindowAttnTableFn(torch.autograd.Function):
+    """window_attention with the bias given as the Swin table [T, h] + index [N, N]: the dense fp32 bias is
+    gathered by one kernel, and the backward turns the attention kernel's bias-gradient partials straight into
+    the table gradient (csrc/kernels/rel_bias.hip) -- instead of index_select / permute / cast forward and
+    sum / cast / zero-fill / index_add backward per block."""
+
+    @staticmethod
+    def forward(ctx, qkv, table, index, mask, num_heads, scale):
+        N = qkv.shape[1]
+        idx, off, pos = _rel_csr(index, table.shape[0])
+        tab = table.contiguous()
+        bias = torch.empty((num_heads, N, N), dtype=torch.float32, device=qkv.device)
+        _lib.call("pdt_rel_bias_gather", tab.data_ptr(), idx.data_ptr(), bias.data_ptr(), num_heads, N * N,
+                  _lib.dtype_code(tab.dtype), _lib.stream_handle(qkv.device))
+        o = _WindowAttnFn.forward(ctx, qkv, bias, mask, num_heads, scale)
+        ctx.table_meta = (table.shape[0], table.dtype, off, pos)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        rows, dt, off, pos = ctx.table_meta
+        dqkv, part = _WindowAttnFn._backward_parts(ctx, do)
+        G, h, N, _ = part.shape
+        dtab = torch.empty((rows, h), dtype=dt, device=part.device)
+        ws = torch.empty(h * N * N, dtype=torch.float32, device=part.device)
+        _lib.call("pdt_rel_bias_scatter", part.data_ptr(), G, h, N * N, off.data_ptr(), pos.data_ptr(), rows,
+                  dtab.data_ptr(), _lib.dtype_code(dt), ws.data_ptr(), _lib.stream_handle(part.device))
+        return dqkv, dtab, None, None, None, None
+
+
+def window_attention_table(qkv, table, index, mask, num_heads: int, scale: float):
+    """window_attention with rel_bias = table[index].permute(2, 0, 1) (Swin's relative-position table [T, h] and
+    index buffer [N, N]), the gather and its backward fused into two small kernels on the GPU."""
+    if (supported(qkv, num_heads) and table.dtype in (torch.float32, torch.bfloat16) and table.dim() == 2
+            and table.shape[1] == num_heads and index.numel() == qkv.shape[1] ** 2):
+        return _WindowAttnTableFn.apply(qkv, table, index, mask, num_heads, scale)
+    N = qkv.shape[1]
+    rel = table[index.reshape(-1)].view(N, N, num_heads).permute(2, 0, 1)
+    return window_attention(qkv, rel, mask, num_heads, scale)
 
 
 def supported(qkv, num_heads) -> bool:

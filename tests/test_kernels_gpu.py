@@ -2242,3 +2242,35 @@ def test_ddp_steal_accumulates_micro_steps_on_gpu():
     finally:
         if created:
             dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("masked", [False, True])
+def test_window_attention_table_matches_gather(dtype, masked):
+    """window_attention_table (rel_bias.hip gather + partials -> table-gradient scatter) vs table[index] through the
+    fp32 reference: output, qkv gradient and the relative-position TABLE gradient."""
+    from pytorch_distributedtraining_amd.models.swinir import SwinTransformerBlock, WindowAttention
+    from pytorch_distributedtraining_amd.ops.window_attention import reference, window_attention_table
+    torch.manual_seed(0)
+    h, d, N, Bw, nw = 6, 10, 64, 128, 16
+    wa = WindowAttention(h * d, 8, h)
+    index = wa.relative_position_index.to(DEV)
+    table = (0.5 * torch.randn(225, h, device=DEV)).to(dtype).requires_grad_()
+    qkv = torch.randn(Bw, N, 3 * h * d, device=DEV, dtype=dtype, requires_grad=True)
+    mask = None
+    if masked:
+        mask = SwinTransformerBlock(60, (32, 32), 6, window_size=8, shift_size=4)._mask((32, 32)).to(DEV)
+        assert mask.shape[0] == nw
+    o = window_attention_table(qkv, table, index, mask, h, d ** -0.5)
+    do = torch.randn_like(o)
+    o.backward(do)
+    tr = table.detach().float().requires_grad_()
+    qr = qkv.detach().float().requires_grad_()
+    rel = tr[index.reshape(-1)].view(N, N, h).permute(2, 0, 1)
+    orf = reference(qr, rel, mask, h, d ** -0.5).float()
+    orf.backward(do.float())
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert rel_err(o, orf) < tol
+    assert rel_err(qkv.grad, qr.grad) < 2 * tol
+    assert table.grad.dtype == dtype and rel_err(table.grad, tr.grad) < 2 * tol
