@@ -269,6 +269,19 @@ constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4 + 32;    // QR KR VR GR, SL
 // [nw, N] uint8 -- Swin's mask is -100 exactly where the query's and key's image regions differ, so the
 // kernel rebuilds it from 64 label bytes per window staged in LDS (one 4-byte read per 4 keys) instead of
 // reading 16 KB of fp32 mask per window and head.
+// q / k / v / dO addressing of the MFMA kernels (element strides inside one window's block, which starts at
+// bw * N * 3C for qkv and bw * N * C for dO in both layouts):
+//   token-major (the projection's output [Bw, N, 3, H, d]): qT = 3C, qH = d, qW = C;  gT = C, gH = d
+//   head-major ([Bw, 3, H, N, d], written by the forward; dO [Bw, H, N, d], pdt_win_bwd_prep): qT = d, qH = N d,
+//   qW = H N d;  gT = d, gH = N d -- one head's 64 token slices are then one contiguous 64 d-element run, so a
+//   wave's staging loads touch ~10 lines per instruction instead of 64 (the per-lane strided slices were ~40 % of
+//   the bf16 kernels' time, profiles/r6/r6p_window_attn_staging_ab.txt).
+// delta: rowsum(dO o O) per (window, head, token) precomputed by pdt_win_bwd_prep (null: the backward computes it
+// from O while staging).
+struct WaLayout {
+  int qT, qH, qW, gT, gH;
+  const float* delta;
+};
 __device__ __forceinline__ f32x4 label_mask(const uint8_t* lab, int base, uint32_t mine) {
   const uint32_t four = *reinterpret_cast<const uint32_t*>(lab + base);
   f32x4 m;
@@ -317,6 +330,11 @@ struct Slice {
   __device__ __forceinline__ void zero() {
 #pragma unroll
     for (int i = 0; i < D / 2; ++i) v[i] = 0u;
+  }
+  __device__ __forceinline__ void store(bf16_t* p) const {
+    uint32_t* d = reinterpret_cast<uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) d[i] = v[i];
   }
   __device__ __forceinline__ float f(int e) const { return bf2f((u16)(v[e >> 1] >> (16 * (e & 1)))); }
   // row tile R[64][16]: token t's 16 dims (zero past D) as two 16-byte stores
@@ -373,7 +391,8 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
                                                                const float* __restrict__ mask,
                                                                const uint8_t* __restrict__ labels, int nw,
                                                                bf16_t* __restrict__ o, float* __restrict__ lse, int Bw,
-                                                               int N, int H, float scale, int P) {
+                                                               int N, int H, float scale, int P, WaLayout LY,
+                                                               bf16_t* __restrict__ hm_out) {
   extern __shared__ __attribute__((aligned(16))) u16 smf[];
   const int C = H * D, C3 = 3 * C;
   const int h = blockIdx.x % H, pb = blockIdx.x / H;
@@ -391,8 +410,12 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
     {
       Slice<D> q, k, v;
       if (lane < N) {
-        const bf16_t* row = qkv + ((int64_t)bw * N + lane) * C3 + h * D;
-        q.load(row); k.load(row + C); v.load(row + 2 * C);
+        const bf16_t* row = qkv + (int64_t)bw * N * C3 + lane * LY.qT + h * LY.qH;
+        q.load(row); k.load(row + LY.qW); v.load(row + 2 * LY.qW);
+        if (hm_out != nullptr) {   // the backward's head-major copy, from the slices already in registers
+          bf16_t* hp = hm_out + (((int64_t)bw * 3 * H + h) * N + lane) * D;
+          q.store(hp); k.store(hp + (int64_t)H * N * D); v.store(hp + 2 * (int64_t)H * N * D);
+        }
       } else {
         q.zero(); k.zero(); v.zero();
       }
@@ -484,7 +507,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask,
     const uint8_t* __restrict__ labels, int nw,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P) {
+    bf16_t* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P, WaLayout LY) {
   extern __shared__ __attribute__((aligned(16))) u16 smb[];
   const int C = H * D, C3 = 3 * C;
   const int h = blockIdx.x % H, pb = blockIdx.x / H;
@@ -516,13 +539,17 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
       float L = 0.f, dl = 0.f;
       if (lane < N) {
         const int64_t tok = (int64_t)bw * N + lane;
-        const bf16_t* row = qkv + tok * C3 + h * D;
-        q.load(row); k.load(row + C); v.load(row + 2 * C);
-        g.load(dout + tok * C + h * D);
-        oo.load(o + tok * C + h * D);
+        const bf16_t* row = qkv + (int64_t)bw * N * C3 + lane * LY.qT + h * LY.qH;
+        q.load(row); k.load(row + LY.qW); v.load(row + 2 * LY.qW);
+        g.load(dout + (int64_t)bw * N * C + lane * LY.gT + h * LY.gH);
         L = lse[((int64_t)bw * H + h) * N + lane];
+        if (LY.delta != nullptr) {
+          dl = LY.delta[((int64_t)bw * H + h) * N + lane];
+        } else {
+          oo.load(o + tok * C + h * D);
 #pragma unroll
-        for (int e = 0; e < D; ++e) dl = fmaf(g.f(e), oo.f(e), dl);
+          for (int e = 0; e < D; ++e) dl = fmaf(g.f(e), oo.f(e), dl);
+        }
       } else {
         q.zero(); k.zero(); v.zero(); g.zero();
       }
@@ -714,6 +741,11 @@ struct RowF {
 #pragma unroll
     for (int i = 0; i < D; ++i) v[i] = 0.f;
   }
+  __device__ __forceinline__ void store(float* p) const {
+    float2* d = reinterpret_cast<float2*>(p);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) d[i] = float2{v[2 * i], v[2 * i + 1]};
+  }
   __device__ __forceinline__ void put(float* R, int t) const {
     float* d = R + t * (D + 1);
 #pragma unroll
@@ -753,7 +785,8 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_f32(const float* __rest
                                                              const float* __restrict__ mask,
                                                              const uint8_t* __restrict__ labels, int nw,
                                                              float* __restrict__ o, float* __restrict__ lse, int Bw,
-                                                             int N, int H, float scale, int P) {
+                                                             int N, int H, float scale, int P, WaLayout LY,
+                                                             float* __restrict__ hm_out) {
   extern __shared__ __attribute__((aligned(16))) float smf32[];
   constexpr int RP = D + 1;
   const int C = H * D, C3 = 3 * C;
@@ -772,8 +805,12 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_f32(const float* __rest
     {
       RowF<D> q, k, v;
       if (lane < N) {
-        const float* row = qkv + ((int64_t)bw * N + lane) * C3 + h * D;
-        q.load(row); k.load(row + C); v.load(row + 2 * C);
+        const float* row = qkv + (int64_t)bw * N * C3 + lane * LY.qT + h * LY.qH;
+        q.load(row); k.load(row + LY.qW); v.load(row + 2 * LY.qW);
+        if (hm_out != nullptr) {   // the backward's head-major copy, from the slices already in registers
+          float* hp = hm_out + (((int64_t)bw * 3 * H + h) * N + lane) * D;
+          q.store(hp); k.store(hp + (int64_t)H * N * D); v.store(hp + 2 * (int64_t)H * N * D);
+        }
       } else {
         q.zero(); k.zero(); v.zero();
       }
@@ -856,7 +893,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_f32(
     const float* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ mask,
     const uint8_t* __restrict__ labels, int nw,
     const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse,
-    float* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P) {
+    float* __restrict__ dqkv, float* __restrict__ dbias_part, int Bw, int N, int H, float scale, int P, WaLayout LY) {
   extern __shared__ __attribute__((aligned(16))) float smb32[];
   constexpr int RP = D + 1;
   const int C = H * D, C3 = 3 * C;
@@ -887,13 +924,17 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_f32(
       float L = 0.f, dl = 0.f;
       if (lane < N) {
         const int64_t tok = (int64_t)bw * N + lane;
-        const float* row = qkv + tok * C3 + h * D;
-        q.load(row); k.load(row + C); v.load(row + 2 * C);
-        g.load(dout + tok * C + h * D);
-        oo.load(o + tok * C + h * D);
+        const float* row = qkv + (int64_t)bw * N * C3 + lane * LY.qT + h * LY.qH;
+        q.load(row); k.load(row + LY.qW); v.load(row + 2 * LY.qW);
+        g.load(dout + (int64_t)bw * N * C + lane * LY.gT + h * LY.gH);
         L = lse[((int64_t)bw * H + h) * N + lane];
+        if (LY.delta != nullptr) {
+          dl = LY.delta[((int64_t)bw * H + h) * N + lane];
+        } else {
+          oo.load(o + tok * C + h * D);
 #pragma unroll
-        for (int e = 0; e < D; ++e) dl = fmaf(g.v[e], oo.v[e], dl);
+          for (int e = 0; e < D; ++e) dl = fmaf(g.v[e], oo.v[e], dl);
+        }
       } else {
         q.zero(); k.zero(); v.zero(); g.zero();
       }
@@ -1022,12 +1063,14 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_f32(
 
 template <int D>
 int wa_f32_fwd_launch(const float* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, float* o,
-                      float* lse, int Bw, int N, int H, float scale, hipStream_t st) {
+                      float* lse, int Bw, int N, int H, float scale, const WaLayout& LY, float* hm_out,
+                      hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 4);
   const size_t lds = f32_fwd_lds<D>();
   const bool full = N == 64;
 #define PDT_WF(M, F) \
-  win_attn_fwd_f32<D, M, F><<<P * H, WA_NT, lds, st>>>(qkv, bias, mask, labels, nw, o, lse, Bw, N, H, scale, P)
+  win_attn_fwd_f32<D, M, F><<<P * H, WA_NT, lds, st>>>(qkv, bias, mask, labels, nw, o, lse, Bw, N, H, scale, P, LY, \
+                                                       hm_out)
   if (labels) { if (full) PDT_WF(2, true); else PDT_WF(2, false); }
   else if (mask) { if (full) PDT_WF(1, true); else PDT_WF(1, false); }
   else { if (full) PDT_WF(0, true); else PDT_WF(0, false); }
@@ -1037,7 +1080,7 @@ int wa_f32_fwd_launch(const float* qkv, const float* bias, const float* mask, co
 template <int D>
 int wa_f32_bwd_launch(const float* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw,
                       const float* o, const float* dout, const float* lse, float* dqkv, float* dbias_part, int Bw,
-                      int N, int H, float scale, hipStream_t st) {
+                      int N, int H, float scale, const WaLayout& LY, hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 2);
   const size_t lds = f32_bwd_lds<D>();
   static bool attr = [] {
@@ -1057,7 +1100,7 @@ int wa_f32_bwd_launch(const float* qkv, const float* bias, const float* mask, co
   const bool full = N == 64;
 #define PDT_WB(M, F, PS)                                                                                         \
   win_attn_bwd_f32<D, M, F, PS><<<P * H, WA_NT, lds, st>>>(qkv, bias, mask, labels, nw, o, dout, lse, dqkv, dbias_part, \
-                                                           Bw, N, H, scale, P)
+                                                           Bw, N, H, scale, P, LY)
   if (labels) {
     if (full) { PDT_WB(2, true, 1); PDT_WB(2, true, 2); }
     else { PDT_WB(2, false, 1); PDT_WB(2, false, 2); }
@@ -1073,6 +1116,84 @@ int wa_f32_bwd_launch(const float* qkv, const float* bias, const float* mask, co
 }
 
 }  // namespace
+
+namespace {
+WaLayout wa_layout(int N, int H, int d, int q_hm, int g_hm, const float* delta) {
+  const int C = H * d;
+  WaLayout L;
+  if (q_hm) { L.qT = d; L.qH = N * d; L.qW = H * N * d; }
+  else { L.qT = 3 * C; L.qH = d; L.qW = C; }
+  if (g_hm) { L.gT = d; L.gH = N * d; }
+  else { L.gT = C; L.gH = d; }
+  L.delta = delta;
+  return L;
+}
+
+// One workgroup per window: the window's token-major dO / O blocks ([N][C], contiguous) staged into LDS with 16-byte
+// loads, dO written back head-major ([H][N][d], also contiguous) one head slice per thread (4-byte units: d, C and
+// the offsets are even).  E: bytes per element.
+constexpr int HM_NT = 256;
+template <int E>
+__device__ __forceinline__ void hm_permute(const uint32_t* __restrict__ sm, uint32_t* __restrict__ dst, int N, int H,
+                                           int d, int parts) {
+  const int du = d * E / 4;                     // 4-byte units per head slice
+  const int row = parts * H * du;               // units per token row
+  for (int i = threadIdx.x; i < parts * H * N; i += HM_NT) {
+    const int wh = i / N, t = i - wh * N;       // slice i of the head-major block = (which * H + h, token t)
+    const uint32_t* s = sm + t * row + wh * du;
+    uint32_t* o = dst + i * du;
+    for (int c = 0; c < du; ++c) o[c] = s[c];
+  }
+}
+template <int E>
+__device__ __forceinline__ void stage_block(const void* src, uint32_t* sm, int bytes) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(src);
+  u32x4* d = reinterpret_cast<u32x4*>(sm);
+  for (int i = threadIdx.x; i < bytes / 16; i += HM_NT) d[i] = s[i];
+}
+
+// dO -> head-major, and delta[bw][h][t] = sum_c dO[t][h d + c] O[t][h d + c] (fp32) from the same staged rows
+template <typename T>
+__global__ __launch_bounds__(HM_NT) void bwd_prep_kernel(const T* __restrict__ dout, const T* __restrict__ o,
+                                                        T* __restrict__ dout_hm, float* __restrict__ delta, int N,
+                                                        int H, int d) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smh[];
+  const int C = H * d;
+  const int bytes = N * C * (int)sizeof(T);
+  uint32_t* sg = smh;
+  uint32_t* so = smh + bytes / 4;
+  stage_block<sizeof(T)>(dout + (int64_t)blockIdx.x * N * C, sg, bytes);
+  stage_block<sizeof(T)>(o + (int64_t)blockIdx.x * N * C, so, bytes);
+  __syncthreads();
+  hm_permute<sizeof(T)>(sg, reinterpret_cast<uint32_t*>(dout_hm + (int64_t)blockIdx.x * N * C), N, H, d, 1);
+  const T* g = reinterpret_cast<const T*>(sg);
+  const T* oo = reinterpret_cast<const T*>(so);
+  for (int i = threadIdx.x; i < H * N; i += HM_NT) {
+    const int h = i / N, t = i - h * N;
+    float s = 0.f;
+    for (int c = 0; c < d; ++c) s = fmaf(to_f<T>(g[t * C + h * d + c]), to_f<T>(oo[t * C + h * d + c]), s);
+    delta[(int64_t)blockIdx.x * H * N + i] = s;
+  }
+}
+}  // namespace
+
+// dout, o [Bw, N, C] token-major -> dout_hm [Bw, H, N, d], delta [Bw, H, N] fp32.  16-byte aligned; N C elem_bytes
+// a multiple of 16.
+PDT_API int pdt_win_bwd_prep(const void* dout, const void* o, void* dout_hm, float* delta, int Bw, int N, int H, int d,
+                             int dt, hipStream_t st) {
+  const int E = dt == kF32 ? 4 : 2;
+  const int64_t bytes = (int64_t)N * H * d * E;
+  if (Bw <= 0 || d % 2 || bytes % 16 || 2 * bytes > 96 * 1024 ||
+      (((uintptr_t)dout | (uintptr_t)o | (uintptr_t)dout_hm) & 15))
+    return (int)hipErrorInvalidValue;
+  if (E == 4)
+    bwd_prep_kernel<float><<<Bw, HM_NT, 2 * bytes, st>>>((const float*)dout, (const float*)o, (float*)dout_hm, delta, N,
+                                                         H, d);
+  else
+    bwd_prep_kernel<bf16_t><<<Bw, HM_NT, 2 * bytes, st>>>((const bf16_t*)dout, (const bf16_t*)o, (bf16_t*)dout_hm,
+                                                          delta, N, H, d);
+  return (int)hipGetLastError();
+}
 
 // grid size the launcher uses (also the number of dbias partials the caller must allocate)
 PDT_API int pdt_win_attn_grid(int Bw) { return Bw < 512 ? Bw : 512; }
@@ -1097,13 +1218,13 @@ PDT_API int pdt_win_attn_mfma_grid(int Bw, int H) { return mfma_blocks_per_head(
 namespace {
 template <int D>
 int wa_fwd_launch(const void* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, void* o,
-                  float* lse, int Bw, int N, int H, float scale, hipStream_t st) {
+                  float* lse, int Bw, int N, int H, float scale, const WaLayout& LY, void* hm_out, hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 4);
   const size_t lds = fwd_mfma_lds();
   const bool full = N == 64;
 #define PDT_WF(M, F)                                                                                          \
   win_attn_fwd_mfma<D, M, F><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, labels, nw, (bf16_t*)o, \
-                                                        lse, Bw, N, H, scale, P)
+                                                        lse, Bw, N, H, scale, P, LY, (bf16_t*)hm_out)
   if (labels) { if (full) PDT_WF(2, true); else PDT_WF(2, false); }
   else if (mask) { if (full) PDT_WF(1, true); else PDT_WF(1, false); }
   else { if (full) PDT_WF(0, true); else PDT_WF(0, false); }
@@ -1113,7 +1234,7 @@ int wa_fwd_launch(const void* qkv, const float* bias, const float* mask, const u
 template <int D>
 int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const uint8_t* labels, int nw, const void* o,
                   const void* dout, const float* lse, void* dqkv, float* dbias_part, int Bw, int N, int H, float scale,
-                  hipStream_t st) {
+                  const WaLayout& LY, hipStream_t st) {
   const int P = mfma_blocks_per_head(Bw, H, 2);
   const size_t lds = bwd_mfma_lds();
   static bool attr = [] {
@@ -1134,7 +1255,7 @@ int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const u
 #define PDT_WB(M, F, PS)                                                                                           \
   win_attn_bwd_mfma<D, M, F, PS><<<P * H, WA_NT, lds, st>>>((const bf16_t*)qkv, bias, mask, labels, nw,              \
                                                             (const bf16_t*)o, (const bf16_t*)dout, lse, (bf16_t*)dqkv, \
-                                                            dbias_part, Bw, N, H, scale, P)
+                                                            dbias_part, Bw, N, H, scale, P, LY)
   if (labels) {
     if (full) { PDT_WB(2, true, 1); PDT_WB(2, true, 2); }
     else { PDT_WB(2, false, 1); PDT_WB(2, false, 2); }
@@ -1152,10 +1273,15 @@ int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const u
 
 // mask [nw, N, N] fp32 or null; labels [nw, N] uint8 region labels or null (takes precedence over mask:
 // mask value = -100 where the query's and key's labels differ, 0 elsewhere)
+// qkv token-major [Bw, N, 3C]; hm_out (nullable) [Bw, 3, H, N, d]: the head-major copy of q / k / v the backward
+// reads (hm = 1), written from the staged slices
 PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
-                                  void* o, float* lse, int Bw, int N, int H, int d, float scale, hipStream_t st) {
+                                  void* o, float* lse, int Bw, int N, int H, int d, float scale, void* hm_out,
+                                  hipStream_t st) {
   if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
-#define PDT_C(D) return wa_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, st)
+  const WaLayout LY = wa_layout(N, H, d, 0, 0, nullptr);
+#define PDT_C(D) \
+  return wa_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }
@@ -1163,30 +1289,39 @@ PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const floa
 // dqkv [Bw, N, 3C] fully written; dbias_part [pdt_win_attn_mfma_grid(Bw, H), H, N, N] fp32 fully written
 PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                   const void* o, const void* dout, const float* lse, void* dqkv, float* dbias_part,
-                                  int Bw, int N, int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+                                  int Bw, int N, int H, int d, float scale, int hm, const float* delta,
+                                  hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (hm && !delta))
+    return (int)hipErrorInvalidValue;
+  const WaLayout LY = wa_layout(N, H, d, hm, hm, delta);
 #define PDT_C(D)                                                                                                   \
   return wa_bwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, dout, lse, dqkv, dbias_part, Bw, N, H, \
-                          scale, st)
+                          scale, LY, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }
 // fp32 MFMA path (same contract as the bf16 one; partials [pdt_win_attn_mfma_grid(Bw, H), H, N, N])
 PDT_API int pdt_win_attn_mfma32_ok(int N, int H, int d) { return mfma_ok(N, H, d, kBF16) ? 1 : 0; }
 PDT_API int pdt_win_attn_mfma32_fwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
-                                    float* o, float* lse, int Bw, int N, int H, int d, float scale, hipStream_t st) {
+                                    float* o, float* lse, int Bw, int N, int H, int d, float scale, float* hm_out,
+                                    hipStream_t st) {
   if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
-#define PDT_C(D) return wa_f32_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, st)
+  const WaLayout LY = wa_layout(N, H, d, 0, 0, nullptr);
+#define PDT_C(D) \
+  return wa_f32_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }
 PDT_API int pdt_win_attn_mfma32_bwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                     const float* o, const float* dout, const float* lse, float* dqkv,
-                                    float* dbias_part, int Bw, int N, int H, int d, float scale, hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
+                                    float* dbias_part, int Bw, int N, int H, int d, float scale, int hm,
+                                    const float* delta, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (hm && !delta))
+    return (int)hipErrorInvalidValue;
+  const WaLayout LY = wa_layout(N, H, d, hm, hm, delta);
 #define PDT_C(D)                                                                                                 \
   return wa_f32_bwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, dout, lse, dqkv, dbias_part, Bw, N, \
-                              H, scale, st)
+                              H, scale, LY, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
 #undef PDT_C
 }

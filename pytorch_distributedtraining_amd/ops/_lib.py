@@ -97,17 +97,18 @@ _SIGS = {
     "pdt_win_attn_mfma_ok": [c_int, c_int, c_int, c_int],
     "pdt_win_attn_mfma_grid": [c_int, c_int],
     "pdt_win_attn_mfma_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                              c_int, c_float, c_void_p],
+                              c_int, c_float, c_void_p, c_void_p],
+    "pdt_win_bwd_prep": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_rel_bias_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "pdt_rel_bias_scatter": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
                              c_void_p],
     "pdt_win_attn_mfma_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
+                              c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p],
     "pdt_win_attn_mfma32_ok": [c_int, c_int, c_int],
     "pdt_win_attn_mfma32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                                c_int, c_float, c_void_p],
+                                c_int, c_float, c_void_p, c_void_p],
     "pdt_win_attn_mfma32_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
+                                c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p],
     "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                          c_int, c_void_p],
     "pdt_win_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

@@ -21,6 +21,14 @@ from . import _lib
 _MASK_T_CACHE: dict = {}
 USE_LABELS = os.environ.get("PDT_WIN_MASK_LABELS", "1") == "1"   # A/B switch: 0 = dense fp32 mask reads
 MFMA_F32 = os.environ.get("PDT_WIN_F32_MFMA", "1") == "1"        # A/B switch: 0 = fp32 on the VALU kernels
+# PDT_WIN_HEAD_MAJOR=0: the MFMA kernels read q / k / v / dO token-major in place (A/B of the head-major relayout)
+HEAD_MAJOR = os.environ.get("PDT_WIN_HEAD_MAJOR", "1") == "1"
+
+
+def _hm_ok(qkv, N, num_heads, d) -> bool:
+    es = qkv.element_size()
+    return (HEAD_MAJOR and d % 2 == 0 and (N * 3 * num_heads * d * es) % 16 == 0
+            and N * 3 * num_heads * d * es <= 96 * 1024 and qkv.data_ptr() % 16 == 0)
 
 
 def _mask_t(mask):
@@ -94,10 +102,16 @@ class _WindowAttnFn(torch.autograd.Function):
             # MFMA kernels: dense bias [h, N(q), N(key)] and mask [nw, N, N], no transposed copies
             m = mask.float().contiguous() if mask is not None else None
             lab = _mask_labels(mask) if (mask is not None and USE_LABELS) else None
+            st = _lib.stream_handle(qkv.device)
+            ctx.hm = _hm_ok(qkv, N, num_heads, d)
+            # the forward writes a head-major copy [Bw, 3, h, N, d] of q / k / v from the slices it stages anyway:
+            # the backward's staging loads then read each head's token slices contiguously; kept for the backward
+            # in place of qkv (same size)
+            hm = torch.empty_like(qkv) if ctx.hm else None
             _lib.call("pdt_win_attn_mfma_fwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_fwd", qkv.data_ptr(),
                       bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
-                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.stream_handle(qkv.device))
-            ctx.save_for_backward(qkv, bias, o, lse)
+                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.ptr(hm), st)
+            ctx.save_for_backward(hm if ctx.hm else qkv, bias, o, lse)
             ctx.mask = (m, lab, nw)
             ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
             return o
@@ -125,13 +139,25 @@ class _WindowAttnFn(torch.autograd.Function):
             Bw, N, C3 = qkv.shape
             d = C3 // 3 // ctx.h
             G = _lib.require().pdt_win_attn_mfma_grid(Bw, ctx.h)
-            dqkv = torch.empty_like(qkv)
+            dqkv = torch.empty_like(qkv)        # token-major (the projection's layout), also when qkv is head-major
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
             do = do.contiguous().to(qkv.dtype)
-            _lib.call("pdt_win_attn_mfma_bwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_bwd", qkv.data_ptr(), bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
-                      o.data_ptr(),
-                      do.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), part.data_ptr(), Bw, N,
-                      ctx.h, d, float(ctx.scale), _lib.stream_handle(qkv.device))
+            st = _lib.stream_handle(qkv.device)
+            delta = None
+            if ctx.hm and do.data_ptr() % 16:
+                do = do.clone()
+            if ctx.hm:
+                # dO head-major + delta = rowsum(dO o O) from one coalesced pass: the kernels stage neither O nor
+                # token-major dO slices
+                g = torch.empty_like(do)
+                delta = torch.empty((Bw, ctx.h, N), dtype=torch.float32, device=qkv.device)
+                _lib.call("pdt_win_bwd_prep", do.data_ptr(), o.data_ptr(), g.data_ptr(), delta.data_ptr(), Bw, N,
+                          ctx.h, d, _lib.dtype_code(qkv.dtype), st)
+                do = g
+            _lib.call("pdt_win_attn_mfma_bwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_bwd", qkv.data_ptr(),
+                      bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                      dqkv.data_ptr(), part.data_ptr(), Bw, N, ctx.h, d, float(ctx.scale), int(ctx.hm),
+                      _lib.ptr(delta), st)
             return dqkv, part
         qkv, bias, bias_t, o, lse = ctx.saved_tensors
         m, m_t, nw = ctx.mask
