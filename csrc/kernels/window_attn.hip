@@ -278,6 +278,15 @@ constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4 + 32;    // QR KR VR GR, SL
 //   the bf16 kernels' time, profiles/r6/r6p_window_attn_staging_ab.txt).
 // delta: rowsum(dO o O) per (window, head, token) precomputed by pdt_win_bwd_prep (null: the backward computes it
 // from O while staging).
+// experiment builds only (-DPDT_WA_EXP_HMSTORE): O and dQ/dK/dV stored head-major (wrong layout for their
+// consumers) -- measures what the strided per-lane output stores cost
+#ifdef PDT_WA_EXP_HMSTORE
+#define WA_DQKV_ADDR(p, bw, t, w) ((p) + ((((int64_t)(bw) * 3 + (w)) * H + h) * N + (t)) * D)
+#define WA_O_ADDR(p, bw, t) ((p) + (((int64_t)(bw) * H + h) * N + (t)) * D)
+#else
+#define WA_DQKV_ADDR(p, bw, t, w) ((p) + ((int64_t)(bw) * N + (t)) * C3 + (w) * C + h * D)
+#define WA_O_ADDR(p, bw, t) ((p) + ((int64_t)(bw) * N + (t)) * C + h * D)
+#endif
 struct WaLayout {
   int qT, qH, qW, gT, gH;
   const float* delta;
@@ -491,7 +500,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_mfma(const bf16_t* __re
       for (int ks = 0; ks < 4; ++ks) acc = mfma32(vt[ks], pack8(p[qt][ks >> 1], ks & 1), acc);
       const int q = 32 * qt + l32;
       if (FULL || q < N) {
-        store_dims<D>(o + ((int64_t)bw * N + q) * C + h * D, acc, 1.f / lsum[qt], hh);
+        store_dims<D>(WA_O_ADDR(o, bw, q), acc, 1.f / lsum[qt], hh);
         if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(lsum[qt]);
       }
     }
@@ -615,7 +624,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
         f32x16 acc = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) acc = mfma32(ktf[ks], dsk[ks], acc);
-        if (FULL || q < N) store_dims<D>(dqkv + ((int64_t)bw * N + q) * C3 + h * D, acc, scale, hh);
+        if (FULL || q < N) store_dims<D>(WA_DQKV_ADDR(dqkv, bw, q, 0), acc, scale, hh);
       }
     } else {
       // lane = key (S layout): P and dS in one sweep; dV = P^T dO, dK = dS^T Q * scale
@@ -661,9 +670,8 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_bwd_mfma(
           }
         }
         if (FULL || key < N) {
-          bf16_t* row = dqkv + ((int64_t)bw * N + key) * C3 + h * D;
-          store_dims<D>(row + C, ak, scale, hh);
-          store_dims<D>(row + 2 * C, av, 1.f, hh);
+          store_dims<D>(WA_DQKV_ADDR(dqkv, bw, key, 1), ak, scale, hh);
+          store_dims<D>(WA_DQKV_ADDR(dqkv, bw, key, 2), av, 1.f, hh);
         }
       }
     }
