@@ -85,12 +85,50 @@ __device__ __forceinline__ void put_block(bf16_t* Xs, int KI, int rows, int lane
   }
 }
 
+// Head-major output (hm_n > 0; Swin's qkv projection feeding the window attention): row m = window w, token t
+// (m = w hm_n + t) and column c = segment s (= which x H + head), dim d (c = s hm_d + d) go to
+// Y[w][s][t][d] (element (w NO + s hm_d) hm_n + t hm_d + d): one head's 16 staged tokens are one contiguous run of
+// 16 hm_d elements.
+// Copied from the [16][NO] staging block in 2-element units (hm_d, NO even); a lane's units inside a segment
+// (q = lane + 64 i < 8 hm_d) are fixed, so their (row, unit) split is computed once per kernel.
+template <typename U>   // U = a 2-element unit (uint32_t for bf16, uint2 for fp32)
+struct HmStore {
+  int r[4], dd[4], nq;
+  __device__ __forceinline__ void init(int hm_d, int lane) {
+    const int du = hm_d / 2;
+    nq = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = lane + 64 * i;
+      r[i] = q / du;
+      dd[i] = q - r[i] * du;
+      if (q < 16 * du) nq = i + 1;
+    }
+  }
+  template <typename T>
+  __device__ __forceinline__ void store(T* __restrict__ Y, const T* Ys, int64_t blk, int rows, int NO, int hm_n,
+                                        int hm_d) const {
+    const int64_t row0 = blk * 16;
+    const int64_t win = row0 / hm_n;
+    const int t0 = (int)(row0 - win * hm_n);
+    T* base = Y + win * hm_n * NO + (int64_t)t0 * hm_d;
+    for (int sg = 0; sg < NO / hm_d; ++sg) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < nq && r[i] < rows)
+          *reinterpret_cast<U*>(base + (int64_t)sg * hm_n * hm_d + r[i] * hm_d + 2 * dd[i]) =
+              *reinterpret_cast<const U*>(Ys + r[i] * NO + sg * hm_d + 2 * dd[i]);
+      }
+    }
+  }
+};
+
 template <int KP, int NP>
 __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ B,
                                                                  const bf16_t* __restrict__ bias,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ colsum_part,
-                                                                 int64_t M, int KI, int NO) {
+                                                                 int64_t M, int KI, int NO, int hm_n, int hm_d) {
   typedef NarrowCfg<KP, NP> Cfg;
   constexpr int XP = Cfg::XP, KS = Cfg::KS, NT = Cfg::NT;
   extern __shared__ __attribute__((aligned(16))) bf16_t nsm[];
@@ -122,6 +160,8 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
     bcol[nt] = (bias != nullptr && n < NO) ? bf2f(bias[n]) : 0.f;
   }
   float cs[3] = {0.f, 0.f, 0.f};                 // COLSUM: columns lane, lane + 64, lane + 128
+  HmStore<uint32_t> hms;
+  if (hm_n > 0) hms.init(hm_d, lane);
 
   const int64_t nblk = (M + 15) / 16;
   const int64_t gw = (int64_t)blockIdx.x * NW + wv, nwaves = (int64_t)gridDim.x * NW;
@@ -160,10 +200,14 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
       }
     }
     wave_sync();
-    bf16_t* dst = Y + blk * 16 * NO;
-    const int tot = rows * NO, n8 = tot >> 3;
-    for (int c = lane; c < n8; c += 64) *reinterpret_cast<u16x8*>(dst + 8 * c) = *reinterpret_cast<const u16x8*>(Ys + 8 * c);
-    for (int e = 8 * n8 + lane; e < tot; e += 64) dst[e] = Ys[e];
+    if (hm_n > 0) {
+      hms.store(Y, Ys, blk, rows, NO, hm_n, hm_d);
+    } else {
+      bf16_t* dst = Y + blk * 16 * NO;
+      const int tot = rows * NO, n8 = tot >> 3;
+      for (int c = lane; c < n8; c += 64) *reinterpret_cast<u16x8*>(dst + 8 * c) = *reinterpret_cast<const u16x8*>(Ys + 8 * c);
+      for (int e = 8 * n8 + lane; e < tot; e += 64) dst[e] = Ys[e];
+    }
   }
   if (colsum_part != nullptr) {
     float* dstp = colsum_part + gw * KI;
@@ -330,7 +374,7 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
                                                                        const float* __restrict__ bias,
                                                                        float* __restrict__ Y,
                                                                        float* __restrict__ colsum_part, int64_t M,
-                                                                       int KI, int NO) {
+                                                                       int KI, int NO, int hm_n, int hm_d) {
   typedef Narrow32Cfg<KP, NP> Cfg;
   constexpr int NT = NP / 16;
   extern __shared__ __attribute__((aligned(16))) float n32[];
@@ -349,6 +393,8 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
     bcol[nt] = (bias != nullptr && n < NO) ? bias[n] : 0.f;
   }
   float cs[3] = {0.f, 0.f, 0.f};
+  HmStore<uint2> hms;
+  if (hm_n > 0) hms.init(hm_d, lane);
   __syncthreads();
   const int64_t nblk = (M + 15) / 16;
   const int64_t gw = (int64_t)blockIdx.x * NW32 + wv, nwaves = (int64_t)gridDim.x * NW32;
@@ -409,9 +455,13 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
       }
     }
     wave_sync();
-    float* dst = Y + blk * 16 * NO;
-    const int n4 = rows * NO / 4;
-    for (int c = lane; c < n4; c += 64) *reinterpret_cast<f32x4*>(dst + 4 * c) = *reinterpret_cast<const f32x4*>(Ys + 4 * c);
+    if (hm_n > 0) {
+      hms.store(Y, Ys, blk, rows, NO, hm_n, hm_d);
+    } else {
+      float* dst = Y + blk * 16 * NO;
+      const int n4 = rows * NO / 4;
+      for (int c = lane; c < n4; c += 64) *reinterpret_cast<f32x4*>(dst + 4 * c) = *reinterpret_cast<const f32x4*>(Ys + 4 * c);
+    }
   }
   if (colsum_part != nullptr) {
     float* dstp = colsum_part + gw * KI;
@@ -548,16 +598,23 @@ PDT_API int pdt_narrow_gemm_partials(int64_t M, int KI, int NO) { return narrow_
 // Y [M, NO] bf16 = X [M, KI] bf16 . B [NO, KI]^T (+ bias [NO] bf16); X, Y contiguous and 16-byte aligned.
 // colsum_out (nullable, fp32 [KI], W dtype by wdt): column sums of X -- written (not accumulated) -- with ws
 // >= (pdt_narrow_gemm_partials(M, KI, NO) + 64) * KI floats (partials + the column reduce's second level).
+// hm_n > 0: Y head-major (narrow_gemm_kernel's HmStore): M % hm_n == 0, hm_n % 16 == 0, NO % hm_d == 0, hm_d even
+// and <= 32
+static bool hm_ok(int64_t M, int NO, int hm_n, int hm_d) {
+  return hm_n == 0 || (hm_n > 0 && hm_n % 16 == 0 && M % hm_n == 0 && hm_d >= 2 && hm_d <= 32 && hm_d % 2 == 0 &&
+                       NO % hm_d == 0);
+}
 PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void* Y, int64_t M, int KI, int NO,
-                            void* colsum_out, int wdt, float* ws, hipStream_t st) {
-  if (!pdt_narrow_gemm_ok(M, KI, NO) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15)) return (int)hipErrorInvalidValue;
+                            void* colsum_out, int wdt, float* ws, int hm_n, int hm_d, hipStream_t st) {
+  if (!pdt_narrow_gemm_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15))
+    return (int)hipErrorInvalidValue;
   const int KP = pad_to(KI, 64) <= 64 ? 64 : pad_to(KI, 64);
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
   const int grid = narrow_grid(M, KI, NO);
   float* part = colsum_out ? ws : nullptr;
 #define PDT_NG(KP_, NP_)                                                                                        \
   narrow_gemm_kernel<KP_, NP_><<<grid, 64 * NW, NW * NarrowCfg<KP_, NP_>::WAVE_ELEMS * sizeof(bf16_t), st>>>(   \
-      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO)
+      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d)
 #define PDT_NG_N(KP_) \
   do { if (NP == 64) PDT_NG(KP_, 64); else if (NP == 128) PDT_NG(KP_, 128); else PDT_NG(KP_, 192); } while (0)
   if (KP == 64) PDT_NG_N(64);
@@ -650,8 +707,9 @@ PDT_API int pdt_narrow_wgrad_f32_ok(int64_t M, int NO, int KI) {
   return sizeof(float) * 2 * 64 * (size_t)(NP + 1 + KP + 1) <= 160 * 1024 ? 1 : 0;
 }
 PDT_API int pdt_narrow_gemm_f32(const float* X, const float* B, const float* bias, float* Y, int64_t M, int KI, int NO,
-                                float* colsum_out, float* ws, hipStream_t st) {
-  if (!pdt_narrow_gemm_f32_ok(M, KI, NO) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15)) return (int)hipErrorInvalidValue;
+                                float* colsum_out, float* ws, int hm_n, int hm_d, hipStream_t st) {
+  if (!pdt_narrow_gemm_f32_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15))
+    return (int)hipErrorInvalidValue;
   const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
   const int grid = narrow32_grid(M);
@@ -659,7 +717,8 @@ PDT_API int pdt_narrow_gemm_f32(const float* X, const float* B, const float* bia
 #define PDT_N32(KP_, NP_)                                                                                         \
   do {                                                                                                            \
     if (!narrow32_attr<KP_, NP_>()) return (int)hipErrorInvalidValue;                                             \
-    narrow_gemm_f32_kernel<KP_, NP_><<<grid, 64 * NW32, narrow32_lds<KP_, NP_>(), st>>>(X, B, bias, Y, part, M, KI, NO); \
+    narrow_gemm_f32_kernel<KP_, NP_><<<grid, 64 * NW32, narrow32_lds<KP_, NP_>(), st>>>(X, B, bias, Y, part, M, KI, NO, \
+                                                                                     hm_n, hm_d);                 \
   } while (0)
 #define PDT_N32_N(KP_) \
   do { if (NP == 64) PDT_N32(KP_, 64); else if (NP == 128) PDT_N32(KP_, 128); else PDT_N32(KP_, 192); } while (0)

@@ -1281,13 +1281,15 @@ int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const u
 
 // mask [nw, N, N] fp32 or null; labels [nw, N] uint8 region labels or null (takes precedence over mask:
 // mask value = -100 where the query's and key's labels differ, 0 elsewhere)
-// qkv token-major [Bw, N, 3C]; hm_out (nullable) [Bw, 3, H, N, d]: the head-major copy of q / k / v the backward
-// reads (hm = 1), written from the staged slices
+// qkv token-major [Bw, N, 3C], or head-major [Bw, 3, H, N, d] with q_hm = 1 (the narrow GEMM's head-major output);
+// hm_out (nullable, token-major qkv only) [Bw, 3, H, N, d]: the head-major copy of q / k / v the backward reads
+// (hm = 1), written from the staged slices
 PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                   void* o, float* lse, int Bw, int N, int H, int d, float scale, void* hm_out,
-                                  hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
-  const WaLayout LY = wa_layout(N, H, d, 0, 0, nullptr);
+                                  int q_hm, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (q_hm && hm_out))
+    return (int)hipErrorInvalidValue;
+  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr);
 #define PDT_C(D) \
   return wa_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
@@ -1312,9 +1314,10 @@ PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const floa
 PDT_API int pdt_win_attn_mfma32_ok(int N, int H, int d) { return mfma_ok(N, H, d, kBF16) ? 1 : 0; }
 PDT_API int pdt_win_attn_mfma32_fwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                     float* o, float* lse, int Bw, int N, int H, int d, float scale, float* hm_out,
-                                    hipStream_t st) {
-  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0)) return (int)hipErrorInvalidValue;
-  const WaLayout LY = wa_layout(N, H, d, 0, 0, nullptr);
+                                    int q_hm, hipStream_t st) {
+  if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (q_hm && hm_out))
+    return (int)hipErrorInvalidValue;
+  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr);
 #define PDT_C(D) \
   return wa_f32_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)

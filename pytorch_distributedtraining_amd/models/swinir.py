@@ -25,10 +25,10 @@ import torch.nn.functional as F
 
 from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
-from ..ops.linear import Linear, linear
+from ..ops.linear import Linear, linear, linear_head_major
 from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
 from ..ops.norms import LayerNorm, add_layer_norm_from_windows, layer_norm_to_windows, window_norm_ok
-from ..ops.window_attention import (fused_window_ok, window_attention, window_attention_table,
+from ..ops.window_attention import (fused_window_ok, head_major_ok, window_attention, window_attention_table,
                                     window_partition_shifted, window_reverse_shifted_add)
 
 # PDT_SWINIR_FUSED_TAIL=0: stock PixelShuffle + de-normalisation (A/B of the fused HIP tail)
@@ -94,7 +94,8 @@ class WindowAttention(nn.Module):
         if x.is_cuda and self.native:
             # fused HIP window attention: reads the qkv projection in place, never materialises the
             # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
-            qkv = self.qkv(x)
+            # the projection writes q / k / v head-major where the narrow GEMM computes it (ops.linear)
+            qkv = linear_head_major(self.qkv, x, N, C // h) if head_major_ok(x, N, h, C // h) else self.qkv(x)
             if REL_TABLE_KERNELS:
                 # the table gather and its gradient scatter fused into two small kernels (ops.window_attention)
                 out = window_attention_table(qkv, self.relative_position_bias_table, self.relative_position_index,

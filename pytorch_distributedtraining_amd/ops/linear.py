@@ -357,13 +357,15 @@ def _as_output(t: torch.Tensor, shape) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, hm=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         # x is (a view of) a flash-attention output whose backward wants colsum(dX) (ops.attention._dout_colsum)
         base = x._base if x._base is not None else x
         ctx.dx_colsum = bias is not None and getattr(base, "_pdt_dx_colsum", False)
         x2 = x.reshape(-1, x.shape[-1])
+        if hm is not None:      # linear_head_major checked the narrow kernel applies and was picked
+            return _as_output(narrow_linear(x2, weight, bias, hm=hm)[0], (*x.shape[:-1], weight.shape[0]))
         if x2.is_contiguous() and _prefer_narrow(x2, weight, bias, "fwd"):
             return _as_output(narrow_linear(x2, weight, bias)[0], (*x.shape[:-1], weight.shape[0]))
         if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
@@ -426,7 +428,7 @@ class _LinearFn(torch.autograd.Function):
             # what a backward returns (a weak reference to it dies), the base's survives through the view
             dbf = dbf if dbf is not None and dbf.dtype == torch.float32 else db.float()
             stash_dx_colsum(dx2, dbf @ w.float())
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 def _lin_residual_fwd(x2, w, b, r2):
@@ -636,6 +638,33 @@ def linear(x, weight, bias=None):
         # an input saved as a recompute recipe (utils.recompute): this Function saves x itself, not a view of it)
         return _LinearFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
+
+
+# PDT_HEAD_MAJOR_QKV=0: Swin's qkv projection always writes token-major (A/B of linear_head_major)
+HEAD_MAJOR_QKV = os.environ.get("PDT_HEAD_MAJOR_QKV", "1") == "1"
+
+
+def linear_head_major(module: "Linear", x: torch.Tensor, n_tok: int, head_dim: int) -> torch.Tensor:
+    """``module(x)`` for a projection whose ONLY consumer is ops.window_attention (Swin's qkv): where the narrow
+    GEMM computes it, the output buffer is written head-major ([windows, 3, heads, n_tok, d], ops.narrow) and the
+    tensor is tagged ``_pdt_head_major = (n_tok, d)``, so the attention's staging loads read each head's token
+    slices contiguously (no relayout pass).  The tensor keeps its logical [..., 3C] shape, and its gradient
+    arrives token-major as usual (the Linear's backward never reads its output).  Anything else: ``module(x)``."""
+    from .narrow import head_major_ok
+    if HEAD_MAJOR_QKV and x.is_cuda and not fp8_enabled():
+        xc = x.to(torch.get_autocast_dtype("cuda")) if torch.is_autocast_enabled("cuda") else x
+        w, b = module.weight, module.bias
+        if torch.is_autocast_enabled("cuda"):
+            w, b = w.to(xc.dtype), (None if b is None else b.to(xc.dtype))
+        x2 = xc.reshape(-1, xc.shape[-1])
+        if (xc.dtype == w.dtype and xc.dtype in (torch.bfloat16, torch.float32) and (b is None or b.dtype == xc.dtype)
+                and x2.is_contiguous() and head_major_ok(x2.shape[0], w.shape[0], (n_tok, head_dim))
+                and _prefer_narrow(x2, w, b, "fwd")):
+            with torch.autocast("cuda", enabled=False):
+                y = _LinearFn.apply(xc, w, b, (n_tok, head_dim))
+            y._pdt_head_major = (n_tok, head_dim)
+            return y
+    return module(x)
 
 
 class Linear(nn.Linear):

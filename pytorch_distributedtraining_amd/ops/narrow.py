@@ -30,10 +30,20 @@ def narrow_ok(x2: torch.Tensor, w: torch.Tensor, bias=None, transposed: bool = F
     return bool(ok(x2.shape[0], k_in, n_out))
 
 
-def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None):
-    """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192."""
+def head_major_ok(M: int, N: int, hm) -> bool:
+    """Whether a head-major output (hm = (tokens per window, head dim)) fits: see narrow_linear."""
+    n_tok, d = hm
+    return n_tok > 0 and n_tok % 16 == 0 and M % n_tok == 0 and 2 <= d <= 32 and d % 2 == 0 and N % d == 0
+
+
+def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None, hm=None):
+    """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192.
+    ``hm = (n_tok, d)``: the output buffer [M, N] is filled HEAD-MAJOR -- rows m = window w x n_tok + token t,
+    columns c = segment s x d + dim -> element ((w N + s d) n_tok + t d + dim), i.e. Swin's qkv as
+    [windows, 3, heads, n_tok, d] for the window attention's staging loads (ops.window_attention)."""
     M, K = x2.shape
     N = w.shape[0]
+    hm_n, hm_d = hm if hm is not None else (0, 0)
     if x2.dtype == torch.float32:      # exact-f32 MFMA kernels (v_mfma_f32_16x16x4_f32)
         lib = _lib.require()
         y = torch.empty((M, N), dtype=torch.float32, device=x2.device)
@@ -42,7 +52,7 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
             cs = torch.empty(K, dtype=torch.float32, device=x2.device)
             ws = torch.empty((lib.pdt_narrow_gemm_f32_partials(M) + 64) * K, dtype=torch.float32, device=x2.device)
         _lib.call("pdt_narrow_gemm_f32", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N,
-                  _lib.ptr(cs), _lib.ptr(ws), _lib.stream_handle(x2.device))
+                  _lib.ptr(cs), _lib.ptr(ws), hm_n, hm_d, _lib.stream_handle(x2.device))
         return y, (cs.to(colsum_dtype) if cs is not None else None)
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
     cs = ws = None
@@ -51,7 +61,7 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
         cs = torch.empty(K, dtype=colsum_dtype, device=x2.device)
         ws = torch.empty((lib.pdt_narrow_gemm_partials(M, K, N) + 64) * K, dtype=torch.float32, device=x2.device)
     _lib.call("pdt_narrow_gemm", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N, _lib.ptr(cs),
-              _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws),
+              _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws), hm_n, hm_d,
               _lib.stream_handle(x2.device))
     return y, cs
 

@@ -87,6 +87,7 @@ class _WindowAttnFn(torch.autograd.Function):
         Bw, N, C3 = qkv.shape
         C = C3 // 3
         d = C // num_heads
+        tag = getattr(qkv, "_pdt_head_major", None)
         qkv = qkv.contiguous()
         bias = rel_bias.float().contiguous()
         nw = mask.shape[0] if mask is not None else 1
@@ -103,18 +104,23 @@ class _WindowAttnFn(torch.autograd.Function):
             m = mask.float().contiguous() if mask is not None else None
             lab = _mask_labels(mask) if (mask is not None and USE_LABELS) else None
             st = _lib.stream_handle(qkv.device)
-            ctx.hm = _hm_ok(qkv, N, num_heads, d)
-            # the forward writes a head-major copy [Bw, 3, h, N, d] of q / k / v from the slices it stages anyway:
-            # the backward's staging loads then read each head's token slices contiguously; kept for the backward
-            # in place of qkv (same size)
-            hm = torch.empty_like(qkv) if ctx.hm else None
+            # qkv already head-major (ops.linear.linear_head_major: the narrow GEMM wrote [Bw, 3, h, N, d]): every
+            # staging load reads contiguous token slices.  Otherwise the forward writes a head-major copy of q / k / v
+            # from the slices it stages anyway, for the backward's staging loads (kept in place of qkv, same size).
+            given = tag is not None
+            if given and tag != (N, d):
+                raise RuntimeError(f"window_attention: head-major qkv tagged {tag}, expected {(N, d)}")
+            ctx.hm = given or _hm_ok(qkv, N, num_heads, d)
+            hm = torch.empty_like(qkv) if (ctx.hm and not given) else None
             _lib.call("pdt_win_attn_mfma_fwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_fwd", qkv.data_ptr(),
                       bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
-                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.ptr(hm), st)
-            ctx.save_for_backward(hm if ctx.hm else qkv, bias, o, lse)
+                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.ptr(hm), int(given), st)
+            ctx.save_for_backward(hm if hm is not None else qkv, bias, o, lse)
             ctx.mask = (m, lab, nw)
             ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
             return o
+        if tag is not None:
+            raise RuntimeError("window_attention: a head-major qkv (linear_head_major) needs the MFMA kernels")
         bias_t = bias.transpose(1, 2).contiguous()
         m, m_t = _mask_t(mask) if mask is not None else (None, None)
         _lib.call("pdt_win_attn_fwd", qkv.data_ptr(), bias_t.data_ptr(), _lib.ptr(m_t), nw, o.data_ptr(),
@@ -238,6 +244,18 @@ def window_attention_table(qkv, table, index, mask, num_heads: int, scale: float
     return window_attention(qkv, rel, mask, num_heads, scale)
 
 
+def head_major_ok(x, N: int, num_heads: int, d: int) -> bool:
+    """Whether window_attention would run the MFMA kernels on a qkv of x's device / dtype (the only consumer that
+    reads a head-major qkv, ops.linear.linear_head_major)."""
+    if not (HEAD_MAJOR and x.is_cuda and _lib.available()):
+        return False
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    lib = _lib.require()
+    if dt == torch.bfloat16:
+        return bool(lib.pdt_win_attn_mfma_ok(N, num_heads, d, _lib.dtype_code(dt)))
+    return dt == torch.float32 and MFMA_F32 and bool(lib.pdt_win_attn_mfma32_ok(N, num_heads, d))
+
+
 def supported(qkv, num_heads) -> bool:
     Bw, N, C3 = qkv.shape
     d = C3 // 3 // num_heads
@@ -249,6 +267,8 @@ def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float):
     """qkv [Bw, N, 3C]; rel_bias [h, N, N]; mask [nw, N, N] or None (window b uses mask b % nw)."""
     if supported(qkv, num_heads):
         return _WindowAttnFn.apply(qkv, rel_bias, mask, num_heads, scale)
+    if getattr(qkv, "_pdt_head_major", None) is not None:
+        raise RuntimeError("window_attention: a head-major qkv (linear_head_major) needs the GPU kernels")
     if qkv.is_cuda:
         _lib.require()          # fail loudly on a GPU box without the kernels
     return reference(qkv, rel_bias, mask, num_heads, scale)

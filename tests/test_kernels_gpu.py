@@ -2274,3 +2274,57 @@ def test_window_attention_table_matches_gather(dtype, masked):
     assert rel_err(o, orf) < tol
     assert rel_err(qkv.grad, qr.grad) < 2 * tol
     assert table.grad.dtype == dtype and rel_err(table.grad, tr.grad) < 2 * tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_narrow_linear_head_major_layout(dt):
+    """narrow_linear(hm=(n_tok, d)) writes exactly the token-major product permuted to [windows, 3H, n_tok, d]."""
+    from pytorch_distributedtraining_amd.ops.narrow import narrow_linear, narrow_ok
+    torch.manual_seed(0)
+    Bw, N, H, d = 300, 64, 6, 10
+    x = torch.randn(Bw * N, 60, device=DEV).to(dt)
+    w = (0.1 * torch.randn(3 * H * d, 60, device=DEV)).to(dt)
+    b = torch.randn(3 * H * d, device=DEV).to(dt)
+    assert narrow_ok(x, w, b)
+    y_tm, _ = narrow_linear(x, w, b)
+    y_hm, _ = narrow_linear(x, w, b, hm=(N, d))
+    ref = y_tm.view(Bw, N, 3 * H, d).permute(0, 2, 1, 3).contiguous().view(-1)
+    torch.testing.assert_close(y_hm.view(-1), ref, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_swin_block_head_major_qkv_matches_token_major(dt, monkeypatch):
+    """A SwinIR block at >= 16,384 tokens (the narrow-GEMM range): the head-major qkv path (linear_head_major ->
+    window attention reading head-major) gives the same outputs and gradients as the token-major path, and is taken."""
+    import pytorch_distributedtraining_amd.ops.linear as L
+    from pytorch_distributedtraining_amd.models.swinir import SwinTransformerBlock
+    from pytorch_distributedtraining_amd.ops import window_attention as WA
+    monkeypatch.setattr(L, "NARROW", "1")        # the narrow GEMM regardless of this box's timing pick
+    torch.manual_seed(0)
+    blk = SwinTransformerBlock(60, (32, 32), 6, window_size=8, shift_size=4).to(DEV).to(dt)
+    x = torch.randn(16, 32 * 32, 60, device=DEV, dtype=dt)
+    tags = []
+    real = WA._WindowAttnFn.forward
+
+    def spy(ctx, qkv, *a):
+        tags.append(getattr(qkv, "_pdt_head_major", None))
+        return real(ctx, qkv, *a)
+    monkeypatch.setattr(WA._WindowAttnFn, "forward", staticmethod(spy))
+
+    def run():
+        blk.zero_grad()
+        xi = x.clone().requires_grad_()
+        y = blk(xi, (32, 32))
+        y.float().square().mean().backward()
+        return y.detach(), xi.grad, blk.attn.qkv.weight.grad.clone(), blk.attn.relative_position_bias_table.grad.clone()
+
+    a = run()
+    assert tags and tags[-1] == (64, 10), tags
+    monkeypatch.setattr(L, "HEAD_MAJOR_QKV", False)
+    tags.clear()
+    b = run()
+    assert tags and tags[-1] is None
+    for u, v in zip(a, b):
+        torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
