@@ -86,42 +86,37 @@ __device__ __forceinline__ void put_block(bf16_t* Xs, int KI, int rows, int lane
 }
 
 // Head-major output (hm_n > 0; Swin's qkv projection feeding the window attention): row m = window w, token t
-// (m = w hm_n + t) and column c = segment s (= which x H + head), dim d (c = s hm_d + d) go to
-// Y[w][s][t][d] (element (w NO + s hm_d) hm_n + t hm_d + d): one head's 16 staged tokens are one contiguous run of
-// 16 hm_d elements.
-// Copied from the [16][NO] staging block in 2-element units (hm_d, NO even); a lane's units inside a segment
-// (q = lane + 64 i < 8 hm_d) are fixed, so their (row, unit) split is computed once per kernel.
-template <typename U>   // U = a 2-element unit (uint32_t for bf16, uint2 for fp32)
-struct HmStore {
-  int r[4], dd[4], nq;
-  __device__ __forceinline__ void init(int hm_d, int lane) {
-    const int du = hm_d / 2;
-    nq = 0;
+// (m = w hm_n + t) and column c = segment s (= which x H + head), dim d (c = s hm_d + d) go to element
+// (w NO + s hm_d) hm_n + t hm_d + d: one head's 16 staged tokens are one contiguous run of 16 hm_d elements,
+// written as 16-byte chunks whose 4 dwords are gathered from the [16][NO] staging block (a dword never straddles
+// two tokens: hm_d even).  Blocks are always full (M % hm_n == 0, hm_n % 16 == 0).  Integer splits by the runtime
+// divisors go through a float reciprocal (exact: operands < 2^12).
+__device__ __forceinline__ int fdiv(int a, float inv) { return __float2int_rz(((float)a + 0.5f) * inv); }
+template <typename T>
+__device__ __forceinline__ void hm_store(T* __restrict__ Y, const T* Ys, int64_t blk, int NO, int hm_n, int hm_d,
+                                         int lane) {
+  const int dpt = hm_d * (int)sizeof(T) / 4;            // dwords per token slice
+  const int cps = 4 * dpt;                               // 16-byte chunks per segment run (16 dpt dwords)
+  const int nch = (NO / hm_d) * cps;
+  const int rowd = NO * (int)sizeof(T) / 4;              // dwords per staged row
+  const float inv_cps = 1.f / (float)cps, inv_dpt = 1.f / (float)dpt;
+  const int64_t row0 = blk * 16;
+  const int64_t win = row0 / hm_n;
+  const int t0 = (int)(row0 - win * hm_n);
+  uint32_t* base = reinterpret_cast<uint32_t*>(Y + win * hm_n * NO + (int64_t)t0 * hm_d);
+  const uint32_t* ys = reinterpret_cast<const uint32_t*>(Ys);
+  const int64_t seg_stride = (int64_t)hm_n * hm_d * (int)sizeof(T) / 4;
+  for (int c = lane; c < nch; c += 64) {
+    const int sg = fdiv(c, inv_cps), k = c - sg * cps;
+    uint32_t v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = lane + 64 * i;
-      r[i] = q / du;
-      dd[i] = q - r[i] * du;
-      if (q < 16 * du) nq = i + 1;
+    for (int j = 0; j < 4; ++j) {
+      const int w = 4 * k + j, r = fdiv(w, inv_dpt), dd = w - r * dpt;
+      v[j] = ys[r * rowd + sg * dpt + dd];
     }
+    *reinterpret_cast<uint4*>(base + sg * seg_stride + 4 * k) = make_uint4(v[0], v[1], v[2], v[3]);
   }
-  template <typename T>
-  __device__ __forceinline__ void store(T* __restrict__ Y, const T* Ys, int64_t blk, int rows, int NO, int hm_n,
-                                        int hm_d) const {
-    const int64_t row0 = blk * 16;
-    const int64_t win = row0 / hm_n;
-    const int t0 = (int)(row0 - win * hm_n);
-    T* base = Y + win * hm_n * NO + (int64_t)t0 * hm_d;
-    for (int sg = 0; sg < NO / hm_d; ++sg) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < nq && r[i] < rows)
-          *reinterpret_cast<U*>(base + (int64_t)sg * hm_n * hm_d + r[i] * hm_d + 2 * dd[i]) =
-              *reinterpret_cast<const U*>(Ys + r[i] * NO + sg * hm_d + 2 * dd[i]);
-      }
-    }
-  }
-};
+}
 
 template <int KP, int NP>
 __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* __restrict__ X,
@@ -160,8 +155,6 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
     bcol[nt] = (bias != nullptr && n < NO) ? bf2f(bias[n]) : 0.f;
   }
   float cs[3] = {0.f, 0.f, 0.f};                 // COLSUM: columns lane, lane + 64, lane + 128
-  HmStore<uint32_t> hms;
-  if (hm_n > 0) hms.init(hm_d, lane);
 
   const int64_t nblk = (M + 15) / 16;
   const int64_t gw = (int64_t)blockIdx.x * NW + wv, nwaves = (int64_t)gridDim.x * NW;
@@ -201,7 +194,7 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
     }
     wave_sync();
     if (hm_n > 0) {
-      hms.store(Y, Ys, blk, rows, NO, hm_n, hm_d);
+      hm_store(Y, Ys, blk, NO, hm_n, hm_d, lane);
     } else {
       bf16_t* dst = Y + blk * 16 * NO;
       const int tot = rows * NO, n8 = tot >> 3;
@@ -393,8 +386,6 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
     bcol[nt] = (bias != nullptr && n < NO) ? bias[n] : 0.f;
   }
   float cs[3] = {0.f, 0.f, 0.f};
-  HmStore<uint2> hms;
-  if (hm_n > 0) hms.init(hm_d, lane);
   __syncthreads();
   const int64_t nblk = (M + 15) / 16;
   const int64_t gw = (int64_t)blockIdx.x * NW32 + wv, nwaves = (int64_t)gridDim.x * NW32;
@@ -456,7 +447,7 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
     }
     wave_sync();
     if (hm_n > 0) {
-      hms.store(Y, Ys, blk, rows, NO, hm_n, hm_d);
+      hm_store(Y, Ys, blk, NO, hm_n, hm_d, lane);
     } else {
       float* dst = Y + blk * 16 * NO;
       const int n4 = rows * NO / 4;
@@ -598,7 +589,7 @@ PDT_API int pdt_narrow_gemm_partials(int64_t M, int KI, int NO) { return narrow_
 // Y [M, NO] bf16 = X [M, KI] bf16 . B [NO, KI]^T (+ bias [NO] bf16); X, Y contiguous and 16-byte aligned.
 // colsum_out (nullable, fp32 [KI], W dtype by wdt): column sums of X -- written (not accumulated) -- with ws
 // >= (pdt_narrow_gemm_partials(M, KI, NO) + 64) * KI floats (partials + the column reduce's second level).
-// hm_n > 0: Y head-major (narrow_gemm_kernel's HmStore): M % hm_n == 0, hm_n % 16 == 0, NO % hm_d == 0, hm_d even
+// hm_n > 0: Y head-major (hm_store): M % hm_n == 0, hm_n % 16 == 0, NO % hm_d == 0, hm_d even
 // and <= 32
 static bool hm_ok(int64_t M, int NO, int hm_n, int hm_d) {
   return hm_n == 0 || (hm_n > 0 && hm_n % 16 == 0 && M % hm_n == 0 && hm_d >= 2 && hm_d <= 32 && hm_d % 2 == 0 &&

@@ -51,19 +51,21 @@ __global__ __launch_bounds__(64 * SUM_WAVES) void rel_bias_sum_kernel(const floa
   }
 }
 
-// out[t][h] = sum over row t's CSR positions of dense[h][p] (fixed order): one thread per (t, h)
+// out[t][h] = sum over row t's CSR positions of dense[h][p]: one wave per (t, h), a lane per position (<= 64 per
+// row for windows up to 8 x 8; longer lists loop), summed in a fixed shuffle order
 template <typename T>
 __global__ __launch_bounds__(RB_NT) void rel_bias_scatter_kernel(const float* __restrict__ dense, int H, int NN,
                                                                 const int* __restrict__ off,
                                                                 const int* __restrict__ pos, int TR,
                                                                 T* __restrict__ out) {
-  const int e = blockIdx.x * RB_NT + threadIdx.x;
+  const int e = blockIdx.x * (RB_NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (e >= TR * H) return;
   const int t = e / H, h = e - t * H;
   const float* d = dense + (int64_t)h * NN;
   float s = 0.f;
-  for (int i = off[t]; i < off[t + 1]; ++i) s += d[pos[i]];
-  out[e] = from_f<T>(s);
+  for (int i = off[t] + lane; i < off[t + 1]; i += 64) s += d[pos[i]];
+  s = wave_sum(s);
+  if (lane == 0) out[e] = from_f<T>(s);
 }
 
 }  // namespace
@@ -87,7 +89,7 @@ PDT_API int pdt_rel_bias_scatter(const float* part, int G, int H, int NN, const 
                                  void* out, int dt, float* ws, hipStream_t st) {
   if (G <= 0 || H <= 0 || NN <= 0 || TR <= 0 || (dt != kF32 && dt != kBF16)) return (int)hipErrorInvalidValue;
   rel_bias_sum_kernel<<<(H * NN + 63) / 64, 64 * SUM_WAVES, 0, st>>>(part, G, H * NN, ws);
-  const int grid = (TR * H + RB_NT - 1) / RB_NT;
+  const int grid = (TR * H + RB_NT / 64 - 1) / (RB_NT / 64);
   if (dt == kF32)
     rel_bias_scatter_kernel<float><<<grid, RB_NT, 0, st>>>(ws, H, NN, off, pos, TR, (float*)out);
   else
