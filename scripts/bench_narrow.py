@@ -42,9 +42,14 @@ for name, K, N, bias, role in [("qkv fwd", 60, 180, True, "fwd"), ("proj fwd", 6
         wl = w.t().contiguous()
         tl = t_ms(lambda: (torch.mm(x, wl), _colsum(x, torch.bfloat16)))
     gb = (M * K + M * N) * 2 / 1e9
+    extra = {}
+    if role == "fwd" and N % 10 == 0:      # head-major output (Swin's qkv: 64-token windows, d = 10)
+        extra["narrow_head_major_us"] = round(1000 * t_ms(lambda: narrow_linear(x, w, b, hm=(64, 10))), 1)
+    if role == "dgrad":                    # without the fused column sum
+        extra["narrow_no_colsum_us"] = round(1000 * t_ms(lambda: narrow_linear(x, w, None)), 1)
     print(json.dumps({"op": name, "M": M, "K": K, "N": N, "narrow_us": round(1000 * tn, 1),
                       "library_us": round(1000 * tl, 1), "narrow_TBps": round(gb / tn, 2),
-                      "speedup": round(tl / tn, 2)}), flush=True)
+                      "speedup": round(tl / tn, 2), **extra}), flush=True)
 for name, N, K in [("qkv wgrad", 180, 60), ("proj wgrad", 60, 60)]:
     dy = torch.randn(M, N, device=dev).bfloat16()
     x = torch.randn(M, K, device=dev).bfloat16()
