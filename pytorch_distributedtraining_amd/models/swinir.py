@@ -191,9 +191,10 @@ class SwinTransformerBlock(nn.Module):
             if WINDOW_NORMS and window_norm_ok(x, H, W, ws, ss) and self.norm1.weight.dtype == self.norm2.weight.dtype:
                 # the roll / partition / reverse permutations ride inside the two LayerNorms (ops.norms WinMap):
                 # norm1 writes window order, norm2 reads the attention output from window order
-                win = layer_norm_to_windows(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, H, W, ws, ss)
+                # (xs: x passed through norm1, so the residual's gradient is added inside norm1's backward pass)
+                win, xs = layer_norm_to_windows(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, H, W, ws, ss)
                 a = self.attn(win, mask=mask).to(x.dtype)
-                y, s = add_layer_norm_from_windows(x, a, self.norm2.weight, self.norm2.bias, self.norm2.eps, H, W,
+                y, s = add_layer_norm_from_windows(xs, a, self.norm2.weight, self.norm2.bias, self.norm2.eps, H, W,
                                                    ws, ss)
                 return self.mlp(y, residual=s)
             h = self.norm1(x).to(x.dtype)

@@ -185,7 +185,9 @@ def _win_norm_bwd(dy2, x2, w, mean, rstd, need_b, dres2, geom, mode):
 
 
 class _NormToWindowsFn(torch.autograd.Function):
-    """y_win = window_partition(roll(LayerNorm(x), -shift)) -- [B, H*W, C] in, [B*nW, ws*ws, C] out, one pass."""
+    """(y_win, x): y_win = window_partition(roll(LayerNorm(x), -shift)) -- [B, H*W, C] in, [B*nW, ws*ws, C] out, one
+    pass -- and x passed through (as _NormPassFn): the block's residual use of x hands its gradient back here and
+    the backward kernel adds it to dx (no separate add over the stream per block)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, eps, geom):
@@ -195,13 +197,15 @@ class _NormToWindowsFn(torch.autograd.Function):
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.geom, ctx.has_bias, ctx.shape = geom, bias is not None, x.shape
         ws = geom[2]
-        return y.view(-1, ws * ws, C)
+        return y.view(-1, ws * ws, C), x
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, ds):
         x2, w, mean, rstd = ctx.saved_tensors
-        dx, _, dw, db = _win_norm_bwd(dy.reshape(-1, x2.shape[1]).contiguous(), x2, w, mean, rstd, ctx.has_bias, None,
-                                      ctx.geom, 1)
+        n = x2.shape[1]
+        dy2 = dy.reshape(-1, n).contiguous() if dy is not None else torch.zeros_like(x2)
+        ds2 = ds.reshape(-1, n).contiguous() if ds is not None else None
+        dx, _, dw, db = _win_norm_bwd(dy2, x2, w, mean, rstd, ctx.has_bias, ds2, ctx.geom, 1)
         return dx.view(ctx.shape), dw, db, None, None
 
 
@@ -230,7 +234,8 @@ class _AddNormFromWindowsFn(torch.autograd.Function):
 
 
 def layer_norm_to_windows(x, weight, bias, eps, H, W, ws, shift):
-    """LayerNorm of [B, H*W, C] written in shifted-window order [B*nW, ws*ws, C] (see window_norm_ok)."""
+    """(LayerNorm of [B, H*W, C] written in shifted-window order [B*nW, ws*ws, C], x) -- use the returned x for the
+    residual so its gradient is folded into this norm's backward (see window_norm_ok)."""
     return _NormToWindowsFn.apply(x, weight, bias, eps, (H, W, ws, shift))
 
 

@@ -2105,9 +2105,9 @@ def test_window_mapped_norms_match_permute_path(H, W, ws, shift, dt):
     assert window_norm_ok(x, H, W, ws, shift)
     nwin = B * (H // ws) * (W // ws)
     mix = torch.randn(C, C, device=DEV) * C ** -0.5        # stands in for the attention: a window-order function
-    win = layer_norm_to_windows(x, w1, b1, 1e-5, H, W, ws, shift)
+    win, xs = layer_norm_to_windows(x, w1, b1, 1e-5, H, W, ws, shift)   # xs: x passed through (gradient folded)
     a = (win.float() @ mix).to(dt)
-    y, s = add_layer_norm_from_windows(x, a, w2, b2, 1e-5, H, W, ws, shift)
+    y, s = add_layer_norm_from_windows(xs, a, w2, b2, 1e-5, H, W, ws, shift)
     gy, gs = torch.randn_like(y), torch.randn_like(s)
     (y.float() * gy.float()).sum().add_((s.float() * gs.float()).sum()).backward()
     xr = x.detach().float().requires_grad_()
