@@ -65,6 +65,50 @@ __device__ __forceinline__ void load_block(const bf16_t* __restrict__ X, int64_t
   }
 }
 
+// ... the same block from a HEAD-MAJOR X ([windows][KI / a_d][a_n][a_d]: ops.window_attention's output for the
+// projection after it): the block's 16 tokens of segment s are one contiguous run of 16 a_d elements at
+// (w KI + s a_d) a_n + t0 a_d; chunk c = lane + 64 i covers elements 8c .. 8c+7 of the concatenated runs (16 a_d % 8
+// == 0).  Blocks are always full (M % a_n == 0, a_n % 16 == 0).
+__device__ __forceinline__ int fdiv_i(int a, float inv) { return __float2int_rz(((float)a + 0.5f) * inv); }
+template <int KP, int NP>
+__device__ __forceinline__ void load_block_hm(const bf16_t* __restrict__ X, int KI, int64_t blk, int lane, int a_n,
+                                              int a_d, u16x8 (&ch)[NarrowCfg<KP, NP>::CH]) {
+  const int64_t r0 = blk * 16;
+  const int64_t win = r0 / a_n;
+  const int t0 = (int)(r0 - win * a_n);
+  const int run = 16 * a_d, n8 = 2 * KI;                // elements per segment run; chunks per block (16 KI / 8)
+  const float inv_run = 1.f / (float)run;
+  const bf16_t* base = X + win * a_n * KI + (int64_t)t0 * a_d;
+#pragma unroll
+  for (int i = 0; i < NarrowCfg<KP, NP>::CH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n8) {
+      const int sg = fdiv_i(8 * c, inv_run), off = 8 * c - sg * run;
+      ch[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)sg * a_n * a_d + off);
+    }
+  }
+}
+template <int KP, int NP>
+__device__ __forceinline__ void put_block_hm(bf16_t* Xs, int KI, int lane, int a_d,
+                                             const u16x8 (&ch)[NarrowCfg<KP, NP>::CH]) {
+  constexpr int XP = NarrowCfg<KP, NP>::XP;
+  const int run = 16 * a_d, n8 = 2 * KI;
+  const float inv_run = 1.f / (float)run, inv_d = 1.f / (float)a_d;
+#pragma unroll
+  for (int i = 0; i < NarrowCfg<KP, NP>::CH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n8) {
+      const int sg = fdiv_i(8 * c, inv_run), off = 8 * c - sg * run;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {               // element pairs never straddle two tokens (a_d even)
+        const int e = off + 2 * k, r = fdiv_i(e, inv_d), dd = e - r * a_d;
+        *reinterpret_cast<uint32_t*>(Xs + r * XP + sg * a_d + dd) =
+            (uint32_t)ch[i][2 * k] | ((uint32_t)ch[i][2 * k + 1] << 16);
+      }
+    }
+  }
+}
+
 template <int KP, int NP>
 __device__ __forceinline__ void put_block(bf16_t* Xs, int KI, int rows, int lane,
                                           const u16x8 (&ch)[NarrowCfg<KP, NP>::CH]) {
@@ -123,7 +167,8 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
                                                                  const bf16_t* __restrict__ B,
                                                                  const bf16_t* __restrict__ bias,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ colsum_part,
-                                                                 int64_t M, int KI, int NO, int hm_n, int hm_d) {
+                                                                 int64_t M, int KI, int NO, int hm_n, int hm_d, int a_n,
+                                                                 int a_d) {
   typedef NarrowCfg<KP, NP> Cfg;
   constexpr int XP = Cfg::XP, KS = Cfg::KS, NT = Cfg::NT;
   extern __shared__ __attribute__((aligned(16))) bf16_t nsm[];
@@ -159,12 +204,19 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
   const int64_t nblk = (M + 15) / 16;
   const int64_t gw = (int64_t)blockIdx.x * NW + wv, nwaves = (int64_t)gridDim.x * NW;
   u16x8 ch[Cfg::CH];
-  if (gw < nblk) load_block<KP, NP>(X, M, KI, gw, lane, ch);
+  if (gw < nblk) {
+    if (a_n > 0) load_block_hm<KP, NP>(X, KI, gw, lane, a_n, a_d, ch);
+    else load_block<KP, NP>(X, M, KI, gw, lane, ch);
+  }
   for (int64_t blk = gw; blk < nblk; blk += nwaves) {
     const int rows = M - blk * 16 < 16 ? (int)(M - blk * 16) : 16;
     wave_sync();                                 // the previous block's LDS reads are done
-    put_block<KP, NP>(Xs, KI, rows, lane, ch);
-    if (blk + nwaves < nblk) load_block<KP, NP>(X, M, KI, blk + nwaves, lane, ch);   // in flight under the MFMAs
+    if (a_n > 0) put_block_hm<KP, NP>(Xs, KI, lane, a_d, ch);
+    else put_block<KP, NP>(Xs, KI, rows, lane, ch);
+    if (blk + nwaves < nblk) {                   // in flight under the MFMAs
+      if (a_n > 0) load_block_hm<KP, NP>(X, KI, blk + nwaves, lane, a_n, a_d, ch);
+      else load_block<KP, NP>(X, M, KI, blk + nwaves, lane, ch);
+    }
     wave_sync();
     f32x4 acc[NT];
 #pragma unroll
@@ -277,11 +329,32 @@ __device__ __forceinline__ void wg_put(bf16_t* img, int pitch, int C, int t, con
   }
 }
 
+// a 64-row block of a HEAD-MAJOR X whose windows are exactly the 64-row blocks ([M / 64][C / a_d][64][a_d]): the
+// block is still one contiguous run (the same 16-byte loads), only the element order differs -- element e = segment
+// s, token r, dim dd goes to image row r, column s a_d + dd (written as element pairs: a_d even)
+template <int CH>
+__device__ __forceinline__ void wg_put_hm(bf16_t* img, int pitch, int C, int t, int a_d, const u16x8 (&v)[CH]) {
+  const float inv_run = 1.f / (float)(WG_ROWS * a_d), inv_d = 1.f / (float)a_d;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int c = t + 64 * WG_WAVES * i;
+    if (8 * c < WG_ROWS * C) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 8 * c + 2 * k;
+        const int sg = fdiv_i(e, inv_run), o = e - sg * WG_ROWS * a_d;
+        const int r = fdiv_i(o, inv_d), dd = o - r * a_d;
+        *reinterpret_cast<uint32_t*>(img + r * pitch + sg * a_d + dd) = (uint32_t)v[i][2 * k] | ((uint32_t)v[i][2 * k + 1] << 16);
+      }
+    }
+  }
+}
+
 template <int NP, int KP>
 __global__ __launch_bounds__(64 * WG_WAVES, 1) void narrow_wgrad_kernel(const bf16_t* __restrict__ dY,
                                                                         const bf16_t* __restrict__ X,
                                                                         float* __restrict__ part, int64_t M, int NO,
-                                                                        int KI) {
+                                                                        int KI, int x_hm_d) {
   typedef WgradCfg<NP, KP> Cfg;
   extern __shared__ __attribute__((aligned(16))) bf16_t wsm[];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -303,7 +376,8 @@ __global__ __launch_bounds__(64 * WG_WAVES, 1) void narrow_wgrad_kernel(const bf
     bf16_t* ys = wsm + (it & 1) * Cfg::BUF;
     bf16_t* xs = ys + WG_ROWS * Cfg::PN;
     wg_put<Cfg::CHY>(ys, Cfg::PN, NO, t, vy);
-    wg_put<Cfg::CHX>(xs, Cfg::PK, KI, t, vx);
+    if (x_hm_d > 0) wg_put_hm<Cfg::CHX>(xs, Cfg::PK, KI, t, x_hm_d, vx);
+    else wg_put<Cfg::CHX>(xs, Cfg::PK, KI, t, vx);
     if (blk + gridDim.x < nblk) {
       wg_load<Cfg::CHY>(dY, M, NO, (blk + gridDim.x) * WG_ROWS, t, vy);
       wg_load<Cfg::CHX>(X, M, KI, (blk + gridDim.x) * WG_ROWS, t, vx);
@@ -595,9 +669,11 @@ static bool hm_ok(int64_t M, int NO, int hm_n, int hm_d) {
   return hm_n == 0 || (hm_n > 0 && hm_n % 16 == 0 && M % hm_n == 0 && hm_d >= 2 && hm_d <= 32 && hm_d % 2 == 0 &&
                        NO % hm_d == 0);
 }
+// a_n > 0: X head-major ([M / a_n][KI / a_d][a_n][a_d], load_block_hm), same constraints as hm_n / hm_d on KI
 PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void* Y, int64_t M, int KI, int NO,
-                            void* colsum_out, int wdt, float* ws, int hm_n, int hm_d, hipStream_t st) {
-  if (!pdt_narrow_gemm_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15))
+                            void* colsum_out, int wdt, float* ws, int hm_n, int hm_d, int a_n, int a_d, hipStream_t st) {
+  if (!pdt_narrow_gemm_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || !hm_ok(M, KI, a_n, a_d) || ((uintptr_t)X & 15) ||
+      ((uintptr_t)Y & 15))
     return (int)hipErrorInvalidValue;
   const int KP = pad_to(KI, 64) <= 64 ? 64 : pad_to(KI, 64);
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
@@ -605,7 +681,7 @@ PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void
   float* part = colsum_out ? ws : nullptr;
 #define PDT_NG(KP_, NP_)                                                                                        \
   narrow_gemm_kernel<KP_, NP_><<<grid, 64 * NW, NW * NarrowCfg<KP_, NP_>::WAVE_ELEMS * sizeof(bf16_t), st>>>(   \
-      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d)
+      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d, a_n, a_d)
 #define PDT_NG_N(KP_) \
   do { if (NP == 64) PDT_NG(KP_, 64); else if (NP == 128) PDT_NG(KP_, 128); else PDT_NG(KP_, 192); } while (0)
   if (KP == 64) PDT_NG_N(64);
@@ -637,15 +713,18 @@ PDT_API int pdt_narrow_wgrad_ok(int64_t M, int NO, int KI) {
 PDT_API int64_t pdt_narrow_wgrad_ws_floats(int64_t M, int NO, int KI) {
   return ((int64_t)wgrad_grid(M) + 64) * NO * KI;
 }
+// x_hm_d > 0: X head-major with 64-token windows ([M / 64][KI / x_hm_d][64][x_hm_d], wg_put_hm)
 PDT_API int pdt_narrow_wgrad(const void* dY, const void* X, void* dW, int64_t M, int NO, int KI, int wdt, float* ws,
-                             hipStream_t st) {
-  if (!pdt_narrow_wgrad_ok(M, NO, KI) || ((uintptr_t)dY & 15) || ((uintptr_t)X & 15)) return (int)hipErrorInvalidValue;
+                             int x_hm_d, hipStream_t st) {
+  if (!pdt_narrow_wgrad_ok(M, NO, KI) || ((uintptr_t)dY & 15) || ((uintptr_t)X & 15) ||
+      (x_hm_d && (M % WG_ROWS || KI % x_hm_d || x_hm_d % 2)))
+    return (int)hipErrorInvalidValue;
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
   const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
   const int grid = wgrad_grid(M);
 #define PDT_WG(NP_, KP_)                                                                                       \
   narrow_wgrad_kernel<NP_, KP_><<<grid, 64 * WG_WAVES, wgrad_lds<NP_, KP_>(), st>>>(                          \
-      (const bf16_t*)dY, (const bf16_t*)X, ws, M, NO, KI)
+      (const bf16_t*)dY, (const bf16_t*)X, ws, M, NO, KI, x_hm_d)
 #define PDT_WG_K(NP_) \
   do { if (KP == 64) PDT_WG(NP_, 64); else if (KP == 128) PDT_WG(NP_, 128); else PDT_WG(NP_, 192); } while (0)
   if (NP == 64) PDT_WG_K(64);

@@ -384,7 +384,9 @@ PDT_API int pdt_swin_mlp_fwd(const void* x, const void* w1, const void* b1, cons
   if (T <= 0 || !swin_mlp_shape_ok(C, H, x, y) || !swin_mlp_shape_ok(C, H, res, res)) return (int)hipErrorInvalidValue;
   const int64_t tiles = (T + 15) / 16;
   int64_t grid = (tiles + 3) / 4;
-  if (grid > 1024) grid = 1024;
+  // workgroups (4 waves each; every wave loads the weights into VGPRs once): PDT_SWIN_MLP_FWD_WG overrides
+  static const int cap = [] { const char* e = getenv("PDT_SWIN_MLP_FWD_WG"); return e ? atoi(e) : 1024; }();
+  if (grid > cap) grid = cap;
   swin_mlp_fwd_kernel<<<(int)grid, 256, 0, st>>>((const bf16_t*)x, (const bf16_t*)w1, (const bf16_t*)b1,
                                                  (const bf16_t*)w2, (const bf16_t*)b2, (const bf16_t*)res, (bf16_t*)y,
                                                  T, C, H);

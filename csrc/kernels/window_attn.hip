@@ -278,17 +278,13 @@ constexpr int BWD_WAVE = 4 * 1024 + 256 + 2 * TT + 4 + 32;    // QR KR VR GR, SL
 //   the bf16 kernels' time, profiles/r6/r6p_window_attn_staging_ab.txt).
 // delta: rowsum(dO o O) per (window, head, token) precomputed by pdt_win_bwd_prep (null: the backward computes it
 // from O while staging).
-// experiment builds only (-DPDT_WA_EXP_HMSTORE): O and dQ/dK/dV stored head-major (wrong layout for their
-// consumers) -- measures what the strided per-lane output stores cost
-#ifdef PDT_WA_EXP_HMSTORE
-#define WA_DQKV_ADDR(p, bw, t, w) ((p) + ((((int64_t)(bw) * 3 + (w)) * H + h) * N + (t)) * D)
-#define WA_O_ADDR(p, bw, t) ((p) + (((int64_t)(bw) * H + h) * N + (t)) * D)
-#else
+// dQ / dK / dV are always written token-major (the qkv projection's backward reads them); O is written token-major
+// ([Bw, N, C]: oT = C, oH = d) or head-major ([Bw, H, N, d]: oT = d, oH = N d) for a projection that reads it so
+// (ops.linear.linear_from_head_major): one head's 64 token slices then leave as one contiguous run.
 #define WA_DQKV_ADDR(p, bw, t, w) ((p) + ((int64_t)(bw) * N + (t)) * C3 + (w) * C + h * D)
-#define WA_O_ADDR(p, bw, t) ((p) + ((int64_t)(bw) * N + (t)) * C + h * D)
-#endif
+#define WA_O_ADDR(p, bw, t) ((p) + (int64_t)(bw) * N * C + (t) * LY.oT + h * LY.oH)
 struct WaLayout {
-  int qT, qH, qW, gT, gH;
+  int qT, qH, qW, gT, gH, oT, oH;
   const float* delta;
 };
 __device__ __forceinline__ f32x4 label_mask(const uint8_t* lab, int base, uint32_t mine) {
@@ -888,7 +884,7 @@ __global__ __launch_bounds__(WA_NT, 2) void win_attn_fwd_f32(const float* __rest
         for (int r = 0; r < 16; ++r) acc = mfma2(VR[(32 * kt + acc_row(r, hh)) * RP + dcl], p[qt][kt][r], acc);
       const int q = 32 * qt + l32;
       if (FULL || q < N) {
-        store_dims_f32<D>(o + ((int64_t)bw * N + q) * C + h * D, acc, 1.f / lsum[qt], hh);
+        store_dims_f32<D>(WA_O_ADDR(o, bw, q), acc, 1.f / lsum[qt], hh);
         if (hh == 0) lse[((int64_t)bw * H + h) * N + q] = mmax[qt] + __logf(lsum[qt]);
       }
     }
@@ -1126,9 +1122,11 @@ int wa_f32_bwd_launch(const float* qkv, const float* bias, const float* mask, co
 }  // namespace
 
 namespace {
-WaLayout wa_layout(int N, int H, int d, int q_hm, int g_hm, const float* delta) {
+WaLayout wa_layout(int N, int H, int d, int q_hm, int g_hm, const float* delta, int o_hm = 0) {
   const int C = H * d;
   WaLayout L;
+  if (o_hm) { L.oT = d; L.oH = N * d; }
+  else { L.oT = C; L.oH = d; }
   if (q_hm) { L.qT = d; L.qH = N * d; L.qW = H * N * d; }
   else { L.qT = 3 * C; L.qH = d; L.qW = C; }
   if (g_hm) { L.gT = d; L.gH = N * d; }
@@ -1160,11 +1158,12 @@ __device__ __forceinline__ void stage_block(const void* src, uint32_t* sm, int b
   for (int i = threadIdx.x; i < bytes / 16; i += HM_NT) d[i] = s[i];
 }
 
-// dO -> head-major, and delta[bw][h][t] = sum_c dO[t][h d + c] O[t][h d + c] (fp32) from the same staged rows
+// dO -> head-major (unless it already is), and delta[bw][h][t] = sum_c dO[t][h d + c] O[t][h d + c] (fp32) from the
+// same staged blocks; g_hm / o_hm: dO / O given head-major ([H][N][d] per window) instead of token-major ([N][C])
 template <typename T>
 __global__ __launch_bounds__(HM_NT) void bwd_prep_kernel(const T* __restrict__ dout, const T* __restrict__ o,
                                                         T* __restrict__ dout_hm, float* __restrict__ delta, int N,
-                                                        int H, int d) {
+                                                        int H, int d, int g_hm, int o_hm) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smh[];
   const int C = H * d;
   const int bytes = N * C * (int)sizeof(T);
@@ -1173,13 +1172,14 @@ __global__ __launch_bounds__(HM_NT) void bwd_prep_kernel(const T* __restrict__ d
   stage_block<sizeof(T)>(dout + (int64_t)blockIdx.x * N * C, sg, bytes);
   stage_block<sizeof(T)>(o + (int64_t)blockIdx.x * N * C, so, bytes);
   __syncthreads();
-  hm_permute<sizeof(T)>(sg, reinterpret_cast<uint32_t*>(dout_hm + (int64_t)blockIdx.x * N * C), N, H, d, 1);
+  if (!g_hm) hm_permute<sizeof(T)>(sg, reinterpret_cast<uint32_t*>(dout_hm + (int64_t)blockIdx.x * N * C), N, H, d, 1);
   const T* g = reinterpret_cast<const T*>(sg);
   const T* oo = reinterpret_cast<const T*>(so);
+  const int gT = g_hm ? d : C, gH = g_hm ? N * d : d, oT = o_hm ? d : C, oH = o_hm ? N * d : d;
   for (int i = threadIdx.x; i < H * N; i += HM_NT) {
     const int h = i / N, t = i - h * N;
     float s = 0.f;
-    for (int c = 0; c < d; ++c) s = fmaf(to_f<T>(g[t * C + h * d + c]), to_f<T>(oo[t * C + h * d + c]), s);
+    for (int c = 0; c < d; ++c) s = fmaf(to_f<T>(g[t * gT + h * gH + c]), to_f<T>(oo[t * oT + h * oH + c]), s);
     delta[(int64_t)blockIdx.x * H * N + i] = s;
   }
 }
@@ -1188,7 +1188,7 @@ __global__ __launch_bounds__(HM_NT) void bwd_prep_kernel(const T* __restrict__ d
 // dout, o [Bw, N, C] token-major -> dout_hm [Bw, H, N, d], delta [Bw, H, N] fp32.  16-byte aligned; N C elem_bytes
 // a multiple of 16.
 PDT_API int pdt_win_bwd_prep(const void* dout, const void* o, void* dout_hm, float* delta, int Bw, int N, int H, int d,
-                             int dt, hipStream_t st) {
+                             int dt, int g_hm, int o_hm, hipStream_t st) {
   const int E = dt == kF32 ? 4 : 2;
   const int64_t bytes = (int64_t)N * H * d * E;
   if (Bw <= 0 || d % 2 || bytes % 16 || 2 * bytes > 96 * 1024 ||
@@ -1196,10 +1196,10 @@ PDT_API int pdt_win_bwd_prep(const void* dout, const void* o, void* dout_hm, flo
     return (int)hipErrorInvalidValue;
   if (E == 4)
     bwd_prep_kernel<float><<<Bw, HM_NT, 2 * bytes, st>>>((const float*)dout, (const float*)o, (float*)dout_hm, delta, N,
-                                                         H, d);
+                                                         H, d, g_hm, o_hm);
   else
     bwd_prep_kernel<bf16_t><<<Bw, HM_NT, 2 * bytes, st>>>((const bf16_t*)dout, (const bf16_t*)o, (bf16_t*)dout_hm,
-                                                          delta, N, H, d);
+                                                          delta, N, H, d, g_hm, o_hm);
   return (int)hipGetLastError();
 }
 
@@ -1286,10 +1286,10 @@ int wa_bwd_launch(const void* qkv, const float* bias, const float* mask, const u
 // (hm = 1), written from the staged slices
 PDT_API int pdt_win_attn_mfma_fwd(const void* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                   void* o, float* lse, int Bw, int N, int H, int d, float scale, void* hm_out,
-                                  int q_hm, hipStream_t st) {
+                                  int q_hm, int o_hm, hipStream_t st) {
   if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (q_hm && hm_out))
     return (int)hipErrorInvalidValue;
-  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr);
+  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr, o_hm);
 #define PDT_C(D) \
   return wa_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)
@@ -1314,10 +1314,10 @@ PDT_API int pdt_win_attn_mfma_bwd(const void* qkv, const float* bias, const floa
 PDT_API int pdt_win_attn_mfma32_ok(int N, int H, int d) { return mfma_ok(N, H, d, kBF16) ? 1 : 0; }
 PDT_API int pdt_win_attn_mfma32_fwd(const float* qkv, const float* bias, const float* mask, const void* labels, int nw,
                                     float* o, float* lse, int Bw, int N, int H, int d, float scale, float* hm_out,
-                                    int q_hm, hipStream_t st) {
+                                    int q_hm, int o_hm, hipStream_t st) {
   if (!mfma_ok(N, H, d, kBF16) || Bw <= 0 || ((mask || labels) && nw <= 0) || (q_hm && hm_out))
     return (int)hipErrorInvalidValue;
-  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr);
+  const WaLayout LY = wa_layout(N, H, d, q_hm, 0, nullptr, o_hm);
 #define PDT_C(D) \
   return wa_f32_fwd_launch<D>(qkv, bias, mask, (const uint8_t*)labels, nw, o, lse, Bw, N, H, scale, LY, hm_out, st)
   PDT_WA_DISPATCH_D(d, PDT_C)

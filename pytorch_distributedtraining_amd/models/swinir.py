@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
-from ..ops.linear import Linear, linear, linear_head_major
+from ..ops.linear import Linear, linear, linear_from_head_major, linear_head_major
 from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
 from ..ops.norms import LayerNorm, add_layer_norm_from_windows, layer_norm_to_windows, window_norm_ok
 from ..ops.window_attention import (fused_window_ok, head_major_ok, window_attention, window_attention_table,
@@ -37,6 +37,8 @@ _FUSED_TAIL = os.environ.get("PDT_SWINIR_FUSED_TAIL", "1") == "1"
 WINDOW_NORMS = os.environ.get("PDT_SWIN_WINDOW_NORMS", "1") == "1"
 # PDT_SWIN_REL_TABLE_KERNELS=0: relative-position bias gathered / scattered by torch ops (A/B)
 REL_TABLE_KERNELS = os.environ.get("PDT_SWIN_REL_TABLE_KERNELS", "1") == "1"
+# PDT_SWIN_HEAD_MAJOR_PROJ=0: the window attention writes its output token-major for the output projection (A/B)
+HEAD_MAJOR_PROJ = os.environ.get("PDT_SWIN_HEAD_MAJOR_PROJ", "1") == "1"
 
 
 def window_partition(x, ws):
@@ -95,15 +97,21 @@ class WindowAttention(nn.Module):
             # fused HIP window attention: reads the qkv projection in place, never materialises the
             # [Bw, h, N, N] bias+mask or the scores (ops/window_attention.py)
             # the projection writes q / k / v head-major where the narrow GEMM computes it (ops.linear)
-            qkv = linear_head_major(self.qkv, x, N, C // h) if head_major_ok(x, N, h, C // h) else self.qkv(x)
+            hm = head_major_ok(x, N, h, C // h)
+            qkv = linear_head_major(self.qkv, x, N, C // h) if hm else self.qkv(x)
+            # bf16: the attention writes its output head-major and the projection reads it so (and its backward
+            # hands dO back head-major) -- ops.linear.linear_from_head_major
+            o_hm = HEAD_MAJOR_PROJ and hm and Bw * N >= 16384 and (
+                torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype) == torch.bfloat16
             if REL_TABLE_KERNELS:
                 # the table gather and its gradient scatter fused into two small kernels (ops.window_attention)
                 out = window_attention_table(qkv, self.relative_position_bias_table, self.relative_position_index,
-                                             mask, h, self.scale)
+                                             mask, h, self.scale, out_head_major=o_hm)
             else:
                 bias = _RelBiasGather.apply(self.relative_position_bias_table, self.relative_position_index.view(-1))
-                out = window_attention(qkv, bias.view(N, N, h).permute(2, 0, 1), mask, h, self.scale)
-            return self.proj(out)
+                out = window_attention(qkv, bias.view(N, N, h).permute(2, 0, 1), mask, h, self.scale,
+                                       out_head_major=o_hm)
+            return linear_from_head_major(self.proj, out)
         qkv = self.qkv(x).reshape(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         bias = self.relative_position_bias_table[self.relative_position_index.view(-1)].view(N, N, h)

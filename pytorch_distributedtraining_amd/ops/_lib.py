@@ -97,8 +97,9 @@ _SIGS = {
     "pdt_win_attn_mfma_ok": [c_int, c_int, c_int, c_int],
     "pdt_win_attn_mfma_grid": [c_int, c_int],
     "pdt_win_attn_mfma_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                              c_int, c_float, c_void_p, c_int, c_void_p],
-    "pdt_win_bwd_prep": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                              c_int, c_float, c_void_p, c_int, c_int, c_void_p],
+    "pdt_win_bwd_prep": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "pdt_rel_bias_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "pdt_rel_bias_scatter": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
                              c_void_p],
@@ -106,7 +107,7 @@ _SIGS = {
                               c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p],
     "pdt_win_attn_mfma32_ok": [c_int, c_int, c_int],
     "pdt_win_attn_mfma32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                                c_int, c_float, c_void_p, c_int, c_void_p],
+                                c_int, c_float, c_void_p, c_int, c_int, c_void_p],
     "pdt_win_attn_mfma32_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p],
     "pdt_win_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
@@ -155,11 +156,11 @@ _SIGS = {
     "pdt_narrow_wgrad_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p],
     "pdt_narrow_wgrad_ok": [c_int64, c_int, c_int],
     "pdt_narrow_wgrad_ws_floats": [c_int64, c_int, c_int],
-    "pdt_narrow_wgrad": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p],
+    "pdt_narrow_wgrad": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "pdt_narrow_gemm_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_partials": [c_int64, c_int, c_int],
     "pdt_narrow_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p,
-                        c_int, c_int, c_void_p],
+                        c_int, c_int, c_int, c_int, c_void_p],
     "pdt_window_perm": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_window_perm_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,

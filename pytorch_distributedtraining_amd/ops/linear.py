@@ -357,8 +357,9 @@ def _as_output(t: torch.Tensor, shape) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, hm=None):
+    def forward(ctx, x, weight, bias, hm=None, in_hm=None):
         ctx.save_for_backward(x, weight)
+        ctx.in_hm = in_hm
         ctx.has_bias = bias is not None
         # x is (a view of) a flash-attention output whose backward wants colsum(dX) (ops.attention._dout_colsum)
         base = x._base if x._base is not None else x
@@ -366,6 +367,8 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if hm is not None:      # linear_head_major checked the narrow kernel applies and was picked
             return _as_output(narrow_linear(x2, weight, bias, hm=hm)[0], (*x.shape[:-1], weight.shape[0]))
+        if in_hm is not None:   # linear_from_head_major: x's buffer is head-major (the window attention's output)
+            return _as_output(narrow_linear(x2, weight, bias, a_hm=in_hm)[0], (*x.shape[:-1], weight.shape[0]))
         if x2.is_contiguous() and _prefer_narrow(x2, weight, bias, "fwd"):
             return _as_output(narrow_linear(x2, weight, bias)[0], (*x.shape[:-1], weight.shape[0]))
         if x2.is_contiguous() and _nt_hip_ok(x2, weight, bias):
@@ -378,6 +381,8 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        if ctx.in_hm is not None:
+            return _LinearFn._backward_head_major(ctx, x, w, dy, dy2) + (None, None)
         dx = dw = db = None
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] and want_db and _bgrad_in_gemm(dy2, w):
@@ -428,7 +433,41 @@ class _LinearFn(torch.autograd.Function):
             # what a backward returns (a weak reference to it dies), the base's survives through the view
             dbf = dbf if dbf is not None and dbf.dtype == torch.float32 else db.float()
             stash_dx_colsum(dx2, dbf @ w.float())
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+    @staticmethod
+    def _backward_head_major(ctx, x, w, dy, dy2):
+        """x was read head-major (linear_from_head_major): the data gradient is written head-major as well (tagged
+        for the window attention's backward), the weight gradient reads x head-major; off the narrow kernels x is
+        put back token-major first."""
+        n_tok, d = ctx.in_hm
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = dw = db = None
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            if narrow_wgrad_ok(dy2, x2, w.dtype) and n_tok == 64:
+                dw = narrow_wgrad(dy2, x2, w.dtype, x_hm_d=d)
+            else:
+                dw = wgrad(dy2, _token_major(x2, n_tok, d), w.dtype)
+        if ctx.needs_input_grad[0]:
+            wt = w.t().contiguous()
+            if narrow_ok(dy2, wt):
+                dx2, cs = narrow_linear(dy2, wt, None, w.dtype if want_db else None, hm=(n_tok, d))
+                dx = dx2.view(*dy.shape[:-1], w.shape[1])
+                dx._pdt_head_major = (n_tok, d)
+                if want_db:
+                    db, want_db = cs, False
+            else:
+                dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+        if want_db:
+            db = _colsum(dy2, w.dtype) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.sum(0).to(w.dtype)
+        return dx, dw, db
+
+
+def _token_major(x2: torch.Tensor, n_tok: int, d: int) -> torch.Tensor:
+    """[M, C] token-major copy of a head-major buffer ([M / n_tok, C / d, n_tok, d])."""
+    M, C = x2.shape
+    return x2.reshape(M // n_tok, C // d, n_tok, d).permute(0, 2, 1, 3).reshape(M, C)
 
 
 def _lin_residual_fwd(x2, w, b, r2):
@@ -665,6 +704,26 @@ def linear_head_major(module: "Linear", x: torch.Tensor, n_tok: int, head_dim: i
             y._pdt_head_major = (n_tok, head_dim)
             return y
     return module(x)
+
+
+def linear_from_head_major(module: "Linear", x: torch.Tensor) -> torch.Tensor:
+    """``module(x)`` for x tagged ``_pdt_head_major = (n_tok, d)`` (ops.window_attention's output written head-major):
+    the narrow GEMM reads the head-major buffer directly, and its backward writes the data gradient head-major for
+    the attention's backward.  Untagged x: ``module(x)``; a tagged x the narrow path cannot take is put back
+    token-major first."""
+    hm = getattr(x, "_pdt_head_major", None)
+    if hm is None:
+        return module(x)
+    n_tok, d = hm
+    w, b = module.weight, module.bias
+    if torch.is_autocast_enabled("cuda"):
+        w, b = w.to(x.dtype), (None if b is None else b.to(x.dtype))
+    x2 = x.reshape(-1, x.shape[-1])
+    if (x.dtype == torch.bfloat16 and w.dtype == x.dtype and (b is None or b.dtype == x.dtype) and not fp8_enabled()
+            and x2.is_contiguous() and narrow_ok(x2, w, b)):
+        with torch.autocast("cuda", enabled=False):
+            return _LinearFn.apply(x, w, b, None, hm)
+    return module(_token_major(x2, n_tok, d).view(x.shape))
 
 
 class Linear(nn.Linear):

@@ -36,14 +36,19 @@ def head_major_ok(M: int, N: int, hm) -> bool:
     return n_tok > 0 and n_tok % 16 == 0 and M % n_tok == 0 and 2 <= d <= 32 and d % 2 == 0 and N % d == 0
 
 
-def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None, hm=None):
+def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None, hm=None,
+                  a_hm=None):
     """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192.
     ``hm = (n_tok, d)``: the output buffer [M, N] is filled HEAD-MAJOR -- rows m = window w x n_tok + token t,
     columns c = segment s x d + dim -> element ((w N + s d) n_tok + t d + dim), i.e. Swin's qkv as
-    [windows, 3, heads, n_tok, d] for the window attention's staging loads (ops.window_attention)."""
+    [windows, 3, heads, n_tok, d] for the window attention's staging loads (ops.window_attention).
+    ``a_hm = (n_tok, d)`` (bf16): x2's buffer is read head-major the same way (the window attention's output)."""
     M, K = x2.shape
     N = w.shape[0]
     hm_n, hm_d = hm if hm is not None else (0, 0)
+    a_n, a_d = a_hm if a_hm is not None else (0, 0)
+    if a_n and x2.dtype != torch.bfloat16:
+        raise ValueError("narrow_linear: a head-major input is bf16 only")
     if x2.dtype == torch.float32:      # exact-f32 MFMA kernels (v_mfma_f32_16x16x4_f32)
         lib = _lib.require()
         y = torch.empty((M, N), dtype=torch.float32, device=x2.device)
@@ -61,7 +66,7 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
         cs = torch.empty(K, dtype=colsum_dtype, device=x2.device)
         ws = torch.empty((lib.pdt_narrow_gemm_partials(M, K, N) + 64) * K, dtype=torch.float32, device=x2.device)
     _lib.call("pdt_narrow_gemm", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N, _lib.ptr(cs),
-              _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws), hm_n, hm_d,
+              _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws), hm_n, hm_d, a_n, a_d,
               _lib.stream_handle(x2.device))
     return y, cs
 
@@ -79,9 +84,12 @@ def narrow_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype)
     return bool(ok(dy2.shape[0], dy2.shape[1], x2.shape[1]))
 
 
-def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, x_hm_d: int = 0) -> torch.Tensor:
     """dW [N, K] = dy2[M, N]^T x2[M, K] on the narrow weight-gradient kernel (transposed LDS reads, one fp32
-    partial per workgroup, fixed-order reduce)."""
+    partial per workgroup, fixed-order reduce).  ``x_hm_d`` (bf16): x2's buffer is head-major with 64-token windows
+    ([M / 64, K / x_hm_d, 64, x_hm_d], the window attention's output)."""
+    if x_hm_d and (dy2.dtype != torch.bfloat16 or dy2.shape[0] % 64):
+        raise ValueError("narrow_wgrad: a head-major x is bf16 with 64-token windows only")
     M, N = dy2.shape
     K = x2.shape[1]
     lib = _lib.require()
@@ -93,5 +101,5 @@ def narrow_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) ->
         return out.to(out_dtype)
     out = torch.empty((N, K), dtype=out_dtype, device=dy2.device)
     _lib.call("pdt_narrow_wgrad", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), M, N, K, _lib.dtype_code(out_dtype),
-              ws.data_ptr(), _lib.stream_handle(dy2.device))
+              ws.data_ptr(), int(x_hm_d), _lib.stream_handle(dy2.device))
     return out

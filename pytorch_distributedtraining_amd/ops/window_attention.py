@@ -83,7 +83,7 @@ def reference(qkv, rel_bias, mask, num_heads, scale):
 
 class _WindowAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, rel_bias, mask, num_heads, scale):
+    def forward(ctx, qkv, rel_bias, mask, num_heads, scale, out_head_major=False):
         Bw, N, C3 = qkv.shape
         C = C3 // 3
         d = C // num_heads
@@ -112,15 +112,22 @@ class _WindowAttnFn(torch.autograd.Function):
                 raise RuntimeError(f"window_attention: head-major qkv tagged {tag}, expected {(N, d)}")
             ctx.hm = given or _hm_ok(qkv, N, num_heads, d)
             hm = torch.empty_like(qkv) if (ctx.hm and not given) else None
+            # O head-major ([Bw, h, N, d]) for a projection that reads it so (ops.linear.linear_from_head_major); the
+            # backward then needs the precomputed-delta path (ctx.hm)
+            ctx.o_hm = bool(out_head_major) and ctx.hm and ctx.mfma == "bf16"
             _lib.call("pdt_win_attn_mfma_fwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_fwd", qkv.data_ptr(),
                       bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw,
-                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.ptr(hm), int(given), st)
+                      o.data_ptr(), lse.data_ptr(), Bw, N, num_heads, d, float(scale), _lib.ptr(hm), int(given),
+                      int(ctx.o_hm), st)
             ctx.save_for_backward(hm if hm is not None else qkv, bias, o, lse)
             ctx.mask = (m, lab, nw)
             ctx.h, ctx.scale, ctx.bias_dtype = num_heads, scale, rel_bias.dtype
+            if ctx.o_hm:
+                o._pdt_head_major = (N, d)
             return o
         if tag is not None:
             raise RuntimeError("window_attention: a head-major qkv (linear_head_major) needs the MFMA kernels")
+        ctx.o_hm = False
         bias_t = bias.transpose(1, 2).contiguous()
         m, m_t = _mask_t(mask) if mask is not None else (None, None)
         _lib.call("pdt_win_attn_fwd", qkv.data_ptr(), bias_t.data_ptr(), _lib.ptr(m_t), nw, o.data_ptr(),
@@ -134,7 +141,7 @@ class _WindowAttnFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         dqkv, part = _WindowAttnFn._backward_parts(ctx, do)
-        return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None
+        return dqkv, part.sum(0).to(ctx.bias_dtype), None, None, None, None
 
     @staticmethod
     def _backward_parts(ctx, do):
@@ -147,18 +154,22 @@ class _WindowAttnFn(torch.autograd.Function):
             G = _lib.require().pdt_win_attn_mfma_grid(Bw, ctx.h)
             dqkv = torch.empty_like(qkv)        # token-major (the projection's layout), also when qkv is head-major
             part = torch.empty((G, ctx.h, N, N), dtype=torch.float32, device=qkv.device)
+            # dO head-major already when the projection's data gradient wrote it so (linear_from_head_major)
+            g_hm = getattr(do, "_pdt_head_major", None) == (N, d)
             do = do.contiguous().to(qkv.dtype)
             st = _lib.stream_handle(qkv.device)
             delta = None
             if ctx.hm and do.data_ptr() % 16:
                 do = do.clone()
+            if g_hm and not ctx.hm:
+                raise RuntimeError("window_attention: head-major dO needs the head-major backward")
             if ctx.hm:
                 # dO head-major + delta = rowsum(dO o O) from one coalesced pass: the kernels stage neither O nor
                 # token-major dO slices
-                g = torch.empty_like(do)
+                g = do if g_hm else torch.empty_like(do)
                 delta = torch.empty((Bw, ctx.h, N), dtype=torch.float32, device=qkv.device)
-                _lib.call("pdt_win_bwd_prep", do.data_ptr(), o.data_ptr(), g.data_ptr(), delta.data_ptr(), Bw, N,
-                          ctx.h, d, _lib.dtype_code(qkv.dtype), st)
+                _lib.call("pdt_win_bwd_prep", do.data_ptr(), o.data_ptr(), None if g_hm else g.data_ptr(),
+                          delta.data_ptr(), Bw, N, ctx.h, d, _lib.dtype_code(qkv.dtype), int(g_hm), int(ctx.o_hm), st)
                 do = g
             _lib.call("pdt_win_attn_mfma_bwd" if ctx.mfma == "bf16" else "pdt_win_attn_mfma32_bwd", qkv.data_ptr(),
                       bias.data_ptr(), _lib.ptr(m), _lib.ptr(lab), nw, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
@@ -210,14 +221,14 @@ class _WindowAttnTableFn(torch.autograd.Function):
     sum / cast / zero-fill / index_add backward per block."""
 
     @staticmethod
-    def forward(ctx, qkv, table, index, mask, num_heads, scale):
+    def forward(ctx, qkv, table, index, mask, num_heads, scale, out_head_major=False):
         N = qkv.shape[1]
         idx, off, pos = _rel_csr(index, table.shape[0])
         tab = table.contiguous()
         bias = torch.empty((num_heads, N, N), dtype=torch.float32, device=qkv.device)
         _lib.call("pdt_rel_bias_gather", tab.data_ptr(), idx.data_ptr(), bias.data_ptr(), num_heads, N * N,
                   _lib.dtype_code(tab.dtype), _lib.stream_handle(qkv.device))
-        o = _WindowAttnFn.forward(ctx, qkv, bias, mask, num_heads, scale)
+        o = _WindowAttnFn.forward(ctx, qkv, bias, mask, num_heads, scale, out_head_major)
         ctx.table_meta = (table.shape[0], table.dtype, off, pos)
         return o
 
@@ -230,18 +241,18 @@ class _WindowAttnTableFn(torch.autograd.Function):
         ws = torch.empty(h * N * N, dtype=torch.float32, device=part.device)
         _lib.call("pdt_rel_bias_scatter", part.data_ptr(), G, h, N * N, off.data_ptr(), pos.data_ptr(), rows,
                   dtab.data_ptr(), _lib.dtype_code(dt), ws.data_ptr(), _lib.stream_handle(part.device))
-        return dqkv, dtab, None, None, None, None
+        return dqkv, dtab, None, None, None, None, None
 
 
-def window_attention_table(qkv, table, index, mask, num_heads: int, scale: float):
+def window_attention_table(qkv, table, index, mask, num_heads: int, scale: float, out_head_major: bool = False):
     """window_attention with rel_bias = table[index].permute(2, 0, 1) (Swin's relative-position table [T, h] and
     index buffer [N, N]), the gather and its backward fused into two small kernels on the GPU."""
     if (supported(qkv, num_heads) and table.dtype in (torch.float32, torch.bfloat16) and table.dim() == 2
             and table.shape[1] == num_heads and index.numel() == qkv.shape[1] ** 2):
-        return _WindowAttnTableFn.apply(qkv, table, index, mask, num_heads, scale)
+        return _WindowAttnTableFn.apply(qkv, table, index, mask, num_heads, scale, out_head_major)
     N = qkv.shape[1]
     rel = table[index.reshape(-1)].view(N, N, num_heads).permute(2, 0, 1)
-    return window_attention(qkv, rel, mask, num_heads, scale)
+    return window_attention(qkv, rel, mask, num_heads, scale, out_head_major)
 
 
 def head_major_ok(x, N: int, num_heads: int, d: int) -> bool:
@@ -263,10 +274,12 @@ def supported(qkv, num_heads) -> bool:
             and num_heads <= 16 and _lib.available())
 
 
-def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float):
-    """qkv [Bw, N, 3C]; rel_bias [h, N, N]; mask [nw, N, N] or None (window b uses mask b % nw)."""
+def window_attention(qkv, rel_bias, mask, num_heads: int, scale: float, out_head_major: bool = False):
+    """qkv [Bw, N, 3C]; rel_bias [h, N, N]; mask [nw, N, N] or None (window b uses mask b % nw).
+    ``out_head_major``: the output MAY come back head-major ([Bw, h, N, d] in the [Bw, N, C] buffer), tagged
+    ``_pdt_head_major`` -- only for a consumer that checks the tag (ops.linear.linear_from_head_major)."""
     if supported(qkv, num_heads):
-        return _WindowAttnFn.apply(qkv, rel_bias, mask, num_heads, scale)
+        return _WindowAttnFn.apply(qkv, rel_bias, mask, num_heads, scale, out_head_major)
     if getattr(qkv, "_pdt_head_major", None) is not None:
         raise RuntimeError("window_attention: a head-major qkv (linear_head_major) needs the GPU kernels")
     if qkv.is_cuda:

@@ -2320,11 +2320,44 @@ def test_swin_block_head_major_qkv_matches_token_major(dt, monkeypatch):
         y.float().square().mean().backward()
         return y.detach(), xi.grad, blk.attn.qkv.weight.grad.clone(), blk.attn.relative_position_bias_table.grad.clone()
 
+    import pytorch_distributedtraining_amd.models.swinir as S
+    proj_in = []
+    real_lfh = L.linear_from_head_major
+
+    def spy_lfh(module, x):
+        proj_in.append(getattr(x, "_pdt_head_major", None))
+        return real_lfh(module, x)
+    monkeypatch.setattr(S, "linear_from_head_major", spy_lfh)
     a = run()
     assert tags and tags[-1] == (64, 10), tags
+    if dt == torch.bfloat16:
+        assert proj_in and proj_in[-1] == (64, 10), proj_in     # the attention output went head-major too
     monkeypatch.setattr(L, "HEAD_MAJOR_QKV", False)
+    monkeypatch.setattr(S, "HEAD_MAJOR_PROJ", False)
     tags.clear()
+    proj_in.clear()
     b = run()
-    assert tags and tags[-1] is None
+    assert tags and tags[-1] is None and proj_in[-1] is None
     for u, v in zip(a, b):
         torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_narrow_head_major_inputs_match_token_major():
+    """narrow_linear(a_hm=...) and narrow_wgrad(x_hm_d=...) read a head-major buffer ([windows, C/d, 64, d]) exactly
+    as the token-major kernels read its permutation."""
+    from pytorch_distributedtraining_amd.ops.narrow import narrow_linear, narrow_wgrad
+    torch.manual_seed(0)
+    Bw, N, H, d = 300, 64, 6, 10
+    C = H * d
+    x_tm = torch.randn(Bw * N, C, device=DEV).bfloat16()
+    x_hm = x_tm.view(Bw, N, H, d).permute(0, 2, 1, 3).contiguous().view(Bw * N, C)
+    w = (0.1 * torch.randn(C, C, device=DEV)).bfloat16()
+    b = torch.randn(C, device=DEV).bfloat16()
+    y_ref, cs_ref = narrow_linear(x_tm, w, b, torch.bfloat16)
+    y, cs = narrow_linear(x_hm, w, b, torch.bfloat16, a_hm=(N, d))
+    torch.testing.assert_close(y, y_ref, rtol=0, atol=0)
+    torch.testing.assert_close(cs, cs_ref, rtol=0, atol=0)
+    dy = torch.randn(Bw * N, C, device=DEV).bfloat16()
+    torch.testing.assert_close(narrow_wgrad(dy, x_hm, torch.bfloat16, x_hm_d=d), narrow_wgrad(dy, x_tm, torch.bfloat16),
+                               rtol=0, atol=0)
