@@ -168,7 +168,7 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
                                                                  const bf16_t* __restrict__ bias,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ colsum_part,
                                                                  int64_t M, int KI, int NO, int hm_n, int hm_d, int a_n,
-                                                                 int a_d) {
+                                                                 int a_d, const bf16_t* __restrict__ R) {
   typedef NarrowCfg<KP, NP> Cfg;
   constexpr int XP = Cfg::XP, KS = Cfg::KS, NT = Cfg::NT;
   extern __shared__ __attribute__((aligned(16))) bf16_t nsm[];
@@ -250,8 +250,20 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
     } else {
       bf16_t* dst = Y + blk * 16 * NO;
       const int tot = rows * NO, n8 = tot >> 3;
-      for (int c = lane; c < n8; c += 64) *reinterpret_cast<u16x8*>(dst + 8 * c) = *reinterpret_cast<const u16x8*>(Ys + 8 * c);
-      for (int e = 8 * n8 + lane; e < tot; e += 64) dst[e] = Ys[e];
+      if (R != nullptr) {                        // + the residual stream (same [M, NO] layout), rounded once
+        const bf16_t* res = R + blk * 16 * NO;
+        for (int c = lane; c < n8; c += 64) {
+          const u16x8 a = *reinterpret_cast<const u16x8*>(Ys + 8 * c), b = *reinterpret_cast<const u16x8*>(res + 8 * c);
+          u16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = f2bf(bf2f(a[k]) + bf2f(b[k]));
+          *reinterpret_cast<u16x8*>(dst + 8 * c) = o;
+        }
+        for (int e = 8 * n8 + lane; e < tot; e += 64) dst[e] = f2bf(bf2f(Ys[e]) + bf2f(res[e]));
+      } else {
+        for (int c = lane; c < n8; c += 64) *reinterpret_cast<u16x8*>(dst + 8 * c) = *reinterpret_cast<const u16x8*>(Ys + 8 * c);
+        for (int e = 8 * n8 + lane; e < tot; e += 64) dst[e] = Ys[e];
+      }
     }
   }
   if (colsum_part != nullptr) {
@@ -441,7 +453,8 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
                                                                        const float* __restrict__ bias,
                                                                        float* __restrict__ Y,
                                                                        float* __restrict__ colsum_part, int64_t M,
-                                                                       int KI, int NO, int hm_n, int hm_d) {
+                                                                       int KI, int NO, int hm_n, int hm_d,
+                                                                       const float* __restrict__ R) {
   typedef Narrow32Cfg<KP, NP> Cfg;
   constexpr int NT = NP / 16;
   extern __shared__ __attribute__((aligned(16))) float n32[];
@@ -525,7 +538,14 @@ __global__ __launch_bounds__(64 * NW32, 1) void narrow_gemm_f32_kernel(const flo
     } else {
       float* dst = Y + blk * 16 * NO;
       const int n4 = rows * NO / 4;
-      for (int c = lane; c < n4; c += 64) *reinterpret_cast<f32x4*>(dst + 4 * c) = *reinterpret_cast<const f32x4*>(Ys + 4 * c);
+      if (R != nullptr) {                        // + the residual stream (same [M, NO] layout)
+        const float* res = R + blk * 16 * NO;
+        for (int c = lane; c < n4; c += 64)
+          *reinterpret_cast<f32x4*>(dst + 4 * c) =
+              *reinterpret_cast<const f32x4*>(Ys + 4 * c) + *reinterpret_cast<const f32x4*>(res + 4 * c);
+      } else {
+        for (int c = lane; c < n4; c += 64) *reinterpret_cast<f32x4*>(dst + 4 * c) = *reinterpret_cast<const f32x4*>(Ys + 4 * c);
+      }
     }
   }
   if (colsum_part != nullptr) {
@@ -670,10 +690,12 @@ static bool hm_ok(int64_t M, int NO, int hm_n, int hm_d) {
                        NO % hm_d == 0);
 }
 // a_n > 0: X head-major ([M / a_n][KI / a_d][a_n][a_d], load_block_hm), same constraints as hm_n / hm_d on KI
+// R (nullable): a residual [M, NO] added in the store (token-major output only; 16-byte aligned)
 PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void* Y, int64_t M, int KI, int NO,
-                            void* colsum_out, int wdt, float* ws, int hm_n, int hm_d, int a_n, int a_d, hipStream_t st) {
+                            void* colsum_out, int wdt, float* ws, int hm_n, int hm_d, int a_n, int a_d, const void* R,
+                            hipStream_t st) {
   if (!pdt_narrow_gemm_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || !hm_ok(M, KI, a_n, a_d) || ((uintptr_t)X & 15) ||
-      ((uintptr_t)Y & 15))
+      ((uintptr_t)Y & 15) || ((uintptr_t)R & 15) || (R && hm_n))
     return (int)hipErrorInvalidValue;
   const int KP = pad_to(KI, 64) <= 64 ? 64 : pad_to(KI, 64);
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
@@ -681,7 +703,8 @@ PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void
   float* part = colsum_out ? ws : nullptr;
 #define PDT_NG(KP_, NP_)                                                                                        \
   narrow_gemm_kernel<KP_, NP_><<<grid, 64 * NW, NW * NarrowCfg<KP_, NP_>::WAVE_ELEMS * sizeof(bf16_t), st>>>(   \
-      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d, a_n, a_d)
+      (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d, a_n, a_d,  \
+      (const bf16_t*)R)
 #define PDT_NG_N(KP_) \
   do { if (NP == 64) PDT_NG(KP_, 64); else if (NP == 128) PDT_NG(KP_, 128); else PDT_NG(KP_, 192); } while (0)
   if (KP == 64) PDT_NG_N(64);
@@ -777,8 +800,9 @@ PDT_API int pdt_narrow_wgrad_f32_ok(int64_t M, int NO, int KI) {
   return sizeof(float) * 2 * 64 * (size_t)(NP + 1 + KP + 1) <= 160 * 1024 ? 1 : 0;
 }
 PDT_API int pdt_narrow_gemm_f32(const float* X, const float* B, const float* bias, float* Y, int64_t M, int KI, int NO,
-                                float* colsum_out, float* ws, int hm_n, int hm_d, hipStream_t st) {
-  if (!pdt_narrow_gemm_f32_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15))
+                                float* colsum_out, float* ws, int hm_n, int hm_d, const float* R, hipStream_t st) {
+  if (!pdt_narrow_gemm_f32_ok(M, KI, NO) || !hm_ok(M, NO, hm_n, hm_d) || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15) ||
+      ((uintptr_t)R & 15) || (R && hm_n))
     return (int)hipErrorInvalidValue;
   const int KP = KI <= 64 ? 64 : KI <= 128 ? 128 : 192;
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
@@ -788,7 +812,7 @@ PDT_API int pdt_narrow_gemm_f32(const float* X, const float* B, const float* bia
   do {                                                                                                            \
     if (!narrow32_attr<KP_, NP_>()) return (int)hipErrorInvalidValue;                                             \
     narrow_gemm_f32_kernel<KP_, NP_><<<grid, 64 * NW32, narrow32_lds<KP_, NP_>(), st>>>(X, B, bias, Y, part, M, KI, NO, \
-                                                                                     hm_n, hm_d);                 \
+                                                                                     hm_n, hm_d, R);              \
   } while (0)
 #define PDT_N32_N(KP_) \
   do { if (NP == 64) PDT_N32(KP_, 64); else if (NP == 128) PDT_N32(KP_, 128); else PDT_N32(KP_, 192); } while (0)

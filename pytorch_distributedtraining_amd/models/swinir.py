@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from ..ops.activations import bias_gelu
 from ..ops.conv import Conv2d3x3, pixel_shuffle_affine
-from ..ops.linear import Linear, linear, linear_from_head_major, linear_head_major
+from ..ops.linear import Linear, linear, linear_from_head_major, linear_head_major, linear_residual
 from ..ops.swin_mlp import fused_mlp, fused_mlp_ok
 from ..ops.norms import LayerNorm, add_layer_norm_from_windows, layer_norm_to_windows, window_norm_ok
 from ..ops.window_attention import (fused_window_ok, head_major_ok, window_attention, window_attention_table,
@@ -39,6 +39,8 @@ WINDOW_NORMS = os.environ.get("PDT_SWIN_WINDOW_NORMS", "1") == "1"
 REL_TABLE_KERNELS = os.environ.get("PDT_SWIN_REL_TABLE_KERNELS", "1") == "1"
 # PDT_SWIN_HEAD_MAJOR_PROJ=0: the window attention writes its output token-major for the output projection (A/B)
 HEAD_MAJOR_PROJ = os.environ.get("PDT_SWIN_HEAD_MAJOR_PROJ", "1") == "1"
+# PDT_SWIN_MLP_RESIDUAL_GEMM=0: the unfused (fp32) MLP adds its residual in a separate pass (A/B)
+MLP_RESIDUAL_GEMM = os.environ.get("PDT_SWIN_MLP_RESIDUAL_GEMM", "1") == "1"
 
 
 def window_partition(x, ws):
@@ -138,9 +140,14 @@ class Mlp(nn.Module):
                     residual is None or (residual.dtype == torch.bfloat16 and residual.shape == x.shape)):
                 # C = 60 -> 120 -> 60: whole MLP in one MFMA kernel per direction (hidden kept on chip)
                 return fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual)
-            # GEMM without bias -> fused bias + erf-GELU kernel (backward also reduces the bias gradient)
+            # GEMM without bias -> fused bias + erf-GELU kernel (backward also reduces the bias gradient); the
+            # residual added in fc2's GEMM store
             h = linear(x, self.fc1.weight)
-            y = self.fc2(bias_gelu(h, self.fc1.bias, approximate="none"))
+            a = bias_gelu(h, self.fc1.bias, approximate="none")
+            if MLP_RESIDUAL_GEMM and residual is not None and residual.dtype == a.dtype == self.fc2.weight.dtype \
+                    and not torch.is_autocast_enabled("cuda"):
+                return linear_residual(a, self.fc2.weight, self.fc2.bias, residual)
+            y = self.fc2(a)
         else:
             y = self.fc2(self.act(self.fc1(x)))
         return y if residual is None else residual + y

@@ -151,7 +151,7 @@ _SIGS = {
     "pdt_narrow_gemm_f32_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_f32_partials": [c_int64],
     "pdt_narrow_gemm_f32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p,
-                            c_int, c_int, c_void_p],
+                            c_int, c_int, c_void_p, c_void_p],
     "pdt_narrow_wgrad_f32_ok": [c_int64, c_int, c_int],
     "pdt_narrow_wgrad_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p],
     "pdt_narrow_wgrad_ok": [c_int64, c_int, c_int],
@@ -160,7 +160,7 @@ _SIGS = {
     "pdt_narrow_gemm_ok": [c_int64, c_int, c_int],
     "pdt_narrow_gemm_partials": [c_int64, c_int, c_int],
     "pdt_narrow_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p,
-                        c_int, c_int, c_int, c_int, c_void_p],
+                        c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "pdt_window_perm": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_window_perm_f32": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "pdt_im2col3x3": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -498,6 +498,9 @@ class _LinearResidualFn(torch.autograd.Function):
         x2 = x2 if x2.is_contiguous() else x2.contiguous()
         r2 = r.reshape(-1, n)
         r2 = r2 if r2.is_contiguous() else r2.contiguous()
+        if r2.data_ptr() % 16 == 0 and r2.dtype == x2.dtype and _prefer_narrow(x2, weight, bias, "fwd"):
+            # narrow linears (SwinIR's MLP fc2): the residual added in the narrow GEMM's store
+            return _as_output(narrow_linear(x2, weight, bias, residual=r2)[0], (*x.shape[:-1], n))
         return _as_output(_lin_residual_fwd(x2, weight, bias, r2), (*x.shape[:-1], n))
 
     @staticmethod
@@ -510,14 +513,22 @@ class _LinearResidualFn(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             x2 = x2 if x2.is_contiguous() else x2.contiguous()
             dw = _wgrad_result(w, dy2, x2)
+        dbf = None
         if ctx.needs_input_grad[0]:
-            if _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
+            if _prefer_narrow(dy2, w, None, "dgrad"):
+                # narrow data gradient, colsum(dY) (the bias gradient) from the same read unless already summed
+                want = ctx.has_bias and (ctx.needs_input_grad[2] or ctx.dx_colsum)
+                pre = take_bias_grad(dy2) if want else None
+                dx2, cs = narrow_linear(dy2, w.t().contiguous(), None, torch.float32 if (want and pre is None) else None)
+                dbf = pre if pre is not None else cs
+            elif _dgrad_via_transpose(dy2.shape[0], w.shape[0], w.shape[1], w):
                 dx2 = nt_matmul(dy2, transpose16(w))
             else:
                 dx2 = torch.mm(dy2, w)
             dx = dx2.view(*dy.shape[:-1], w.shape[1])
         if ctx.has_bias and (ctx.needs_input_grad[2] or ctx.dx_colsum):
-            dbf = take_bias_grad(dy2)
+            if dbf is None:
+                dbf = take_bias_grad(dy2)
             if dbf is None:
                 dbf = _colsum(dy2, torch.float32) if (dy2.is_cuda and colsum_ok(dy2.shape[1])) else dy2.float().sum(0)
             db = dbf.to(w.dtype)

@@ -37,18 +37,22 @@ def head_major_ok(M: int, N: int, hm) -> bool:
 
 
 def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: torch.dtype | None = None, hm=None,
-                  a_hm=None):
+                  a_hm=None, residual=None):
     """(x2 @ w.T + bias, colsum(x2) in ``colsum_dtype`` or None) -- x2 [M, K], w [N, K], K, N <= 192.
     ``hm = (n_tok, d)``: the output buffer [M, N] is filled HEAD-MAJOR -- rows m = window w x n_tok + token t,
     columns c = segment s x d + dim -> element ((w N + s d) n_tok + t d + dim), i.e. Swin's qkv as
     [windows, 3, heads, n_tok, d] for the window attention's staging loads (ops.window_attention).
-    ``a_hm = (n_tok, d)`` (bf16): x2's buffer is read head-major the same way (the window attention's output)."""
+    ``a_hm = (n_tok, d)`` (bf16): x2's buffer is read head-major the same way (the window attention's output).
+    ``residual`` [M, N] (x2's dtype, contiguous, 16-byte aligned, token-major output only): added in the store."""
     M, K = x2.shape
     N = w.shape[0]
     hm_n, hm_d = hm if hm is not None else (0, 0)
     a_n, a_d = a_hm if a_hm is not None else (0, 0)
     if a_n and x2.dtype != torch.bfloat16:
         raise ValueError("narrow_linear: a head-major input is bf16 only")
+    if residual is not None and (hm is not None or residual.dtype != x2.dtype or not residual.is_contiguous()
+                                 or tuple(residual.shape) != (M, N) or residual.data_ptr() % 16):
+        raise ValueError("narrow_linear: residual must be a contiguous, 16-byte aligned [M, N] of x2's dtype")
     if x2.dtype == torch.float32:      # exact-f32 MFMA kernels (v_mfma_f32_16x16x4_f32)
         lib = _lib.require()
         y = torch.empty((M, N), dtype=torch.float32, device=x2.device)
@@ -57,7 +61,7 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
             cs = torch.empty(K, dtype=torch.float32, device=x2.device)
             ws = torch.empty((lib.pdt_narrow_gemm_f32_partials(M) + 64) * K, dtype=torch.float32, device=x2.device)
         _lib.call("pdt_narrow_gemm_f32", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N,
-                  _lib.ptr(cs), _lib.ptr(ws), hm_n, hm_d, _lib.stream_handle(x2.device))
+                  _lib.ptr(cs), _lib.ptr(ws), hm_n, hm_d, _lib.ptr(residual), _lib.stream_handle(x2.device))
         return y, (cs.to(colsum_dtype) if cs is not None else None)
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
     cs = ws = None
@@ -67,7 +71,7 @@ def narrow_linear(x2: torch.Tensor, w: torch.Tensor, bias=None, colsum_dtype: to
         ws = torch.empty((lib.pdt_narrow_gemm_partials(M, K, N) + 64) * K, dtype=torch.float32, device=x2.device)
     _lib.call("pdt_narrow_gemm", x2.data_ptr(), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), M, K, N, _lib.ptr(cs),
               _lib.dtype_code(colsum_dtype) if colsum_dtype is not None else 0, _lib.ptr(ws), hm_n, hm_d, a_n, a_d,
-              _lib.stream_handle(x2.device))
+              _lib.ptr(residual), _lib.stream_handle(x2.device))
     return y, cs
 
 

@@ -2361,3 +2361,27 @@ def test_narrow_head_major_inputs_match_token_major():
     dy = torch.randn(Bw * N, C, device=DEV).bfloat16()
     torch.testing.assert_close(narrow_wgrad(dy, x_hm, torch.bfloat16, x_hm_d=d), narrow_wgrad(dy, x_tm, torch.bfloat16),
                                rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_linear_residual_narrow_matches_torch(dt, monkeypatch):
+    """linear_residual on a narrow shape (SwinIR's MLP fc2, 120 -> 60 over 16,384+ tokens): the residual added in the
+    narrow GEMM's store, the narrow data gradient with the fused bias gradient -- vs fp32 torch."""
+    import pytorch_distributedtraining_amd.ops.linear as L
+    monkeypatch.setattr(L, "NARROW", "1")
+    torch.manual_seed(0)
+    M, K, N = 16384 + 64, 120, 60
+    x = torch.randn(M, K, device=DEV).to(dt).requires_grad_()
+    w = (0.1 * torch.randn(N, K, device=DEV)).to(dt).requires_grad_()
+    b = torch.randn(N, device=DEV).to(dt).requires_grad_()
+    r = torch.randn(M, N, device=DEV).to(dt).requires_grad_()
+    y = L.linear_residual(x, w, b, r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br, rr = (t.detach().float().requires_grad_() for t in (x, w, b, r))
+    (F.linear(xr, wr, br) + rr).backward(dy.float())
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-5
+    assert rel_err(y, F.linear(xr, wr, br) + rr) < tol
+    for t, ref in ((x, xr), (w, wr), (b, br), (r, rr)):
+        assert rel_err(t.grad, ref.grad) < 2 * tol
