@@ -514,15 +514,20 @@ __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes
 struct WinMap {
   int H, W, ws, shift, mode;
 };
+// 32-bit unsigned divisions (the host keeps rows < 2^31): the 64-bit division this was written with cost ~100 VALU
+// per call, once per row in every narrow-row norm pass of a Swin block
 __device__ __forceinline__ int64_t img_to_win(int64_t r, const WinMap& m) {
-  const int per_img = m.H * m.W;
-  const int64_t b = r / per_img;
-  const int t = (int)(r - b * per_img);
-  int h = t / m.W - m.shift, w = t % m.W - m.shift;
+  const uint32_t per_img = (uint32_t)(m.H * m.W);
+  const uint32_t r32 = (uint32_t)r;
+  const uint32_t b = r32 / per_img;
+  const uint32_t t = r32 - b * per_img;
+  const uint32_t th = t / (uint32_t)m.W;
+  int h = (int)th - m.shift, w = (int)(t - th * (uint32_t)m.W) - m.shift;
   if (h < 0) h += m.H;
   if (w < 0) w += m.W;
-  const int wh = h / m.ws, i = h - wh * m.ws, ww = w / m.ws, j = w - ww * m.ws;
-  return b * per_img + (int64_t)(wh * (m.W / m.ws) + ww) * m.ws * m.ws + i * m.ws + j;
+  const uint32_t ws = (uint32_t)m.ws;
+  const uint32_t wh = (uint32_t)h / ws, i = (uint32_t)h - wh * ws, ww = (uint32_t)w / ws, j = (uint32_t)w - ww * ws;
+  return (int64_t)b * per_img + (int64_t)((wh * ((uint32_t)m.W / ws) + ww) * ws * ws + i * ws + j);
 }
 
 template <typename T, typename W, bool RMS>
