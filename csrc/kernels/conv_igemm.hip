@@ -44,11 +44,13 @@ struct Geo {
 // channels 4c .. 4c+3); zero outside the image (the convolution's padding)
 __device__ __forceinline__ void load_x(const bf16_t* __restrict__ X, const Geo& g, int64_t blk, int lane,
                                        u16x4 (&v)[LD_PER_LANE]) {
-  const int wb = g.W / 16;
-  const int64_t nh = blk / wb;
-  const int w0 = (int)(blk - nh * wb) * 16;
-  const int h = (int)(nh % g.H);
-  const int64_t n = nh / g.H;
+  // 32-bit divisions (blocks < 2^31, host check): 64-bit ones cost ~100 VALU each per block
+  const uint32_t wb = (uint32_t)(g.W / 16), b32 = (uint32_t)blk;
+  const uint32_t nh = b32 / wb;
+  const int w0 = (int)(b32 - nh * wb) * 16;
+  const uint32_t n32 = nh / (uint32_t)g.H;
+  const int h = (int)(nh - n32 * (uint32_t)g.H);
+  const int64_t n = n32;
   const int cq = g.CI / 4, tot = 3 * 18 * cq;
 #pragma unroll
   for (int i = 0; i < LD_PER_LANE; ++i) {
@@ -151,7 +153,7 @@ size_t igemm_lds() { return sizeof(bf16_t) * ((size_t)16 * NT * BP + (size_t)NWV
 
 PDT_API int pdt_conv3x3_igemm_ok(int N, int H, int W, int CI, int CO) {
   return (N > 0 && H > 0 && W % 16 == 0 && CI >= 4 && CI <= 64 && CI % 4 == 0 && CO >= 4 && CO <= 64 &&
-          CO % 4 == 0) ? 1 : 0;
+          CO % 4 == 0 && (int64_t)N * H * (W / 16) < (1ll << 31)) ? 1 : 0;
 }
 
 // X [N, H, W, CI] bf16 NHWC-contiguous (8-byte aligned); Wk [CO][9][64] bf16 (tap-major, channels zero-padded to 64:

@@ -73,12 +73,12 @@ __device__ __forceinline__ int fdiv_i(int a, float inv) { return __float2int_rz(
 template <int KP, int NP>
 __device__ __forceinline__ void load_block_hm(const bf16_t* __restrict__ X, int KI, int64_t blk, int lane, int a_n,
                                               int a_d, u16x8 (&ch)[NarrowCfg<KP, NP>::CH]) {
-  const int64_t r0 = blk * 16;
-  const int64_t win = r0 / a_n;
-  const int t0 = (int)(r0 - win * a_n);
+  const uint32_t r0 = (uint32_t)(blk * 16);             // M < 2^31 (hm_ok): 32-bit division
+  const uint32_t win = r0 / (uint32_t)a_n;
+  const int t0 = (int)(r0 - win * (uint32_t)a_n);
   const int run = 16 * a_d, n8 = 2 * KI;                // elements per segment run; chunks per block (16 KI / 8)
   const float inv_run = 1.f / (float)run;
-  const bf16_t* base = X + win * a_n * KI + (int64_t)t0 * a_d;
+  const bf16_t* base = X + (int64_t)win * a_n * KI + (int64_t)t0 * a_d;
 #pragma unroll
   for (int i = 0; i < NarrowCfg<KP, NP>::CH; ++i) {
     const int c = lane + 64 * i;
@@ -144,10 +144,10 @@ __device__ __forceinline__ void hm_store(T* __restrict__ Y, const T* Ys, int64_t
   const int nch = (NO / hm_d) * cps;
   const int rowd = NO * (int)sizeof(T) / 4;              // dwords per staged row
   const float inv_cps = 1.f / (float)cps, inv_dpt = 1.f / (float)dpt;
-  const int64_t row0 = blk * 16;
-  const int64_t win = row0 / hm_n;
-  const int t0 = (int)(row0 - win * hm_n);
-  uint32_t* base = reinterpret_cast<uint32_t*>(Y + win * hm_n * NO + (int64_t)t0 * hm_d);
+  const uint32_t row0 = (uint32_t)(blk * 16);           // M < 2^31 (hm_ok): 32-bit division
+  const uint32_t win = row0 / (uint32_t)hm_n;
+  const int t0 = (int)(row0 - win * (uint32_t)hm_n);
+  uint32_t* base = reinterpret_cast<uint32_t*>(Y + (int64_t)win * hm_n * NO + (int64_t)t0 * hm_d);
   const uint32_t* ys = reinterpret_cast<const uint32_t*>(Ys);
   const int64_t seg_stride = (int64_t)hm_n * hm_d * (int)sizeof(T) / 4;
   for (int c = lane; c < nch; c += 64) {
@@ -686,8 +686,8 @@ PDT_API int pdt_narrow_gemm_partials(int64_t M, int KI, int NO) { return narrow_
 // hm_n > 0: Y head-major (hm_store): M % hm_n == 0, hm_n % 16 == 0, NO % hm_d == 0, hm_d even
 // and <= 32
 static bool hm_ok(int64_t M, int NO, int hm_n, int hm_d) {
-  return hm_n == 0 || (hm_n > 0 && hm_n % 16 == 0 && M % hm_n == 0 && hm_d >= 2 && hm_d <= 32 && hm_d % 2 == 0 &&
-                       NO % hm_d == 0);
+  return hm_n == 0 || (hm_n > 0 && hm_n % 16 == 0 && M % hm_n == 0 && M < (1ll << 31) && hm_d >= 2 && hm_d <= 32 &&
+                       hm_d % 2 == 0 && NO % hm_d == 0);
 }
 // a_n > 0: X head-major ([M / a_n][KI / a_d][a_n][a_d], load_block_hm), same constraints as hm_n / hm_d on KI
 // R (nullable): a residual [M, NO] added in the store (token-major output only; 16-byte aligned)
