@@ -160,26 +160,38 @@ __global__ __launch_bounds__(NT) void bias_gelu_bwd_db_narrow(const T* __restric
 template <typename T>
 __global__ __launch_bounds__(NT) void swiglu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
                                                         int F) {
-  const int64_t n8 = rows * (F / 8);
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
-    const int64_t r = i / (F / 8);
-    const int j = (int)(i % (F / 8)) * 8;
+  // (row, column) advanced incrementally (one 64-bit division per thread, not per vector)
+  const int f8 = F / 8;
+  const int64_t n8 = rows * f8, i0 = blockIdx.x * (int64_t)NT + threadIdx.x, stride = (int64_t)gridDim.x * NT;
+  const int64_t dr = stride / f8;
+  const int dj = (int)(stride - dr * f8);
+  int64_t r = i0 / f8;
+  int j8 = (int)(i0 - r * f8);
+  for (int64_t i = i0; i < n8; i += stride) {
+    const int j = 8 * j8;
     float a[8], b[8], o[8];
     Vec8<T>::load(x + r * 2 * F + j, a);
     Vec8<T>::load(x + r * 2 * F + F + j, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = a[k] / (1.f + __expf(-a[k])) * b[k];
     Vec8<T>::store(y + r * F + j, o);
+    r += dr;
+    j8 += dj;
+    if (j8 >= f8) { j8 -= f8; ++r; }
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(NT) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                         T* __restrict__ dx, int64_t rows, int F) {
-  const int64_t n8 = rows * (F / 8);
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
-    const int64_t r = i / (F / 8);
-    const int j = (int)(i % (F / 8)) * 8;
+  const int f8 = F / 8;
+  const int64_t n8 = rows * f8, i0 = blockIdx.x * (int64_t)NT + threadIdx.x, stride = (int64_t)gridDim.x * NT;
+  const int64_t dr = stride / f8;
+  const int dj = (int)(stride - dr * f8);
+  int64_t r = i0 / f8;
+  int j8 = (int)(i0 - r * f8);
+  for (int64_t i = i0; i < n8; i += stride) {
+    const int j = 8 * j8;
     float a[8], b[8], g[8], da[8], db[8];
     Vec8<T>::load(x + r * 2 * F + j, a);
     Vec8<T>::load(x + r * 2 * F + F + j, b);
@@ -193,6 +205,9 @@ __global__ __launch_bounds__(NT) void swiglu_bwd_kernel(const T* __restrict__ dy
     }
     Vec8<T>::store(dx + r * 2 * F + j, da);
     Vec8<T>::store(dx + r * 2 * F + F + j, db);
+    r += dr;
+    j8 += dj;
+    if (j8 >= f8) { j8 -= f8; ++r; }
   }
 }
 

@@ -84,14 +84,15 @@ def test_bias_gelu(approx, dt, rows, N):
     assert rel_err(b.grad, br.grad) < tol
 
 
-def test_swiglu():
+@pytest.mark.parametrize("rows,Fh", [(129, 512), (20011, 2000)])   # the second: many grid-stride passes per thread
+def test_swiglu(rows, Fh):
     from pytorch_distributedtraining_amd.ops import swiglu
-    x = torch.randn(129, 2 * 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(rows, 2 * Fh, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     y = swiglu(x)
     dy = torch.randn_like(y)
     y.backward(dy)
     xr = x.detach().float().requires_grad_()
-    yr = F.silu(xr[:, :512]) * xr[:, 512:]
+    yr = F.silu(xr[:, :Fh]) * xr[:, Fh:]
     yr.backward(dy.float())
     assert rel_err(y, yr) < 1e-2 and rel_err(x.grad, xr.grad) < 1e-2
 
