@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv3x3_igemm_kernel(const bf16_t
     }
     wave_sync();
     bf16_t* dst = Y + blk * 16 * g.CO;         // 16 consecutive pixels of one row: contiguous in NHWC
-    const int n8 = 2 * g.CO;                   // 16 * CO / 8 chunks (CO % 4 == 0)
+    const int n8 = 2 * g.CO;                   // 16 * CO / 8 whole chunks for any CO
     for (int c = lane; c < n8; c += 64) *reinterpret_cast<u16x8*>(dst + 8 * c) = *reinterpret_cast<const u16x8*>(Ys + 8 * c);
   }
 }
@@ -152,8 +152,10 @@ size_t igemm_lds() { return sizeof(bf16_t) * ((size_t)16 * NT * BP + (size_t)NWV
 }  // namespace
 
 PDT_API int pdt_conv3x3_igemm_ok(int N, int H, int W, int CI, int CO) {
-  return (N > 0 && H > 0 && W % 16 == 0 && CI >= 4 && CI <= 64 && CI % 4 == 0 && CO >= 4 && CO <= 64 &&
-          CO % 4 == 0 && (int64_t)N * H * (W / 16) < (1ll << 31)) ? 1 : 0;
+  // (any CO <= 64: a block's 16 x CO outputs are 2 CO whole 16-byte chunks -- CO = 3 is the data gradient of an
+  // RGB-input conv, the perceptual loss's first VGG layer)
+  return (N > 0 && H > 0 && W % 16 == 0 && CI >= 4 && CI <= 64 && CI % 4 == 0 && CO >= 1 && CO <= 64 &&
+          (int64_t)N * H * (W / 16) < (1ll << 31)) ? 1 : 0;
 }
 
 // X [N, H, W, CI] bf16 NHWC-contiguous (8-byte aligned); Wk [CO][9][64] bf16 (tap-major, channels zero-padded to 64:

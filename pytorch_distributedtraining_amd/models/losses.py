@@ -9,9 +9,29 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.conv import conv3x3
+
+# PDT_PERCEPT_OWN_CONVS=0: every feature conv on torch / MIOpen (A/B).  Default: in bf16 the <= 64-channel convs
+# (RGB -> 64, 64 -> 64) run ops.conv's kernels -- the RGB conv's data gradient (64 -> 3 channels) was one 0.78 ms CK
+# kernel per micro-step, the implicit-GEMM conv takes it at any output width up to 64 (SwinIR feat 561 -> 574
+# samples/s); fp32 stays on MIOpen (im2col + fp32 GEMM measured 4 % slower there)
+_OWN_CONVS = os.environ.get("PDT_PERCEPT_OWN_CONVS", "1") == "1"
+
+
+class _NarrowConv(nn.Conv2d):
+    """nn.Conv2d(c, v, 3, padding=1) (same parameters / state_dict) that runs ops.conv.conv3x3 in bf16."""
+
+    def forward(self, x):
+        dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) else x.dtype
+        if x.is_cuda and dt == torch.bfloat16:
+            return conv3x3(x, self.weight, self.bias)
+        return super().forward(x)
 
 _CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256]
 _TAPS = {3: "relu1_2", 8: "relu2_2", 15: "relu3_3"}
@@ -25,7 +45,8 @@ class PerceptualLoss(nn.Module):
             if v == "M":
                 layers.append(nn.MaxPool2d(2))
             else:
-                layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=False)]
+                conv = (_NarrowConv if (_OWN_CONVS and c <= 64 and v <= 64) else nn.Conv2d)(c, v, 3, padding=1)
+                layers += [conv, nn.ReLU(inplace=False)]
                 c = v
         self.features = nn.Sequential(*layers)
         g = torch.Generator().manual_seed(seed)

@@ -2386,3 +2386,22 @@ def test_linear_residual_narrow_matches_torch(dt, monkeypatch):
     assert rel_err(y, F.linear(xr, wr, br) + rr) < tol
     for t, ref in ((x, xr), (w, wr), (b, br), (r, rr)):
         assert rel_err(t.grad, ref.grad) < 2 * tol
+
+
+@pytest.mark.gpu
+def test_conv3x3_rgb_input_grad_on_igemm(monkeypatch):
+    """The data gradient of an RGB-input conv (64 -> 3 output channels) on the implicit-GEMM kernel (any CO <= 64),
+    as the perceptual loss's first VGG layer runs it -- vs fp32 F.conv2d."""
+    import pytorch_distributedtraining_amd.ops.conv as CV
+    monkeypatch.setattr(CV, "IGEMM", "1")
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, 32, 48, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    w = (0.1 * torch.randn(64, 3, 3, 3, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(64, device=DEV)).to(torch.bfloat16)
+    y = CV.conv3x3(x, w, b)
+    dy = torch.randn_like(y).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    F.conv2d(xr, w.float(), b.float(), 1, 1).backward(dy.float())
+    assert rel_err(x.grad, xr.grad) < 1e-2
