@@ -694,6 +694,13 @@ def linear(x, weight, bias=None):
 HEAD_MAJOR_QKV = os.environ.get("PDT_HEAD_MAJOR_QKV", "1") == "1"
 
 
+def _has_hooks(module: nn.Module) -> bool:
+    """Forward / pre-forward hooks on the module (or globally): the head-major paths call the GEMM directly, so they
+    step aside for anything that expects to see ``module(x)``."""
+    return bool(module._forward_hooks or module._forward_pre_hooks or nn.modules.module._global_forward_hooks
+                or nn.modules.module._global_forward_pre_hooks)
+
+
 def linear_head_major(module: "Linear", x: torch.Tensor, n_tok: int, head_dim: int) -> torch.Tensor:
     """``module(x)`` for a projection whose ONLY consumer is ops.window_attention (Swin's qkv): where the narrow
     GEMM computes it, the output buffer is written head-major ([windows, 3, heads, n_tok, d], ops.narrow) and the
@@ -701,7 +708,7 @@ def linear_head_major(module: "Linear", x: torch.Tensor, n_tok: int, head_dim: i
     slices contiguously (no relayout pass).  The tensor keeps its logical [..., 3C] shape, and its gradient
     arrives token-major as usual (the Linear's backward never reads its output).  Anything else: ``module(x)``."""
     from .narrow import head_major_ok
-    if HEAD_MAJOR_QKV and x.is_cuda and not fp8_enabled():
+    if HEAD_MAJOR_QKV and x.is_cuda and not fp8_enabled() and not _has_hooks(module):
         xc = x.to(torch.get_autocast_dtype("cuda")) if torch.is_autocast_enabled("cuda") else x
         w, b = module.weight, module.bias
         if torch.is_autocast_enabled("cuda"):
@@ -726,6 +733,8 @@ def linear_from_head_major(module: "Linear", x: torch.Tensor) -> torch.Tensor:
     if hm is None:
         return module(x)
     n_tok, d = hm
+    if _has_hooks(module):     # hooks see the module's usual call on a token-major input
+        return module(_token_major(x.reshape(-1, x.shape[-1]), n_tok, d).view(x.shape))
     w, b = module.weight, module.bias
     if torch.is_autocast_enabled("cuda"):
         w, b = w.to(x.dtype), (None if b is None else b.to(x.dtype))
