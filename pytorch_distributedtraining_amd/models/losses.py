@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import conv3x3
+from ..ops.pool import MaxPool2d
 
 # PDT_PERCEPT_OWN_CONVS=0: every feature conv on torch / MIOpen (A/B).  Default: in bf16 the <= 64-channel convs
 # (RGB -> 64, 64 -> 64) run ops.conv's kernels -- the RGB conv's data gradient (64 -> 3 channels) was one 0.78 ms CK
@@ -43,7 +44,8 @@ class PerceptualLoss(nn.Module):
         layers, c = [], 3
         for v in _CFG:
             if v == "M":
-                layers.append(nn.MaxPool2d(2))
+                # channels-last bf16: ops.pool's kernels (one slot byte per output, gather backward); else torch
+                layers.append(MaxPool2d(2) if _OWN_CONVS else nn.MaxPool2d(2))
             else:
                 conv = (_NarrowConv if (_OWN_CONVS and c <= 64 and v <= 64) else nn.Conv2d)(c, v, 3, padding=1)
                 layers += [conv, nn.ReLU(inplace=False)]
