@@ -37,7 +37,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 struct Geo {
-  int N, H, W, CI, CO;
+  int N, H, W, CI, CO, relu;   // relu: max(0, .) on the biased output (a conv + ReLU pair in one pass)
 };
 
 // the 3 x 18 input pixels of block `blk` (n, h, w0) as 8-byte chunks: chunk q = lane + 64 i -> (row r, pixel p,
@@ -136,7 +136,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv3x3_igemm_kernel(const bf16_t
       const int n = 16 * nt + l16;
       if (n < g.CO) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Ys[(4 * lg + r) * g.CO + n] = f2bf(acc[nt][r] + bcol[nt]);
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[nt][r] + bcol[nt];
+          Ys[(4 * lg + r) * g.CO + n] = f2bf(g.relu ? fmaxf(v, 0.f) : v);
+        }
       }
     }
     wave_sync();
@@ -160,11 +163,12 @@ PDT_API int pdt_conv3x3_igemm_ok(int N, int H, int W, int CI, int CO) {
 
 // X [N, H, W, CI] bf16 NHWC-contiguous (8-byte aligned); Wk [CO][9][64] bf16 (tap-major, channels zero-padded to 64:
 // Wk[co][kh*3+kw][ci] = w[co][ci][kh][kw]); bias [CO] or null; Y [N, H, W, CO] bf16 (16-byte aligned).
-PDT_API int pdt_conv3x3_igemm(const void* X, const void* Wk, const void* bias, void* Y, int N, int H, int W, int CI,
-                              int CO, hipStream_t st) {
+// relu != 0: y = max(0, conv + bias)
+PDT_API int pdt_conv3x3_igemm_act(const void* X, const void* Wk, const void* bias, void* Y, int N, int H, int W,
+                                  int CI, int CO, int relu, hipStream_t st) {
   if (!pdt_conv3x3_igemm_ok(N, H, W, CI, CO) || ((uintptr_t)X & 7) || ((uintptr_t)Y & 15) || ((uintptr_t)Wk & 15))
     return (int)hipErrorInvalidValue;
-  const Geo g{N, H, W, CI, CO};
+  const Geo g{N, H, W, CI, CO, relu};
   const int64_t nblk = (int64_t)N * H * (W / 16);
   const int64_t want = (nblk + NWV - 1) / NWV;
   const int grid = (int)(want < 256 ? want : 256);          // one 8-wave workgroup per CU (the LDS weight tile)
@@ -176,4 +180,9 @@ PDT_API int pdt_conv3x3_igemm(const void* X, const void* Wk, const void* bias, v
   conv3x3_igemm_kernel<4><<<grid, 64 * NWV, igemm_lds<4>(), st>>>((const bf16_t*)X, (const bf16_t*)Wk,
                                                                  (const bf16_t*)bias, (bf16_t*)Y, g);
   return (int)hipGetLastError();
+}
+
+PDT_API int pdt_conv3x3_igemm(const void* X, const void* Wk, const void* bias, void* Y, int N, int H, int W, int CI,
+                              int CO, hipStream_t st) {
+  return pdt_conv3x3_igemm_act(X, Wk, bias, Y, N, H, W, CI, CO, 0, st);
 }

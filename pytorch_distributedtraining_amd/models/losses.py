@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import conv3x3
+from ..ops.conv import conv3x3_relu
 from ..ops.pool import MaxPool2d
 
 # PDT_PERCEPT_OWN_CONVS=0: every feature conv on torch / MIOpen (A/B).  Default: in bf16 the <= 64-channel convs
@@ -25,14 +25,15 @@ from ..ops.pool import MaxPool2d
 _OWN_CONVS = os.environ.get("PDT_PERCEPT_OWN_CONVS", "1") == "1"
 
 
-class _NarrowConv(nn.Conv2d):
-    """nn.Conv2d(c, v, 3, padding=1) (same parameters / state_dict) that runs ops.conv.conv3x3 in bf16."""
+class _NarrowConvReLU(nn.Conv2d):
+    """relu(nn.Conv2d(c, v, 3, padding=1)(x)) (same parameters / state_dict; the ReLU slot after it in ``features``
+    is an Identity): in bf16 ops.conv.conv3x3_relu -- the ReLU in the implicit-GEMM conv's store."""
 
     def forward(self, x):
         dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) else x.dtype
         if x.is_cuda and dt == torch.bfloat16:
-            return conv3x3(x, self.weight, self.bias)
-        return super().forward(x)
+            return conv3x3_relu(x, self.weight, self.bias)
+        return F.relu(super().forward(x))
 
 _CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256]
 _TAPS = {3: "relu1_2", 8: "relu2_2", 15: "relu3_3"}
@@ -47,8 +48,10 @@ class PerceptualLoss(nn.Module):
                 # channels-last bf16: ops.pool's kernels (one slot byte per output, gather backward); else torch
                 layers.append(MaxPool2d(2) if _OWN_CONVS else nn.MaxPool2d(2))
             else:
-                conv = (_NarrowConv if (_OWN_CONVS and c <= 64 and v <= 64) else nn.Conv2d)(c, v, 3, padding=1)
-                layers += [conv, nn.ReLU(inplace=False)]
+                if _OWN_CONVS and c <= 64 and v <= 64:
+                    layers += [_NarrowConvReLU(c, v, 3, padding=1), nn.Identity()]
+                else:
+                    layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=False)]
                 c = v
         self.features = nn.Sequential(*layers)
         g = torch.Generator().manual_seed(seed)

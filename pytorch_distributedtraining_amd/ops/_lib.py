@@ -146,6 +146,8 @@ _SIGS = {
                          c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "pdt_conv3x3_igemm_ok": [c_int, c_int, c_int, c_int, c_int],
     "pdt_conv3x3_igemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "pdt_conv3x3_igemm_act": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_void_p],
     "pdt_l1_partials": [c_int64],
     "pdt_l1_fwd_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p],
     "pdt_narrow_gemm_f32_ok": [c_int64, c_int, c_int],

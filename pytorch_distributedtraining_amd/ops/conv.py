@@ -96,12 +96,13 @@ def _w_taps_flip(w: torch.Tensor) -> torch.Tensor:
     return F.pad(m, (0, 64 - co)).reshape(ci, 9 * 64).to(torch.bfloat16).contiguous()
 
 
-def _igemm(t: torch.Tensor, wk: torch.Tensor, bias, co: int) -> torch.Tensor:
-    """3x3 conv of the NHWC-contiguous [N, C, H, W] ``t`` with the prepared tap weight -> channels_last output."""
+def _igemm(t: torch.Tensor, wk: torch.Tensor, bias, co: int, relu: bool = False) -> torch.Tensor:
+    """3x3 conv of the NHWC-contiguous [N, C, H, W] ``t`` with the prepared tap weight -> channels_last output
+    (``relu``: max(0, .) in the same store)."""
     N, C, H, W = t.shape
     y = torch.empty((N, H, W, co), dtype=torch.bfloat16, device=t.device)
-    _lib.call("pdt_conv3x3_igemm", t.data_ptr(), wk.data_ptr(), _lib.ptr(bias), y.data_ptr(), N, H, W, C, co,
-              _lib.stream_handle(t.device))
+    _lib.call("pdt_conv3x3_igemm_act", t.data_ptr(), wk.data_ptr(), _lib.ptr(bias), y.data_ptr(), N, H, W, C, co,
+              int(relu), _lib.stream_handle(t.device))
     return y.permute(0, 3, 1, 2)
 
 
@@ -140,35 +141,70 @@ class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        N, C, H, W = x.shape
-        co = weight.shape[0]
-        dym = _nhwc_rows(dy)
-        if not dym.is_contiguous():
-            dym = dym.contiguous()
-        dx = dw = db = None
-        if ctx.needs_input_grad[1]:
-            kp = _round8(9 * C)
-            cols = _im2col(x, kp)
-            # [Cout, (kh, kw, c)]: K = N*H*W rows (295k for SwinIR) -> the row-split batched weight-gradient
-            # GEMM of ops.linear (one mm here ran at 27 TFLOP/s: 710 us per 60->60 conv, r1_v9 profile)
-            g = wgrad(dym, cols, torch.float32)[:, :9 * C]
-            dw = g.reshape(co, 3, 3, C).permute(0, 3, 1, 2).to(weight.dtype)
-            del cols
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _colsum(dym, weight.dtype) if colsum_ok(co) and dym.is_contiguous() else \
-                dym.float().sum(0).to(weight.dtype)
-        if ctx.needs_input_grad[0]:
-            kq = _round8(9 * co)
-            dyc = dym.view(N, H, W, co).permute(0, 3, 1, 2)         # NHWC-contiguous view of dY
-            if _igemm_ok(dyc, co, C):
-                wf = _w_taps_flip(weight)
-                if _prefer_igemm(("dgrad", tuple(dy.shape), C, dy.device), lambda: _igemm(dyc, wf, None, C),
-                                 lambda: _im2col(dy, kq) @ _w_flip_rows(weight.to(dy.dtype), kq)):
-                    return _igemm(dyc, wf, None, C), dw, db
-            dcols = _im2col(dy, kq)
-            dxm = dcols @ _w_flip_rows(weight.to(dy.dtype), kq)    # [P, Cin]
-            dx = dxm.view(N, H, W, C).permute(0, 3, 1, 2)
-        return dx, dw, db
+        return _conv3x3_bwd(x, weight, ctx.has_bias, ctx.needs_input_grad, dy)
+
+
+def _conv3x3_bwd(x, weight, has_bias, needs, dy):
+    """(dx, dw, db) of a 3x3 / stride-1 / pad-1 conv (``needs``: which of x, weight, bias want a gradient)."""
+    N, C, H, W = x.shape
+    co = weight.shape[0]
+    dym = _nhwc_rows(dy)
+    if not dym.is_contiguous():
+        dym = dym.contiguous()
+    dx = dw = db = None
+    if needs[1]:
+        kp = _round8(9 * C)
+        cols = _im2col(x, kp)
+        # [Cout, (kh, kw, c)]: K = N*H*W rows (295k for SwinIR) -> the row-split batched weight-gradient
+        # GEMM of ops.linear (one mm here ran at 27 TFLOP/s: 710 us per 60->60 conv, r1_v9 profile)
+        g = wgrad(dym, cols, torch.float32)[:, :9 * C]
+        dw = g.reshape(co, 3, 3, C).permute(0, 3, 1, 2).to(weight.dtype)
+        del cols
+    if has_bias and needs[2]:
+        db = _colsum(dym, weight.dtype) if colsum_ok(co) and dym.is_contiguous() else \
+            dym.float().sum(0).to(weight.dtype)
+    if needs[0]:
+        kq = _round8(9 * co)
+        dyc = dym.view(N, H, W, co).permute(0, 3, 1, 2)         # NHWC-contiguous view of dY
+        if _igemm_ok(dyc, co, C):
+            wf = _w_taps_flip(weight)
+            if _prefer_igemm(("dgrad", tuple(dy.shape), C, dy.device), lambda: _igemm(dyc, wf, None, C),
+                             lambda: _im2col(dy, kq) @ _w_flip_rows(weight.to(dy.dtype), kq)):
+                return _igemm(dyc, wf, None, C), dw, db
+        dcols = _im2col(dy, kq)
+        dxm = dcols @ _w_flip_rows(weight.to(dy.dtype), kq)    # [P, Cin]
+        dx = dxm.view(N, H, W, C).permute(0, 3, 1, 2)
+    return dx, dw, db
+
+
+class _Conv3x3ReluFn(torch.autograd.Function):
+    """relu(conv3x3(x)) with the ReLU in the implicit-GEMM conv's store; backward masks dY by y > 0 (one pass) and
+    runs the conv's backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = _igemm(x, _w_taps(weight), bias, weight.shape[0], relu=True)
+        ctx.save_for_backward(x, weight, y)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        return _conv3x3_bwd(x, weight, ctx.has_bias, ctx.needs_input_grad,
+                            torch.ops.aten.threshold_backward(dy, y, 0))
+
+
+def conv3x3_relu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """relu(conv3x3(x, weight, bias)): one implicit-GEMM pass where the kernel applies (bf16, NHWC, <= 64 channels)."""
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return conv3x3_relu(x.to(dt), weight.to(dt), None if bias is None else bias.to(dt))
+    if (x.is_cuda and x.dim() == 4 and weight.dtype == x.dtype and _igemm_ok(x, x.shape[1], weight.shape[0])
+            and (bias is None or bias.dtype == torch.bfloat16)):
+        return _Conv3x3ReluFn.apply(x, weight, bias)
+    return F.relu(conv3x3(x, weight, bias))
 
 
 def conv3x3(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:

@@ -2405,3 +2405,24 @@ def test_conv3x3_rgb_input_grad_on_igemm(monkeypatch):
     xr = x.detach().float().requires_grad_()
     F.conv2d(xr, w.float(), b.float(), 1, 1).backward(dy.float())
     assert rel_err(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.gpu
+def test_conv3x3_relu_fused_matches_torch(monkeypatch):
+    """conv3x3_relu: the ReLU in the implicit-GEMM conv's store, backward masked by y > 0 -- vs fp32 torch, all grads."""
+    import pytorch_distributedtraining_amd.ops.conv as CV
+    monkeypatch.setattr(CV, "IGEMM", "1")
+    torch.manual_seed(0)
+    x = torch.randn(2, 64, 32, 48, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    w = (0.05 * torch.randn(64, 64, 3, 3, device=DEV)).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(64, device=DEV)).to(torch.bfloat16).requires_grad_()
+    y = CV.conv3x3_relu(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.relu(F.conv2d(xr, wr, br, 1, 1))
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    for t, r in ((x, xr), (w, wr), (b, br)):
+        assert rel_err(t.grad, r.grad) < 2e-2, rel_err(t.grad, r.grad)
