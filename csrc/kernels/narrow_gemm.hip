@@ -162,7 +162,11 @@ __device__ __forceinline__ void hm_store(T* __restrict__ Y, const T* Ys, int64_t
   }
 }
 
-template <int KP, int NP>
+// MODE (compile time, so the plain instantiations carry none of the optional paths' registers -- a runtime switch
+// had cost the K = 180 kernel 46 spilled VGPRs): 0 plain, NG_HMY head-major output, NG_HMA head-major input,
+// NG_RES residual add
+enum { NG_PLAIN = 0, NG_HMY = 1, NG_HMA = 2, NG_RES = 3 };
+template <int KP, int NP, int MODE>
 __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ B,
                                                                  const bf16_t* __restrict__ bias,
@@ -205,16 +209,16 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
   const int64_t gw = (int64_t)blockIdx.x * NW + wv, nwaves = (int64_t)gridDim.x * NW;
   u16x8 ch[Cfg::CH];
   if (gw < nblk) {
-    if (a_n > 0) load_block_hm<KP, NP>(X, KI, gw, lane, a_n, a_d, ch);
+    if constexpr (MODE == NG_HMA) load_block_hm<KP, NP>(X, KI, gw, lane, a_n, a_d, ch);
     else load_block<KP, NP>(X, M, KI, gw, lane, ch);
   }
   for (int64_t blk = gw; blk < nblk; blk += nwaves) {
     const int rows = M - blk * 16 < 16 ? (int)(M - blk * 16) : 16;
     wave_sync();                                 // the previous block's LDS reads are done
-    if (a_n > 0) put_block_hm<KP, NP>(Xs, KI, lane, a_d, ch);
+    if constexpr (MODE == NG_HMA) put_block_hm<KP, NP>(Xs, KI, lane, a_d, ch);
     else put_block<KP, NP>(Xs, KI, rows, lane, ch);
     if (blk + nwaves < nblk) {                   // in flight under the MFMAs
-      if (a_n > 0) load_block_hm<KP, NP>(X, KI, blk + nwaves, lane, a_n, a_d, ch);
+      if constexpr (MODE == NG_HMA) load_block_hm<KP, NP>(X, KI, blk + nwaves, lane, a_n, a_d, ch);
       else load_block<KP, NP>(X, M, KI, blk + nwaves, lane, ch);
     }
     wave_sync();
@@ -245,12 +249,12 @@ __global__ __launch_bounds__(64 * NW, 2) void narrow_gemm_kernel(const bf16_t* _
       }
     }
     wave_sync();
-    if (hm_n > 0) {
+    if constexpr (MODE == NG_HMY) {
       hm_store(Y, Ys, blk, NO, hm_n, hm_d, lane);
     } else {
       bf16_t* dst = Y + blk * 16 * NO;
       const int tot = rows * NO, n8 = tot >> 3;
-      if (R != nullptr) {                        // + the residual stream (same [M, NO] layout), rounded once
+      if constexpr (MODE == NG_RES) {            // + the residual stream (same [M, NO] layout), rounded once
         const bf16_t* res = R + blk * 16 * NO;
         for (int c = lane; c < n8; c += 64) {
           const u16x8 a = *reinterpret_cast<const u16x8*>(Ys + 8 * c), b = *reinterpret_cast<const u16x8*>(res + 8 * c);
@@ -701,10 +705,19 @@ PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void
   const int NP = NO <= 64 ? 64 : NO <= 128 ? 128 : 192;
   const int grid = narrow_grid(M, KI, NO);
   float* part = colsum_out ? ws : nullptr;
-#define PDT_NG(KP_, NP_)                                                                                        \
-  narrow_gemm_kernel<KP_, NP_><<<grid, 64 * NW, NW * NarrowCfg<KP_, NP_>::WAVE_ELEMS * sizeof(bf16_t), st>>>(   \
+  if ((hm_n > 0) + (a_n > 0) + (R != nullptr) > 1) return (int)hipErrorInvalidValue;   // one optional mode at a time
+  const int mode = hm_n > 0 ? NG_HMY : a_n > 0 ? NG_HMA : R != nullptr ? NG_RES : NG_PLAIN;
+#define PDT_NGM(KP_, NP_, M_)                                                                                    \
+  narrow_gemm_kernel<KP_, NP_, M_><<<grid, 64 * NW, NW * NarrowCfg<KP_, NP_>::WAVE_ELEMS * sizeof(bf16_t), st>>>( \
       (const bf16_t*)X, (const bf16_t*)B, (const bf16_t*)bias, (bf16_t*)Y, part, M, KI, NO, hm_n, hm_d, a_n, a_d,  \
       (const bf16_t*)R)
+#define PDT_NG(KP_, NP_)                                                                                        \
+  do {                                                                                                          \
+    if (mode == NG_HMY) PDT_NGM(KP_, NP_, NG_HMY);                                                              \
+    else if (mode == NG_HMA) PDT_NGM(KP_, NP_, NG_HMA);                                                         \
+    else if (mode == NG_RES) PDT_NGM(KP_, NP_, NG_RES);                                                         \
+    else PDT_NGM(KP_, NP_, NG_PLAIN);                                                                           \
+  } while (0)
 #define PDT_NG_N(KP_) \
   do { if (NP == 64) PDT_NG(KP_, 64); else if (NP == 128) PDT_NG(KP_, 128); else PDT_NG(KP_, 192); } while (0)
   if (KP == 64) PDT_NG_N(64);
@@ -712,6 +725,7 @@ PDT_API int pdt_narrow_gemm(const void* X, const void* B, const void* bias, void
   else PDT_NG(192, 64);
 #undef PDT_NG_N
 #undef PDT_NG
+#undef PDT_NGM
   if (colsum_out) {
     const int R = grid * NW;
     float* ws2 = ws + (int64_t)R * KI;
